@@ -1,0 +1,241 @@
+"""Benchmark: SST block decode + re-encode, device-resident (BASELINE.json).
+
+    python bench.py [--gpus N --steps K --warmup W --blocks B]
+
+One "step" = one fused decode -> re-encode pass (sstc_roundtrip_blocks) over
+B blocks resident in HBM (default B = 65 536 uniform 4188 B blocks, 16 B keys /
+100 B values = BASELINE config 2).  With N > 1 (torchrun, one rank per GPU)
+every rank owns its own disjoint shard of B blocks (weak scaling, no data-path
+collective); the barrier and the max-over-ranks timing are the only
+communication.  value = input bytes of all ranks / max-over-ranks time, GiB/s.
+
+Input blocks are produced on the GPU by the codec's own encoder from records
+generated on the host (synthetic, deterministic); a warm-up round trip is
+checked for identity before timing.
+
+roofline: the dominant kernel is rt_fast_kernel.  Algorithmic bytes per launch
+= B x (4188 read + 4188 written); duration = HIP events on
+the codec's stream around each sstc_roundtrip_blocks call (includes the
+per-call counter reset and the deferred-block kernel's empty launch, so the
+fraction is slightly conservative); peak = 8 TB/s (MI355X_MICROARCH.md).
+traffic = HBM bytes per launch from rocprofv3 PMC passes (FETCH_SIZE x 2 for
+gfx950 + WRITE_SIZE, KB units), read from profiles/pmc_traffic.json when it was
+collected for this workload, else null.
+
+cpu_baseline: the reference's own code (oracle/_ref/libsstref.so: BlockReader +
+BlockReaderIterator -> BlockBuilder), one thread, on a bounded sample of the
+same blocks; falls back to the clean-room oracle ("port") if the reference
+build is absent.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "lsm-kv-storage_amd"))
+
+import sstcodec  # noqa: E402
+from sstcodec import workload as W  # noqa: E402
+from sstcodec.codec import RecordTable  # noqa: E402
+
+PER_BLOCK = 28
+BLOCK_BYTES = 4188
+HBM_PEAK_GBPS = 8000.0
+METRIC = "GiB/s SST block decode+re-encode (device-resident), 4 KiB blocks, 1/2/4/8 GPU"
+
+
+def make_blocks(codec, dev, nblocks, rank):
+    """Uniform blocks for this rank's shard: keys k%015d of global record
+    index, 100 B values from splitmix64 (seed 1 + rank), ascending txns."""
+    n = nblocks * PER_BLOCK
+    start = rank * n
+    rec = W.uniform_records(n, key_index=np.arange(start, start + n, dtype=np.uint64), seed=1 + rank,
+                            txn_start=1 + start)
+    table = RecordTable.from_numpy(rec, dev)
+    first = torch.arange(0, n + 1, PER_BLOCK, dtype=torch.int64, device=dev)
+    ksrc = torch.from_numpy(rec["key_src"]).to(dev)
+    vsrc = torch.from_numpy(rec["val_src"]).to(dev)
+    src, off, ln = codec.encode(table, ksrc, vsrc, first)
+    del table, ksrc, vsrc
+    return src, off[:-1].contiguous(), ln.contiguous()
+
+
+def time_roundtrip(codec, src, dst, off, ln, steps, warmup, stream, dist_on):
+    import ctypes
+    nb = off.numel()
+    out_len = torch.empty(nb, dtype=torch.int64, device=src.device)
+    status = torch.empty(nb, dtype=torch.int32, device=src.device)
+    ptr = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    args = (ptr(src), ptr(dst), ptr(off), ptr(ln), nb, 0, ptr(out_len), ptr(status))
+    codec._stream()
+    for _ in range(warmup):
+        rc = codec.roundtrip_raw(*args)
+        assert rc == 0
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
+    if dist_on:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    evs[0].record(stream)
+    for i in range(steps):
+        codec.roundtrip_raw(*args)
+        evs[i + 1].record(stream)
+    torch.cuda.synchronize()
+    if dist_on:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    per_launch = [evs[i].elapsed_time(evs[i + 1]) for i in range(steps)]
+    return wall, per_launch, out_len, status
+
+
+def cpu_baseline(sample_src, sample_off, sample_len, seconds=10.0):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    kind = "reference"
+    try:
+        lib = O.RefLib()
+        run = lambda: lib.roundtrip(sample_src, sample_off, sample_len, dst=dst)  # noqa: E731
+    except (FileNotFoundError, OSError):
+        kind = "port"
+        lib = O.Oracle()
+        run = lambda: lib.roundtrip(sample_src, sample_off, sample_len, 0)  # noqa: E731
+    dst = np.zeros_like(sample_src)
+    run()  # warm
+    passes = 0
+    t0 = time.perf_counter()
+    while True:
+        run()
+        passes += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    nbytes = passes * int(sample_len.sum())
+    return {"value": nbytes / el / 2 ** 30, "unit": "GiB/s", "cores": 1, "kind": kind,
+            "sample": f"{sample_len.size} blocks x {int(sample_len[0])} B (same uniform workload), "
+                      f"{passes} passes in {el:.1f} s, 1 thread, decode (BlockReader/Iterator) + "
+                      f"re-encode (BlockBuilder) in host memory"}
+
+
+def read_traffic(nblocks):
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(p) as f:
+            d = json.load(f)
+        if int(d.get("nblocks", -1)) == nblocks and d.get("kernel") and d.get("hbm_bytes_per_launch"):
+            return float(d["hbm_bytes_per_launch"])
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def copy_peak(dev, nbytes=1 << 30, reps=10):
+    a = torch.empty(nbytes // 4, dtype=torch.float32, device=dev)
+    b = torch.empty_like(a)
+    b.copy_(a)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        b.copy_(a)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    del a, b
+    return 2 * nbytes / (ms * 1e-3) / 1e9
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--blocks", type=int, default=65536, help="blocks per GPU (config 2: 65536)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist_on = world > 1
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if dist_on:
+        dist.init_process_group("nccl", device_id=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    codec = sstcodec.Codec(local)
+    nb = args.blocks
+    codec.reserve(nb, nb * PER_BLOCK)
+    src, off, ln = make_blocks(codec, dev, nb, rank)
+    torch.cuda.synchronize()
+    assert int(ln.min()) == BLOCK_BYTES == int(ln.max())
+    dst = torch.empty_like(src)
+
+    wall, per_launch, out_len, status = time_roundtrip(codec, src, dst, off, ln, args.steps, args.warmup,
+                                                       stream, dist_on)
+    # correctness of what was timed: identity round trip, no block errors
+    ok = bool(torch.equal(dst, src)) and bool((status == 0).all()) and bool((out_len == BLOCK_BYTES).all())
+    if not ok:
+        raise SystemExit("round trip output differs from input: timing invalid")
+
+    t = torch.tensor([wall], dtype=torch.float64, device=dev)
+    if dist_on:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    wall_max = float(t.item())
+    in_bytes = nb * BLOCK_BYTES
+    total_in = in_bytes * world * args.steps
+    value = total_in / wall_max / 2 ** 30
+    ms_step = wall_max / args.steps * 1e3
+
+    launch_ms = float(np.mean(per_launch))
+    alg = 2 * in_bytes  # read + written per launch
+    achieved = alg / (launch_ms * 1e-3) / 1e9
+    traffic = read_traffic(nb)
+
+    if rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (uniform 16 B keys k%015d / 100 B splitmix64 values, blocks built on GPU by "
+                    "the codec's encoder; identity round trip verified)",
+            "config": {"workload": "config2: batch decode+re-encode of 65536 x 4188 B device-resident "
+                                   "blocks per GPU (28 PUTs each), fused rt_fast_kernel",
+                       "blocks_per_gpu": nb, "block_bytes": BLOCK_BYTES, "records_per_gpu": nb * PER_BLOCK,
+                       "txn_mode": "compat", "parallelism": f"shard{world}"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
+                         "kernel": "rt_fast_kernel", "alg_bytes_per_launch": alg,
+                         "launch_ms_events": round(launch_ms, 5)},
+        }
+        if world == 1:
+            out["roofline"]["copy_peak_GBps"] = round(copy_peak(dev), 1)
+            if not args.no_cpu_baseline:
+                k = min(nb, 16384)
+                s = src[: k * BLOCK_BYTES].cpu().numpy()
+                o = off[:k].cpu().numpy().view(np.uint64)
+                l_ = ln[:k].cpu().numpy().view(np.uint64)
+                out["cpu_baseline"] = cpu_baseline(s, o, l_, args.cpu_seconds)
+        print(json.dumps(out), flush=True)
+    if dist_on:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,163 @@
+/*
+ * sstcodec.h — C-ABI of the MI355X SST block codec (libsstcodec.so).
+ *
+ * Drop-in boundary for the byte work of the reference's sstable layer
+ * (NamHoaiNguyen/LSM-KV-Storage).  The reference has no FFI; its boundary is the
+ * C++ class API of sstable/ (see INTEGRATION.md).  Each entry point below says
+ * which reference interface it replaces.
+ *
+ * Conventions
+ *   - Every pointer named d_* is DEVICE memory (hipMalloc / torch CUDA tensor)
+ *     owned by the caller.  Nothing in this header takes ownership.
+ *   - All work is enqueued on the context's stream; calls return after enqueue
+ *     (asynchronous) unless documented otherwise.  A call whose workspace need
+ *     exceeds what the context holds grows it (synchronising the stream); after
+ *     sstc_ctx_reserve() for the largest batch no call allocates or
+ *     synchronises, so a sequence of calls can be captured into a hipGraph.
+ *   - Return value: 0 = SSTC_OK, negative = error; the thread-local message is
+ *     in sstc_last_error_string().  Per-block data errors are NOT call errors:
+ *     they are reported in d_block_status[] (SSTC_BLK_*) and counted in the
+ *     context error counter (sstc_ctx_error_count).
+ *   - Re-entrancy: no global mutable state.  A context is used by one host
+ *     thread at a time; concurrent TableBuilders (reference db/db_impl.cc:
+ *     354-362) each own a context.
+ *
+ * Block format (reference sstable/block_builder.h:14-57), all little-endian:
+ *   block       = data entries | offset entries | extra
+ *   PUT entry   = u8 type(0) | u32 key_len | key | u32 val_len | val | u64 txn
+ *   DEL entry   = u8 type(1) | u32 key_len | key | u64 txn
+ *   offset      = u64 entry_start | u64 entry_size            (16 B per entry)
+ *   extra       = u64 num_entries | u64 offset_section_start   (16 B)
+ *
+ * Record model: value fields are encoded iff val_len != SSTC_NO_VALUE (the
+ * reference's `value.data() != nullptr`, block_builder.cc:19-21,56).  Decode
+ * gives DELETE records SSTC_NO_VALUE (block_reader.cc:84-88).
+ */
+#ifndef SSTCODEC_H
+#define SSTCODEC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SSTC_ABI_VERSION 1u
+#define SSTC_NO_VALUE 0xFFFFFFFFu
+#define SSTC_TYPE_PUT 0u     /* db/status.h:13 ValueType::PUT     */
+#define SSTC_TYPE_DELETED 1u /* db/status.h:15 ValueType::DELETED */
+#define SSTC_MAX_KEY 4096u   /* common/macros.h:29 kMaxKeySize     */
+
+/* call status */
+#define SSTC_OK 0
+#define SSTC_E_INVALID_ARG -1
+#define SSTC_E_HIP -2
+#define SSTC_E_NOMEM -3
+#define SSTC_E_NO_DEVICE -4
+#define SSTC_E_CAPACITY -5 /* workspace too small: call sstc_ctx_reserve */
+
+/* per-block status, d_block_status[b] */
+#define SSTC_BLK_OK 0
+#define SSTC_BLK_TOO_SMALL 1      /* block shorter than its 16 B extra            */
+#define SSTC_BLK_EMPTY 2          /* num_entries == 0 (FlushBlock never writes it) */
+#define SSTC_BLK_OFFSETS_RANGE 3  /* offset section outside [0, len-16)           */
+#define SSTC_BLK_ENTRY_RANGE 4    /* an entry runs outside the data section        */
+#define SSTC_BLK_BAD_TYPE 5       /* type byte not PUT/DELETED                     */
+#define SSTC_BLK_KEY_TOO_LONG 6   /* key_len > 4096 (block_builder.cc:38 assert)   */
+#define SSTC_BLK_TOO_LARGE 7      /* block >= 4 GiB                                */
+
+/* txn read mode.  COMPAT reproduces BlockReader::GetTransactionIdFromDataEntry
+ * (block_reader.cc:104-114): it tests value.empty() instead of the type, so an
+ * empty-value PUT reads its txn as (txn & 0xffffffff) << 32 and a re-encode
+ * writes that value.  CORRECT reads the field the encoder wrote. */
+#define SSTC_TXN_COMPAT 0u
+#define SSTC_TXN_CORRECT 1u
+
+typedef struct sstc_ctx sstc_ctx;
+
+/* Structure-of-arrays record table in device memory (one element per record).
+ * key_off / val_off are byte offsets into the key / value source buffer given
+ * alongside (for decode output: into d_src). */
+typedef struct sstc_records {
+  uint8_t *type;
+  uint32_t *key_len;
+  uint32_t *val_len; /* SSTC_NO_VALUE = no value fields */
+  uint64_t *txn;
+  uint64_t *key_off;
+  uint64_t *val_off;
+} sstc_records;
+
+uint32_t sstc_version(void);
+const char *sstc_last_error_string(void);
+
+/* Context: device, stream and workspace.  stream is a hipStream_t (NULL = the
+ * null stream); it may be changed between calls with sstc_ctx_set_stream. */
+int sstc_ctx_create(int device, void *stream, sstc_ctx **out);
+int sstc_ctx_destroy(sstc_ctx *ctx);
+int sstc_ctx_set_stream(sstc_ctx *ctx, void *stream);
+/* Pre-size the workspace for up to max_blocks blocks and max_records records. */
+int sstc_ctx_reserve(sstc_ctx *ctx, uint64_t max_blocks, uint64_t max_records);
+/* Synchronise the stream; return the number of blocks that failed since the
+ * last reset (per-block codes are in the callers' d_block_status arrays). */
+int sstc_ctx_error_count(sstc_ctx *ctx, uint64_t *out);
+int sstc_ctx_reset_errors(sstc_ctx *ctx);
+
+/* ---- decode (replaces TableReader::CreateAndSetupDataForBlockReader,
+ *      sstable/table_reader.cc:212-241, and the BlockReader field accessors,
+ *      sstable/block_reader.cc:59-114, for a batch of blocks) ---------------- */
+
+/* Exclusive scan of per-block entry counts from the 16 B extras.
+ * d_rec_base has nblocks+1 elements; d_rec_base[nblocks] = total records.  A
+ * block whose extra is malformed counts 0 records. */
+int sstc_count_records(sstc_ctx *ctx, const uint8_t *d_src, const uint64_t *d_blk_off,
+                       const uint64_t *d_blk_len, uint64_t nblocks, uint64_t *d_rec_base);
+
+/* Parse every entry of every block into the record table at d_rec_base[b] + i.
+ * Key/value offsets are absolute offsets into d_src.  d_block_status may be
+ * NULL. */
+int sstc_decode_blocks(sstc_ctx *ctx, const uint8_t *d_src, const uint64_t *d_blk_off,
+                       const uint64_t *d_blk_len, uint64_t nblocks, const uint64_t *d_rec_base,
+                       sstc_records out, uint32_t txn_mode, uint32_t *d_block_status);
+
+/* ---- encode (replaces BlockBuilder::AddEntry/EncodeExtraInfo and the block
+ *      write of TableBuilder::FlushBlock, sstable/block_builder.cc:12-109,
+ *      sstable/table_builder.cc:62-99) --------------------------------------- */
+
+/* Greedy block segmentation of TableBuilder::AddEntry (table_builder.cc:57-59):
+ * a block is closed right after the record that brings sum(entry_size + 16) to
+ * >= block_threshold.  Writes record-index boundaries d_blk_first[0..nb] and the
+ * block count to *d_nblocks (device). d_blk_first needs nrec+1 elements. */
+int sstc_segment_records(sstc_ctx *ctx, const uint32_t *d_key_len, const uint32_t *d_val_len,
+                         uint64_t nrec, uint64_t block_threshold, uint64_t *d_blk_first,
+                         uint64_t *d_nblocks);
+
+/* Encode records [d_blk_first[b], d_blk_first[b+1]) into block b, blocks laid
+ * out back-to-back from byte out_base of d_dst.  The record table holds nrec
+ * records and every d_blk_first[] value is <= nrec.  Writes d_out_blk_len[b]
+ * (nblocks elements) and d_out_blk_off[0..nblocks] (nblocks+1 elements; the
+ * last one is the end offset).  Keys are read at d_key_src + key_off[r], values
+ * at d_val_src + val_off[r].  An empty range encodes a 16 B block with
+ * num_entries = 0 (TableBuilder::FlushBlock never writes one, so callers skip
+ * empty ranges). */
+int sstc_encode_blocks(sstc_ctx *ctx, const uint8_t *d_key_src, const uint8_t *d_val_src,
+                       sstc_records in, uint64_t nrec, const uint64_t *d_blk_first,
+                       uint64_t nblocks, uint64_t out_base, uint8_t *d_dst,
+                       uint64_t *d_out_blk_off, uint64_t *d_out_blk_len);
+
+/* ---- fused device-resident decode -> re-encode (the compaction pass-through
+ *      of db/compact.cc:254-302 for blocks whose records all survive) -------- */
+
+/* Decode every block and re-encode its records; block b is written at
+ * d_blk_off[b] of d_dst (d_dst must not alias d_src).  d_out_blk_len[b] gets
+ * the re-encoded size (0 on error); d_block_status[b] the decode status.
+ * Either output pointer may be NULL. */
+int sstc_roundtrip_blocks(sstc_ctx *ctx, const uint8_t *d_src, uint8_t *d_dst,
+                          const uint64_t *d_blk_off, const uint64_t *d_blk_len,
+                          uint64_t nblocks, uint32_t txn_mode, uint64_t *d_out_blk_len,
+                          uint32_t *d_block_status);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SSTCODEC_H */

@@ -1,0 +1,260 @@
+// sstc_api.hip — extern "C" implementation of include/sstcodec.h.
+//
+// Host side of the boundary: argument checks, the per-context workspace and
+// the launch sequences.  No compute happens here and there is no CPU fallback:
+// every entry point fails with SSTC_E_NO_DEVICE when no HIP device exists.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "../../include/sstcodec.h"
+#include "sstc_launch.h"
+
+struct sstc_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  uint64_t cap_blocks = 0, cap_records = 0, cap_scan = 0, cap_jump = 0;
+  uint32_t *slow_list = nullptr;            // cap_blocks
+  uint32_t *slow_count = nullptr;           // 1
+  unsigned long long *err_count = nullptr;  // 1
+  uint64_t *scan_ws = nullptr;              // cap_scan
+  uint64_t *sizes = nullptr;                // cap_records + 1
+  uint64_t *P = nullptr;                    // cap_records + 1
+  uint32_t *jump = nullptr;                 // cap_jump
+};
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const char *what, hipError_t e = hipSuccess) {
+  g_last_error = what;
+  if (e != hipSuccess) {
+    g_last_error += ": ";
+    g_last_error += hipGetErrorString(e);
+  }
+  return code;
+}
+
+#define SSTC_HIP(call, what)                                                                       \
+  do {                                                                                             \
+    hipError_t e_ = (call);                                                                        \
+    if (e_ != hipSuccess) return fail(SSTC_E_HIP, what, e_);                                       \
+  } while (0)
+
+int bind_device(sstc_ctx *c) {
+  int cur = -1;
+  if (hipGetDevice(&cur) != hipSuccess) return fail(SSTC_E_NO_DEVICE, "no HIP device");
+  if (cur != c->device) SSTC_HIP(hipSetDevice(c->device), "hipSetDevice");
+  return SSTC_OK;
+}
+
+template <class T> int grow(sstc_ctx *c, T *&p, uint64_t &cap, uint64_t need, const char *what) {
+  if (need <= cap && p) return SSTC_OK;
+  SSTC_HIP(hipStreamSynchronize(c->stream), "hipStreamSynchronize before workspace growth");
+  if (p) SSTC_HIP(hipFree(p), "hipFree");
+  p = nullptr;
+  cap = 0;
+  uint64_t n = need < 1024 ? 1024 : need;
+  n += n / 4; // headroom
+  if (hipMalloc(reinterpret_cast<void **>(&p), n * sizeof(T)) != hipSuccess) {
+    p = nullptr;
+    return fail(SSTC_E_NOMEM, what);
+  }
+  cap = n;
+  return SSTC_OK;
+}
+
+int ensure_scan(sstc_ctx *c, uint64_t n) {
+  return grow(c, c->scan_ws, c->cap_scan, sstc::scan_workspace_elems(n), "scan workspace");
+}
+
+int ensure_blocks(sstc_ctx *c, uint64_t nb) {
+  int r = grow(c, c->slow_list, c->cap_blocks, nb, "block workspace");
+  if (r) return r;
+  return ensure_scan(c, nb + 1);
+}
+
+int ensure_records(sstc_ctx *c, uint64_t nr) {
+  uint64_t cap = c->cap_records;
+  int r = grow(c, c->sizes, cap, nr + 1, "record workspace");
+  if (r) return r;
+  uint64_t cap2 = c->cap_records;
+  r = grow(c, c->P, cap2, nr + 1, "record workspace");
+  if (r) return r;
+  c->cap_records = cap < cap2 ? cap : cap2;
+  return ensure_scan(c, nr + 1);
+}
+
+uint32_t bit_length(uint64_t v) {
+  uint32_t b = 0;
+  while (v) {
+    b++;
+    v >>= 1;
+  }
+  return b;
+}
+
+bool bad_records(const sstc_records &r) {
+  return !r.type || !r.key_len || !r.val_len || !r.txn || !r.key_off || !r.val_off;
+}
+
+} // namespace
+
+extern "C" {
+
+uint32_t sstc_version(void) { return SSTC_ABI_VERSION; }
+
+const char *sstc_last_error_string(void) { return g_last_error.c_str(); }
+
+int sstc_ctx_create(int device, void *stream, sstc_ctx **out) {
+  if (!out) return fail(SSTC_E_INVALID_ARG, "out is NULL");
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+    return fail(SSTC_E_NO_DEVICE, "no HIP device: libsstcodec has no CPU path");
+  if (device < 0 || device >= ndev) return fail(SSTC_E_INVALID_ARG, "device index out of range");
+  sstc_ctx *c = new sstc_ctx();
+  c->device = device;
+  c->stream = static_cast<hipStream_t>(stream);
+  if (int r = bind_device(c)) {
+    delete c;
+    return r;
+  }
+  if (hipMalloc(reinterpret_cast<void **>(&c->slow_count), 64) != hipSuccess) {
+    delete c;
+    return fail(SSTC_E_NOMEM, "context counters");
+  }
+  c->err_count = reinterpret_cast<unsigned long long *>(reinterpret_cast<char *>(c->slow_count) + 8);
+  if (hipMemset(c->slow_count, 0, 64) != hipSuccess) {
+    (void)hipFree(c->slow_count);
+    delete c;
+    return fail(SSTC_E_HIP, "context counters");
+  }
+  *out = c;
+  return SSTC_OK;
+}
+
+int sstc_ctx_destroy(sstc_ctx *c) {
+  if (!c) return SSTC_OK;
+  bind_device(c);
+  (void)hipStreamSynchronize(c->stream);
+  for (void *p : {static_cast<void *>(c->slow_list), static_cast<void *>(c->slow_count),
+                  static_cast<void *>(c->scan_ws), static_cast<void *>(c->sizes),
+                  static_cast<void *>(c->P), static_cast<void *>(c->jump)})
+    if (p) (void)hipFree(p);
+  delete c;
+  return SSTC_OK;
+}
+
+int sstc_ctx_set_stream(sstc_ctx *c, void *stream) {
+  if (!c) return fail(SSTC_E_INVALID_ARG, "ctx is NULL");
+  c->stream = static_cast<hipStream_t>(stream);
+  return SSTC_OK;
+}
+
+int sstc_ctx_reserve(sstc_ctx *c, uint64_t max_blocks, uint64_t max_records) {
+  if (!c) return fail(SSTC_E_INVALID_ARG, "ctx is NULL");
+  if (int r = bind_device(c)) return r;
+  if (int r = ensure_blocks(c, max_blocks)) return r;
+  if (int r = ensure_records(c, max_records)) return r;
+  return SSTC_OK;
+}
+
+int sstc_ctx_error_count(sstc_ctx *c, uint64_t *out) {
+  if (!c || !out) return fail(SSTC_E_INVALID_ARG, "NULL argument");
+  if (int r = bind_device(c)) return r;
+  unsigned long long v = 0;
+  SSTC_HIP(hipMemcpyAsync(&v, c->err_count, sizeof(v), hipMemcpyDeviceToHost, c->stream), "error count copy");
+  SSTC_HIP(hipStreamSynchronize(c->stream), "hipStreamSynchronize");
+  *out = v;
+  return SSTC_OK;
+}
+
+int sstc_ctx_reset_errors(sstc_ctx *c) {
+  if (!c) return fail(SSTC_E_INVALID_ARG, "ctx is NULL");
+  if (int r = bind_device(c)) return r;
+  SSTC_HIP(hipMemsetAsync(c->err_count, 0, sizeof(unsigned long long), c->stream), "reset errors");
+  return SSTC_OK;
+}
+
+int sstc_count_records(sstc_ctx *c, const uint8_t *d_src, const uint64_t *d_blk_off,
+                       const uint64_t *d_blk_len, uint64_t nblocks, uint64_t *d_rec_base) {
+  if (!c || !d_rec_base || (nblocks && (!d_src || !d_blk_off || !d_blk_len)))
+    return fail(SSTC_E_INVALID_ARG, "sstc_count_records: NULL argument");
+  if (int r = bind_device(c)) return r;
+  if (int r = ensure_scan(c, nblocks + 1)) return r;
+  SSTC_HIP(sstc::launch_count(d_src, d_blk_off, d_blk_len, nblocks, d_rec_base, c->stream), "count kernel");
+  SSTC_HIP(sstc::launch_scan(d_rec_base, nblocks, 0, d_rec_base, c->scan_ws, c->stream), "scan");
+  return SSTC_OK;
+}
+
+int sstc_decode_blocks(sstc_ctx *c, const uint8_t *d_src, const uint64_t *d_blk_off,
+                       const uint64_t *d_blk_len, uint64_t nblocks, const uint64_t *d_rec_base,
+                       sstc_records out, uint32_t txn_mode, uint32_t *d_block_status) {
+  if (!c || (nblocks && (!d_src || !d_blk_off || !d_blk_len || !d_rec_base || bad_records(out))))
+    return fail(SSTC_E_INVALID_ARG, "sstc_decode_blocks: NULL argument");
+  if (txn_mode > SSTC_TXN_CORRECT) return fail(SSTC_E_INVALID_ARG, "bad txn_mode");
+  if (int r = bind_device(c)) return r;
+  sstc::DecArgs a{d_src, d_blk_off, d_blk_len, nblocks, d_rec_base, out, txn_mode, d_block_status,
+                  c->err_count};
+  SSTC_HIP(sstc::launch_decode(a, c->stream), "decode kernel");
+  return SSTC_OK;
+}
+
+int sstc_segment_records(sstc_ctx *c, const uint32_t *d_key_len, const uint32_t *d_val_len,
+                         uint64_t nrec, uint64_t block_threshold, uint64_t *d_blk_first,
+                         uint64_t *d_nblocks) {
+  if (!c || !d_blk_first || !d_nblocks || (nrec && (!d_key_len || !d_val_len)))
+    return fail(SSTC_E_INVALID_ARG, "sstc_segment_records: NULL argument");
+  if (nrec >= 0xFFFFFFFFull) return fail(SSTC_E_INVALID_ARG, "too many records for one call");
+  if (int r = bind_device(c)) return r;
+  if (int r = ensure_records(c, nrec)) return r;
+  const uint32_t levels = bit_length(nrec) ? bit_length(nrec) : 1;
+  if (int r = grow(c, c->jump, c->cap_jump, static_cast<uint64_t>(levels) * (nrec + 1), "jump tables")) return r;
+  // weights = entry_size + 16 (block_builder.cc:33), Pw = exclusive scan
+  SSTC_HIP(sstc::launch_enc_sizes(d_key_len, d_val_len, nrec, 16, c->sizes, c->stream), "weights");
+  SSTC_HIP(sstc::launch_scan(c->sizes, nrec, 0, c->P, c->scan_ws, c->stream), "scan");
+  SSTC_HIP(sstc::launch_segment(c->P, nrec, block_threshold, c->jump, levels, d_nblocks, d_blk_first, c->stream),
+           "segment kernels");
+  return SSTC_OK;
+}
+
+int sstc_encode_blocks(sstc_ctx *c, const uint8_t *d_key_src, const uint8_t *d_val_src,
+                       sstc_records in, uint64_t nrec, const uint64_t *d_blk_first,
+                       uint64_t nblocks, uint64_t out_base, uint8_t *d_dst,
+                       uint64_t *d_out_blk_off, uint64_t *d_out_blk_len) {
+  if (!c || !d_out_blk_off || (nblocks && (!d_blk_first || !d_dst || !d_out_blk_len)) ||
+      (nrec && (!d_key_src || !d_val_src || bad_records(in))))
+    return fail(SSTC_E_INVALID_ARG, "sstc_encode_blocks: NULL argument");
+  if (int r = bind_device(c)) return r;
+  if (int r = ensure_records(c, nrec)) return r;
+  if (int r = ensure_scan(c, nblocks + 1)) return r;
+  SSTC_HIP(sstc::launch_enc_sizes(in.key_len, in.val_len, nrec, 0, c->sizes, c->stream), "sizes");
+  SSTC_HIP(sstc::launch_scan(c->sizes, nrec, 0, c->P, c->scan_ws, c->stream), "scan");
+  SSTC_HIP(sstc::launch_enc_blk_len(c->P, d_blk_first, nblocks, d_out_blk_len, c->stream), "block sizes");
+  SSTC_HIP(sstc::launch_scan(d_out_blk_len, nblocks, out_base, d_out_blk_off, c->scan_ws, c->stream), "scan");
+  sstc::EncArgs a{d_key_src, d_val_src, in, d_blk_first, nblocks, c->P, d_out_blk_off, d_out_blk_len, d_dst};
+  SSTC_HIP(sstc::launch_enc_emit(a, c->stream), "emit kernel");
+  return SSTC_OK;
+}
+
+int sstc_roundtrip_blocks(sstc_ctx *c, const uint8_t *d_src, uint8_t *d_dst,
+                          const uint64_t *d_blk_off, const uint64_t *d_blk_len, uint64_t nblocks,
+                          uint32_t txn_mode, uint64_t *d_out_blk_len, uint32_t *d_block_status) {
+  if (!c || (nblocks && (!d_src || !d_dst || !d_blk_off || !d_blk_len)))
+    return fail(SSTC_E_INVALID_ARG, "sstc_roundtrip_blocks: NULL argument");
+  if (d_src == d_dst && nblocks) return fail(SSTC_E_INVALID_ARG, "d_dst must not alias d_src");
+  if (txn_mode > SSTC_TXN_CORRECT) return fail(SSTC_E_INVALID_ARG, "bad txn_mode");
+  if (nblocks >= 0xFFFFFFFFull) return fail(SSTC_E_INVALID_ARG, "too many blocks for one call");
+  if (int r = bind_device(c)) return r;
+  if (int r = ensure_blocks(c, nblocks)) return r;
+  sstc::RtArgs a{d_src, d_dst, d_blk_off, d_blk_len, nblocks, txn_mode, d_out_blk_len, d_block_status,
+                 c->slow_list, c->slow_count, c->err_count};
+  SSTC_HIP(sstc::launch_roundtrip(a, c->stream), "roundtrip kernels");
+  return SSTC_OK;
+}
+
+} // extern "C"

@@ -1,0 +1,139 @@
+// sstc_device.h — device-side helpers for the SST block codec kernels (gfx950).
+//
+// Byte-format facts used everywhere (reference sstable/block_builder.h:14-57):
+// every multi-byte field is little-endian and sits at an arbitrary byte offset
+// (blocks are packed back-to-back, fields follow variable-length keys), so all
+// field reads go through the unaligned helpers below: two or three aligned
+// dword reads + v_alignbyte_b32, never a misaligned wide access.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace sstc {
+
+constexpr uint32_t kWave = 64;
+constexpr uint32_t kNoValue = 0xFFFFFFFFu;
+constexpr uint32_t kTypePut = 0, kTypeDeleted = 1;
+constexpr uint32_t kMaxKey = 4096;
+
+enum BlkStatus : uint32_t {
+  kBlkOk = 0,
+  kBlkTooSmall = 1,
+  kBlkEmpty = 2,
+  kBlkOffsetsRange = 3,
+  kBlkEntryRange = 4,
+  kBlkBadType = 5,
+  kBlkKeyTooLong = 6,
+  kBlkTooLarge = 7,
+};
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) void gbl_void_t;
+
+__device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
+
+// wave-uniform value -> SGPR (tells the compiler the value is uniform)
+__device__ __forceinline__ uint32_t uniform(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint64_t uniform64(uint64_t v) {
+  uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v));
+  uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v >> 32));
+  return (static_cast<uint64_t>(hi) << 32) | lo;
+}
+
+// ---- LDS image reads (image is padded by >= 16 bytes past its last byte) ----
+__device__ __forceinline__ uint32_t lds_u8(const uint8_t *img, uint32_t off) { return img[off]; }
+
+__device__ __forceinline__ uint32_t lds_u32u(const uint8_t *img, uint32_t off) {
+  const uint32_t *w = reinterpret_cast<const uint32_t *>(img + (off & ~3u));
+  return __builtin_amdgcn_alignbyte(w[1], w[0], off & 3u);
+}
+
+__device__ __forceinline__ uint64_t lds_u64u(const uint8_t *img, uint32_t off) {
+  const uint32_t *w = reinterpret_cast<const uint32_t *>(img + (off & ~3u));
+  const uint32_t a = w[0], b = w[1], c = w[2], sh = off & 3u;
+  const uint32_t lo = __builtin_amdgcn_alignbyte(b, a, sh);
+  const uint32_t hi = __builtin_amdgcn_alignbyte(c, b, sh);
+  return (static_cast<uint64_t>(hi) << 32) | lo;
+}
+
+// Unaligned LDS stores.  `aligned4` must be wave-uniform for good code.
+__device__ __forceinline__ void lds_st_u64u(uint8_t *img, uint32_t off, uint64_t v) {
+  if ((off & 3u) == 0) {
+    uint32_t *w = reinterpret_cast<uint32_t *>(img + off);
+    w[0] = static_cast<uint32_t>(v);
+    w[1] = static_cast<uint32_t>(v >> 32);
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; j++) img[off + j] = static_cast<uint8_t>(v >> (8 * j));
+  }
+}
+
+// ---- global reads at arbitrary byte offsets ---------------------------------
+// Only dwords that hold a requested byte are touched, so a field that ends at
+// the last byte of an allocation never reads past it.
+__device__ __forceinline__ uint32_t g_u8(const uint8_t *p) { return *p; }
+
+__device__ __forceinline__ uint32_t g_u32u(const uint8_t *p) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  const uint32_t *w = reinterpret_cast<const uint32_t *>(a & ~uintptr_t(3));
+  const uint32_t sh = a & 3u;
+  const uint32_t lo = w[0];
+  const uint32_t hi = sh ? w[1] : 0u;
+  return __builtin_amdgcn_alignbyte(hi, lo, sh);
+}
+
+__device__ __forceinline__ uint64_t g_u64u(const uint8_t *p) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  const uint32_t *w = reinterpret_cast<const uint32_t *>(a & ~uintptr_t(3));
+  const uint32_t sh = a & 3u;
+  const uint32_t x = w[0], y = w[1];
+  const uint32_t z = sh ? w[2] : 0u;
+  const uint32_t lo = __builtin_amdgcn_alignbyte(y, x, sh);
+  const uint32_t hi = __builtin_amdgcn_alignbyte(z, y, sh);
+  return (static_cast<uint64_t>(hi) << 32) | lo;
+}
+
+// ---- wave-level primitives (wave64) -----------------------------------------
+__device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v) {
+  const uint32_t lane = lane_id();
+#pragma unroll
+  for (uint32_t d = 1; d < kWave; d <<= 1) {
+    const uint32_t t = __shfl_up(v, d, kWave);
+    if (lane >= d) v += t;
+  }
+  return v;
+}
+
+__device__ __forceinline__ uint64_t wave_incl_scan_u64(uint64_t v) {
+  const uint32_t lane = lane_id();
+#pragma unroll
+  for (uint32_t d = 1; d < kWave; d <<= 1) {
+    const uint64_t t = __shfl_up(v, d, kWave);
+    if (lane >= d) v += t;
+  }
+  return v;
+}
+
+__device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
+#pragma unroll
+  for (uint32_t d = kWave / 2; d > 0; d >>= 1) v += __shfl_xor(v, d, kWave);
+  return v;
+}
+
+// LDS writes of one lane are made visible to the other lanes of the SAME wave:
+// LDS executes a wave's DS instructions in order, so only a compiler barrier
+// and the lgkmcnt drain are needed (no s_barrier).
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// One record's entry size (reference sstable/block_builder.cc:19-21).
+__device__ __forceinline__ uint64_t entry_size(uint32_t key_len, uint32_t val_len) {
+  return 13ull + key_len + (val_len != kNoValue ? 4ull + val_len : 0ull);
+}
+
+} // namespace sstc

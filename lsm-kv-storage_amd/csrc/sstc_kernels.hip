@@ -1,0 +1,766 @@
+// sstc_kernels.hip — CDNA4 (gfx950) kernels of the SST block codec.
+//
+// Kernels (each cites the reference function whose byte work it replaces):
+//   rt_fast_kernel      fused decode -> re-encode, one wave per block staged in
+//                       LDS by LDS-DMA (global_load_lds_dwordx4).  Handles every
+//                       block that fits a wave slot and whose entries are packed
+//                       back-to-back (every block the reference writes).
+//   rt_generic_kernel   same contract for the blocks the fast kernel defers
+//                       (larger than a slot, or entries not packed): one
+//                       workgroup per block, fields read straight from HBM.
+//   count_kernel        per-block entry count from the 16 B extra
+//                       (TableReader::CreateAndSetupDataForBlockReader,
+//                       sstable/table_reader.cc:226-232).
+//   decode_kernel       per-entry parse into a record table
+//                       (BlockReader accessors, sstable/block_reader.cc:59-114).
+//   enc_*_kernel        records -> blocks (BlockBuilder, block_builder.cc:12-109).
+//   seg_*_kernel        greedy block segmentation of TableBuilder::AddEntry
+//                       (table_builder.cc:57-59) by pointer doubling.
+//   scan_*_kernel       device-wide exclusive scan (u64) used by the above.
+#include "sstc_device.h"
+#include "sstc_launch.h"
+
+namespace sstc {
+
+// ---------------------------------------------------------------------------
+// Entry parse, shared by every decode path.  Mirrors the reference reader
+// (block_reader.cc:59-114) plus the bounds checks the reference does not do
+// (their failure codes are the SSTC_BLK_* values).  Offsets are block-relative.
+// ---------------------------------------------------------------------------
+struct Entry {
+  uint32_t code;
+  uint32_t type;
+  uint32_t klen;
+  uint32_t vlen; // kNoValue for DELETE
+  uint64_t txn;  // as decoded (compat quirk applied when asked)
+  uint64_t size; // recomputed entry size
+};
+
+struct LdsReader {
+  const uint8_t *img; // image byte 0 == block byte 0
+  __device__ uint32_t u8(uint64_t o) const { return lds_u8(img, static_cast<uint32_t>(o)); }
+  __device__ uint32_t u32(uint64_t o) const { return lds_u32u(img, static_cast<uint32_t>(o)); }
+  __device__ uint64_t u64(uint64_t o) const { return lds_u64u(img, static_cast<uint32_t>(o)); }
+};
+
+struct GlobalReader {
+  const uint8_t *blk;
+  __device__ uint32_t u8(uint64_t o) const { return g_u8(blk + o); }
+  __device__ uint32_t u32(uint64_t o) const { return g_u32u(blk + o); }
+  __device__ uint64_t u64(uint64_t o) const { return g_u64u(blk + o); }
+};
+
+template <class R>
+__device__ __forceinline__ Entry parse_entry(const R &rd, uint64_t s, uint64_t doff,
+                                             uint32_t txn_mode) {
+  Entry e;
+  e.code = kBlkOk;
+  e.type = 0;
+  e.klen = 0;
+  e.vlen = kNoValue;
+  e.txn = 0;
+  e.size = 0;
+  if (s >= doff || doff - s < 5) {
+    e.code = kBlkEntryRange;
+    return e;
+  }
+  e.type = rd.u8(s);
+  if (e.type > kTypeDeleted) {
+    e.code = kBlkBadType;
+    return e;
+  }
+  e.klen = rd.u32(s + 1);
+  if (e.klen > kMaxKey) {
+    e.code = kBlkKeyTooLong;
+    return e;
+  }
+  uint64_t p = s + 5 + e.klen;
+  if (e.type != kTypeDeleted) {
+    if (p + 4 > doff) {
+      e.code = kBlkEntryRange;
+      return e;
+    }
+    e.vlen = rd.u32(p);
+    p += 4ull + e.vlen;
+  }
+  if (p + 8 > doff) {
+    e.code = kBlkEntryRange;
+    return e;
+  }
+  // value.empty() test of GetTransactionIdFromDataEntry (block_reader.cc:109-111)
+  const bool quirk = txn_mode == 0u && e.type != kTypeDeleted && e.vlen == 0u;
+  e.txn = rd.u64(quirk ? s + 5 + e.klen : p);
+  e.size = p + 8 - s;
+  return e;
+}
+
+// Block-level checks on the 16 B extra (table_reader.cc:226-232).
+__device__ __forceinline__ uint32_t check_extra(uint64_t len, uint64_t n, uint64_t doff) {
+  if (n == 0) return kBlkEmpty;
+  if (doff > len - 16 || n > (len - 16 - doff) / 16) return kBlkOffsetsRange;
+  return kBlkOk;
+}
+
+// ---------------------------------------------------------------------------
+// Fused round trip, fast path: one wave per block.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kRtWaves = 4;
+constexpr uint32_t kRtSlot = kRtSlotBytes; // bytes of LDS per wave
+
+__global__ __launch_bounds__(kRtWaves *kWave) void rt_fast_kernel(RtArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kRtWaves * kRtSlot];
+  const uint32_t wave = uniform(threadIdx.x / kWave);
+  const uint32_t lane = lane_id();
+  const uint64_t b = static_cast<uint64_t>(blockIdx.x) * kRtWaves + wave;
+  if (b >= a.nblocks) return;
+  uint8_t *img = lds + wave * kRtSlot;
+
+  const uint64_t off = uniform64(a.blk_off[b]);
+  const uint64_t len = uniform64(a.blk_len[b]);
+  const uint32_t pad = static_cast<uint32_t>(off & 15u);
+  if (len < 16 || len + pad + 16 > kRtSlot) { // not for this path
+    if (lane == 0) a.slow_list[atomicAdd(a.slow_count, 1u)] = static_cast<uint32_t>(b);
+    return;
+  }
+  const uint32_t L = static_cast<uint32_t>(len);
+
+  // ---- stage [off & ~15, off + len) into LDS: 16 B per lane, 1 KiB per wave
+  //      instruction, LDS destination = wave-uniform base + lane * 16.
+  const uint32_t nchunk = (pad + L + 15u) >> 4;
+  const uint8_t *g = a.src + (off - pad);
+  for (uint32_t c0 = 0; c0 < nchunk; c0 += kWave) {
+    const uint32_t c = c0 + lane;
+    if (c < nchunk)
+      __builtin_amdgcn_global_load_lds((gbl_void_t *)(g + 16u * c), (lds_void_t *)(img + 16u * c0),
+                                       16, 0, 0);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  // ---- decode: extra, then entries 64 at a time
+  const LdsReader rd{img + pad};
+  const uint64_t n64 = rd.u64(L - 16);
+  const uint64_t doff64 = rd.u64(L - 8);
+  uint32_t st = check_extra(L, n64, doff64);
+  const uint32_t n = static_cast<uint32_t>(n64);
+  const uint32_t doff = static_cast<uint32_t>(doff64);
+  // in-place re-encode needs the exact packed layout
+  bool canon = st == kBlkOk && static_cast<uint64_t>(doff) + 16ull * n + 16 == L;
+  uint32_t carry = 0;
+  if (st == kBlkOk) {
+    for (uint32_t i0 = 0; i0 < n; i0 += kWave) {
+      const uint32_t i = i0 + lane;
+      Entry e{};
+      uint64_t s = 0;
+      if (i < n) {
+        s = rd.u64(doff + 16ull * i);
+        e = parse_entry(rd, s, doff, a.txn_mode);
+      }
+      const uint64_t bad = __ballot(e.code != kBlkOk);
+      if (bad) {
+        st = __shfl(e.code, __ffsll(static_cast<long long>(bad)) - 1, kWave);
+        break;
+      }
+      const uint32_t sz = static_cast<uint32_t>(e.size);
+      const uint32_t incl = wave_incl_scan_u32(sz);
+      const bool mism = i < n && s != static_cast<uint64_t>(carry + incl - sz);
+      canon = canon && !__any(mism);
+      carry += __shfl(incl, kWave - 1, kWave);
+    }
+  }
+  if (st != kBlkOk) {
+    if (lane == 0) {
+      if (a.status) a.status[b] = st;
+      if (a.out_len) a.out_len[b] = 0;
+      atomicAdd(a.err_count, 1ull);
+    }
+    return;
+  }
+  if (!canon || carry != doff) { // valid but not packed: generic path re-encodes it
+    if (lane == 0) a.slow_list[atomicAdd(a.slow_count, 1u)] = static_cast<uint32_t>(b);
+    return;
+  }
+
+  // ---- re-encode in place.  Entries stay where they are (starts == scan of
+  //      recomputed sizes), so each entry's encoding of its decoded fields is
+  //      already in the image except the txn rewritten by the compat reader;
+  //      the offset section and the extra are regenerated from the scan.
+  uint8_t *wimg = img + pad;
+  carry = 0;
+  for (uint32_t i0 = 0; i0 < n; i0 += kWave) {
+    const uint32_t i = i0 + lane;
+    uint32_t sz = 0;
+    uint64_t s = 0;
+    Entry e{};
+    if (i < n) {
+      s = rd.u64(doff + 16ull * i);
+      e = parse_entry(rd, s, doff, a.txn_mode);
+      sz = static_cast<uint32_t>(e.size);
+    }
+    const uint32_t incl = wave_incl_scan_u32(sz);
+    if (i < n) {
+      const uint32_t start = carry + incl - sz;
+      lds_st_u64u(wimg, doff + 16u * i, start);
+      lds_st_u64u(wimg, doff + 16u * i + 8u, sz);
+      if (a.txn_mode == 0u && e.type != kTypeDeleted && e.vlen == 0u)
+        lds_st_u64u(wimg, static_cast<uint32_t>(s) + 9u + e.klen, e.txn);
+    }
+    carry += __shfl(incl, kWave - 1, kWave);
+  }
+  if (lane == 0) {
+    lds_st_u64u(wimg, L - 16, n);
+    lds_st_u64u(wimg, L - 8, carry);
+  }
+  wave_lds_sync();
+
+  // ---- write back: whole 16 B chunks with dwordx4 stores; the two edge chunks
+  //      (shared with the neighbouring blocks) byte by byte.
+  uint8_t *gd = a.dst + (off - pad);
+  for (uint32_t c0 = 0; c0 < nchunk; c0 += kWave) {
+    const uint32_t c = c0 + lane;
+    if (c >= nchunk) continue;
+    const uint32_t lo = 16u * c;
+    if (lo >= pad && lo + 16u <= pad + L) {
+      const u32x4 v = *reinterpret_cast<const u32x4 *>(img + lo);
+      __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(gd + lo));
+    } else {
+      const uint32_t x0 = lo < pad ? pad : lo;
+      const uint32_t x1 = lo + 16u < pad + L ? lo + 16u : pad + L;
+      for (uint32_t x = x0; x < x1; x++) gd[x] = img[x];
+    }
+  }
+  if (lane == 0) {
+    if (a.status) a.status[b] = kBlkOk;
+    if (a.out_len) a.out_len[b] = L;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Generic round trip: one 256-thread workgroup per deferred block, entries in
+// windows of 256.  Pass 1 validates everything (a failing block is left
+// untouched), pass 2 emits.  Each output entry is the input entry's bytes at
+// its new (packed) position with the decoded txn re-applied; offset section and
+// extra are regenerated.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kGenThreads = 256;
+
+__device__ __forceinline__ uint64_t block_excl_scan_u64(uint64_t v, uint64_t *sm, uint64_t &total) {
+  // sm: kGenThreads/64 + 1 slots
+  const uint32_t tid = threadIdx.x, lane = lane_id(), w = tid / kWave;
+  const uint64_t incl = wave_incl_scan_u64(v);
+  if (lane == kWave - 1) sm[w] = incl;
+  __syncthreads();
+  uint64_t base = 0, tot = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < kGenThreads / kWave; k++) {
+    const uint64_t x = sm[k];
+    if (k < w) base += x;
+    tot += x;
+  }
+  __syncthreads();
+  total = tot;
+  return base + incl - v;
+}
+
+__global__ __launch_bounds__(kGenThreads) void rt_generic_kernel(RtArgs a) {
+  __shared__ uint64_t s_src[kGenThreads]; // input entry start
+  __shared__ uint64_t s_out[kGenThreads]; // output entry start
+  __shared__ uint64_t s_txn[kGenThreads];
+  __shared__ uint32_t s_patch[kGenThreads]; // 1 = compat txn rewrite
+  __shared__ uint32_t s_klen[kGenThreads];
+  __shared__ uint64_t s_red[kGenThreads / kWave + 1];
+  __shared__ uint32_t s_err;
+
+  const uint32_t cnt = *a.slow_count;
+  const uint32_t tid = threadIdx.x;
+  for (uint32_t item = blockIdx.x; item < cnt; item += gridDim.x) {
+    const uint64_t b = a.slow_list[item];
+    const uint64_t off = a.blk_off[b], len = a.blk_len[b];
+    const uint8_t *blk = a.src + off;
+    const GlobalReader rd{blk};
+    uint32_t st = kBlkOk;
+    uint64_t n = 0, doff = 0;
+    if (len < 16) {
+      st = kBlkTooSmall;
+    } else {
+      n = rd.u64(len - 16);
+      doff = rd.u64(len - 8);
+      st = check_extra(len, n, doff);
+    }
+    // pass 1: validate all entries, total data bytes
+    uint64_t data = 0;
+    if (st == kBlkOk) {
+      for (uint64_t w0 = 0; w0 < n; w0 += kGenThreads) {
+        if (tid == 0) s_err = 0xFFFFFFFFu;
+        __syncthreads();
+        const uint64_t i = w0 + tid;
+        uint64_t sz = 0;
+        if (i < n) {
+          const Entry e = parse_entry(rd, rd.u64(doff + 16 * i), doff, a.txn_mode);
+          if (e.code != kBlkOk) atomicMin(&s_err, (tid << 8) | e.code);
+          sz = e.size;
+        }
+        uint64_t tot;
+        block_excl_scan_u64(sz, s_red, tot);
+        data += tot;
+        const uint32_t err = s_err;
+        __syncthreads();
+        if (err != 0xFFFFFFFFu) {
+          st = err & 0xFFu;
+          break;
+        }
+      }
+    }
+    const uint64_t out_len = data + 16 * n + 16;
+    if (st == kBlkOk && out_len >= (1ull << 32)) st = kBlkTooLarge;
+    if (st != kBlkOk) {
+      if (tid == 0) {
+        if (a.status) a.status[b] = st;
+        if (a.out_len) a.out_len[b] = 0;
+        atomicAdd(a.err_count, 1ull);
+      }
+      continue;
+    }
+    uint8_t *out = a.dst + off;
+    // pass 2: emit entries window by window
+    uint64_t carry = 0;
+    for (uint64_t w0 = 0; w0 < n; w0 += kGenThreads) {
+      const uint64_t i = w0 + tid;
+      uint64_t sz = 0;
+      if (i < n) {
+        const uint64_t s = rd.u64(doff + 16 * i);
+        const Entry e = parse_entry(rd, s, doff, a.txn_mode);
+        sz = e.size;
+        s_src[tid] = s;
+        s_txn[tid] = e.txn;
+        s_klen[tid] = e.klen;
+        s_patch[tid] = (a.txn_mode == 0u && e.type != kTypeDeleted && e.vlen == 0u) ? 1u : 0u;
+      }
+      uint64_t tot;
+      const uint64_t ex = block_excl_scan_u64(sz, s_red, tot);
+      if (i < n) {
+        s_out[tid] = carry + ex;
+        // offset entry (start, size) regenerated
+        const uint64_t oe = data + 16 * i;
+        for (int j = 0; j < 8; j++) out[oe + j] = static_cast<uint8_t>((carry + ex) >> (8 * j));
+        for (int j = 0; j < 8; j++) out[oe + 8 + j] = static_cast<uint8_t>(sz >> (8 * j));
+      }
+      __syncthreads();
+      const uint32_t wn = static_cast<uint32_t>(n - w0 < kGenThreads ? n - w0 : kGenThreads);
+      const uint64_t x_begin = carry, x_end = carry + tot;
+      for (uint64_t x = x_begin + tid; x < x_end; x += kGenThreads) {
+        // entry r of this window holding output byte x
+        uint32_t lo = 0, hi = wn - 1;
+        while (lo < hi) {
+          const uint32_t mid = (lo + hi + 1) >> 1;
+          if (s_out[mid] <= x) lo = mid;
+          else hi = mid - 1;
+        }
+        const uint64_t rel = x - s_out[lo];
+        uint8_t v;
+        const uint64_t tx0 = 9ull + s_klen[lo];
+        if (s_patch[lo] && rel >= tx0 && rel < tx0 + 8)
+          v = static_cast<uint8_t>(s_txn[lo] >> (8 * (rel - tx0)));
+        else
+          v = blk[s_src[lo] + rel];
+        out[x] = v;
+      }
+      carry += tot;
+      __syncthreads();
+    }
+    if (tid == 0) {
+      const uint64_t oe = data + 16 * n;
+      for (int j = 0; j < 8; j++) out[oe + j] = static_cast<uint8_t>(n >> (8 * j));
+      for (int j = 0; j < 8; j++) out[oe + 8 + j] = static_cast<uint8_t>(data >> (8 * j));
+      if (a.status) a.status[b] = kBlkOk;
+      if (a.out_len) a.out_len[b] = out_len;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Decode to the record table.
+// ---------------------------------------------------------------------------
+__global__ void count_kernel(const uint8_t *src, const uint64_t *blk_off, const uint64_t *blk_len,
+                             uint64_t nblocks, uint64_t *counts) {
+  const uint64_t b = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (b >= nblocks) return;
+  const uint64_t len = blk_len[b];
+  uint64_t c = 0;
+  if (len >= 16) {
+    const uint8_t *blk = src + blk_off[b];
+    const uint64_t n = g_u64u(blk + len - 16), doff = g_u64u(blk + len - 8);
+    if (check_extra(len, n, doff) == kBlkOk) c = n;
+  }
+  counts[b] = c;
+}
+
+constexpr uint32_t kDecWaves = 4;
+
+__global__ __launch_bounds__(kDecWaves *kWave) void decode_kernel(DecArgs a) {
+  const uint32_t wave = uniform(threadIdx.x / kWave);
+  const uint32_t lane = lane_id();
+  const uint64_t b = static_cast<uint64_t>(blockIdx.x) * kDecWaves + wave;
+  if (b >= a.nblocks) return;
+  const uint64_t off = uniform64(a.blk_off[b]);
+  const uint64_t len = uniform64(a.blk_len[b]);
+  const uint64_t base = uniform64(a.rec_base[b]);
+  const uint8_t *blk = a.src + off;
+  const GlobalReader rd{blk};
+  uint32_t st = kBlkOk;
+  uint64_t n = 0, doff = 0;
+  if (len < 16) {
+    st = kBlkTooSmall;
+  } else {
+    n = rd.u64(len - 16);
+    doff = rd.u64(len - 8);
+    st = check_extra(len, n, doff);
+  }
+  if (st == kBlkOk) {
+    for (uint64_t i0 = 0; i0 < n; i0 += kWave) {
+      const uint64_t i = i0 + lane;
+      Entry e{};
+      uint64_t s = 0;
+      if (i < n) {
+        s = rd.u64(doff + 16 * i);
+        e = parse_entry(rd, s, doff, a.txn_mode);
+      }
+      const uint64_t bad = __ballot(e.code != kBlkOk);
+      if (bad) {
+        st = __shfl(e.code, __ffsll(static_cast<long long>(bad)) - 1, kWave);
+        break;
+      }
+      if (i < n) {
+        const uint64_t r = base + i;
+        a.out.type[r] = static_cast<uint8_t>(e.type);
+        a.out.key_len[r] = e.klen;
+        a.out.val_len[r] = e.vlen;
+        a.out.txn[r] = e.txn;
+        a.out.key_off[r] = off + s + 5;
+        a.out.val_off[r] = e.type != kTypeDeleted ? off + s + 9 + e.klen : 0;
+      }
+    }
+  }
+  if (lane == 0) {
+    if (a.status) a.status[b] = st;
+    if (st != kBlkOk) atomicAdd(a.err_count, 1ull);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Encode: records -> blocks.
+// ---------------------------------------------------------------------------
+__global__ void enc_sizes_kernel(const uint32_t *klen, const uint32_t *vlen, uint64_t nrec,
+                                 uint64_t add, uint64_t *sizes) {
+  const uint64_t r = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (r < nrec) sizes[r] = entry_size(klen[r], vlen[r]) + add;
+}
+
+__global__ void enc_blk_len_kernel(const uint64_t *P, const uint64_t *blk_first, uint64_t nblocks,
+                                   uint64_t *blk_len) {
+  const uint64_t b = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (b >= nblocks) return;
+  const uint64_t f0 = blk_first[b], f1 = blk_first[b + 1];
+  blk_len[b] = (P[f1] - P[f0]) + 16 * (f1 - f0) + 16;
+}
+
+// One workgroup per block; each thread assembles 16-byte output chunks aligned
+// to the destination address.  A chunk that lies inside one key or value span
+// is funnel-shifted from five source dwords; any other chunk is assembled byte
+// by byte through a per-thread LDS slot.
+constexpr uint32_t kEncThreads = 256;
+
+__device__ __forceinline__ u32x4 load16_unaligned(const uint8_t *p) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  const uint32_t *w = reinterpret_cast<const uint32_t *>(a & ~uintptr_t(3));
+  const uint32_t sh = a & 3u;
+  const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3];
+  const uint32_t w4 = sh ? w[4] : 0u;
+  u32x4 v;
+  v.x = __builtin_amdgcn_alignbyte(w1, w0, sh);
+  v.y = __builtin_amdgcn_alignbyte(w2, w1, sh);
+  v.z = __builtin_amdgcn_alignbyte(w3, w2, sh);
+  v.w = __builtin_amdgcn_alignbyte(w4, w3, sh);
+  return v;
+}
+
+__global__ __launch_bounds__(kEncThreads) void enc_emit_kernel(EncArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t slot[kEncThreads * 16];
+  const uint64_t b = blockIdx.x;
+  const uint32_t tid = threadIdx.x;
+  const uint64_t f0 = a.blk_first[b], f1 = a.blk_first[b + 1];
+  const uint64_t n = f1 - f0;
+  const uint64_t P0 = a.P[f0];
+  const uint64_t D = a.P[f1] - P0;
+  const uint64_t bo = a.out_blk_off[b];
+  const uint64_t L = a.out_blk_len[b];
+  uint8_t *dst = a.dst;
+  uint8_t *my = slot + 16 * tid;
+
+  const uint64_t c_first = bo >> 4, c_end = (bo + L + 15) >> 4;
+  for (uint64_t c = c_first + tid; c < c_end; c += kEncThreads) {
+    const int64_t x0 = static_cast<int64_t>(16 * c) - static_cast<int64_t>(bo);
+    const uint64_t xs = x0 < 0 ? 0 : static_cast<uint64_t>(x0);
+    const uint64_t xe = static_cast<uint64_t>(x0 + 16) < L ? static_cast<uint64_t>(x0 + 16) : L;
+    const bool full = x0 >= 0 && static_cast<uint64_t>(x0) + 16 <= L;
+    // entry cursor for the first data byte of this chunk
+    uint64_t r = f0;
+    if (xs < D) {
+      uint64_t lo = f0, hi = f1 - 1;
+      while (lo < hi) {
+        const uint64_t mid = (lo + hi + 1) >> 1;
+        if (a.P[mid] - P0 <= xs) lo = mid;
+        else hi = mid - 1;
+      }
+      r = lo;
+      // fast path: the whole chunk inside one key or value span
+      if (full) {
+        const uint64_t o = a.P[r] - P0;
+        const uint32_t kl = a.in.key_len[r], vl = a.in.val_len[r];
+        const uint64_t rel = xs - o;
+        const uint8_t *sp = nullptr;
+        if (rel >= 5 && rel + 16 <= 5ull + kl) sp = a.key_src + a.in.key_off[r] + (rel - 5);
+        else if (vl != kNoValue && rel >= 9ull + kl && rel + 16 <= 9ull + kl + vl)
+          sp = a.val_src + a.in.val_off[r] + (rel - 9 - kl);
+        if (sp) {
+          __builtin_nontemporal_store(load16_unaligned(sp), reinterpret_cast<u32x4 *>(dst + 16 * c));
+          continue;
+        }
+      }
+    }
+    for (uint64_t x = xs; x < xe; x++) {
+      uint32_t v;
+      if (x < D) {
+        while (r + 1 < f1 && a.P[r + 1] - P0 <= x) r++;
+        const uint64_t rel = x - (a.P[r] - P0);
+        const uint32_t kl = a.in.key_len[r], vl = a.in.val_len[r];
+        if (rel == 0) v = a.in.type[r];
+        else if (rel < 5) v = (kl >> (8 * (rel - 1))) & 0xFFu;
+        else if (rel < 5ull + kl) v = a.key_src[a.in.key_off[r] + rel - 5];
+        else if (vl != kNoValue && rel < 9ull + kl) v = (vl >> (8 * (rel - 5 - kl))) & 0xFFu;
+        else if (vl != kNoValue && rel < 9ull + kl + vl) v = a.val_src[a.in.val_off[r] + rel - 9 - kl];
+        else {
+          const uint64_t t0 = 5ull + kl + (vl != kNoValue ? 4ull + vl : 0ull);
+          v = static_cast<uint32_t>(a.in.txn[r] >> (8 * (rel - t0))) & 0xFFu;
+        }
+      } else if (x < D + 16 * n) {
+        const uint64_t i = (x - D) >> 4, j = (x - D) & 15;
+        const uint64_t val = j < 8 ? a.P[f0 + i] - P0 : a.P[f0 + i + 1] - a.P[f0 + i];
+        v = static_cast<uint32_t>(val >> (8 * (j & 7))) & 0xFFu;
+      } else {
+        const uint64_t j = x - D - 16 * n;
+        const uint64_t val = j < 8 ? n : D;
+        v = static_cast<uint32_t>(val >> (8 * (j & 7))) & 0xFFu;
+      }
+      if (full) my[x - xs] = static_cast<uint8_t>(v);
+      else dst[bo + x] = static_cast<uint8_t>(v);
+    }
+    if (full) {
+      __builtin_nontemporal_store(*reinterpret_cast<const u32x4 *>(my),
+                                  reinterpret_cast<u32x4 *>(dst + 16 * c));
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Greedy segmentation by pointer doubling.
+// nxt[i] = one past the last record of a block that starts at record i;
+// chain from 0 = block starts.  J_{k+1} = J_k o J_k.
+// ---------------------------------------------------------------------------
+__global__ void seg_next_kernel(const uint64_t *Pw, uint64_t nrec, uint64_t threshold,
+                                uint32_t *J0) {
+  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i > nrec) return;
+  if (i == nrec) {
+    J0[i] = static_cast<uint32_t>(nrec);
+    return;
+  }
+  const uint64_t target = Pw[i] + threshold; // first e >= i with Pw[e+1] >= target
+  if (Pw[nrec] < target) {
+    J0[i] = static_cast<uint32_t>(nrec);
+    return;
+  }
+  uint64_t lo = i, hi = nrec - 1;
+  while (lo < hi) {
+    const uint64_t mid = (lo + hi) >> 1;
+    if (Pw[mid + 1] >= target) hi = mid;
+    else lo = mid + 1;
+  }
+  J0[i] = static_cast<uint32_t>(lo + 1);
+}
+
+__global__ void seg_double_kernel(const uint32_t *Jk, uint32_t *Jk1, uint64_t nrec) {
+  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i <= nrec) Jk1[i] = Jk[Jk[i]];
+}
+
+__global__ void seg_depth_kernel(const uint32_t *J, uint32_t levels, uint64_t stride, uint64_t nrec,
+                                 uint64_t *d_nblocks, uint64_t *blk_first) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  uint64_t pos = 0, cnt = 0;
+  if (nrec > 0) {
+    for (int k = static_cast<int>(levels) - 1; k >= 0; k--) {
+      const uint32_t nx = J[static_cast<uint64_t>(k) * stride + pos];
+      if (nx < nrec) {
+        pos = nx;
+        cnt += 1ull << k;
+      }
+    }
+    cnt += 1;
+  }
+  *d_nblocks = cnt;
+  blk_first[cnt] = nrec;
+}
+
+__global__ void seg_emit_kernel(const uint32_t *J, uint32_t levels, uint64_t stride,
+                                const uint64_t *d_nblocks, uint64_t *blk_first) {
+  const uint64_t t = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (t >= *d_nblocks) return;
+  uint64_t pos = 0;
+  for (uint32_t k = 0; k < levels; k++)
+    if ((t >> k) & 1) pos = J[static_cast<uint64_t>(k) * stride + pos];
+  blk_first[t] = pos;
+}
+
+// ---------------------------------------------------------------------------
+// Device-wide exclusive scan of u64: reduce-then-scan, 2048 items per tile.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kScanThreads = 256, kScanItems = 8, kScanTile = kScanThreads * kScanItems;
+
+__device__ __forceinline__ uint64_t wg_excl_scan_u64(uint64_t v, uint64_t &total) {
+  __shared__ uint64_t sm[kScanThreads / kWave];
+  const uint32_t lane = lane_id(), w = threadIdx.x / kWave;
+  const uint64_t incl = wave_incl_scan_u64(v);
+  if (lane == kWave - 1) sm[w] = incl;
+  __syncthreads();
+  uint64_t base = 0, tot = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < kScanThreads / kWave; k++) {
+    const uint64_t x = sm[k];
+    if (k < w) base += x;
+    tot += x;
+  }
+  __syncthreads();
+  total = tot;
+  return base + incl - v;
+}
+
+__global__ __launch_bounds__(kScanThreads) void scan_reduce_kernel(const uint64_t *in, uint64_t n,
+                                                                   uint64_t *partials) {
+  const uint64_t t0 = static_cast<uint64_t>(blockIdx.x) * kScanTile + threadIdx.x * kScanItems;
+  uint64_t s = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < kScanItems; j++)
+    if (t0 + j < n) s += in[t0 + j];
+  uint64_t tot;
+  wg_excl_scan_u64(s, tot);
+  if (threadIdx.x == 0) partials[blockIdx.x] = tot;
+}
+
+// out[i] = carry_in + sum(in[0..i)), out[n] = carry_in + total.  in may alias out.
+__global__ __launch_bounds__(kScanThreads) void scan_apply_kernel(const uint64_t *in, uint64_t n,
+                                                                  const uint64_t *tile_base,
+                                                                  uint64_t carry_in, uint64_t *out) {
+  const uint64_t t0 = static_cast<uint64_t>(blockIdx.x) * kScanTile + threadIdx.x * kScanItems;
+  uint64_t v[kScanItems];
+  uint64_t s = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < kScanItems; j++) {
+    v[j] = t0 + j < n ? in[t0 + j] : 0;
+    s += v[j];
+  }
+  uint64_t tot;
+  uint64_t run = wg_excl_scan_u64(s, tot) + carry_in + (tile_base ? tile_base[blockIdx.x] : 0);
+#pragma unroll
+  for (uint32_t j = 0; j < kScanItems; j++) {
+    if (t0 + j < n) out[t0 + j] = run;
+    run += v[j];
+  }
+  if (n == 0) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) out[0] = carry_in;
+  } else if (t0 <= n - 1 && n - 1 < t0 + kScanItems) {
+    out[n] = run; // the thread holding the last element writes the total
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Launch wrappers
+// ---------------------------------------------------------------------------
+static inline uint32_t grid_for(uint64_t n, uint32_t per) { return static_cast<uint32_t>((n + per - 1) / per); }
+
+hipError_t launch_roundtrip(const RtArgs &a, hipStream_t s) {
+  hipError_t e = hipMemsetAsync(a.slow_count, 0, sizeof(uint32_t), s);
+  if (e != hipSuccess) return e;
+  if (a.nblocks) rt_fast_kernel<<<grid_for(a.nblocks, kRtWaves), kRtWaves * kWave, 0, s>>>(a);
+  // deferred blocks are few for reference-written input: one persistent
+  // workgroup per CU walks the list
+  const uint32_t g = static_cast<uint32_t>(a.nblocks < 256 ? (a.nblocks ? a.nblocks : 1) : 256);
+  rt_generic_kernel<<<g, kGenThreads, 0, s>>>(a);
+  return hipGetLastError();
+}
+
+hipError_t launch_count(const uint8_t *src, const uint64_t *blk_off, const uint64_t *blk_len,
+                        uint64_t nblocks, uint64_t *counts, hipStream_t s) {
+  if (nblocks) count_kernel<<<grid_for(nblocks, 256), 256, 0, s>>>(src, blk_off, blk_len, nblocks, counts);
+  return hipGetLastError();
+}
+
+hipError_t launch_decode(const DecArgs &a, hipStream_t s) {
+  if (a.nblocks) decode_kernel<<<grid_for(a.nblocks, kDecWaves), kDecWaves * kWave, 0, s>>>(a);
+  return hipGetLastError();
+}
+
+uint64_t scan_workspace_elems(uint64_t n) {
+  uint64_t tot = 0;
+  uint64_t m = (n + kScanTile - 1) / kScanTile;
+  while (m > 1) {
+    tot += m + 1;
+    m = (m + kScanTile - 1) / kScanTile;
+  }
+  return tot + 2;
+}
+
+hipError_t launch_scan(const uint64_t *in, uint64_t n, uint64_t carry_in, uint64_t *out, uint64_t *ws,
+                       hipStream_t s) {
+  const uint64_t tiles = (n + kScanTile - 1) / kScanTile;
+  if (tiles <= 1) {
+    scan_apply_kernel<<<1, kScanThreads, 0, s>>>(in, n, nullptr, carry_in, out);
+    return hipGetLastError();
+  }
+  uint64_t *partials = ws;           // tiles elements
+  uint64_t *tile_base = ws;          // scanned in place (tiles + 1 elements)
+  scan_reduce_kernel<<<static_cast<uint32_t>(tiles), kScanThreads, 0, s>>>(in, n, partials);
+  hipError_t e = launch_scan(partials, tiles, 0, tile_base, ws + tiles + 1, s);
+  if (e != hipSuccess) return e;
+  scan_apply_kernel<<<static_cast<uint32_t>(tiles), kScanThreads, 0, s>>>(in, n, tile_base, carry_in, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_enc_sizes(const uint32_t *klen, const uint32_t *vlen, uint64_t nrec, uint64_t add,
+                            uint64_t *sizes, hipStream_t s) {
+  if (nrec) enc_sizes_kernel<<<grid_for(nrec, 256), 256, 0, s>>>(klen, vlen, nrec, add, sizes);
+  return hipGetLastError();
+}
+
+hipError_t launch_enc_blk_len(const uint64_t *P, const uint64_t *blk_first, uint64_t nblocks,
+                              uint64_t *blk_len, hipStream_t s) {
+  if (nblocks) enc_blk_len_kernel<<<grid_for(nblocks, 256), 256, 0, s>>>(P, blk_first, nblocks, blk_len);
+  return hipGetLastError();
+}
+
+hipError_t launch_enc_emit(const EncArgs &a, hipStream_t s) {
+  if (a.nblocks) enc_emit_kernel<<<static_cast<uint32_t>(a.nblocks), kEncThreads, 0, s>>>(a);
+  return hipGetLastError();
+}
+
+hipError_t launch_segment(const uint64_t *Pw, uint64_t nrec, uint64_t threshold, uint32_t *J,
+                          uint32_t levels, uint64_t *d_nblocks, uint64_t *blk_first, hipStream_t s) {
+  const uint64_t stride = nrec + 1;
+  seg_next_kernel<<<grid_for(nrec + 1, 256), 256, 0, s>>>(Pw, nrec, threshold, J);
+  for (uint32_t k = 0; k + 1 < levels; k++)
+    seg_double_kernel<<<grid_for(nrec + 1, 256), 256, 0, s>>>(J + k * stride, J + (k + 1) * stride, nrec);
+  seg_depth_kernel<<<1, 64, 0, s>>>(J, levels, stride, nrec, d_nblocks, blk_first);
+  if (nrec) seg_emit_kernel<<<grid_for(nrec, 256), 256, 0, s>>>(J, levels, stride, d_nblocks, blk_first);
+  return hipGetLastError();
+}
+
+} // namespace sstc

@@ -1,0 +1,66 @@
+// sstc_launch.h — kernel argument blocks and host-side launch wrappers.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/sstcodec.h"
+
+namespace sstc {
+
+constexpr uint32_t kRtSlotBytes = 4608; // LDS bytes per wave in rt_fast_kernel
+
+struct RtArgs {
+  const uint8_t *src;
+  uint8_t *dst;
+  const uint64_t *blk_off;
+  const uint64_t *blk_len;
+  uint64_t nblocks;
+  uint32_t txn_mode;
+  uint64_t *out_len;   // may be null
+  uint32_t *status;    // may be null
+  uint32_t *slow_list; // nblocks entries (workspace)
+  uint32_t *slow_count;
+  unsigned long long *err_count;
+};
+
+struct DecArgs {
+  const uint8_t *src;
+  const uint64_t *blk_off;
+  const uint64_t *blk_len;
+  uint64_t nblocks;
+  const uint64_t *rec_base;
+  sstc_records out;
+  uint32_t txn_mode;
+  uint32_t *status; // may be null
+  unsigned long long *err_count;
+};
+
+struct EncArgs {
+  const uint8_t *key_src;
+  const uint8_t *val_src;
+  sstc_records in;
+  const uint64_t *blk_first;
+  uint64_t nblocks;
+  const uint64_t *P; // exclusive scan of entry sizes, nrec+1
+  const uint64_t *out_blk_off;
+  const uint64_t *out_blk_len;
+  uint8_t *dst;
+};
+
+hipError_t launch_roundtrip(const RtArgs &a, hipStream_t s);
+hipError_t launch_count(const uint8_t *src, const uint64_t *blk_off, const uint64_t *blk_len,
+                        uint64_t nblocks, uint64_t *counts, hipStream_t s);
+hipError_t launch_decode(const DecArgs &a, hipStream_t s);
+uint64_t scan_workspace_elems(uint64_t n);
+hipError_t launch_scan(const uint64_t *in, uint64_t n, uint64_t carry_in, uint64_t *out, uint64_t *ws,
+                       hipStream_t s);
+hipError_t launch_enc_sizes(const uint32_t *klen, const uint32_t *vlen, uint64_t nrec, uint64_t add,
+                            uint64_t *sizes, hipStream_t s);
+hipError_t launch_enc_blk_len(const uint64_t *P, const uint64_t *blk_first, uint64_t nblocks,
+                              uint64_t *blk_len, hipStream_t s);
+hipError_t launch_enc_emit(const EncArgs &a, hipStream_t s);
+hipError_t launch_segment(const uint64_t *Pw, uint64_t nrec, uint64_t threshold, uint32_t *J,
+                          uint32_t levels, uint64_t *d_nblocks, uint64_t *blk_first, hipStream_t s);
+
+} // namespace sstc

@@ -1,0 +1,77 @@
+"""ctypes binding of libsstcodec.so (include/sstcodec.h).
+
+The library is loaded from the in-tree build (lsm-kv-storage_amd/lib/).  There
+is no fallback: if the library is missing, or no GPU is present, calls raise.
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+PKG_ROOT = os.path.dirname(HERE)
+LIB_PATH = os.path.join(PKG_ROOT, "lib", "libsstcodec.so")
+HEADER = os.path.join(os.path.dirname(PKG_ROOT), "include", "sstcodec.h")
+
+SSTC_OK = 0
+SSTC_NO_VALUE = 0xFFFFFFFF
+SSTC_TXN_COMPAT = 0
+SSTC_TXN_CORRECT = 1
+BLK_STATUS = {0: "OK", 1: "TOO_SMALL", 2: "EMPTY", 3: "OFFSETS_RANGE", 4: "ENTRY_RANGE",
+              5: "BAD_TYPE", 6: "KEY_TOO_LONG", 7: "TOO_LARGE"}
+
+c_u8p = ctypes.c_void_p
+c_u64 = ctypes.c_uint64
+c_u32 = ctypes.c_uint32
+c_vp = ctypes.c_void_p
+
+
+class Records(ctypes.Structure):
+    """sstc_records: device pointers of the SoA record table."""
+    _fields_ = [("type", c_vp), ("key_len", c_vp), ("val_len", c_vp), ("txn", c_vp),
+                ("key_off", c_vp), ("val_off", c_vp)]
+
+
+class SstcError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def load():
+    """Load (once) and return the ctypes library.  Raises if it is not built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise SstcError(f"{LIB_PATH} is not built (run lsm-kv-storage_amd/build.py); "
+                        "the SST codec has no CPU fallback")
+    lib = ctypes.CDLL(LIB_PATH)
+    P = ctypes.POINTER
+    sig = {
+        "sstc_version": (c_u32, []),
+        "sstc_last_error_string": (ctypes.c_char_p, []),
+        "sstc_ctx_create": (ctypes.c_int, [ctypes.c_int, c_vp, P(c_vp)]),
+        "sstc_ctx_destroy": (ctypes.c_int, [c_vp]),
+        "sstc_ctx_set_stream": (ctypes.c_int, [c_vp, c_vp]),
+        "sstc_ctx_reserve": (ctypes.c_int, [c_vp, c_u64, c_u64]),
+        "sstc_ctx_error_count": (ctypes.c_int, [c_vp, P(c_u64)]),
+        "sstc_ctx_reset_errors": (ctypes.c_int, [c_vp]),
+        "sstc_count_records": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_u64, c_vp]),
+        "sstc_decode_blocks": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_u64, c_vp, Records, c_u32, c_vp]),
+        "sstc_segment_records": (ctypes.c_int, [c_vp, c_vp, c_vp, c_u64, c_u64, c_vp, c_vp]),
+        "sstc_encode_blocks": (ctypes.c_int, [c_vp, c_vp, c_vp, Records, c_u64, c_vp, c_u64, c_u64,
+                                              c_vp, c_vp, c_vp]),
+        "sstc_roundtrip_blocks": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_u64, c_u32, c_vp, c_vp]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(rc, what):
+    if rc != SSTC_OK:
+        msg = load().sstc_last_error_string()
+        raise SstcError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")

@@ -1,0 +1,167 @@
+"""Torch-facing wrapper of the C-ABI (device buffers are torch CUDA tensors).
+
+PyTorch here is plumbing only: it owns device memory and the stream; all codec
+work runs in libsstcodec.so's HIP kernels.  u64 arrays are carried in int64
+tensors and u32 arrays in int32 tensors (bit-identical; SSTC_NO_VALUE is -1).
+"""
+import ctypes
+
+import torch
+
+from . import _lib
+from ._lib import Records, check, load
+
+
+def _p(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def _dev(t, dtype, device):
+    if not torch.is_tensor(t):
+        import numpy as np
+        t = torch.from_numpy(np.ascontiguousarray(t).view({
+            torch.uint8: np.uint8, torch.int32: np.int32, torch.int64: np.int64}[dtype]))
+    if t.dtype != dtype:
+        t = t.view(dtype) if t.element_size() == torch.empty((), dtype=dtype).element_size() else t.to(dtype)
+    return t.to(device, non_blocking=False).contiguous()
+
+
+class RecordTable:
+    """SoA record table on the device (see include/sstcodec.h sstc_records)."""
+
+    FIELDS = (("type", torch.uint8), ("key_len", torch.int32), ("val_len", torch.int32),
+              ("txn", torch.int64), ("key_off", torch.int64), ("val_off", torch.int64))
+
+    def __init__(self, n, device, tensors=None):
+        self.n = int(n)
+        if tensors is None:
+            tensors = {k: torch.empty(max(self.n, 1), dtype=dt, device=device) for k, dt in self.FIELDS}
+        self.t = tensors
+
+    @classmethod
+    def from_numpy(cls, rec, device):
+        n = len(rec["type"])
+        t = {k: _dev(rec[k], dt, device) for k, dt in cls.FIELDS}
+        return cls(n, device, t)
+
+    def c(self):
+        return Records(*[self.t[k].data_ptr() for k, _ in self.FIELDS])
+
+    def to_numpy(self):
+        import numpy as np
+        view = {torch.uint8: np.uint8, torch.int32: np.uint32, torch.int64: np.uint64}
+        return {k: self.t[k][: self.n].cpu().numpy().view(view[dt]) for k, dt in self.FIELDS}
+
+
+class Codec:
+    """One sstc_ctx bound to a device; calls run on torch's current stream."""
+
+    def __init__(self, device=None):
+        lib = load()
+        if device is None:
+            device = torch.cuda.current_device()
+        self.device = torch.device("cuda", device)
+        self.lib = lib
+        h = ctypes.c_void_p()
+        check(lib.sstc_ctx_create(int(device), ctypes.c_void_p(0), ctypes.byref(h)), "sstc_ctx_create")
+        self.h = h
+
+    def close(self):
+        if self.h:
+            self.lib.sstc_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _stream(self):
+        s = torch.cuda.current_stream(self.device).cuda_stream
+        check(self.lib.sstc_ctx_set_stream(self.h, ctypes.c_void_p(s)), "sstc_ctx_set_stream")
+
+    def reserve(self, max_blocks, max_records):
+        self._stream()
+        check(self.lib.sstc_ctx_reserve(self.h, int(max_blocks), int(max_records)), "sstc_ctx_reserve")
+
+    def error_count(self):
+        self._stream()
+        v = ctypes.c_uint64()
+        check(self.lib.sstc_ctx_error_count(self.h, ctypes.byref(v)), "sstc_ctx_error_count")
+        return v.value
+
+    def reset_errors(self):
+        self._stream()
+        check(self.lib.sstc_ctx_reset_errors(self.h), "sstc_ctx_reset_errors")
+
+    # ---- fused round trip -------------------------------------------------
+    def roundtrip(self, src, blk_off, blk_len, dst=None, txn_mode=_lib.SSTC_TXN_COMPAT,
+                  out_len=None, status=None):
+        nb = blk_off.numel()
+        if dst is None:
+            dst = torch.zeros_like(src)
+        if out_len is None:
+            out_len = torch.empty(max(nb, 1), dtype=torch.int64, device=self.device)
+        if status is None:
+            status = torch.empty(max(nb, 1), dtype=torch.int32, device=self.device)
+        self._stream()
+        check(self.lib.sstc_roundtrip_blocks(self.h, _p(src), _p(dst), _p(blk_off), _p(blk_len), nb,
+                                             txn_mode, _p(out_len), _p(status)), "sstc_roundtrip_blocks")
+        return dst, out_len, status
+
+    def roundtrip_raw(self, src, dst, blk_off, blk_len, nb, txn_mode=_lib.SSTC_TXN_COMPAT,
+                      out_len=None, status=None):
+        """Minimal-overhead launch for timing loops (pointers pre-resolved by caller)."""
+        return self.lib.sstc_roundtrip_blocks(self.h, src, dst, blk_off, blk_len, nb, txn_mode,
+                                              out_len, status)
+
+    # ---- decode ------------------------------------------------------------
+    def count(self, src, blk_off, blk_len):
+        nb = blk_off.numel()
+        rec_base = torch.empty(nb + 1, dtype=torch.int64, device=self.device)
+        self._stream()
+        check(self.lib.sstc_count_records(self.h, _p(src), _p(blk_off), _p(blk_len), nb, _p(rec_base)),
+              "sstc_count_records")
+        return rec_base
+
+    def decode(self, src, blk_off, blk_len, txn_mode=_lib.SSTC_TXN_COMPAT, rec_base=None, status=None):
+        nb = blk_off.numel()
+        if rec_base is None:
+            rec_base = self.count(src, blk_off, blk_len)
+        total = int(rec_base[nb].item())
+        table = RecordTable(total, self.device)
+        if status is None:
+            status = torch.empty(max(nb, 1), dtype=torch.int32, device=self.device)
+        self._stream()
+        check(self.lib.sstc_decode_blocks(self.h, _p(src), _p(blk_off), _p(blk_len), nb, _p(rec_base),
+                                          table.c(), txn_mode, _p(status)), "sstc_decode_blocks")
+        return table, rec_base, status
+
+    # ---- encode ------------------------------------------------------------
+    def segment(self, table, threshold):
+        n = table.n
+        first = torch.empty(n + 1, dtype=torch.int64, device=self.device)
+        nb = torch.empty(1, dtype=torch.int64, device=self.device)
+        self._stream()
+        check(self.lib.sstc_segment_records(self.h, _p(table.t["key_len"]), _p(table.t["val_len"]), n,
+                                            int(threshold), _p(first), _p(nb)), "sstc_segment_records")
+        k = int(nb.item())
+        return first[: k + 1]
+
+    def encode(self, table, key_src, val_src, blk_first, out_base=0, dst=None):
+        nb = blk_first.numel() - 1
+        out_off = torch.empty(nb + 1, dtype=torch.int64, device=self.device)
+        out_len = torch.empty(max(nb, 1), dtype=torch.int64, device=self.device)
+        if dst is None:
+            # exact size: data + 16 per record + 16 per block
+            sizes = 13 + table.t["key_len"][: table.n].to(torch.int64)
+            vl = table.t["val_len"][: table.n].to(torch.int64)
+            sizes = sizes + torch.where(vl == -1, torch.zeros_like(vl), 4 + (vl & 0xFFFFFFFF))
+            total = int(sizes.sum().item()) + 16 * table.n + 16 * nb + int(out_base)
+            dst = torch.zeros(max(total, 1), dtype=torch.uint8, device=self.device)
+        self._stream()
+        check(self.lib.sstc_encode_blocks(self.h, _p(key_src), _p(val_src), table.c(), table.n, _p(blk_first),
+                                          nb, int(out_base), _p(dst), _p(out_off), _p(out_len)),
+              "sstc_encode_blocks")
+        return dst, out_off, out_len[:nb]

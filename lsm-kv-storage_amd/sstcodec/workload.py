@@ -1,0 +1,124 @@
+"""Deterministic synthetic record sets for the SST block codec (numpy only).
+
+The shapes follow SURVEY.md §8(d): 16 B keys "k%015d", 100 B values drawn from
+a splitmix64 stream, ascending txn ids.  A record set is a dict of numpy arrays
+in the layout of include/sstcodec.h's sstc_records plus the key/value arenas:
+
+    type u8, key_len u32, val_len u32 (NO_VALUE = no value fields), txn u64,
+    key_off u64 (into key_src), val_off u64 (into val_src), key_src u8, val_src u8
+"""
+import numpy as np
+
+NO_VALUE = 0xFFFFFFFF
+TYPE_PUT = 0
+TYPE_DELETED = 1
+
+_GAMMA = np.uint64(0x9E3779B97F4A7C15)
+
+
+def splitmix64(seed, n, start=0):
+    """n outputs of splitmix64 seeded with `seed`, from counter `start`."""
+    with np.errstate(over="ignore"):
+        z = np.uint64(seed) + (np.arange(start + 1, start + n + 1, dtype=np.uint64) * _GAMMA)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))
+
+
+def random_bytes(seed, nbytes, start_word=0):
+    words = splitmix64(seed, (nbytes + 7) // 8, start_word)
+    return words.view(np.uint8)[:nbytes].copy()
+
+
+def fixed_keys(index, width=16):
+    """Keys "k%0{width-1}d" % index as one contiguous arena (width bytes each)."""
+    index = np.asarray(index, dtype=np.uint64)
+    nd = width - 1
+    pw = np.uint64(10) ** np.arange(nd - 1, -1, -1, dtype=np.uint64)
+    digits = (index[:, None] // pw[None, :]) % np.uint64(10)
+    out = np.empty((index.size, width), dtype=np.uint8)
+    out[:, 0] = ord("k")
+    out[:, 1:] = (digits + np.uint64(ord("0"))).astype(np.uint8)
+    return out.reshape(-1)
+
+
+def uniform_records(n, key_index=None, seed=1, value_len=100, txn_start=1, key_width=16):
+    """n PUT records, key_width-byte keys, value_len-byte random values."""
+    if key_index is None:
+        key_index = np.arange(n, dtype=np.uint64)
+    key_src = fixed_keys(key_index, key_width)
+    val_src = random_bytes(seed, n * value_len)
+    return {
+        "type": np.zeros(n, np.uint8),
+        "key_len": np.full(n, key_width, np.uint32),
+        "val_len": np.full(n, value_len, np.uint32),
+        "txn": np.arange(txn_start, txn_start + n, dtype=np.uint64),
+        "key_off": np.arange(n, dtype=np.uint64) * np.uint64(key_width),
+        "val_off": np.arange(n, dtype=np.uint64) * np.uint64(value_len),
+        "key_src": key_src,
+        "val_src": val_src,
+    }
+
+
+def mixed_records(n, seed=7, max_key=48, max_val=300, p_delete=0.1, p_empty_val=0.05,
+                  p_empty_key=0.02, sorted_keys=True):
+    """Records with ragged keys/values, DELETEs, empty keys and empty values
+    (the empty-value PUT exercises the reference's txn quirk)."""
+    rng = np.random.default_rng(seed)
+    klen = rng.integers(1, max_key + 1, n).astype(np.uint32)
+    klen[rng.random(n) < p_empty_key] = 0
+    vlen = rng.integers(1, max_val + 1, n).astype(np.uint32)
+    vlen[rng.random(n) < p_empty_val] = 0
+    typ = (rng.random(n) < p_delete).astype(np.uint8)
+    vlen[typ == TYPE_DELETED] = NO_VALUE
+    key_off = np.zeros(n, np.uint64)
+    key_off[1:] = np.cumsum(klen[:-1].astype(np.uint64))
+    key_src = rng.integers(0x20, 0x7F, int(klen.sum(dtype=np.uint64)) + 8, dtype=np.uint8)
+    vbytes = np.where(vlen == NO_VALUE, 0, vlen).astype(np.uint64)
+    val_off = np.zeros(n, np.uint64)
+    val_off[1:] = np.cumsum(vbytes[:-1])
+    val_src = rng.integers(0, 256, int(vbytes.sum()) + 8, dtype=np.uint8)
+    val_off[typ == TYPE_DELETED] = 0
+    txn = rng.integers(1, 1 << 62, n, dtype=np.uint64)
+    return {
+        "type": typ,
+        "key_len": klen,
+        "val_len": vlen,
+        "txn": txn,
+        "key_off": key_off,
+        "val_off": val_off,
+        "key_src": key_src,
+        "val_src": val_src,
+    }
+
+
+def entry_sizes(rec):
+    """Per-record entry size (reference sstable/block_builder.cc:19-21)."""
+    vl = rec["val_len"].astype(np.uint64)
+    has = rec["val_len"] != NO_VALUE
+    return np.uint64(13) + rec["key_len"].astype(np.uint64) + np.where(has, np.uint64(4) + vl, np.uint64(0))
+
+
+def segment(rec, threshold):
+    """Greedy block boundaries of TableBuilder::AddEntry (table_builder.cc:57-59),
+    host-side: the block closes right after the record whose cumulative
+    (entry_size + 16) reaches `threshold`.  Returns the nblocks+1 boundaries."""
+    w = entry_sizes(rec) + np.uint64(16)
+    firsts = [0]
+    acc = 0
+    wl = w.tolist()
+    for i, x in enumerate(wl):
+        acc += x
+        if acc >= threshold:
+            firsts.append(i + 1)
+            acc = 0
+    if firsts[-1] != len(wl):
+        firsts.append(len(wl))
+    return np.asarray(firsts, dtype=np.uint64)
+
+
+def uniform_block_layout(nblocks, per_block=28, key_len=16, val_len=100):
+    """Offsets/lengths of nblocks back-to-back uniform blocks."""
+    blen = per_block * (13 + key_len + 4 + val_len + 16) + 16
+    off = np.arange(nblocks, dtype=np.uint64) * np.uint64(blen)
+    return off, np.full(nblocks, blen, np.uint64)

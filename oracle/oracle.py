@@ -1,0 +1,242 @@
+"""ctypes wrappers of the CPU checkers (TEST INFRASTRUCTURE ONLY).
+
+    Oracle  -> oracle/liboracle.so       clean-room C restatement (sst_oracle.c)
+    RefLib  -> oracle/_ref/libsstref.so  the reference's own sstable sources
+                                          (+ ref_harness.cc), built by
+                                          oracle/Makefile when /root/reference
+                                          is present
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg use this
+module, always as the checker / the CPU baseline, never as the product path.
+Record sets use the layout of sstcodec.workload (numpy arrays).
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ORACLE_SO = os.path.join(HERE, "liboracle.so")
+REF_SO = os.path.join(HERE, "_ref", "libsstref.so")
+NO_VALUE = 0xFFFFFFFF
+
+_vp = ctypes.c_void_p
+_u64 = ctypes.c_uint64
+
+
+def build(quiet=True):
+    """Build liboracle.so (and _ref/libsstref.so when /root/reference exists)."""
+    subprocess.run(["make", "-C", HERE, "-j8"], check=True,
+                   stdout=subprocess.DEVNULL if quiet else None)
+
+
+def _ptr(a):
+    return a.ctypes.data_as(_vp) if a is not None else _vp(0)
+
+
+def _rec_args(rec):
+    r = {k: np.ascontiguousarray(rec[k]) for k in
+         ("type", "key_len", "val_len", "txn", "key_off", "val_off", "key_src", "val_src")}
+    r["type"] = r["type"].astype(np.uint8, copy=False)
+    r["key_len"] = r["key_len"].astype(np.uint32, copy=False)
+    r["val_len"] = r["val_len"].astype(np.uint32, copy=False)
+    for k in ("txn", "key_off", "val_off"):
+        r[k] = r[k].astype(np.uint64, copy=False)
+    if r["key_src"].size == 0:
+        r["key_src"] = np.zeros(8, np.uint8)
+    if r["val_src"].size == 0:
+        r["val_src"] = np.zeros(8, np.uint8)
+    return r
+
+
+def entry_sizes(rec):
+    vl = rec["val_len"].astype(np.uint64)
+    has = rec["val_len"] != NO_VALUE
+    return np.uint64(13) + rec["key_len"].astype(np.uint64) + np.where(has, np.uint64(4) + vl, np.uint64(0))
+
+
+def block_bytes(rec, lo=0, hi=None):
+    hi = len(rec["type"]) if hi is None else hi
+    s = entry_sizes({k: rec[k][lo:hi] for k in ("key_len", "val_len")})
+    return int(s.sum()) + 16 * (hi - lo) + 16
+
+
+class Oracle:
+    """liboracle.so: the clean-room restatement."""
+
+    def __init__(self, path=ORACLE_SO):
+        if not os.path.exists(path):
+            build()
+        self.lib = lib = ctypes.CDLL(path)
+        lib.orc_block_encode.restype = _u64
+        lib.orc_block_encode.argtypes = [_u64] + [_vp] * 9
+        lib.orc_block_decode.restype = ctypes.c_int
+        lib.orc_block_decode.argtypes = [_vp, _u64, _u64, ctypes.c_int] + [_vp] * 7
+        lib.orc_roundtrip_blocks.restype = _u64
+        lib.orc_roundtrip_blocks.argtypes = [_vp, _vp, _vp, _u64, ctypes.c_int, _vp, _vp, _vp]
+        lib.orc_segment.restype = _u64
+        lib.orc_segment.argtypes = [_u64, _vp, _vp, _u64, _vp]
+        lib.orc_table_build.restype = _u64
+        lib.orc_table_build.argtypes = [_u64] + [_vp] * 8 + [_u64, _vp]
+        lib.orc_table_index.restype = _u64
+        lib.orc_table_index.argtypes = [_vp, _u64, _u64] + [_vp] * 8
+
+    def encode_block(self, rec, lo=0, hi=None):
+        hi = len(rec["type"]) if hi is None else hi
+        r = _rec_args(rec)
+        out = np.zeros(block_bytes(rec, lo, hi) + 16, np.uint8)
+        sl = lambda k: _ptr(r[k][lo:]) if hi > lo else _ptr(r[k])  # noqa: E731
+        n = self.lib.orc_block_encode(hi - lo, sl("type"), sl("key_len"), sl("val_len"), sl("txn"),
+                                      _ptr(r["key_src"]), sl("key_off"), _ptr(r["val_src"]), sl("val_off"),
+                                      _ptr(out))
+        return out[:n]
+
+    def encode_blocks(self, rec, blk_first, base=0):
+        """Blocks for record ranges blk_first[b]..blk_first[b+1], back to back."""
+        parts, offs, lens = [], [], []
+        pos = base
+        for b in range(len(blk_first) - 1):
+            blk = self.encode_block(rec, int(blk_first[b]), int(blk_first[b + 1]))
+            parts.append(blk)
+            offs.append(pos)
+            lens.append(blk.size)
+            pos += blk.size
+        data = np.concatenate(parts) if parts else np.zeros(0, np.uint8)
+        return data, np.asarray(offs, np.uint64), np.asarray(lens, np.uint64)
+
+    def decode_block(self, blk, txn_mode=0, base=0):
+        blk = np.ascontiguousarray(blk, dtype=np.uint8)
+        cap = max(blk.size // 13 + 1, 1)
+        out = {"type": np.zeros(cap, np.uint8), "key_len": np.zeros(cap, np.uint32),
+               "val_len": np.zeros(cap, np.uint32), "txn": np.zeros(cap, np.uint64),
+               "key_off": np.zeros(cap, np.uint64), "val_off": np.zeros(cap, np.uint64)}
+        n = _u64()
+        st = self.lib.orc_block_decode(_ptr(blk), blk.size, base, txn_mode, _ptr(out["type"]),
+                                       _ptr(out["key_len"]), _ptr(out["val_len"]), _ptr(out["txn"]),
+                                       _ptr(out["key_off"]), _ptr(out["val_off"]), ctypes.byref(n))
+        k = min(n.value, cap)
+        return st, {key: v[:k] for key, v in out.items()}
+
+    def roundtrip(self, src, blk_off, blk_len, txn_mode=0):
+        src = np.ascontiguousarray(src, np.uint8)
+        blk_off = np.ascontiguousarray(blk_off, np.uint64)
+        blk_len = np.ascontiguousarray(blk_len, np.uint64)
+        dst = np.zeros_like(src)
+        nb = blk_off.size
+        out_len = np.zeros(max(nb, 1), np.uint64)
+        status = np.zeros(max(nb, 1), np.uint32)
+        bad = self.lib.orc_roundtrip_blocks(_ptr(src), _ptr(blk_off), _ptr(blk_len), nb, txn_mode, _ptr(dst),
+                                            _ptr(out_len), _ptr(status))
+        return dst, out_len[:nb], status[:nb], bad
+
+    def segment(self, rec, threshold):
+        r = _rec_args(rec)
+        n = len(r["type"])
+        first = np.zeros(n + 1, np.uint64)
+        nb = self.lib.orc_segment(n, _ptr(r["key_len"]), _ptr(r["val_len"]), threshold, _ptr(first))
+        return first[: nb + 1]
+
+    def table_build(self, rec, threshold):
+        r = _rec_args(rec)
+        n = len(r["type"])
+        args = [n, _ptr(r["type"]), _ptr(r["key_len"]), _ptr(r["val_len"]), _ptr(r["txn"]),
+                _ptr(r["key_src"]), _ptr(r["key_off"]), _ptr(r["val_src"]), _ptr(r["val_off"]), threshold]
+        size = self.lib.orc_table_build(*args, _vp(0))
+        out = np.zeros(size, np.uint8)
+        self.lib.orc_table_build(*args, _ptr(out))
+        return out
+
+    def table_index(self, file_bytes, cap=1 << 20):
+        f = np.ascontiguousarray(file_bytes, np.uint8)
+        cap = min(cap, f.size // 24 + 1)
+        o = {k: np.zeros(cap, np.uint64) for k in ("blk_off", "blk_len", "first_key_off", "last_key_off")}
+        o["first_key_len"] = np.zeros(cap, np.uint32)
+        o["last_key_len"] = np.zeros(cap, np.uint32)
+        mn, mx = _u64(), _u64()
+        nb = self.lib.orc_table_index(_ptr(f), f.size, cap, _ptr(o["blk_off"]), _ptr(o["blk_len"]),
+                                      _ptr(o["first_key_off"]), _ptr(o["first_key_len"]),
+                                      _ptr(o["last_key_off"]), _ptr(o["last_key_len"]),
+                                      ctypes.byref(mn), ctypes.byref(mx))
+        if nb == 2 ** 64 - 1:
+            return None
+        k = min(nb, cap)
+        res = {key: v[:k] for key, v in o.items()}
+        res["nblocks"] = nb
+        res["min_txn"] = mn.value
+        res["max_txn"] = mx.value
+        return res
+
+
+class RefLib:
+    """oracle/_ref/libsstref.so: the reference's own sstable code."""
+
+    def __init__(self, path=REF_SO):
+        if not os.path.exists(path):
+            raise FileNotFoundError(path)
+        self.lib = lib = ctypes.CDLL(path)
+        lib.ref_block_encode.restype = _u64
+        lib.ref_block_encode.argtypes = [_u64] + [_vp] * 9
+        lib.ref_block_decode.restype = _u64
+        lib.ref_block_decode.argtypes = [_vp, _u64] + [_vp] * 6
+        lib.ref_roundtrip_blocks.restype = _u64
+        lib.ref_roundtrip_blocks.argtypes = [_vp, _vp, _vp, _u64, _vp, _vp]
+        lib.ref_table_build.restype = _u64
+        lib.ref_table_build.argtypes = [ctypes.c_char_p, _u64, _u64] + [_vp] * 8
+        lib.ref_table_index.restype = _u64
+        lib.ref_table_index.argtypes = [ctypes.c_char_p, _u64, _u64] + [_vp] * 6
+
+    def encode_block(self, rec, lo=0, hi=None):
+        hi = len(rec["type"]) if hi is None else hi
+        r = _rec_args(rec)
+        out = np.zeros(block_bytes(rec, lo, hi) + 16, np.uint8)
+        sl = lambda k: _ptr(r[k][lo:]) if hi > lo else _ptr(r[k])  # noqa: E731
+        n = self.lib.ref_block_encode(hi - lo, sl("type"), sl("key_len"), sl("val_len"), sl("txn"),
+                                      _ptr(r["key_src"]), sl("key_off"), _ptr(r["val_src"]), sl("val_off"),
+                                      _ptr(out))
+        return out[:n]
+
+    def decode_block(self, blk):
+        blk = np.ascontiguousarray(blk, np.uint8)
+        cap = max(blk.size // 13 + 1, 1)
+        out = {"type": np.zeros(cap, np.uint8), "key_len": np.zeros(cap, np.uint32),
+               "val_len": np.zeros(cap, np.uint32), "txn": np.zeros(cap, np.uint64),
+               "key_off": np.zeros(cap, np.uint64), "val_off": np.zeros(cap, np.uint64)}
+        n = self.lib.ref_block_decode(_ptr(blk), blk.size, _ptr(out["type"]), _ptr(out["key_len"]),
+                                      _ptr(out["val_len"]), _ptr(out["txn"]), _ptr(out["key_off"]),
+                                      _ptr(out["val_off"]))
+        return {k: v[:n] for k, v in out.items()}
+
+    def roundtrip(self, src, blk_off, blk_len, dst=None):
+        src = np.ascontiguousarray(src, np.uint8)
+        blk_off = np.ascontiguousarray(blk_off, np.uint64)
+        blk_len = np.ascontiguousarray(blk_len, np.uint64)
+        if dst is None:
+            dst = np.zeros_like(src)
+        out_len = np.zeros(max(blk_off.size, 1), np.uint64)
+        total = self.lib.ref_roundtrip_blocks(_ptr(src), _ptr(blk_off), _ptr(blk_len), blk_off.size, _ptr(dst),
+                                              _ptr(out_len))
+        return dst, out_len[: blk_off.size], total
+
+    def table_build(self, path, rec, block_size=4096):
+        r = _rec_args(rec)
+        n = len(r["type"])
+        fs = self.lib.ref_table_build(path.encode(), block_size, n, _ptr(r["type"]), _ptr(r["key_len"]),
+                                      _ptr(r["val_len"]), _ptr(r["txn"]), _ptr(r["key_src"]),
+                                      _ptr(r["key_off"]), _ptr(r["val_src"]), _ptr(r["val_off"]))
+        return fs
+
+    def table_index(self, path, file_size, cap=1 << 16):
+        o = {"blk_off": np.zeros(cap, np.uint64), "blk_len": np.zeros(cap, np.uint64),
+             "first_key_len": np.zeros(cap, np.uint32), "last_key_len": np.zeros(cap, np.uint32)}
+        fk = np.zeros(4096, np.uint8)
+        lk = np.zeros(4096, np.uint8)
+        nb = self.lib.ref_table_index(path.encode(), file_size, cap, _ptr(o["blk_off"]), _ptr(o["blk_len"]),
+                                      _ptr(o["first_key_len"]), _ptr(o["last_key_len"]), _ptr(fk), _ptr(lk))
+        if nb == 2 ** 64 - 1:
+            return None
+        res = {k: v[:nb] for k, v in o.items()}
+        res["nblocks"] = nb
+        res["first_key"] = bytes(fk[: int(res["first_key_len"][0])]) if nb else b""
+        res["last_key"] = bytes(lk[: int(res["last_key_len"][-1])]) if nb else b""
+        return res

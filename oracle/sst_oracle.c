@@ -1,0 +1,261 @@
+/*
+ * sst_oracle.c — CPU restatement of the reference SST block codec.
+ * TEST INFRASTRUCTURE ONLY (see sst_oracle.h).  Plain scalar C on purpose: it
+ * is the checker, never the product.
+ */
+#include "sst_oracle.h"
+
+#include <string.h>
+
+static uint32_t rd32(const uint8_t *p) {
+  uint32_t v;
+  memcpy(&v, p, 4);
+  return v;
+}
+static uint64_t rd64(const uint8_t *p) {
+  uint64_t v;
+  memcpy(&v, p, 8);
+  return v;
+}
+static void wr32(uint8_t *p, uint32_t v) { memcpy(p, &v, 4); }
+static void wr64(uint8_t *p, uint64_t v) { memcpy(p, &v, 8); }
+
+/* sstable/block_builder.cc:19-21 */
+uint32_t orc_entry_size(uint32_t key_len, uint32_t val_len) {
+  return 1u + 4u + key_len + (val_len != ORC_NO_VALUE ? 4u + val_len : 0u) + 8u;
+}
+
+/* sstable/block_builder.cc:12-109: data entries, then one 16 B offset entry
+ * (start, size) per record, then extra = (num_entries, data bytes). */
+uint64_t orc_block_encode(uint64_t n, const uint8_t *type, const uint32_t *key_len,
+                          const uint32_t *val_len, const uint64_t *txn,
+                          const uint8_t *key_src, const uint64_t *key_off,
+                          const uint8_t *val_src, const uint64_t *val_off,
+                          uint8_t *out) {
+  uint64_t pos = 0;
+  for (uint64_t i = 0; i < n; i++) { /* EncodeDataEntry :36-77 */
+    out[pos] = type[i];
+    wr32(out + pos + 1, key_len[i]);
+    memcpy(out + pos + 5, key_src + key_off[i], key_len[i]);
+    pos += 5 + (uint64_t)key_len[i];
+    if (val_len[i] != ORC_NO_VALUE) {
+      wr32(out + pos, val_len[i]);
+      if (val_len[i]) memcpy(out + pos + 4, val_src + val_off[i], val_len[i]);
+      pos += 4 + (uint64_t)val_len[i];
+    }
+    wr64(out + pos, txn[i]);
+    pos += 8;
+  }
+  const uint64_t data_bytes = pos;
+  uint64_t start = 0;
+  for (uint64_t i = 0; i < n; i++) { /* EncodeOffsetEntry :79-93 */
+    const uint64_t sz = orc_entry_size(key_len[i], val_len[i]);
+    wr64(out + pos, start);
+    wr64(out + pos + 8, sz);
+    pos += 16;
+    start += sz;
+  }
+  wr64(out + pos, n); /* EncodeExtraInfo :95-109 */
+  wr64(out + pos + 8, data_bytes);
+  return pos + 16;
+}
+
+int orc_block_count(const uint8_t *blk, uint64_t len, uint64_t *n_out) {
+  *n_out = 0;
+  if (len < 16) return ORC_BLK_TOO_SMALL;
+  *n_out = rd64(blk + len - 16);
+  return ORC_BLK_OK;
+}
+
+int orc_block_decode(const uint8_t *blk, uint64_t len, uint64_t base, int txn_mode,
+                     uint8_t *type, uint32_t *key_len, uint32_t *val_len,
+                     uint64_t *txn, uint64_t *key_off, uint64_t *val_off,
+                     uint64_t *n_out) {
+  *n_out = 0;
+  if (len < 16) return ORC_BLK_TOO_SMALL;
+  /* table_reader.cc:226-232: n at [size-16], offset section start at [size-8] */
+  const uint64_t n = rd64(blk + len - 16);
+  const uint64_t off = rd64(blk + len - 8);
+  if (n == 0) return ORC_BLK_EMPTY;
+  if (off > len - 16 || n > (len - 16 - off) / 16) return ORC_BLK_OFFSETS_RANGE;
+  *n_out = n;
+  for (uint64_t i = 0; i < n; i++) {
+    /* table_reader.cc:11-20: only the start half of an offset entry is read */
+    const uint64_t s = rd64(blk + off + 16 * i);
+    if (s >= off || off - s < 5) return ORC_BLK_ENTRY_RANGE;
+    const uint8_t t = blk[s];                      /* block_reader.cc:59-68 */
+    if (t > ORC_TYPE_DELETED) return ORC_BLK_BAD_TYPE;
+    const uint32_t kl = rd32(blk + s + 1);         /* block_reader.cc:70-82 */
+    if (kl > ORC_MAX_KEY) return ORC_BLK_KEY_TOO_LONG;
+    uint64_t p = s + 5 + kl;
+    uint32_t vl = ORC_NO_VALUE;
+    uint64_t vo = 0;
+    if (t != ORC_TYPE_DELETED) {                   /* block_reader.cc:84-102 */
+      if (p + 4 > off) return ORC_BLK_ENTRY_RANGE;
+      vl = rd32(blk + p);
+      vo = p + 4;
+      p = vo + vl;
+    }
+    if (p + 8 > off) return ORC_BLK_ENTRY_RANGE;
+    uint64_t tx = rd64(blk + p);                   /* block_reader.cc:104-114 */
+    if (txn_mode == ORC_TXN_COMPAT && t != ORC_TYPE_DELETED && vl == 0) {
+      /* value.empty() is true, so the reference reads 8 bytes at the value
+       * length field: (txn & 0xffffffff) << 32 */
+      tx = rd64(blk + s + 5 + kl);
+    }
+    type[i] = t;
+    key_len[i] = kl;
+    key_off[i] = base + s + 5;
+    val_len[i] = vl;
+    val_off[i] = t != ORC_TYPE_DELETED ? base + vo : 0;
+    txn[i] = tx;
+  }
+  return ORC_BLK_OK;
+}
+
+/* Bounded scratch for the per-block records of the roundtrip. A block holds at
+ * most (len-16)/29 entries (13 B minimal entry + 16 B offset entry). */
+#define ORC_RT_MAX 65536
+uint64_t orc_roundtrip_blocks(const uint8_t *src, const uint64_t *blk_off,
+                              const uint64_t *blk_len, uint64_t nblocks,
+                              int txn_mode, uint8_t *dst, uint64_t *out_len,
+                              uint32_t *status) {
+  static uint8_t type[ORC_RT_MAX];
+  static uint32_t kl[ORC_RT_MAX], vl[ORC_RT_MAX];
+  static uint64_t tx[ORC_RT_MAX], ko[ORC_RT_MAX], vo[ORC_RT_MAX];
+  uint64_t bad = 0;
+  for (uint64_t b = 0; b < nblocks; b++) {
+    const uint8_t *blk = src + blk_off[b];
+    uint64_t n = 0;
+    int st = ORC_BLK_OK;
+    if (blk_len[b] >= 16 && blk_len[b] / 29 + 1 > ORC_RT_MAX) {
+      st = ORC_BLK_OFFSETS_RANGE;
+    } else {
+      st = orc_block_decode(blk, blk_len[b], 0, txn_mode, type, kl, vl, tx, ko, vo, &n);
+    }
+    status[b] = (uint32_t)st;
+    if (st != ORC_BLK_OK) {
+      out_len[b] = 0;
+      bad++;
+      continue;
+    }
+    out_len[b] = orc_block_encode(n, type, kl, vl, tx, blk, ko, blk, vo, dst + blk_off[b]);
+  }
+  return bad;
+}
+
+uint64_t orc_segment(uint64_t n, const uint32_t *key_len, const uint32_t *val_len,
+                     uint64_t threshold, uint64_t *blk_first) {
+  uint64_t nb = 0, acc = 0;
+  for (uint64_t i = 0; i < n; i++) {
+    if (acc == 0) blk_first[nb++] = i;
+    acc += orc_entry_size(key_len[i], val_len[i]) + 16; /* block_builder.cc:33 */
+    if (acc >= threshold) acc = 0;                       /* table_builder.cc:57 */
+  }
+  blk_first[nb] = n;
+  return nb;
+}
+
+static uint64_t meta_entry(uint8_t *out, const uint8_t *fk, uint32_t fkl,
+                           const uint8_t *lk, uint32_t lkl, uint64_t off,
+                           uint64_t len) {
+  /* TableBuilder::AddIndexBlockEntry, sstable/table_builder.cc:101-145 */
+  if (out) {
+    wr32(out, fkl);
+    memcpy(out + 4, fk, fkl);
+    wr32(out + 4 + fkl, lkl);
+    memcpy(out + 8 + fkl, lk, lkl);
+    wr64(out + 8 + fkl + lkl, off);
+    wr64(out + 16 + fkl + lkl, len);
+  }
+  return 24 + (uint64_t)fkl + lkl;
+}
+
+uint64_t orc_table_build(uint64_t n, const uint8_t *type, const uint32_t *key_len,
+                         const uint32_t *val_len, const uint64_t *txn,
+                         const uint8_t *key_src, const uint64_t *key_off,
+                         const uint8_t *val_src, const uint64_t *val_off,
+                         uint64_t threshold, uint8_t *out) {
+  /* pass 1: data blocks (segmentation of AddEntry, FlushBlock :62-99) */
+  uint64_t pos = 0, nb = 0, start = 0, acc = 0;
+  uint64_t min_txn = UINT64_MAX, max_txn = 0;
+  for (uint64_t i = 0; i < n; i++) {
+    if (txn[i] < min_txn) min_txn = txn[i];
+    if (txn[i] > max_txn) max_txn = txn[i];
+    acc += orc_entry_size(key_len[i], val_len[i]) + 16;
+    if (acc >= threshold || i + 1 == n) {
+      const uint64_t m = i + 1 - start;
+      uint64_t sz = 16;
+      for (uint64_t j = start; j <= i; j++) sz += orc_entry_size(key_len[j], val_len[j]) + 16;
+      if (out)
+        orc_block_encode(m, type + start, key_len + start, val_len + start, txn + start,
+                         key_src, key_off + start, val_src, val_off + start, out + pos);
+      pos += sz;
+      nb++;
+      start = i + 1;
+      acc = 0;
+    }
+  }
+  /* pass 2: meta section (one entry per block, in block order) */
+  const uint64_t meta_off = pos;
+  start = 0;
+  acc = 0;
+  uint64_t boff = 0;
+  for (uint64_t i = 0; i < n; i++) {
+    acc += orc_entry_size(key_len[i], val_len[i]) + 16;
+    if (acc >= threshold || i + 1 == n) {
+      uint64_t sz = 16;
+      for (uint64_t j = start; j <= i; j++) sz += orc_entry_size(key_len[j], val_len[j]) + 16;
+      pos += meta_entry(out ? out + pos : NULL, key_src + key_off[start], key_len[start],
+                        key_src + key_off[i], key_len[i], boff, sz);
+      boff += sz;
+      start = i + 1;
+      acc = 0;
+    }
+  }
+  const uint64_t meta_len = pos - meta_off;
+  /* footer, TableBuilder::EncodeExtraInfo :179-211 */
+  if (out) {
+    wr64(out + pos, nb);
+    wr64(out + pos + 8, meta_off);
+    wr64(out + pos + 16, meta_len);
+    wr64(out + pos + 24, min_txn);
+    wr64(out + pos + 32, max_txn);
+  }
+  return pos + 40;
+}
+
+uint64_t orc_table_index(const uint8_t *file, uint64_t bytes, uint64_t cap,
+                         uint64_t *blk_off, uint64_t *blk_len,
+                         uint64_t *first_key_off, uint32_t *first_key_len,
+                         uint64_t *last_key_off, uint32_t *last_key_len,
+                         uint64_t *min_txn, uint64_t *max_txn) {
+  if (bytes < 40) return UINT64_MAX;
+  /* DecodeExtraInfo, sstable/table_reader.cc:52-84 (file_size - 40 - 1 with
+   * file_size = bytes + 1) */
+  const uint8_t *f = file + bytes - 40;
+  const uint64_t nb = rd64(f), moff = rd64(f + 8), mlen = rd64(f + 16);
+  *min_txn = rd64(f + 24);
+  *max_txn = rd64(f + 32);
+  if (moff > bytes - 40 || mlen > bytes - 40 - moff) return UINT64_MAX;
+  /* FetchBlockIndexInfo :86-156, sequential length-prefixed walk */
+  uint64_t p = moff;
+  const uint64_t end = moff + mlen;
+  for (uint64_t i = 0; i < nb; i++) {
+    if (p + 4 > end) return UINT64_MAX;
+    const uint32_t fkl = rd32(file + p);
+    if (p + 4 + (uint64_t)fkl + 4 > end) return UINT64_MAX;
+    const uint32_t lkl = rd32(file + p + 4 + fkl);
+    if (p + 24 + (uint64_t)fkl + lkl > end) return UINT64_MAX;
+    if (i < cap) {
+      first_key_off[i] = p + 4;
+      first_key_len[i] = fkl;
+      last_key_off[i] = p + 8 + fkl;
+      last_key_len[i] = lkl;
+      blk_off[i] = rd64(file + p + 8 + fkl + lkl);
+      blk_len[i] = rd64(file + p + 16 + fkl + lkl);
+    }
+    p += 24 + (uint64_t)fkl + lkl;
+  }
+  return nb;
+}

@@ -1,0 +1,114 @@
+/*
+ * sst_oracle.h — CPU restatement of the reference SST block codec.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and the
+ * cpu_baseline leg of bench.py may load this library, and only as the checker.
+ * The product path (lsm-kv-storage_amd/) never links or calls it.
+ *
+ * Pinned against: (1) the known-answer vectors of the reference's own tests
+ * (tests/test_block.cc:57-187, tests/test_sst.cc:64-148), restated in
+ * tests/golden/; (2) fixtures produced by the reference sources themselves,
+ * compiled here by oracle/Makefile into oracle/_ref/libsstref.so and dumped by
+ * tests/golden/make_golden.py.
+ *
+ * Record model (shared with include/sstcodec.h): one record = (type, key, value,
+ * txn).  Value fields are present in the encoding iff val_len != ORC_NO_VALUE;
+ * that is the reference's `value.data() != nullptr` test
+ * (sstable/block_builder.cc:19-21,56).  A decoded DELETE gets ORC_NO_VALUE
+ * because BlockReader::GetValueFromDataEntry returns a null view for it
+ * (sstable/block_reader.cc:84-88).
+ */
+#ifndef SST_ORACLE_H
+#define SST_ORACLE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ORC_NO_VALUE 0xFFFFFFFFu
+#define ORC_TYPE_PUT 0
+#define ORC_TYPE_DELETED 1
+#define ORC_MAX_KEY 4096u /* common/macros.h:29 kMaxKeySize */
+
+/* txn read mode: COMPAT reproduces BlockReader::GetTransactionIdFromDataEntry
+ * (sstable/block_reader.cc:104-114), which tests value.empty() instead of the
+ * type, so an empty-value PUT yields (txn & 0xffffffff) << 32.  CORRECT reads
+ * the txn field where the encoder put it. */
+#define ORC_TXN_COMPAT 0
+#define ORC_TXN_CORRECT 1
+
+/* per-block decode status (same numbering as SSTC_BLK_* in include/sstcodec.h) */
+#define ORC_BLK_OK 0
+#define ORC_BLK_TOO_SMALL 1
+#define ORC_BLK_EMPTY 2
+#define ORC_BLK_OFFSETS_RANGE 3
+#define ORC_BLK_ENTRY_RANGE 4
+#define ORC_BLK_BAD_TYPE 5
+#define ORC_BLK_KEY_TOO_LONG 6
+
+uint32_t orc_entry_size(uint32_t key_len, uint32_t val_len);
+
+/* BlockBuilder::AddEntry x n + EncodeExtraInfo (sstable/block_builder.cc:12-109).
+ * Writes data section | offset section | extra into out; returns block bytes. */
+uint64_t orc_block_encode(uint64_t n, const uint8_t *type, const uint32_t *key_len,
+                          const uint32_t *val_len, const uint64_t *txn,
+                          const uint8_t *key_src, const uint64_t *key_off,
+                          const uint8_t *val_src, const uint64_t *val_off,
+                          uint8_t *out);
+
+/* Parse the 16 B trailer of a block (sstable/table_reader.cc:226-232). */
+int orc_block_count(const uint8_t *blk, uint64_t len, uint64_t *n_out);
+
+/* TableReader::CreateAndSetupDataForBlockReader + BlockReader accessors
+ * (sstable/table_reader.cc:212-241, sstable/block_reader.cc:59-114).
+ * key_off/val_off are written relative to `base` + block start (i.e. absolute
+ * when blk == src + base).  Returns ORC_BLK_*. */
+int orc_block_decode(const uint8_t *blk, uint64_t len, uint64_t base, int txn_mode,
+                     uint8_t *type, uint32_t *key_len, uint32_t *val_len,
+                     uint64_t *txn, uint64_t *key_off, uint64_t *val_off,
+                     uint64_t *n_out);
+
+/* Decode every block then re-encode its records with the block encoder, output
+ * at the same offset as the input block: what compaction does to a block whose
+ * records all survive (db/compact.cc:254-302 with no drops).  out_len[b] gets
+ * the re-encoded size, status[b] the decode status (block left untouched in dst
+ * on error). Returns number of failed blocks. */
+uint64_t orc_roundtrip_blocks(const uint8_t *src, const uint64_t *blk_off,
+                              const uint64_t *blk_len, uint64_t nblocks,
+                              int txn_mode, uint8_t *dst, uint64_t *out_len,
+                              uint32_t *status);
+
+/* Greedy block segmentation of TableBuilder::AddEntry (sstable/table_builder.cc:
+ * 47-59, block_builder.cc:33): the current block is flushed right after the
+ * record that brings sum(entry_size + 16) to >= threshold.  Writes nblocks+1
+ * record-index boundaries into blk_first; returns nblocks. */
+uint64_t orc_segment(uint64_t n, const uint32_t *key_len, const uint32_t *val_len,
+                     uint64_t threshold, uint64_t *blk_first);
+
+/* Whole SST image (TableBuilder AddEntry... Finish, sstable/table_builder.cc:
+ * 35-211) for records already in order.  Returns the byte count written to out
+ * (file size on disk; TableBuilder::GetFileSize() reports this + 1,
+ * sstable/table_builder.cc:228).  out may be NULL to size it. */
+uint64_t orc_table_build(uint64_t n, const uint8_t *type, const uint32_t *key_len,
+                         const uint32_t *val_len, const uint64_t *txn,
+                         const uint8_t *key_src, const uint64_t *key_off,
+                         const uint8_t *val_src, const uint64_t *val_off,
+                         uint64_t threshold, uint8_t *out);
+
+/* Footer + meta section parse (sstable/table_reader.cc:52-156).  bytes = file
+ * bytes on disk.  Fills up to cap blocks; returns the block count from the
+ * footer, or UINT64_MAX on a malformed file. first/last key offsets point into
+ * file. */
+uint64_t orc_table_index(const uint8_t *file, uint64_t bytes, uint64_t cap,
+                         uint64_t *blk_off, uint64_t *blk_len,
+                         uint64_t *first_key_off, uint32_t *first_key_len,
+                         uint64_t *last_key_off, uint32_t *last_key_len,
+                         uint64_t *min_txn, uint64_t *max_txn);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

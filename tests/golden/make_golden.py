@@ -1,0 +1,157 @@
+"""Generate the golden fixtures under tests/golden/ from the REFERENCE itself.
+
+    make -C oracle && python tests/golden/make_golden.py
+
+Every expected output below comes from oracle/_ref/libsstref.so, i.e. the
+reference's own sstable sources (/root/reference) compiled by oracle/Makefile:
+BlockBuilder for encode, BlockReader/BlockReaderIterator for decode, both for
+the decode -> re-encode round trip, TableBuilder/TableReader for whole SSTs.
+The inputs are deterministic (seeded).  Fixtures are data (inputs + expected
+outputs) saved as .npz (no pickles) and are small enough to commit.
+"""
+import os
+import sys
+import tempfile
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+sys.path.insert(0, os.path.join(ROOT, "lsm-kv-storage_amd"))
+
+from oracle import RefLib  # noqa: E402
+from sstcodec import workload as W  # noqa: E402
+
+REC_KEYS = ("type", "key_len", "val_len", "txn", "key_off", "val_off")
+
+
+def records_from_list(items):
+    """items: (type, key bytes, value bytes or None, txn)."""
+    ks = b"".join(k for _, k, _, _ in items)
+    vs = b"".join(v for _, _, v, _ in items if v is not None)
+    ko, vo, kl, vl = [], [], [], []
+    kp = vp = 0
+    for _, k, v, _ in items:
+        ko.append(kp)
+        kl.append(len(k))
+        kp += len(k)
+        if v is None:
+            vo.append(0)
+            vl.append(W.NO_VALUE)
+        else:
+            vo.append(vp)
+            vl.append(len(v))
+            vp += len(v)
+    return {
+        "type": np.array([t for t, _, _, _ in items], np.uint8),
+        "key_len": np.array(kl, np.uint32), "val_len": np.array(vl, np.uint32),
+        "txn": np.array([t for _, _, _, t in items], np.uint64),
+        "key_off": np.array(ko, np.uint64), "val_off": np.array(vo, np.uint64),
+        "key_src": np.frombuffer(ks + b"\0" * 8, np.uint8).copy(),
+        "val_src": np.frombuffer(vs + b"\0" * 8, np.uint8).copy(),
+    }
+
+
+def ref_blocks(ref, rec, first):
+    parts, offs, lens = [], [], []
+    pos = 0
+    for b in range(len(first) - 1):
+        blk = ref.encode_block(rec, int(first[b]), int(first[b + 1]))
+        parts.append(blk)
+        offs.append(pos)
+        lens.append(blk.size)
+        pos += blk.size
+    return np.concatenate(parts), np.array(offs, np.uint64), np.array(lens, np.uint64)
+
+
+def ref_decode_all(ref, src, offs, lens):
+    out = {k: [] for k in REC_KEYS}
+    base = [0]
+    for o, l in zip(offs, lens):
+        d = ref.decode_block(src[int(o):int(o + l)])
+        for k in REC_KEYS:
+            v = d[k].copy()
+            if k == "key_off":
+                v = v + np.uint64(o)
+            if k == "val_off":
+                v = np.where(d["val_len"] != W.NO_VALUE, v + np.uint64(o), 0).astype(np.uint64)
+            out[k].append(v)
+        base.append(base[-1] + len(d["type"]))
+    res = {"dec_" + k: np.concatenate(v) for k, v in out.items()}
+    res["dec_rec_base"] = np.array(base, np.uint64)
+    return res
+
+
+def save(name, **arrays):
+    path = os.path.join(HERE, name)
+    np.savez_compressed(path, **arrays)
+    print(f"{name}: {os.path.getsize(path)} bytes")
+
+
+def block_set(ref, name, rec, first, extra=None):
+    src, offs, lens = ref_blocks(ref, rec, first)
+    rt, rt_len, _ = ref.roundtrip(src, offs, lens)
+    arrays = {"src": src, "blk_off": offs, "blk_len": lens, "blk_first": np.asarray(first, np.uint64),
+              "rt_dst": rt, "rt_len": rt_len}
+    arrays.update(ref_decode_all(ref, src, offs, lens))
+    arrays.update({"rec_" + k: rec[k] for k in REC_KEYS + ("key_src", "val_src")})
+    if extra:
+        arrays.update(extra)
+    save(name, **arrays)
+
+
+def main():
+    ref = RefLib()
+
+    # 1. tests/test_block.cc:57-138 (BasicEncode) and :140-187 (EdgeCasesEncode)
+    basic = records_from_list([(0, b"apple", b"value1", 12345), (0, b"apply", b"success", 9876),
+                               (0, b"colossus", b"thunder", 2 ** 32 - 1)])
+    edge = records_from_list([(0, b"", b"", 10)])
+    block_set(ref, "kat_basic.npz", basic, [0, 3])
+    block_set(ref, "kat_edge.npz", edge, [0, 1])
+
+    # 2. config-1 block: 28 uniform PUTs, keys k%015d, 100 B values (seed 1)
+    uni = W.uniform_records(28, seed=1, txn_start=1)
+    block_set(ref, "block_uniform.npz", uni, [0, 28])
+
+    # 3. ragged records with DELETEs, empty keys/values, segmented at 4096
+    mixed = W.mixed_records(600, seed=11)
+    first = W.segment(mixed, 4096)
+    block_set(ref, "blocks_mixed.npz", mixed, first)
+
+    # 4. edge blocks: >64 entries per block, single huge entry, all-DELETE,
+    #    max-size key, empty-value PUT runs (txn quirk), 1-entry blocks
+    items = []
+    items += [(1, b"d%04d" % i, None, 1000 + i) for i in range(150)]           # 150 tiny DELETEs
+    items += [(0, b"e%04d" % i, b"", (7 << 32) + i) for i in range(70)]        # empty-value PUTs
+    items += [(0, b"K" * 4096, b"v" * 33, 5)]                                  # max key
+    items += [(0, b"big", bytes(range(256)) * 270, 6)]                         # 69120 B value
+    items += [(0, b"", b"x", 2 ** 64 - 2)]                                     # empty key
+    items += [(1, b"", None, 0)]                                               # empty DELETE
+    edge_rec = records_from_list(items)
+    edge_first = [0, 150, 220, 221, 222, 224]
+    block_set(ref, "blocks_edge.npz", edge_rec, edge_first)
+
+    # 5. SSTs written by the reference TableBuilder
+    with tempfile.TemporaryDirectory() as td:
+        # tests/test_sst.cc:116-148: three PUTs with txn 0 -> 230 B file
+        mini = records_from_list([(0, b"apple", b"value1", 0), (0, b"apply", b"success", 0),
+                                  (0, b"colossus", b"thunder", 0)])
+        p = os.path.join(td, "1.sst")
+        fs = ref.table_build(p, mini, 4096)
+        f = np.fromfile(p, np.uint8)
+        save("table_mini.npz", sst=f, file_size=np.array([fs], np.uint64),
+             **{"rec_" + k: mini[k] for k in REC_KEYS + ("key_src", "val_src")})
+        for T in (4096, 32768):
+            p = os.path.join(td, f"t{T}.sst")
+            fs = ref.table_build(p, mixed, T)
+            f = np.fromfile(p, np.uint8)
+            idx = ref.table_index(p, fs)
+            save(f"table_mixed_{T}.npz", sst=f, file_size=np.array([fs], np.uint64),
+                 idx_blk_off=idx["blk_off"], idx_blk_len=idx["blk_len"],
+                 idx_first_key_len=idx["first_key_len"], idx_last_key_len=idx["last_key_len"])
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,274 @@
+"""GPU parity: the HIP kernels (through the C-ABI) against the oracle and the
+reference's golden fixtures.  Bit-exact everywhere (integer/byte work)."""
+import numpy as np
+import pytest
+import torch
+from conftest import BLOCK_SETS, REC_KEYS, golden_records, load_golden
+from sstcodec import workload as W
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module")
+def codec():
+    import sstcodec
+    return sstcodec.Codec(0)
+
+
+def t8(a):
+    return torch.from_numpy(np.ascontiguousarray(a, np.uint8)).to(DEV)
+
+
+def t64(a):
+    return torch.from_numpy(np.ascontiguousarray(a, np.uint64).view(np.int64)).to(DEV)
+
+
+def cpu_u64(t):
+    return t.cpu().numpy().view(np.uint64)
+
+
+def run_roundtrip(codec, src, offs, lens, mode=0, dst_fill=0):
+    s = t8(src)
+    d = torch.full_like(s, dst_fill)
+    dst, out_len, status = codec.roundtrip(s, t64(offs), t64(lens), dst=d, txn_mode=mode)
+    torch.cuda.synchronize()
+    n = len(offs)
+    return dst.cpu().numpy(), cpu_u64(out_len)[:n], status.cpu().numpy()[:n].astype(np.uint32)
+
+
+def oracle_rt(oracle, src, offs, lens, mode=0, dst_fill=0):
+    d, l, s, _ = oracle.roundtrip(src, offs, lens, mode)
+    if dst_fill:
+        # oracle writes into zeros; emulate a pre-filled destination
+        base = np.full_like(src, dst_fill)
+        for o, ln, st in zip(offs, l, s):
+            if st == 0:
+                base[int(o):int(o + ln)] = d[int(o):int(o + ln)]
+        d = base
+    return d, l, s
+
+
+# ---------------------------------------------------------------- round trip
+@pytest.mark.parametrize("name", BLOCK_SETS)
+def test_roundtrip_golden(codec, name):
+    g = load_golden(name)
+    dst, out_len, status = run_roundtrip(codec, g["src"], g["blk_off"], g["blk_len"])
+    assert (status == 0).all()
+    assert np.array_equal(out_len, g["rt_len"])
+    assert np.array_equal(dst, g["rt_dst"])
+    dst1, _, _ = run_roundtrip(codec, g["src"], g["blk_off"], g["blk_len"], mode=1)
+    assert np.array_equal(dst1, g["src"])
+
+
+@pytest.mark.parametrize("seed", range(6))
+@pytest.mark.parametrize("T", [4096, 32768])
+def test_roundtrip_random_vs_oracle(codec, oracle, seed, T):
+    rec = W.mixed_records(3000, seed=seed, max_val=1500 if T == 4096 else 5000)
+    first = oracle.segment(rec, T)
+    src, offs, lens = oracle.encode_blocks(rec, first, base=seed * 3)  # unaligned start
+    src = np.concatenate([np.zeros(seed * 3, np.uint8), src, np.zeros(5, np.uint8)])
+    for mode in (0, 1):
+        got = run_roundtrip(codec, src, offs, lens, mode, dst_fill=0xA5)
+        want = oracle_rt(oracle, src, offs, lens, mode, dst_fill=0xA5)
+        assert np.array_equal(got[2], want[2])
+        assert np.array_equal(got[1], want[1])
+        assert np.array_equal(got[0], want[0])
+
+
+def test_roundtrip_scattered_blocks(codec, oracle):
+    """Blocks in arbitrary order with gaps between them (a batch gathered from
+    several SSTs): every byte outside the blocks must stay untouched."""
+    rec = W.mixed_records(2000, seed=42)
+    first = oracle.segment(rec, 4096)
+    data, offs, lens = oracle.encode_blocks(rec, first)
+    rng = np.random.default_rng(0)
+    order = rng.permutation(len(lens))
+    gaps = rng.integers(0, 40, len(lens))
+    parts, noffs, pos = [], np.zeros(len(lens), np.uint64), 0
+    for g_, b in zip(gaps, order):
+        parts.append(np.full(g_, 0x5A, np.uint8))
+        pos += int(g_)
+        noffs[b] = pos
+        parts.append(data[int(offs[b]):int(offs[b] + lens[b])])
+        pos += int(lens[b])
+    src = np.concatenate(parts)
+    got = run_roundtrip(codec, src, noffs, lens, 0, dst_fill=0x33)
+    want = oracle_rt(oracle, src, noffs, lens, 0, dst_fill=0x33)
+    assert np.array_equal(got[0], want[0]) and np.array_equal(got[1], want[1])
+
+
+def test_roundtrip_non_canonical(codec, oracle):
+    """Entries not packed (gap before the offset section, entries listed out of
+    order): valid for the reference reader, re-encode packs them."""
+    rec = W.mixed_records(40, seed=5, max_val=60)
+    blk = oracle.encode_block(rec)
+    n = 40
+    D = int(blk[-8:].view(np.uint64)[0])
+    offsec = blk[D:D + 16 * n].copy()
+    # 1) 24 junk bytes between data section and offset section
+    b1 = np.concatenate([blk[:D], np.full(24, 0xEE, np.uint8), offsec,
+                         np.array([n], np.uint64).view(np.uint8), np.array([D + 24], np.uint64).view(np.uint8)])
+    # 2) offset entries reversed (record order changes)
+    rev = offsec.reshape(n, 16)[::-1].reshape(-1)
+    b2 = np.concatenate([blk[:D], rev, blk[-16:]])
+    src = np.concatenate([b1, np.zeros(7, np.uint8), b2])
+    offs = np.array([0, b1.size + 7], np.uint64)
+    lens = np.array([b1.size, b2.size], np.uint64)
+    got = run_roundtrip(codec, src, offs, lens, 0, dst_fill=0x11)
+    want = oracle_rt(oracle, src, offs, lens, 0, dst_fill=0x11)
+    assert (got[2] == 0).all()
+    assert np.array_equal(got[1], want[1]) and np.array_equal(got[0], want[0])
+    assert got[1][0] == b1.size - 24
+
+
+def test_roundtrip_errors(codec, oracle):
+    g = load_golden("kat_basic.npz")
+    good = g["src"]
+    blocks = [good.copy() for _ in range(8)]
+    blocks[1][-16:-8] = 0                                                   # EMPTY
+    blocks[2][-8:] = np.array([10_000], np.uint64).view(np.uint8)           # OFFSETS_RANGE
+    blocks[3][89 + 16:89 + 24] = np.array([88], np.uint64).view(np.uint8)   # ENTRY_RANGE
+    blocks[4][28] = 7                                                       # BAD_TYPE
+    blocks[5][29:33] = np.array([5000], np.uint32).view(np.uint8)           # KEY_TOO_LONG
+    blocks[6] = blocks[6][:9]                                               # TOO_SMALL
+    src = np.concatenate(blocks)
+    lens = np.array([b.size for b in blocks], np.uint64)
+    offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint64)
+    codec.reset_errors()
+    got = run_roundtrip(codec, src, offs, lens, 0, dst_fill=0x77)
+    want = oracle_rt(oracle, src, offs, lens, 0, dst_fill=0x77)
+    assert got[2].tolist() == [0, 2, 3, 4, 5, 6, 1, 0]
+    assert np.array_equal(got[2], want[2])
+    assert np.array_equal(got[0], want[0])
+    assert codec.error_count() == 6
+
+
+def test_roundtrip_empty_batch(codec):
+    s = torch.zeros(16, dtype=torch.uint8, device=DEV)
+    e = torch.zeros(0, dtype=torch.int64, device=DEV)
+    codec.roundtrip(s, e, e)
+    torch.cuda.synchronize()
+
+
+# -------------------------------------------------------------------- decode
+@pytest.mark.parametrize("name", BLOCK_SETS)
+def test_decode_golden(codec, name):
+    g = load_golden(name)
+    for mode in (0, 1):
+        table, rec_base, status = codec.decode(t8(g["src"]), t64(g["blk_off"]), t64(g["blk_len"]), txn_mode=mode)
+        torch.cuda.synchronize()
+        assert (status.cpu().numpy()[: len(g["blk_off"])] == 0).all()
+        assert np.array_equal(cpu_u64(rec_base), g["dec_rec_base"])
+        got = table.to_numpy()
+        for k in REC_KEYS:
+            want = g["dec_" + k]
+            if k == "txn" and mode == 1:
+                want = g["rec_txn"]  # blocks hold the records in order
+            assert np.array_equal(got[k], want), (name, mode, k)
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_decode_random_vs_oracle(codec, oracle, seed):
+    rec = W.mixed_records(5000, seed=20 + seed, max_val=900)
+    first = oracle.segment(rec, 4096)
+    src, offs, lens = oracle.encode_blocks(rec, first, base=1)
+    src = np.concatenate([[9], src]).astype(np.uint8)
+    table, rec_base, status = codec.decode(t8(src), t64(offs), t64(lens), txn_mode=1)
+    got = table.to_numpy()
+    # oracle per block, offsets absolute
+    parts = {k: [] for k in REC_KEYS}
+    for o, l in zip(offs, lens):
+        st, d = oracle.decode_block(src[int(o):int(o + l)], 1, int(o))
+        assert st == 0
+        for k in REC_KEYS:
+            parts[k].append(d[k])
+    for k in REC_KEYS:
+        assert np.array_equal(got[k], np.concatenate(parts[k])), k
+    # decode(encode(records)) == records (keys/values compared by bytes)
+    assert np.array_equal(got["txn"], rec["txn"]) and np.array_equal(got["type"], rec["type"])
+
+
+# -------------------------------------------------------------------- encode
+def records_table(rec):
+    from sstcodec.codec import RecordTable
+    return RecordTable.from_numpy(rec, torch.device(DEV))
+
+
+@pytest.mark.parametrize("name", BLOCK_SETS)
+def test_encode_golden(codec, name):
+    g = load_golden(name)
+    rec = golden_records(g)
+    dst, off, ln = codec.encode(records_table(rec), t8(rec["key_src"]), t8(rec["val_src"]), t64(g["blk_first"]))
+    torch.cuda.synchronize()
+    assert np.array_equal(cpu_u64(ln), g["blk_len"])
+    assert np.array_equal(cpu_u64(off)[:-1], g["blk_off"])
+    assert np.array_equal(dst.cpu().numpy()[: g["src"].size], g["src"])
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_encode_random_vs_oracle(codec, oracle, seed):
+    rec = W.mixed_records(4000, seed=50 + seed, max_val=3000 if seed % 2 else 200)
+    T = [4096, 8192, 32768, 4096][seed]
+    first = oracle.segment(rec, T)
+    want, woff, wlen = oracle.encode_blocks(rec, first, base=seed)
+    dst, off, ln = codec.encode(records_table(rec), t8(rec["key_src"]), t8(rec["val_src"]), t64(first),
+                                out_base=seed)
+    torch.cuda.synchronize()
+    assert np.array_equal(cpu_u64(off)[:-1], woff) and np.array_equal(cpu_u64(ln), wlen)
+    assert np.array_equal(dst.cpu().numpy()[seed:seed + want.size], want)
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_segment_vs_oracle(codec, oracle, seed):
+    rec = W.mixed_records([1, 37, 3000, 20000][seed], seed=70 + seed, max_val=[10, 500, 5000, 300][seed])
+    for T in (4096, 8192, 32768):
+        want = oracle.segment(rec, T)
+        got = cpu_u64(codec.segment(records_table(rec), T))
+        assert np.array_equal(got, want), (seed, T)
+
+
+def test_decode_then_encode_is_roundtrip(codec, oracle):
+    """Unfused pipeline: decode -> (records stay in HBM) -> encode with the
+    input block boundaries == fused round trip."""
+    g = load_golden("blocks_mixed.npz")
+    src = t8(g["src"])
+    table, rec_base, status = codec.decode(src, t64(g["blk_off"]), t64(g["blk_len"]), txn_mode=0)
+    dst, off, ln = codec.encode(table, src, src, rec_base)
+    torch.cuda.synchronize()
+    assert np.array_equal(dst.cpu().numpy()[: g["rt_dst"].size], g["rt_dst"])
+
+
+# --------------------------------------------- full size (BASELINE configs)
+def uniform_blocks(codec, nblocks, seed=1):
+    n = nblocks * 28
+    rec = W.uniform_records(n, seed=seed)
+    first = np.arange(0, n + 1, 28, dtype=np.uint64)
+    dst, off, ln = codec.encode(records_table(rec), t8(rec["key_src"]), t8(rec["val_src"]), t64(first))
+    return rec, dst, off[:-1].contiguous(), ln
+
+
+def test_config2_full_size_properties(codec, oracle):
+    """65 536 x 4188 B blocks: encode(GPU) -> round trip -> identity; decode ->
+    records equal the generator's; a sample of blocks equal the oracle's."""
+    nb = 65536
+    rec, src, off, ln = uniform_blocks(codec, nb)
+    torch.cuda.synchronize()
+    assert int(ln.min()) == int(ln.max()) == 4188 and src.numel() == nb * 4188
+    dst, out_len, status = codec.roundtrip(src, off, ln, txn_mode=0)
+    torch.cuda.synchronize()
+    assert bool((status[:nb] == 0).all()) and bool((out_len[:nb] == 4188).all())
+    assert torch.equal(dst, src)
+    # sampled bit-exact check against the oracle encoder
+    srcn = src.cpu().numpy()
+    for b in (0, 1, 777, nb - 1):
+        want = oracle.encode_block(rec, 28 * b, 28 * b + 28)
+        assert np.array_equal(srcn[4188 * b:4188 * (b + 1)], want)
+    table, rec_base, st = codec.decode(src, off, ln)
+    got = table.to_numpy()
+    assert np.array_equal(got["txn"], rec["txn"]) and (got["key_len"] == 16).all() and (got["val_len"] == 100).all()
+    # key bytes gathered through the decoded offsets equal the generator's keys
+    ko = got["key_off"][:1000].astype(np.int64)
+    keys = srcn[ko[:, None] + np.arange(16)[None, :]]
+    assert np.array_equal(keys.reshape(-1), rec["key_src"][:16000])
