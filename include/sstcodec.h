@@ -66,6 +66,9 @@ extern "C" {
 #define SSTC_BLK_BAD_TYPE 5       /* type byte not PUT/DELETED                     */
 #define SSTC_BLK_KEY_TOO_LONG 6   /* key_len > 4096 (block_builder.cc:38 assert)   */
 #define SSTC_BLK_TOO_LARGE 7      /* block >= 4 GiB                                */
+#define SSTC_BLK_NO_ROOM 8        /* round trip: re-encoded block longer than the  */
+                                  /* input block (overlapping offset entries)     */
+#define SSTC_BLK_COUNT_MISMATCH 9 /* decode: num_entries != d_rec_base difference  */
 
 /* txn read mode.  COMPAT reproduces BlockReader::GetTransactionIdFromDataEntry
  * (block_reader.cc:104-114): it tests value.empty() instead of the type, so an

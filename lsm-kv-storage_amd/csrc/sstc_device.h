@@ -26,6 +26,8 @@ enum BlkStatus : uint32_t {
   kBlkBadType = 5,
   kBlkKeyTooLong = 6,
   kBlkTooLarge = 7,
+  kBlkNoRoom = 8,
+  kBlkCountMismatch = 9,
 };
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));

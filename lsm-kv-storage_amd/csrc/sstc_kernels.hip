@@ -312,6 +312,7 @@ __global__ __launch_bounds__(kGenThreads) void rt_generic_kernel(RtArgs a) {
     }
     const uint64_t out_len = data + 16 * n + 16;
     if (st == kBlkOk && out_len >= (1ull << 32)) st = kBlkTooLarge;
+    if (st == kBlkOk && out_len > len) st = kBlkNoRoom; // written in place of the input block
     if (st != kBlkOk) {
       if (tid == 0) {
         if (a.status) a.status[b] = st;
@@ -415,6 +416,7 @@ __global__ __launch_bounds__(kDecWaves *kWave) void decode_kernel(DecArgs a) {
     doff = rd.u64(len - 8);
     st = check_extra(len, n, doff);
   }
+  if (st == kBlkOk && n != uniform64(a.rec_base[b + 1]) - base) st = kBlkCountMismatch;
   if (st == kBlkOk) {
     for (uint64_t i0 = 0; i0 < n; i0 += kWave) {
       const uint64_t i = i0 + lane;

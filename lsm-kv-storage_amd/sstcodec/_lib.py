@@ -16,7 +16,8 @@ SSTC_NO_VALUE = 0xFFFFFFFF
 SSTC_TXN_COMPAT = 0
 SSTC_TXN_CORRECT = 1
 BLK_STATUS = {0: "OK", 1: "TOO_SMALL", 2: "EMPTY", 3: "OFFSETS_RANGE", 4: "ENTRY_RANGE",
-              5: "BAD_TYPE", 6: "KEY_TOO_LONG", 7: "TOO_LARGE"}
+              5: "BAD_TYPE", 6: "KEY_TOO_LONG", 7: "TOO_LARGE",
+              8: "NO_ROOM", 9: "COUNT_MISMATCH"}
 
 c_u8p = ctypes.c_void_p
 c_u64 = ctypes.c_uint64

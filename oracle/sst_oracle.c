@@ -133,6 +133,12 @@ uint64_t orc_roundtrip_blocks(const uint8_t *src, const uint64_t *blk_off,
     } else {
       st = orc_block_decode(blk, blk_len[b], 0, txn_mode, type, kl, vl, tx, ko, vo, &n);
     }
+    if (st == ORC_BLK_OK) {
+      uint64_t sz = 16 + 16 * n;
+      for (uint64_t i = 0; i < n; i++) sz += orc_entry_size(kl[i], vl[i]);
+      if (sz >= (1ull << 32)) st = ORC_BLK_TOO_LARGE;
+      else if (sz > blk_len[b]) st = ORC_BLK_NO_ROOM; /* re-encoded in place of the input */
+    }
     status[b] = (uint32_t)st;
     if (st != ORC_BLK_OK) {
       out_len[b] = 0;

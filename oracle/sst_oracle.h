@@ -48,6 +48,8 @@ extern "C" {
 #define ORC_BLK_ENTRY_RANGE 4
 #define ORC_BLK_BAD_TYPE 5
 #define ORC_BLK_KEY_TOO_LONG 6
+#define ORC_BLK_TOO_LARGE 7
+#define ORC_BLK_NO_ROOM 8
 
 uint32_t orc_entry_size(uint32_t key_len, uint32_t val_len);
 

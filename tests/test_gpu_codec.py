@@ -272,3 +272,33 @@ def test_config2_full_size_properties(codec, oracle):
     ko = got["key_off"][:1000].astype(np.int64)
     keys = srcn[ko[:, None] + np.arange(16)[None, :]]
     assert np.array_equal(keys.reshape(-1), rec["key_src"][:16000])
+
+
+def test_roundtrip_overlapping_entries_no_room(codec, oracle):
+    """Offset entries that all point at entry 0: valid to the reference reader,
+    but the re-encoded block is longer than its slot -> NO_ROOM, untouched."""
+    rec = W.mixed_records(30, seed=9, max_val=50)
+    blk = oracle.encode_block(rec)
+    D = int(blk[-8:].view(np.uint64)[0])
+    big = blk.copy()
+    n = 30
+    offs_ = big[D:D + 16 * n].reshape(n, 16)
+    offs_[:, :8] = 0  # every start -> 0
+    # make entry 0 the largest so 30 copies overflow
+    src = np.concatenate([big, blk])
+    offs = np.array([0, big.size], np.uint64)
+    lens = np.array([big.size, blk.size], np.uint64)
+    got = run_roundtrip(codec, src, offs, lens, 0, dst_fill=0x42)
+    want = oracle_rt(oracle, src, offs, lens, 0, dst_fill=0x42)
+    assert np.array_equal(got[2], want[2]) and np.array_equal(got[0], want[0])
+    assert np.array_equal(got[1], want[1])
+
+
+def test_decode_count_mismatch(codec):
+    g = load_golden("blocks_mixed.npz")
+    rb = g["dec_rec_base"].copy()
+    rb[1:] += 1  # block 0 claims one record more than its extra says
+    table, _, status = codec.decode(t8(g["src"]), t64(g["blk_off"]), t64(g["blk_len"]), rec_base=t64(rb))
+    torch.cuda.synchronize()
+    st = status.cpu().numpy()[: len(g["blk_off"])]
+    assert st[0] == 9 and (st[1:] == 0).all()
