@@ -13,10 +13,10 @@ Input blocks are produced on the GPU by the codec's own encoder from records
 generated on the host (synthetic, deterministic); a warm-up round trip is
 checked for identity before timing.
 
-roofline: the dominant kernel is rt_fast_kernel.  Algorithmic bytes per launch
+roofline: the dominant (only) kernel of a step is rt_kernel.  Algorithmic bytes per launch
 = B x (4188 read + 4188 written); duration = HIP events on
 the codec's stream around each sstc_roundtrip_blocks call (includes the
-per-call counter reset and the deferred-block kernel's empty launch, so the
+launch gap between back-to-back calls, so the
 fraction is slightly conservative); peak = 8 TB/s (MI355X_MICROARCH.md).
 traffic = HBM bytes per launch from rocprofv3 PMC passes (FETCH_SIZE x 2 for
 gfx950 + WRITE_SIZE, KB units), read from profiles/pmc_traffic.json when it was
@@ -215,12 +215,12 @@ def main():
             "data": "synthetic (uniform 16 B keys k%015d / 100 B splitmix64 values, blocks built on GPU by "
                     "the codec's encoder; identity round trip verified)",
             "config": {"workload": "config2: batch decode+re-encode of 65536 x 4188 B device-resident "
-                                   "blocks per GPU (28 PUTs each), fused rt_fast_kernel",
+                                   "blocks per GPU (28 PUTs each), fused rt_kernel",
                        "blocks_per_gpu": nb, "block_bytes": BLOCK_BYTES, "records_per_gpu": nb * PER_BLOCK,
                        "txn_mode": "compat", "parallelism": f"shard{world}"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                         "kernel": "rt_fast_kernel", "alg_bytes_per_launch": alg,
+                         "kernel": "rt_kernel", "alg_bytes_per_launch": alg,
                          "launch_ms_events": round(launch_ms, 5)},
         }
         if world == 1:

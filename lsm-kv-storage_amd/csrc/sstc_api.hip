@@ -15,9 +15,8 @@
 struct sstc_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
-  uint64_t cap_blocks = 0, cap_records = 0, cap_scan = 0, cap_jump = 0;
-  uint32_t *slow_list = nullptr;            // cap_blocks
-  uint32_t *slow_count = nullptr;           // 1
+  uint64_t cap_records = 0, cap_scan = 0, cap_jump = 0;
+  void *counters = nullptr;                 // 64 B: error counter
   unsigned long long *err_count = nullptr;  // 1
   uint64_t *scan_ws = nullptr;              // cap_scan
   uint64_t *sizes = nullptr;                // cap_records + 1
@@ -71,11 +70,7 @@ int ensure_scan(sstc_ctx *c, uint64_t n) {
   return grow(c, c->scan_ws, c->cap_scan, sstc::scan_workspace_elems(n), "scan workspace");
 }
 
-int ensure_blocks(sstc_ctx *c, uint64_t nb) {
-  int r = grow(c, c->slow_list, c->cap_blocks, nb, "block workspace");
-  if (r) return r;
-  return ensure_scan(c, nb + 1);
-}
+int ensure_blocks(sstc_ctx *c, uint64_t nb) { return ensure_scan(c, nb + 1); }
 
 int ensure_records(sstc_ctx *c, uint64_t nr) {
   uint64_t cap = c->cap_records;
@@ -123,13 +118,13 @@ int sstc_ctx_create(int device, void *stream, sstc_ctx **out) {
     delete c;
     return r;
   }
-  if (hipMalloc(reinterpret_cast<void **>(&c->slow_count), 64) != hipSuccess) {
+  if (hipMalloc(&c->counters, 64) != hipSuccess) {
     delete c;
     return fail(SSTC_E_NOMEM, "context counters");
   }
-  c->err_count = reinterpret_cast<unsigned long long *>(reinterpret_cast<char *>(c->slow_count) + 8);
-  if (hipMemset(c->slow_count, 0, 64) != hipSuccess) {
-    (void)hipFree(c->slow_count);
+  c->err_count = static_cast<unsigned long long *>(c->counters);
+  if (hipMemset(c->counters, 0, 64) != hipSuccess) {
+    (void)hipFree(c->counters);
     delete c;
     return fail(SSTC_E_HIP, "context counters");
   }
@@ -141,7 +136,7 @@ int sstc_ctx_destroy(sstc_ctx *c) {
   if (!c) return SSTC_OK;
   bind_device(c);
   (void)hipStreamSynchronize(c->stream);
-  for (void *p : {static_cast<void *>(c->slow_list), static_cast<void *>(c->slow_count),
+  for (void *p : {c->counters,
                   static_cast<void *>(c->scan_ws), static_cast<void *>(c->sizes),
                   static_cast<void *>(c->P), static_cast<void *>(c->jump)})
     if (p) (void)hipFree(p);
@@ -250,9 +245,8 @@ int sstc_roundtrip_blocks(sstc_ctx *c, const uint8_t *d_src, uint8_t *d_dst,
   if (txn_mode > SSTC_TXN_CORRECT) return fail(SSTC_E_INVALID_ARG, "bad txn_mode");
   if (nblocks >= 0xFFFFFFFFull) return fail(SSTC_E_INVALID_ARG, "too many blocks for one call");
   if (int r = bind_device(c)) return r;
-  if (int r = ensure_blocks(c, nblocks)) return r;
   sstc::RtArgs a{d_src, d_dst, d_blk_off, d_blk_len, nblocks, txn_mode, d_out_blk_len, d_block_status,
-                 c->slow_list, c->slow_count, c->err_count};
+                 c->err_count};
   SSTC_HIP(sstc::launch_roundtrip(a, c->stream), "roundtrip kernels");
   return SSTC_OK;
 }

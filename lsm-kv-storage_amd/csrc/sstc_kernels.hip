@@ -1,13 +1,11 @@
 // sstc_kernels.hip — CDNA4 (gfx950) kernels of the SST block codec.
 //
 // Kernels (each cites the reference function whose byte work it replaces):
-//   rt_fast_kernel      fused decode -> re-encode, one wave per block staged in
-//                       LDS by LDS-DMA (global_load_lds_dwordx4).  Handles every
-//                       block that fits a wave slot and whose entries are packed
-//                       back-to-back (every block the reference writes).
-//   rt_generic_kernel   same contract for the blocks the fast kernel defers
-//                       (larger than a slot, or entries not packed): one
-//                       workgroup per block, fields read straight from HBM.
+//   rt_kernel           fused decode -> re-encode, one wave per block; small
+//                       blocks staged in LDS by LDS-DMA (global_load_lds_dwordx4),
+//                       large ones parsed from HBM and streamed through the
+//                       wave's LDS slot (replaces the per-block work of
+//                       db/compact.cc:254-302 on surviving records).
 //   count_kernel        per-block entry count from the 16 B extra
 //                       (TableReader::CreateAndSetupDataForBlockReader,
 //                       sstable/table_reader.cc:226-232).
@@ -102,12 +100,164 @@ __device__ __forceinline__ uint32_t check_extra(uint64_t len, uint64_t n, uint64
 }
 
 // ---------------------------------------------------------------------------
-// Fused round trip, fast path: one wave per block.
+// Fused round trip: ONE kernel, one wave per block, every block size.
+//
+//   1. a block that fits the wave's LDS slot is staged whole by LDS-DMA
+//      (global_load_lds_dwordx4, 1 KiB per wave instruction); a larger block is
+//      parsed straight from HBM and later streamed through the slot in windows;
+//   2. decode: 16 B extra, then entries 64 per round (one lane per entry),
+//      validated exactly like the oracle; a wave-wide scan of the recomputed
+//      entry sizes gives each entry's re-encoded start;
+//   3. re-encode.  When the starts equal the stored starts (entries packed
+//      back-to-back: every block the reference writes) each entry's encoding
+//      of its decoded fields already sits at its output position, except the
+//      txn the compat reader rewrites, so the block is re-emitted from the
+//      staged bytes with the offset section, the extra and those txns
+//      regenerated.  Otherwise (entries out of order / gaps, valid for the
+//      reference reader) the wave re-packs the entries one output byte at a
+//      time (rare, malformed-ish input).
 // ---------------------------------------------------------------------------
 constexpr uint32_t kRtWaves = 4;
-constexpr uint32_t kRtSlot = kRtSlotBytes; // bytes of LDS per wave
+constexpr uint32_t kRtSlot = kRtSlotBytes;     // LDS bytes per wave
+constexpr uint32_t kRtWinChunks = 256;         // 16 B chunks per streaming window
 
-__global__ __launch_bounds__(kRtWaves *kWave) void rt_fast_kernel(RtArgs a) {
+struct Pass1 {
+  uint32_t st;
+  bool canon;
+  bool quirk; // some entry gets its txn rewritten (compat mode)
+  uint64_t data; // sum of recomputed entry sizes
+};
+
+template <class R>
+__device__ __forceinline__ Pass1 rt_pass1(const R &rd, uint64_t L, uint64_t n, uint64_t doff,
+                                          uint32_t txn_mode) {
+  Pass1 p{kBlkOk, doff + 16 * n + 16 == L, false, 0};
+  const uint32_t lane = lane_id();
+  for (uint64_t i0 = 0; i0 < n; i0 += kWave) {
+    const uint64_t i = i0 + lane;
+    Entry e{};
+    uint64_t s = 0;
+    if (i < n) {
+      s = rd.u64(doff + 16 * i);
+      e = parse_entry(rd, s, doff, txn_mode);
+    }
+    const uint64_t bad = __ballot(e.code != kBlkOk);
+    if (bad) {
+      p.st = __shfl(e.code, __ffsll(static_cast<long long>(bad)) - 1, kWave);
+      return p;
+    }
+    const uint64_t incl = wave_incl_scan_u64(e.size);
+    const bool mism = i < n && s != p.data + incl - e.size;
+    p.canon = p.canon && !__any(mism);
+    p.quirk = p.quirk || __any(i < n && txn_mode == 0u && e.type != kTypeDeleted && e.vlen == 0u);
+    p.data += __shfl(incl, kWave - 1, kWave);
+  }
+  p.canon = p.canon && p.data == doff;
+  return p;
+}
+
+// LDS image byte writes of a 64-bit little-endian value clipped to [lo, hi)
+// (positions relative to the image).
+__device__ __forceinline__ void img_put64_clipped(uint8_t *img, int64_t pos, uint64_t v, int64_t lo,
+                                                  int64_t hi) {
+  if (pos >= lo && pos + 8 <= hi && ((pos & 3) == 0)) {
+    uint32_t *w = reinterpret_cast<uint32_t *>(img + pos);
+    w[0] = static_cast<uint32_t>(v);
+    w[1] = static_cast<uint32_t>(v >> 32);
+    return;
+  }
+  for (int j = 0; j < 8; j++)
+    if (pos + j >= lo && pos + j < hi) img[pos + j] = static_cast<uint8_t>(v >> (8 * j));
+}
+
+__device__ __forceinline__ void g_put64_bytes(uint8_t *p, uint64_t v) {
+  for (int j = 0; j < 8; j++) p[j] = static_cast<uint8_t>(v >> (8 * j));
+}
+
+// Store image bytes [c0*16, (c0+cnt)*16) to gd at the same positions; only the
+// bytes in [keep_lo, keep_hi) belong to this block (edge chunks are shared
+// with the neighbouring blocks and are written byte by byte).
+__device__ __forceinline__ void store_window(const uint8_t *img, uint8_t *gd, uint32_t cnt, int64_t base,
+                                             int64_t keep_lo, int64_t keep_hi) {
+  const uint32_t lane = lane_id();
+  for (uint32_t c0 = 0; c0 < cnt; c0 += kWave) {
+    const uint32_t c = c0 + lane;
+    if (c >= cnt) continue;
+    const int64_t lo = base + 16 * static_cast<int64_t>(c);
+    if (lo >= keep_lo && lo + 16 <= keep_hi) {
+      const u32x4 v = *reinterpret_cast<const u32x4 *>(img + 16 * c);
+      __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(gd + lo));
+    } else {
+      const int64_t x0 = lo < keep_lo ? keep_lo : lo;
+      const int64_t x1 = lo + 16 < keep_hi ? lo + 16 : keep_hi;
+      for (int64_t x = x0; x < x1; x++) gd[x] = img[x - base];
+    }
+  }
+}
+
+// Non-packed block: re-pack entries into dst (byte-granular, global memory).
+__device__ void rt_repack_wave(const RtArgs &a, const uint8_t *blk, uint8_t *out, uint64_t n, uint64_t doff,
+                               uint64_t data, uint8_t *slot) {
+  const uint32_t lane = lane_id();
+  const GlobalReader rd{blk};
+  uint64_t *s_src = reinterpret_cast<uint64_t *>(slot);          // 64 x 8
+  uint64_t *s_out = s_src + kWave;                              // 64 x 8
+  uint64_t *s_txn = s_out + kWave;                              // 64 x 8
+  uint32_t *s_kl = reinterpret_cast<uint32_t *>(s_txn + kWave); // 64 x 4
+  uint32_t *s_pt = s_kl + kWave;                                // 64 x 4
+  uint64_t carry = 0;
+  for (uint64_t i0 = 0; i0 < n; i0 += kWave) {
+    const uint64_t i = i0 + lane;
+    Entry e{};
+    uint64_t s = 0;
+    if (i < n) {
+      s = rd.u64(doff + 16 * i);
+      e = parse_entry(rd, s, doff, a.txn_mode);
+    }
+    const uint64_t incl = wave_incl_scan_u64(e.size);
+    const uint64_t o = carry + incl - e.size;
+    if (i < n) {
+      s_src[lane] = s;
+      s_out[lane] = o;
+      s_txn[lane] = e.txn;
+      s_kl[lane] = e.klen;
+      s_pt[lane] = (a.txn_mode == 0u && e.type != kTypeDeleted && e.vlen == 0u) ? 1u : 0u;
+      g_put64_bytes(out + data + 16 * i, o);
+      g_put64_bytes(out + data + 16 * i + 8, e.size);
+    }
+    wave_lds_sync();
+    const uint64_t tot = __shfl(incl, kWave - 1, kWave);
+    const uint32_t wn = static_cast<uint32_t>(n - i0 < kWave ? n - i0 : kWave);
+    for (uint64_t x = carry + lane; x < carry + tot; x += kWave) {
+      uint32_t lo = 0, hi = wn - 1;
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        if (s_out[mid] <= x) lo = mid;
+        else hi = mid - 1;
+      }
+      const uint64_t rel = x - s_out[lo];
+      const uint64_t t0 = 9ull + s_kl[lo];
+      out[x] = (s_pt[lo] && rel >= t0 && rel < t0 + 8) ? static_cast<uint8_t>(s_txn[lo] >> (8 * (rel - t0)))
+                                                        : blk[s_src[lo] + rel];
+    }
+    wave_lds_sync();
+    carry += tot;
+  }
+  if (lane == 0) {
+    g_put64_bytes(out + data + 16 * n, n);
+    g_put64_bytes(out + data + 16 * n + 8, data);
+  }
+}
+
+__device__ __forceinline__ void rt_report(const RtArgs &a, uint64_t b, uint32_t st, uint64_t out_len) {
+  if (lane_id() == 0) {
+    if (a.status) a.status[b] = st;
+    if (a.out_len) a.out_len[b] = st == kBlkOk ? out_len : 0;
+    if (st != kBlkOk) atomicAdd(a.err_count, 1ull);
+  }
+}
+
+__global__ __launch_bounds__(kRtWaves *kWave, 8) void rt_kernel(RtArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kRtWaves * kRtSlot];
   const uint32_t wave = uniform(threadIdx.x / kWave);
   const uint32_t lane = lane_id();
@@ -118,265 +268,134 @@ __global__ __launch_bounds__(kRtWaves *kWave) void rt_fast_kernel(RtArgs a) {
   const uint64_t off = uniform64(a.blk_off[b]);
   const uint64_t len = uniform64(a.blk_len[b]);
   const uint32_t pad = static_cast<uint32_t>(off & 15u);
-  if (len < 16 || len + pad + 16 > kRtSlot) { // not for this path
-    if (lane == 0) a.slow_list[atomicAdd(a.slow_count, 1u)] = static_cast<uint32_t>(b);
-    return;
-  }
+  if (len < 16) return rt_report(a, b, kBlkTooSmall, 0);
+  if (len >= (1ull << 32)) return rt_report(a, b, kBlkTooLarge, 0);
   const uint32_t L = static_cast<uint32_t>(len);
-
-  // ---- stage [off & ~15, off + len) into LDS: 16 B per lane, 1 KiB per wave
-  //      instruction, LDS destination = wave-uniform base + lane * 16.
-  const uint32_t nchunk = (pad + L + 15u) >> 4;
   const uint8_t *g = a.src + (off - pad);
-  for (uint32_t c0 = 0; c0 < nchunk; c0 += kWave) {
-    const uint32_t c = c0 + lane;
-    if (c < nchunk)
-      __builtin_amdgcn_global_load_lds((gbl_void_t *)(g + 16u * c), (lds_void_t *)(img + 16u * c0),
-                                       16, 0, 0);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  uint8_t *gd = a.dst + (off - pad);
+  const uint32_t nchunk = (pad + L + 15u) >> 4;
 
-  // ---- decode: extra, then entries 64 at a time
-  const LdsReader rd{img + pad};
-  const uint64_t n64 = rd.u64(L - 16);
-  const uint64_t doff64 = rd.u64(L - 8);
-  uint32_t st = check_extra(L, n64, doff64);
-  const uint32_t n = static_cast<uint32_t>(n64);
-  const uint32_t doff = static_cast<uint32_t>(doff64);
-  // in-place re-encode needs the exact packed layout
-  bool canon = st == kBlkOk && static_cast<uint64_t>(doff) + 16ull * n + 16 == L;
-  uint32_t carry = 0;
-  if (st == kBlkOk) {
-    for (uint32_t i0 = 0; i0 < n; i0 += kWave) {
+  if (pad + L + 16 <= kRtSlot) {
+    // ------------------------------------------------ small block, staged
+    for (uint32_t c0 = 0; c0 < nchunk; c0 += kWave) {
+      const uint32_t c = c0 + lane;
+      if (c < nchunk)
+        __builtin_amdgcn_global_load_lds((gbl_void_t *)(g + 16u * c), (lds_void_t *)(img + 16u * c0), 16,
+                                         0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const LdsReader rd{img + pad};
+    const uint64_t n = uniform64(rd.u64(L - 16));
+    const uint64_t doff = uniform64(rd.u64(L - 8));
+    uint32_t st = check_extra(L, n, doff);
+    if (st != kBlkOk) return rt_report(a, b, st, 0);
+    const Pass1 p = rt_pass1(rd, L, n, doff, a.txn_mode);
+    if (p.st != kBlkOk) return rt_report(a, b, p.st, 0);
+    if (!p.canon) {
+      const uint64_t out_len = p.data + 16 * n + 16;
+      if (out_len > L) return rt_report(a, b, kBlkNoRoom, 0);
+      rt_repack_wave(a, a.src + off, a.dst + off, n, doff, p.data, img);
+      return rt_report(a, b, kBlkOk, out_len);
+    }
+    // re-encode in place: offset section (start, size) from the scan, extra,
+    // compat txns
+    uint8_t *wimg = img + pad;
+    const uint32_t nn = static_cast<uint32_t>(n), dd = static_cast<uint32_t>(doff);
+    uint32_t carry = 0;
+    for (uint32_t i0 = 0; i0 < nn; i0 += kWave) {
       const uint32_t i = i0 + lane;
+      uint32_t sz = 0;
       Entry e{};
       uint64_t s = 0;
-      if (i < n) {
-        s = rd.u64(doff + 16ull * i);
+      if (i < nn) {
+        s = rd.u64(dd + 16ull * i);
         e = parse_entry(rd, s, doff, a.txn_mode);
+        sz = static_cast<uint32_t>(e.size);
       }
-      const uint64_t bad = __ballot(e.code != kBlkOk);
-      if (bad) {
-        st = __shfl(e.code, __ffsll(static_cast<long long>(bad)) - 1, kWave);
-        break;
-      }
-      const uint32_t sz = static_cast<uint32_t>(e.size);
       const uint32_t incl = wave_incl_scan_u32(sz);
-      const bool mism = i < n && s != static_cast<uint64_t>(carry + incl - sz);
-      canon = canon && !__any(mism);
+      if (i < nn) {
+        lds_st_u64u(wimg, dd + 16u * i, carry + incl - sz);
+        lds_st_u64u(wimg, dd + 16u * i + 8u, sz);
+        if (p.quirk && e.type != kTypeDeleted && e.vlen == 0u)
+          lds_st_u64u(wimg, static_cast<uint32_t>(s) + 9u + e.klen, e.txn);
+      }
       carry += __shfl(incl, kWave - 1, kWave);
     }
-  }
-  if (st != kBlkOk) {
     if (lane == 0) {
-      if (a.status) a.status[b] = st;
-      if (a.out_len) a.out_len[b] = 0;
-      atomicAdd(a.err_count, 1ull);
+      lds_st_u64u(wimg, L - 16, n);
+      lds_st_u64u(wimg, L - 8, carry);
     }
-    return;
-  }
-  if (!canon || carry != doff) { // valid but not packed: generic path re-encodes it
-    if (lane == 0) a.slow_list[atomicAdd(a.slow_count, 1u)] = static_cast<uint32_t>(b);
-    return;
+    wave_lds_sync();
+    store_window(img, gd, nchunk, 0, pad, pad + L);
+    return rt_report(a, b, kBlkOk, L);
   }
 
-  // ---- re-encode in place.  Entries stay where they are (starts == scan of
-  //      recomputed sizes), so each entry's encoding of its decoded fields is
-  //      already in the image except the txn rewritten by the compat reader;
-  //      the offset section and the extra are regenerated from the scan.
-  uint8_t *wimg = img + pad;
-  carry = 0;
-  for (uint32_t i0 = 0; i0 < n; i0 += kWave) {
-    const uint32_t i = i0 + lane;
-    uint32_t sz = 0;
-    uint64_t s = 0;
-    Entry e{};
-    if (i < n) {
-      s = rd.u64(doff + 16ull * i);
-      e = parse_entry(rd, s, doff, a.txn_mode);
-      sz = static_cast<uint32_t>(e.size);
+  // -------------------------------------------------- large block, streamed
+  const uint8_t *blk = a.src + off;
+  const GlobalReader rd{blk};
+  const uint64_t n = uniform64(rd.u64(L - 16));
+  const uint64_t doff = uniform64(rd.u64(L - 8));
+  uint32_t st = check_extra(L, n, doff);
+  if (st != kBlkOk) return rt_report(a, b, st, 0);
+  const Pass1 p = rt_pass1(rd, L, n, doff, a.txn_mode);
+  if (p.st != kBlkOk) return rt_report(a, b, p.st, 0);
+  if (!p.canon) {
+    const uint64_t out_len = p.data + 16 * n + 16;
+    if (out_len > L) return rt_report(a, b, kBlkNoRoom, 0);
+    rt_repack_wave(a, blk, a.dst + off, n, doff, p.data, img);
+    return rt_report(a, b, kBlkOk, out_len);
+  }
+  const int64_t ob = static_cast<int64_t>(doff);           // offset section start (block-relative)
+  const int64_t oe = ob + 16 * static_cast<int64_t>(n);    // its end == L - 16
+  for (uint32_t w = 0; w < nchunk; w += kRtWinChunks) {
+    const uint32_t cnt = nchunk - w < kRtWinChunks ? nchunk - w : kRtWinChunks;
+    for (uint32_t c0 = 0; c0 < cnt; c0 += kWave) {
+      const uint32_t c = c0 + lane;
+      if (c < cnt)
+        __builtin_amdgcn_global_load_lds((gbl_void_t *)(g + 16u * (w + c)), (lds_void_t *)(img + 16u * c0), 16,
+                                         0, 0);
     }
-    const uint32_t incl = wave_incl_scan_u32(sz);
-    if (i < n) {
-      const uint32_t start = carry + incl - sz;
-      lds_st_u64u(wimg, doff + 16u * i, start);
-      lds_st_u64u(wimg, doff + 16u * i + 8u, sz);
-      if (a.txn_mode == 0u && e.type != kTypeDeleted && e.vlen == 0u)
-        lds_st_u64u(wimg, static_cast<uint32_t>(s) + 9u + e.klen, e.txn);
-    }
-    carry += __shfl(incl, kWave - 1, kWave);
-  }
-  if (lane == 0) {
-    lds_st_u64u(wimg, L - 16, n);
-    lds_st_u64u(wimg, L - 8, carry);
-  }
-  wave_lds_sync();
-
-  // ---- write back: whole 16 B chunks with dwordx4 stores; the two edge chunks
-  //      (shared with the neighbouring blocks) byte by byte.
-  uint8_t *gd = a.dst + (off - pad);
-  for (uint32_t c0 = 0; c0 < nchunk; c0 += kWave) {
-    const uint32_t c = c0 + lane;
-    if (c >= nchunk) continue;
-    const uint32_t lo = 16u * c;
-    if (lo >= pad && lo + 16u <= pad + L) {
-      const u32x4 v = *reinterpret_cast<const u32x4 *>(img + lo);
-      __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(gd + lo));
-    } else {
-      const uint32_t x0 = lo < pad ? pad : lo;
-      const uint32_t x1 = lo + 16u < pad + L ? lo + 16u : pad + L;
-      for (uint32_t x = x0; x < x1; x++) gd[x] = img[x];
-    }
-  }
-  if (lane == 0) {
-    if (a.status) a.status[b] = kBlkOk;
-    if (a.out_len) a.out_len[b] = L;
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Generic round trip: one 256-thread workgroup per deferred block, entries in
-// windows of 256.  Pass 1 validates everything (a failing block is left
-// untouched), pass 2 emits.  Each output entry is the input entry's bytes at
-// its new (packed) position with the decoded txn re-applied; offset section and
-// extra are regenerated.
-// ---------------------------------------------------------------------------
-constexpr uint32_t kGenThreads = 256;
-
-__device__ __forceinline__ uint64_t block_excl_scan_u64(uint64_t v, uint64_t *sm, uint64_t &total) {
-  // sm: kGenThreads/64 + 1 slots
-  const uint32_t tid = threadIdx.x, lane = lane_id(), w = tid / kWave;
-  const uint64_t incl = wave_incl_scan_u64(v);
-  if (lane == kWave - 1) sm[w] = incl;
-  __syncthreads();
-  uint64_t base = 0, tot = 0;
-#pragma unroll
-  for (uint32_t k = 0; k < kGenThreads / kWave; k++) {
-    const uint64_t x = sm[k];
-    if (k < w) base += x;
-    tot += x;
-  }
-  __syncthreads();
-  total = tot;
-  return base + incl - v;
-}
-
-__global__ __launch_bounds__(kGenThreads) void rt_generic_kernel(RtArgs a) {
-  __shared__ uint64_t s_src[kGenThreads]; // input entry start
-  __shared__ uint64_t s_out[kGenThreads]; // output entry start
-  __shared__ uint64_t s_txn[kGenThreads];
-  __shared__ uint32_t s_patch[kGenThreads]; // 1 = compat txn rewrite
-  __shared__ uint32_t s_klen[kGenThreads];
-  __shared__ uint64_t s_red[kGenThreads / kWave + 1];
-  __shared__ uint32_t s_err;
-
-  const uint32_t cnt = *a.slow_count;
-  const uint32_t tid = threadIdx.x;
-  for (uint32_t item = blockIdx.x; item < cnt; item += gridDim.x) {
-    const uint64_t b = a.slow_list[item];
-    const uint64_t off = a.blk_off[b], len = a.blk_len[b];
-    const uint8_t *blk = a.src + off;
-    const GlobalReader rd{blk};
-    uint32_t st = kBlkOk;
-    uint64_t n = 0, doff = 0;
-    if (len < 16) {
-      st = kBlkTooSmall;
-    } else {
-      n = rd.u64(len - 16);
-      doff = rd.u64(len - 8);
-      st = check_extra(len, n, doff);
-    }
-    // pass 1: validate all entries, total data bytes
-    uint64_t data = 0;
-    if (st == kBlkOk) {
-      for (uint64_t w0 = 0; w0 < n; w0 += kGenThreads) {
-        if (tid == 0) s_err = 0xFFFFFFFFu;
-        __syncthreads();
-        const uint64_t i = w0 + tid;
-        uint64_t sz = 0;
-        if (i < n) {
-          const Entry e = parse_entry(rd, rd.u64(doff + 16 * i), doff, a.txn_mode);
-          if (e.code != kBlkOk) atomicMin(&s_err, (tid << 8) | e.code);
-          sz = e.size;
-        }
-        uint64_t tot;
-        block_excl_scan_u64(sz, s_red, tot);
-        data += tot;
-        const uint32_t err = s_err;
-        __syncthreads();
-        if (err != 0xFFFFFFFFu) {
-          st = err & 0xFFu;
-          break;
-        }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // window = block bytes [wlo, whi); image byte 0 == block byte wlo
+    const int64_t wlo = 16 * static_cast<int64_t>(w) - pad;
+    const int64_t whi = wlo + 16 * static_cast<int64_t>(cnt);
+    if (whi > ob && wlo < oe) {
+      const int64_t a0 = wlo > ob ? wlo : ob;
+      const int64_t a1 = whi < oe ? whi : oe;
+      const uint64_t i_lo = static_cast<uint64_t>(a0 - ob) >> 4;
+      const uint64_t i_hi = (static_cast<uint64_t>(a1 - ob) + 15) >> 4;
+      for (uint64_t i = i_lo + lane; i < i_hi; i += kWave) {
+        const uint64_t s = rd.u64(doff + 16 * i);
+        const uint64_t s1 = i + 1 < n ? rd.u64(doff + 16 * (i + 1)) : doff; // packed: size = next start - start
+        const int64_t pos = ob + 16 * static_cast<int64_t>(i) - wlo;
+        img_put64_clipped(img, pos, s, 0, whi - wlo);
+        img_put64_clipped(img, pos + 8, s1 - s, 0, whi - wlo);
       }
     }
-    const uint64_t out_len = data + 16 * n + 16;
-    if (st == kBlkOk && out_len >= (1ull << 32)) st = kBlkTooLarge;
-    if (st == kBlkOk && out_len > len) st = kBlkNoRoom; // written in place of the input block
-    if (st != kBlkOk) {
-      if (tid == 0) {
-        if (a.status) a.status[b] = st;
-        if (a.out_len) a.out_len[b] = 0;
-        atomicAdd(a.err_count, 1ull);
-      }
-      continue;
+    if (lane == 0 && whi > oe) {
+      img_put64_clipped(img, oe - wlo, n, 0, whi - wlo);
+      img_put64_clipped(img, oe + 8 - wlo, doff, 0, whi - wlo);
     }
+    wave_lds_sync();
+    store_window(img, gd, cnt, 16 * static_cast<int64_t>(w), pad, pad + static_cast<int64_t>(L));
+    wave_lds_sync();
+  }
+  if (p.quirk) {
+    // compat txn rewrites after every bulk store of this wave has landed
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     uint8_t *out = a.dst + off;
-    // pass 2: emit entries window by window
-    uint64_t carry = 0;
-    for (uint64_t w0 = 0; w0 < n; w0 += kGenThreads) {
-      const uint64_t i = w0 + tid;
-      uint64_t sz = 0;
+    for (uint64_t i0 = 0; i0 < n; i0 += kWave) {
+      const uint64_t i = i0 + lane;
       if (i < n) {
         const uint64_t s = rd.u64(doff + 16 * i);
         const Entry e = parse_entry(rd, s, doff, a.txn_mode);
-        sz = e.size;
-        s_src[tid] = s;
-        s_txn[tid] = e.txn;
-        s_klen[tid] = e.klen;
-        s_patch[tid] = (a.txn_mode == 0u && e.type != kTypeDeleted && e.vlen == 0u) ? 1u : 0u;
+        if (e.type != kTypeDeleted && e.vlen == 0u) g_put64_bytes(out + s + 9 + e.klen, e.txn);
       }
-      uint64_t tot;
-      const uint64_t ex = block_excl_scan_u64(sz, s_red, tot);
-      if (i < n) {
-        s_out[tid] = carry + ex;
-        // offset entry (start, size) regenerated
-        const uint64_t oe = data + 16 * i;
-        for (int j = 0; j < 8; j++) out[oe + j] = static_cast<uint8_t>((carry + ex) >> (8 * j));
-        for (int j = 0; j < 8; j++) out[oe + 8 + j] = static_cast<uint8_t>(sz >> (8 * j));
-      }
-      __syncthreads();
-      const uint32_t wn = static_cast<uint32_t>(n - w0 < kGenThreads ? n - w0 : kGenThreads);
-      const uint64_t x_begin = carry, x_end = carry + tot;
-      for (uint64_t x = x_begin + tid; x < x_end; x += kGenThreads) {
-        // entry r of this window holding output byte x
-        uint32_t lo = 0, hi = wn - 1;
-        while (lo < hi) {
-          const uint32_t mid = (lo + hi + 1) >> 1;
-          if (s_out[mid] <= x) lo = mid;
-          else hi = mid - 1;
-        }
-        const uint64_t rel = x - s_out[lo];
-        uint8_t v;
-        const uint64_t tx0 = 9ull + s_klen[lo];
-        if (s_patch[lo] && rel >= tx0 && rel < tx0 + 8)
-          v = static_cast<uint8_t>(s_txn[lo] >> (8 * (rel - tx0)));
-        else
-          v = blk[s_src[lo] + rel];
-        out[x] = v;
-      }
-      carry += tot;
-      __syncthreads();
-    }
-    if (tid == 0) {
-      const uint64_t oe = data + 16 * n;
-      for (int j = 0; j < 8; j++) out[oe + j] = static_cast<uint8_t>(n >> (8 * j));
-      for (int j = 0; j < 8; j++) out[oe + 8 + j] = static_cast<uint8_t>(data >> (8 * j));
-      if (a.status) a.status[b] = kBlkOk;
-      if (a.out_len) a.out_len[b] = out_len;
     }
   }
+  return rt_report(a, b, kBlkOk, L);
 }
+
 
 // ---------------------------------------------------------------------------
 // Decode to the record table.
@@ -690,13 +709,7 @@ __global__ __launch_bounds__(kScanThreads) void scan_apply_kernel(const uint64_t
 static inline uint32_t grid_for(uint64_t n, uint32_t per) { return static_cast<uint32_t>((n + per - 1) / per); }
 
 hipError_t launch_roundtrip(const RtArgs &a, hipStream_t s) {
-  hipError_t e = hipMemsetAsync(a.slow_count, 0, sizeof(uint32_t), s);
-  if (e != hipSuccess) return e;
-  if (a.nblocks) rt_fast_kernel<<<grid_for(a.nblocks, kRtWaves), kRtWaves * kWave, 0, s>>>(a);
-  // deferred blocks are few for reference-written input: one persistent
-  // workgroup per CU walks the list
-  const uint32_t g = static_cast<uint32_t>(a.nblocks < 256 ? (a.nblocks ? a.nblocks : 1) : 256);
-  rt_generic_kernel<<<g, kGenThreads, 0, s>>>(a);
+  if (a.nblocks) rt_kernel<<<grid_for(a.nblocks, kRtWaves), kRtWaves * kWave, 0, s>>>(a);
   return hipGetLastError();
 }
 

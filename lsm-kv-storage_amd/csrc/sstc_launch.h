@@ -19,8 +19,6 @@ struct RtArgs {
   uint32_t txn_mode;
   uint64_t *out_len;   // may be null
   uint32_t *status;    // may be null
-  uint32_t *slow_list; // nblocks entries (workspace)
-  uint32_t *slow_count;
   unsigned long long *err_count;
 };
 

@@ -302,3 +302,33 @@ def test_decode_count_mismatch(codec):
     torch.cuda.synchronize()
     st = status.cpu().numpy()[: len(g["blk_off"])]
     assert st[0] == 9 and (st[1:] == 0).all()
+
+
+def test_roundtrip_large_blocks_streamed(codec, oracle):
+    """Blocks larger than a wave's LDS slot (streamed path): 1-entry 64 KiB
+    values, and 32 KiB-threshold blocks of small entries (offset section spans
+    several windows), including compat txn rewrites in a large block."""
+    items = []
+    rng = np.random.default_rng(3)
+    for i in range(12):
+        items.append((0, b"big%03d" % i, rng.integers(0, 256, int(rng.integers(5000, 70000)), dtype=np.uint8).tobytes(), 10 + i))
+    rec_big = _records(items)
+    first_big = np.arange(0, 13, dtype=np.uint64)
+    small = W.mixed_records(3000, seed=77, max_val=40, p_empty_val=0.2, p_delete=0.2)
+    first_small = oracle.segment(small, 32768)
+    for rec, first in ((rec_big, first_big), (small, first_small)):
+        src, offs, lens = oracle.encode_blocks(rec, first, base=3)
+        src = np.concatenate([np.zeros(3, np.uint8), src, np.zeros(1, np.uint8)])
+        assert lens.max() > 4608
+        for mode in (0, 1):
+            got = run_roundtrip(codec, src, offs, lens, mode, dst_fill=0x5C)
+            want = oracle_rt(oracle, src, offs, lens, mode, dst_fill=0x5C)
+            assert (got[2] == 0).all()
+            assert np.array_equal(got[1], want[1]) and np.array_equal(got[0], want[0])
+
+
+def _records(items):
+    import sys
+    sys.path.insert(0, __import__("os").path.join(__import__("conftest").ROOT, "tests", "golden"))
+    from make_golden import records_from_list
+    return records_from_list(items)
