@@ -57,8 +57,9 @@ def build(verbose=False):
             continue
         o = os.path.join(LIB, "obj", os.path.basename(src) + ".o")
         if _newer(o, [s] + headers + [h for h in host_headers if os.path.exists(h)]):
-            cmd = [hipcc, "-O2", "-std=c++17", "-fPIC", "-Wall", "-x", "c++",
-                   "-I" + os.path.join(ROOT, "include"), "-c", s, "-o", o]
+            rocm = os.path.dirname(os.path.dirname(os.path.realpath(hipcc)))
+            cmd = [os.environ.get("CXX", "g++"), "-O2", "-std=c++17", "-fPIC", "-Wall", "-D__HIP_PLATFORM_AMD__",
+                   "-I" + os.path.join(rocm, "include"), "-I" + os.path.join(ROOT, "include"), "-c", s, "-o", o]
             if verbose:
                 print(" ".join(cmd))
             subprocess.run(cmd, check=True)

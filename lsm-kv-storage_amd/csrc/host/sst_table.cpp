@@ -1,0 +1,423 @@
+// sst_table.cpp — host C++ mirror of the reference TableBuilder / TableReader
+// over the codec C-ABI.  See include/sstc_table.h.
+//
+// Byte work (block serialisation, block parse) happens in the GPU kernels via
+// sstc_encode_blocks / sstc_count_records / sstc_decode_blocks.  What stays on
+// the host is what the reference does per block or per table, not per byte:
+// block boundaries (a running sum per AddEntry), the meta section (one entry per
+// block), the 40 B footer, and the file I/O.
+#include "sstc_table.h"
+
+#include <fcntl.h>
+#include <hip/hip_runtime_api.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <cerrno>
+#include <cstring>
+#include <memory>
+#include <stdexcept>
+
+namespace sstc {
+namespace {
+
+uint64_t entry_size(uint32_t klen, uint32_t vlen) {
+  return 13ull + klen + (vlen != SSTC_NO_VALUE ? 4ull + vlen : 0ull); // block_builder.cc:19-21
+}
+
+void put32(std::vector<uint8_t> &b, uint32_t v) {
+  const uint8_t *p = reinterpret_cast<const uint8_t *>(&v);
+  b.insert(b.end(), p, p + 4);
+}
+void put64(std::vector<uint8_t> &b, uint64_t v) {
+  const uint8_t *p = reinterpret_cast<const uint8_t *>(&v);
+  b.insert(b.end(), p, p + 8);
+}
+uint32_t get32(const uint8_t *p) {
+  uint32_t v;
+  std::memcpy(&v, p, 4);
+  return v;
+}
+uint64_t get64(const uint8_t *p) {
+  uint64_t v;
+  std::memcpy(&v, p, 8);
+  return v;
+}
+
+bool pwrite_all(int fd, const uint8_t *buf, size_t size, uint64_t off) {
+  while (size > 0) { // io/linux_file.cc:138-157 semantics: retry on EINTR
+    ssize_t w = ::pwrite64(fd, buf, size, static_cast<off64_t>(off));
+    if (w < 0) {
+      if (errno == EINTR) continue;
+      return false;
+    }
+    buf += w;
+    size -= static_cast<size_t>(w);
+    off += static_cast<uint64_t>(w);
+  }
+  return true;
+}
+
+bool pread_all(int fd, uint8_t *buf, size_t size, uint64_t off) {
+  while (size > 0) {
+    ssize_t r = ::pread(fd, buf, size, static_cast<off64_t>(off));
+    if (r < 0) {
+      if (errno == EINTR) continue;
+      return false;
+    }
+    if (r == 0) return false;
+    buf += r;
+    size -= static_cast<size_t>(r);
+    off += static_cast<uint64_t>(r);
+  }
+  return true;
+}
+
+// RAII device buffer
+struct DevBuf {
+  void *p = nullptr;
+  explicit DevBuf(size_t n) {
+    if (hipMalloc(&p, n ? n : 16) != hipSuccess) throw std::runtime_error("hipMalloc failed");
+  }
+  ~DevBuf() {
+    if (p) (void)hipFree(p);
+  }
+  template <class T> T *as() const { return static_cast<T *>(p); }
+};
+
+template <class T> DevBuf upload(const std::vector<T> &v) {
+  DevBuf d(v.size() * sizeof(T));
+  if (!v.empty() && hipMemcpy(d.p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice) != hipSuccess)
+    throw std::runtime_error("hipMemcpy H2D failed");
+  return d;
+}
+
+void check(int rc, const char *what) {
+  if (rc != SSTC_OK) throw std::runtime_error(std::string(what) + ": " + sstc_last_error_string());
+}
+
+} // namespace
+
+// ---------------------------------------------------------------- TableBuilder
+TableBuilder::TableBuilder(std::string filename, uint64_t block_threshold, sstc_ctx *ctx)
+    : filename_(std::move(filename)), threshold_(block_threshold), ctx_(ctx) {}
+
+TableBuilder::~TableBuilder() {
+  if (fd_ >= 0) ::close(fd_);
+}
+
+bool TableBuilder::Open() {
+  // io/linux_file.cc:99-119: an existing file is opened WITHOUT O_TRUNC (stale
+  // tail bytes survive a shorter rewrite); a new one is created.
+  ::chmod(filename_.c_str(), 0644);
+  const bool create = ::access(filename_.c_str(), F_OK) != 0;
+  const int flags = create ? (O_TRUNC | O_WRONLY | O_CREAT) : O_WRONLY;
+  fd_ = ::open(filename_.c_str(), flags, 0644);
+  return fd_ >= 0;
+}
+
+void TableBuilder::AddEntry(std::string_view key, std::string_view value, uint64_t txn_id,
+                            uint8_t value_type) {
+  // table_builder.cc:35-60
+  if (table_smallest_key_.empty()) table_smallest_key_ = std::string(key);
+  type_.push_back(value_type);
+  key_len_.push_back(static_cast<uint32_t>(key.size()));
+  key_off_.push_back(keys_.size());
+  keys_.insert(keys_.end(), key.begin(), key.end());
+  if (value.data()) {
+    val_len_.push_back(static_cast<uint32_t>(value.size()));
+    val_off_.push_back(vals_.size());
+    vals_.insert(vals_.end(), value.begin(), value.end());
+  } else {
+    val_len_.push_back(SSTC_NO_VALUE);
+    val_off_.push_back(0);
+  }
+  txn_.push_back(txn_id);
+  if (txn_id < min_txn_) min_txn_ = txn_id;
+  if (txn_id > max_txn_) max_txn_ = txn_id;
+  table_largest_key_ = std::string(key);
+  data_size_ += key.size() + (value.data() ? value.size() : 0);
+  block_size_ += entry_size(key_len_.back(), val_len_.back()) + 16; // block_builder.cc:33
+  if (block_size_ >= threshold_) FlushBlock();
+}
+
+void TableBuilder::FlushBlock() {
+  if (block_size_ == 0) return; // table_builder.cc:65-68: empty block not written
+  blk_first_.push_back(type_.size());
+  block_size_ = 0;
+}
+
+void TableBuilder::Finish() {
+  if (fd_ < 0) throw std::runtime_error("TableBuilder::Finish: file not open");
+  FlushBlock();
+  const uint64_t n = type_.size();
+  const uint64_t nb = blk_first_.size() - 1;
+  uint64_t data_bytes = 16 * nb + 16 * n;
+  for (uint64_t i = 0; i < n; i++) data_bytes += entry_size(key_len_[i], val_len_[i]);
+
+  std::vector<uint8_t> file(data_bytes);
+  std::vector<uint64_t> blk_off(nb + 1), blk_len(nb);
+  if (nb) {
+    if (keys_.empty()) keys_.push_back(0);
+    if (vals_.empty()) vals_.push_back(0);
+    DevBuf d_type = upload(type_), d_kl = upload(key_len_), d_vl = upload(val_len_), d_txn = upload(txn_),
+           d_ko = upload(key_off_), d_vo = upload(val_off_), d_keys = upload(keys_), d_vals = upload(vals_),
+           d_first = upload(blk_first_);
+    DevBuf d_dst(data_bytes), d_off((nb + 1) * 8), d_len(nb * 8);
+    sstc_records rec{d_type.as<uint8_t>(), d_kl.as<uint32_t>(), d_vl.as<uint32_t>(),
+                     d_txn.as<uint64_t>(), d_ko.as<uint64_t>(), d_vo.as<uint64_t>()};
+    check(sstc_encode_blocks(ctx_, d_keys.as<uint8_t>(), d_vals.as<uint8_t>(), rec, n, d_first.as<uint64_t>(), nb,
+                             0, d_dst.as<uint8_t>(), d_off.as<uint64_t>(), d_len.as<uint64_t>()),
+          "sstc_encode_blocks");
+    uint64_t errs = 0;
+    check(sstc_ctx_error_count(ctx_, &errs), "sstc_ctx_error_count"); // synchronises the stream
+    if (hipMemcpy(file.data(), d_dst.p, data_bytes, hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(blk_off.data(), d_off.p, (nb + 1) * 8, hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(blk_len.data(), d_len.p, nb * 8, hipMemcpyDeviceToHost) != hipSuccess)
+      throw std::runtime_error("hipMemcpy D2H failed");
+  }
+  // meta section: one entry per block (table_builder.cc:101-145)
+  const uint64_t meta_off = data_bytes;
+  for (uint64_t b = 0; b < nb; b++) {
+    const uint64_t f = blk_first_[b], l = blk_first_[b + 1] - 1;
+    put32(file, key_len_[f]);
+    file.insert(file.end(), keys_.begin() + key_off_[f], keys_.begin() + key_off_[f] + key_len_[f]);
+    put32(file, key_len_[l]);
+    file.insert(file.end(), keys_.begin() + key_off_[l], keys_.begin() + key_off_[l] + key_len_[l]);
+    put64(file, blk_off[b]);
+    put64(file, blk_len[b]);
+  }
+  const uint64_t meta_len = file.size() - meta_off;
+  // footer (table_builder.cc:179-211)
+  put64(file, nb);
+  put64(file, meta_off);
+  put64(file, meta_len);
+  put64(file, min_txn_);
+  put64(file, max_txn_);
+  if (!pwrite_all(fd_, file.data(), file.size(), 0))
+    throw std::runtime_error("Error when flushing sstable"); // table_builder.cc:155-170
+  current_offset_ = file.size();
+  if (::fsync(fd_) < 0) throw std::runtime_error("fsync failed");
+}
+
+// ----------------------------------------------------------------- TableReader
+TableReader *TableReader::Open(const std::string &filename, uint64_t file_size, sstc_ctx *ctx) {
+  std::unique_ptr<TableReader> tr(new TableReader());
+  tr->ctx_ = ctx;
+  tr->fd_ = ::open(filename.c_str(), O_RDONLY);
+  if (tr->fd_ < 0 || file_size < 41) return nullptr;
+  tr->bytes_ = file_size - 1;
+  uint8_t foot[40];
+  // DecodeExtraInfo: footer at file_size - 40 - 1 (table_reader.cc:52-84)
+  if (!pread_all(tr->fd_, foot, 40, tr->bytes_ - 40)) return nullptr;
+  const uint64_t nb = get64(foot), moff = get64(foot + 8), mlen = get64(foot + 16);
+  tr->min_txn_ = get64(foot + 24);
+  tr->max_txn_ = get64(foot + 32);
+  if (moff > tr->bytes_ - 40 || mlen > tr->bytes_ - 40 - moff) return nullptr;
+  tr->meta_off_ = moff;
+  std::vector<uint8_t> meta(mlen);
+  if (mlen && !pread_all(tr->fd_, meta.data(), mlen, moff)) return nullptr;
+  // FetchBlockIndexInfo (table_reader.cc:86-156): sequential length-prefixed walk
+  uint64_t p = 0;
+  for (uint64_t i = 0; i < nb; i++) {
+    if (p + 4 > mlen) return nullptr;
+    const uint32_t fk = get32(&meta[p]);
+    if (p + 8 + fk > mlen) return nullptr;
+    const uint32_t lk = get32(&meta[p + 4 + fk]);
+    if (p + 24 + fk + lk > mlen) return nullptr;
+    BlockIndex bi;
+    bi.smallest_key.assign(reinterpret_cast<const char *>(&meta[p + 4]), fk);
+    bi.largest_key.assign(reinterpret_cast<const char *>(&meta[p + 8 + fk]), lk);
+    bi.offset = get64(&meta[p + 8 + fk + lk]);
+    bi.size = get64(&meta[p + 16 + fk + lk]);
+    tr->index_.push_back(std::move(bi));
+    p += 24 + fk + lk;
+  }
+  return tr.release();
+}
+
+TableReader::~TableReader() {
+  if (fd_ >= 0) ::close(fd_);
+}
+
+int TableReader::DecodeAll(uint32_t txn_mode, std::vector<uint8_t> &data, std::vector<uint8_t> &type,
+                           std::vector<uint32_t> &key_len, std::vector<uint32_t> &val_len,
+                           std::vector<uint64_t> &txn, std::vector<uint64_t> &key_off,
+                           std::vector<uint64_t> &val_off) {
+  const uint64_t nb = index_.size();
+  data.resize(meta_off_);
+  if (meta_off_ && !pread_all(fd_, data.data(), meta_off_, 0)) return SSTC_E_INVALID_ARG;
+  std::vector<uint64_t> off(nb), len(nb);
+  for (uint64_t b = 0; b < nb; b++) {
+    off[b] = index_[b].offset;
+    len[b] = index_[b].size;
+    if (off[b] > meta_off_ || len[b] > meta_off_ - off[b]) return SSTC_E_INVALID_ARG;
+  }
+  if (data.empty()) data.push_back(0);
+  DevBuf d_src = upload(data), d_off = upload(off), d_len = upload(len), d_base((nb + 1) * 8),
+         d_status(nb * 4 + 4);
+  check(sstc_count_records(ctx_, d_src.as<uint8_t>(), d_off.as<uint64_t>(), d_len.as<uint64_t>(), nb,
+                           d_base.as<uint64_t>()),
+        "sstc_count_records");
+  uint64_t errs = 0;
+  check(sstc_ctx_error_count(ctx_, &errs), "sync");
+  std::vector<uint64_t> base(nb + 1);
+  if (hipMemcpy(base.data(), d_base.p, (nb + 1) * 8, hipMemcpyDeviceToHost) != hipSuccess) return SSTC_E_HIP;
+  const uint64_t n = base[nb];
+  DevBuf d_type(n + 1), d_kl(4 * n + 4), d_vl(4 * n + 4), d_txn(8 * n + 8), d_ko(8 * n + 8), d_vo(8 * n + 8);
+  sstc_records rec{d_type.as<uint8_t>(), d_kl.as<uint32_t>(), d_vl.as<uint32_t>(),
+                   d_txn.as<uint64_t>(), d_ko.as<uint64_t>(), d_vo.as<uint64_t>()};
+  check(sstc_decode_blocks(ctx_, d_src.as<uint8_t>(), d_off.as<uint64_t>(), d_len.as<uint64_t>(), nb,
+                           d_base.as<uint64_t>(), rec, txn_mode, d_status.as<uint32_t>()),
+        "sstc_decode_blocks");
+  check(sstc_ctx_error_count(ctx_, &errs), "sync");
+  std::vector<uint32_t> status(nb);
+  type.resize(n);
+  key_len.resize(n);
+  val_len.resize(n);
+  txn.resize(n);
+  key_off.resize(n);
+  val_off.resize(n);
+  bool ok = hipMemcpy(status.data(), d_status.p, nb * 4, hipMemcpyDeviceToHost) == hipSuccess;
+  ok = ok && hipMemcpy(type.data(), d_type.p, n, hipMemcpyDeviceToHost) == hipSuccess;
+  ok = ok && hipMemcpy(key_len.data(), d_kl.p, 4 * n, hipMemcpyDeviceToHost) == hipSuccess;
+  ok = ok && hipMemcpy(val_len.data(), d_vl.p, 4 * n, hipMemcpyDeviceToHost) == hipSuccess;
+  ok = ok && hipMemcpy(txn.data(), d_txn.p, 8 * n, hipMemcpyDeviceToHost) == hipSuccess;
+  ok = ok && hipMemcpy(key_off.data(), d_ko.p, 8 * n, hipMemcpyDeviceToHost) == hipSuccess;
+  ok = ok && hipMemcpy(val_off.data(), d_vo.p, 8 * n, hipMemcpyDeviceToHost) == hipSuccess;
+  if (!ok) return SSTC_E_HIP;
+  for (uint64_t b = 0; b < nb; b++)
+    if (status[b] != SSTC_BLK_OK) return static_cast<int>(status[b]);
+  return SSTC_BLK_OK;
+}
+
+} // namespace sstc
+
+// ----------------------------------------------------------------------- C shim
+struct sstc_table_builder {
+  sstc::TableBuilder tb;
+};
+struct sstc_table_reader {
+  std::unique_ptr<sstc::TableReader> tr;
+  uint32_t cached_mode = 0xFFFFFFFFu;
+  std::vector<uint8_t> data, type;
+  std::vector<uint32_t> kl, vl;
+  std::vector<uint64_t> txn, ko, vo;
+  int status = 0;
+};
+
+extern "C" {
+
+int sstc_tb_create(const char *path, uint64_t block_threshold, sstc_ctx *ctx, sstc_table_builder **out) {
+  if (!path || !ctx || !out || block_threshold == 0) return SSTC_E_INVALID_ARG;
+  *out = new sstc_table_builder{sstc::TableBuilder(path, block_threshold, ctx)};
+  return SSTC_OK;
+}
+
+int sstc_tb_open(sstc_table_builder *tb) {
+  if (!tb) return SSTC_E_INVALID_ARG;
+  return tb->tb.Open() ? SSTC_OK : SSTC_E_INVALID_ARG;
+}
+
+int sstc_tb_add(sstc_table_builder *tb, const uint8_t *key, uint32_t key_len, const uint8_t *val,
+                uint32_t val_len, uint64_t txn, uint8_t type) {
+  if (!tb || (!key && key_len)) return SSTC_E_INVALID_ARG;
+  static const char kEmpty[1] = {0};
+  std::string_view k(key ? reinterpret_cast<const char *>(key) : kEmpty, key_len);
+  std::string_view v = val ? std::string_view(reinterpret_cast<const char *>(val), val_len) : std::string_view{};
+  tb->tb.AddEntry(k, v, txn, type);
+  return SSTC_OK;
+}
+
+int sstc_tb_add_batch(sstc_table_builder *tb, uint64_t n, const uint8_t *type, const uint32_t *key_len,
+                      const uint32_t *val_len, const uint64_t *txn, const uint8_t *key_src,
+                      const uint64_t *key_off, const uint8_t *val_src, const uint64_t *val_off) {
+  if (!tb) return SSTC_E_INVALID_ARG;
+  static const char kEmpty[1] = {0};
+  for (uint64_t i = 0; i < n; i++) {
+    std::string_view k(key_len[i] ? reinterpret_cast<const char *>(key_src + key_off[i]) : kEmpty, key_len[i]);
+    std::string_view v;
+    if (val_len[i] != SSTC_NO_VALUE)
+      v = std::string_view(val_len[i] ? reinterpret_cast<const char *>(val_src + val_off[i]) : kEmpty, val_len[i]);
+    tb->tb.AddEntry(k, v, txn[i], type[i]);
+  }
+  return SSTC_OK;
+}
+
+int sstc_tb_finish(sstc_table_builder *tb) {
+  if (!tb) return SSTC_E_INVALID_ARG;
+  try {
+    tb->tb.Finish();
+  } catch (const std::exception &) {
+    return SSTC_E_HIP;
+  }
+  return SSTC_OK;
+}
+
+uint64_t sstc_tb_file_size(const sstc_table_builder *tb) { return tb ? tb->tb.GetFileSize() : 0; }
+uint64_t sstc_tb_num_blocks(const sstc_table_builder *tb) { return tb ? tb->tb.GetNumBlocks() : 0; }
+
+int sstc_tb_destroy(sstc_table_builder *tb) {
+  delete tb;
+  return SSTC_OK;
+}
+
+int sstc_tr_open(const char *path, uint64_t file_size, sstc_ctx *ctx, sstc_table_reader **out) {
+  if (!path || !ctx || !out) return SSTC_E_INVALID_ARG;
+  sstc::TableReader *r = sstc::TableReader::Open(path, file_size, ctx);
+  if (!r) return SSTC_E_INVALID_ARG;
+  *out = new sstc_table_reader();
+  (*out)->tr.reset(r);
+  return SSTC_OK;
+}
+
+uint64_t sstc_tr_num_blocks(const sstc_table_reader *tr) { return tr ? tr->tr->GetBlockIndex().size() : 0; }
+
+int sstc_tr_block_index(const sstc_table_reader *tr, uint64_t *blk_off, uint64_t *blk_len) {
+  if (!tr || !blk_off || !blk_len) return SSTC_E_INVALID_ARG;
+  const auto &idx = tr->tr->GetBlockIndex();
+  for (size_t i = 0; i < idx.size(); i++) {
+    blk_off[i] = idx[i].offset;
+    blk_len[i] = idx[i].size;
+  }
+  return SSTC_OK;
+}
+
+static int tr_decode(sstc_table_reader *tr, uint32_t mode) {
+  if (tr->cached_mode == mode) return tr->status;
+  try {
+    tr->status = tr->tr->DecodeAll(mode, tr->data, tr->type, tr->kl, tr->vl, tr->txn, tr->ko, tr->vo);
+  } catch (const std::exception &) {
+    tr->status = SSTC_E_HIP;
+  }
+  tr->cached_mode = mode;
+  return tr->status;
+}
+
+uint64_t sstc_tr_num_records(sstc_table_reader *tr, uint32_t txn_mode) {
+  if (!tr || tr_decode(tr, txn_mode) < 0) return 0;
+  return tr->type.size();
+}
+
+int sstc_tr_decode_all(sstc_table_reader *tr, uint32_t txn_mode, uint8_t *type, uint32_t *key_len,
+                       uint32_t *val_len, uint64_t *txn, uint64_t *key_off, uint64_t *val_off) {
+  if (!tr) return SSTC_E_INVALID_ARG;
+  const int st = tr_decode(tr, txn_mode);
+  const size_t n = tr->type.size();
+  if (n) {
+    std::memcpy(type, tr->type.data(), n);
+    std::memcpy(key_len, tr->kl.data(), 4 * n);
+    std::memcpy(val_len, tr->vl.data(), 4 * n);
+    std::memcpy(txn, tr->txn.data(), 8 * n);
+    std::memcpy(key_off, tr->ko.data(), 8 * n);
+    std::memcpy(val_off, tr->vo.data(), 8 * n);
+  }
+  return st;
+}
+
+int sstc_tr_destroy(sstc_table_reader *tr) {
+  delete tr;
+  return SSTC_OK;
+}
+
+} // extern "C"
