@@ -14,6 +14,7 @@
 
 struct sstc_ctx {
   int device = 0;
+  uint32_t num_cus = 256;
   hipStream_t stream = nullptr;
   uint64_t cap_records = 0, cap_scan = 0, cap_jump = 0;
   void *counters = nullptr;                 // 64 B: error counter
@@ -118,6 +119,9 @@ int sstc_ctx_create(int device, void *stream, sstc_ctx **out) {
     delete c;
     return r;
   }
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
+    c->num_cus = static_cast<uint32_t>(cus);
   if (hipMalloc(&c->counters, 64) != hipSuccess) {
     delete c;
     return fail(SSTC_E_NOMEM, "context counters");
@@ -246,7 +250,7 @@ int sstc_roundtrip_blocks(sstc_ctx *c, const uint8_t *d_src, uint8_t *d_dst,
   if (nblocks >= 0xFFFFFFFFull) return fail(SSTC_E_INVALID_ARG, "too many blocks for one call");
   if (int r = bind_device(c)) return r;
   sstc::RtArgs a{d_src, d_dst, d_blk_off, d_blk_len, nblocks, txn_mode, d_out_blk_len, d_block_status,
-                 c->err_count};
+                 c->err_count, c->num_cus};
   SSTC_HIP(sstc::launch_roundtrip(a, c->stream), "roundtrip kernels");
   return SSTC_OK;
 }

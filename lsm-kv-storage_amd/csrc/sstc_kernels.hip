@@ -257,80 +257,76 @@ __device__ __forceinline__ void rt_report(const RtArgs &a, uint64_t b, uint32_t 
   }
 }
 
-__global__ __launch_bounds__(kRtWaves *kWave, 8) void rt_kernel(RtArgs a) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds[kRtWaves * kRtSlot];
-  const uint32_t wave = uniform(threadIdx.x / kWave);
+// Issue the LDS-DMA of a small block ([off & ~15, off + L) -> img); returns the
+// number of wave-level DMA instructions issued (for counted vmcnt waits).
+template <int AUX = 0>
+__device__ __forceinline__ uint32_t rt_stage(const uint8_t *g, uint8_t *img, uint32_t nchunk) {
   const uint32_t lane = lane_id();
-  const uint64_t b = static_cast<uint64_t>(blockIdx.x) * kRtWaves + wave;
-  if (b >= a.nblocks) return;
-  uint8_t *img = lds + wave * kRtSlot;
+  uint32_t k = 0;
+  for (uint32_t c0 = 0; c0 < nchunk; c0 += kWave, k++) {
+    const uint32_t c = c0 + lane;
+    if (c < nchunk)
+      __builtin_amdgcn_global_load_lds((gbl_void_t *)(g + 16u * c), (lds_void_t *)(img + 16u * c0), 16, 0, AUX);
+  }
+  return k;
+}
 
-  const uint64_t off = uniform64(a.blk_off[b]);
-  const uint64_t len = uniform64(a.blk_len[b]);
-  const uint32_t pad = static_cast<uint32_t>(off & 15u);
-  if (len < 16) return rt_report(a, b, kBlkTooSmall, 0);
-  if (len >= (1ull << 32)) return rt_report(a, b, kBlkTooLarge, 0);
-  const uint32_t L = static_cast<uint32_t>(len);
+// A block staged whole in img (image byte pad == block byte 0).
+__device__ __forceinline__ void rt_small(const RtArgs &a, uint64_t b, uint8_t *img, uint64_t off, uint32_t L,
+                                         uint32_t pad) {
+  const uint32_t lane = lane_id();
+  const LdsReader rd{img + pad};
+  const uint64_t n = uniform64(rd.u64(L - 16));
+  const uint64_t doff = uniform64(rd.u64(L - 8));
+  uint32_t st = check_extra(L, n, doff);
+  if (st != kBlkOk) return rt_report(a, b, st, 0);
+  const Pass1 p = rt_pass1(rd, L, n, doff, a.txn_mode);
+  if (p.st != kBlkOk) return rt_report(a, b, p.st, 0);
+  if (!p.canon) {
+    const uint64_t out_len = p.data + 16 * n + 16;
+    if (out_len > L) return rt_report(a, b, kBlkNoRoom, 0);
+    rt_repack_wave(a, a.src + off, a.dst + off, n, doff, p.data, img);
+    return rt_report(a, b, kBlkOk, out_len);
+  }
+  // re-encode in place: offset section (start, size) from the scan, extra,
+  // compat txns
+  uint8_t *wimg = img + pad;
+  const uint32_t nn = static_cast<uint32_t>(n), dd = static_cast<uint32_t>(doff);
+  uint32_t carry = 0;
+  for (uint32_t i0 = 0; i0 < nn; i0 += kWave) {
+    const uint32_t i = i0 + lane;
+    uint32_t sz = 0;
+    Entry e{};
+    uint64_t s = 0;
+    if (i < nn) {
+      s = rd.u64(dd + 16ull * i);
+      e = parse_entry(rd, s, doff, a.txn_mode);
+      sz = static_cast<uint32_t>(e.size);
+    }
+    const uint32_t incl = wave_incl_scan_u32(sz);
+    if (i < nn) {
+      lds_st_u64u(wimg, dd + 16u * i, carry + incl - sz);
+      lds_st_u64u(wimg, dd + 16u * i + 8u, sz);
+      if (p.quirk && e.type != kTypeDeleted && e.vlen == 0u)
+        lds_st_u64u(wimg, static_cast<uint32_t>(s) + 9u + e.klen, e.txn);
+    }
+    carry += __shfl(incl, kWave - 1, kWave);
+  }
+  if (lane == 0) {
+    lds_st_u64u(wimg, L - 16, n);
+    lds_st_u64u(wimg, L - 8, carry);
+  }
+  wave_lds_sync();
+  store_window(img, a.dst + (off - pad), (pad + L + 15u) >> 4, 0, pad, pad + L);
+  rt_report(a, b, kBlkOk, L);
+}
+
+// A block larger than the slot: parsed from HBM, streamed through img.
+__device__ void rt_large(const RtArgs &a, uint64_t b, uint8_t *img, uint64_t off, uint32_t L, uint32_t pad) {
+  const uint32_t lane = lane_id();
   const uint8_t *g = a.src + (off - pad);
   uint8_t *gd = a.dst + (off - pad);
   const uint32_t nchunk = (pad + L + 15u) >> 4;
-
-  if (pad + L + 16 <= kRtSlot) {
-    // ------------------------------------------------ small block, staged
-    for (uint32_t c0 = 0; c0 < nchunk; c0 += kWave) {
-      const uint32_t c = c0 + lane;
-      if (c < nchunk)
-        __builtin_amdgcn_global_load_lds((gbl_void_t *)(g + 16u * c), (lds_void_t *)(img + 16u * c0), 16,
-                                         0, 0);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const LdsReader rd{img + pad};
-    const uint64_t n = uniform64(rd.u64(L - 16));
-    const uint64_t doff = uniform64(rd.u64(L - 8));
-    uint32_t st = check_extra(L, n, doff);
-    if (st != kBlkOk) return rt_report(a, b, st, 0);
-    const Pass1 p = rt_pass1(rd, L, n, doff, a.txn_mode);
-    if (p.st != kBlkOk) return rt_report(a, b, p.st, 0);
-    if (!p.canon) {
-      const uint64_t out_len = p.data + 16 * n + 16;
-      if (out_len > L) return rt_report(a, b, kBlkNoRoom, 0);
-      rt_repack_wave(a, a.src + off, a.dst + off, n, doff, p.data, img);
-      return rt_report(a, b, kBlkOk, out_len);
-    }
-    // re-encode in place: offset section (start, size) from the scan, extra,
-    // compat txns
-    uint8_t *wimg = img + pad;
-    const uint32_t nn = static_cast<uint32_t>(n), dd = static_cast<uint32_t>(doff);
-    uint32_t carry = 0;
-    for (uint32_t i0 = 0; i0 < nn; i0 += kWave) {
-      const uint32_t i = i0 + lane;
-      uint32_t sz = 0;
-      Entry e{};
-      uint64_t s = 0;
-      if (i < nn) {
-        s = rd.u64(dd + 16ull * i);
-        e = parse_entry(rd, s, doff, a.txn_mode);
-        sz = static_cast<uint32_t>(e.size);
-      }
-      const uint32_t incl = wave_incl_scan_u32(sz);
-      if (i < nn) {
-        lds_st_u64u(wimg, dd + 16u * i, carry + incl - sz);
-        lds_st_u64u(wimg, dd + 16u * i + 8u, sz);
-        if (p.quirk && e.type != kTypeDeleted && e.vlen == 0u)
-          lds_st_u64u(wimg, static_cast<uint32_t>(s) + 9u + e.klen, e.txn);
-      }
-      carry += __shfl(incl, kWave - 1, kWave);
-    }
-    if (lane == 0) {
-      lds_st_u64u(wimg, L - 16, n);
-      lds_st_u64u(wimg, L - 8, carry);
-    }
-    wave_lds_sync();
-    store_window(img, gd, nchunk, 0, pad, pad + L);
-    return rt_report(a, b, kBlkOk, L);
-  }
-
-  // -------------------------------------------------- large block, streamed
   const uint8_t *blk = a.src + off;
   const GlobalReader rd{blk};
   const uint64_t n = uniform64(rd.u64(L - 16));
@@ -345,16 +341,12 @@ __global__ __launch_bounds__(kRtWaves *kWave, 8) void rt_kernel(RtArgs a) {
     rt_repack_wave(a, blk, a.dst + off, n, doff, p.data, img);
     return rt_report(a, b, kBlkOk, out_len);
   }
-  const int64_t ob = static_cast<int64_t>(doff);           // offset section start (block-relative)
-  const int64_t oe = ob + 16 * static_cast<int64_t>(n);    // its end == L - 16
+  const int64_t ob = static_cast<int64_t>(doff);        // offset section start (block-relative)
+  const int64_t oe = ob + 16 * static_cast<int64_t>(n); // its end == L - 16
   for (uint32_t w = 0; w < nchunk; w += kRtWinChunks) {
     const uint32_t cnt = nchunk - w < kRtWinChunks ? nchunk - w : kRtWinChunks;
-    for (uint32_t c0 = 0; c0 < cnt; c0 += kWave) {
-      const uint32_t c = c0 + lane;
-      if (c < cnt)
-        __builtin_amdgcn_global_load_lds((gbl_void_t *)(g + 16u * (w + c)), (lds_void_t *)(img + 16u * c0), 16,
-                                         0, 0);
-    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // previous window's stores read img
+    rt_stage(g + 16ull * w, img, cnt);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     // window = block bytes [wlo, whi); image byte 0 == block byte wlo
     const int64_t wlo = 16 * static_cast<int64_t>(w) - pad;
@@ -393,9 +385,50 @@ __global__ __launch_bounds__(kRtWaves *kWave, 8) void rt_kernel(RtArgs a) {
       }
     }
   }
-  return rt_report(a, b, kBlkOk, L);
+  rt_report(a, b, kBlkOk, L);
 }
 
+// 0: staged small block, 1: large block, 2: error reported
+__device__ __forceinline__ uint32_t rt_classify(const RtArgs &a, uint64_t b, uint64_t &off, uint32_t &L,
+                                                uint32_t &pad) {
+  off = uniform64(a.blk_off[b]);
+  const uint64_t len = uniform64(a.blk_len[b]);
+  pad = static_cast<uint32_t>(off & 15u);
+  L = static_cast<uint32_t>(len);
+  if (len < 16) {
+    rt_report(a, b, kBlkTooSmall, 0);
+    return 2;
+  }
+  if (len >= (1ull << 32)) {
+    rt_report(a, b, kBlkTooLarge, 0);
+    return 2;
+  }
+  return pad + L + 16 <= kRtSlot ? 0u : 1u;
+}
+
+// One block per wave, 4 waves per workgroup, grid covers every block.  The
+// staging DMA uses sc0 (aux = 1): in the A/B of profiles/r01_ab_variants.md it
+// was the fastest of {4, 8, 16, 2, 1 waves per WG} x {default, sc0, nt, sc0|nt}
+// within noise at 256 MiB and +5 % at 1 GiB; a persistent double-buffered
+// variant was 40 % slower.  The structure runs at the speed of the same
+// LDS-staged copy without any parse (the parse is hidden under HBM time).
+__global__ __launch_bounds__(kRtWaves *kWave, 8) void rt_kernel(RtArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kRtWaves * kRtSlot];
+  const uint32_t wave = uniform(threadIdx.x / kWave);
+  const uint64_t b = static_cast<uint64_t>(blockIdx.x) * kRtWaves + wave;
+  if (b >= a.nblocks) return;
+  uint8_t *img = lds + wave * kRtSlot;
+  uint64_t off;
+  uint32_t L, pad;
+  const uint32_t cls = rt_classify(a, b, off, L, pad);
+  if (cls == 0) {
+    rt_stage<1>(a.src + (off - pad), img, (pad + L + 15u) >> 4);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    rt_small(a, b, img, off, L, pad);
+  } else if (cls == 1) {
+    rt_large(a, b, img, off, L, pad);
+  }
+}
 
 // ---------------------------------------------------------------------------
 // Decode to the record table.

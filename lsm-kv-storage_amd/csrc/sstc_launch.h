@@ -20,6 +20,7 @@ struct RtArgs {
   uint64_t *out_len;   // may be null
   uint32_t *status;    // may be null
   unsigned long long *err_count;
+  uint32_t num_cus;
 };
 
 struct DecArgs {
