@@ -41,6 +41,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "lsm-kv-storage_amd"))
 
 import sstcodec  # noqa: E402
+from sstcodec import shard  # noqa: E402
 from sstcodec import workload as W  # noqa: E402
 from sstcodec.codec import RecordTable  # noqa: E402
 
@@ -54,8 +55,8 @@ def make_blocks(codec, dev, nblocks, rank):
     """Uniform blocks for this rank's shard: keys k%015d of global record
     index, 100 B values from splitmix64 (seed 1 + rank), ascending txns."""
     n = nblocks * PER_BLOCK
-    start = rank * n
-    rec = W.uniform_records(n, key_index=np.arange(start, start + n, dtype=np.uint64), seed=1 + rank,
+    start, end = shard.record_range(rank, n)
+    rec = W.uniform_records(n, key_index=np.arange(start, end, dtype=np.uint64), seed=1 + rank,
                             txn_start=1 + start)
     table = RecordTable.from_numpy(rec, dev)
     first = torch.arange(0, n + 1, PER_BLOCK, dtype=torch.int64, device=dev)
@@ -122,6 +123,48 @@ def cpu_baseline(sample_src, sample_off, sample_len, seconds=10.0):
                       f"re-encode (BlockBuilder) in host memory"}
 
 
+def e2e_rate(codec, src, off, ln, dev, chunk_blocks=8192, reps=3):
+    """Host-memory -> host-memory rate: pinned H2D, fused kernel, D2H, chunked
+    and pipelined over 3 streams (copies overlap kernels and each other).
+    Returns GiB/s of input bytes.  PCIe-bound by construction."""
+    nb = off.numel()
+    nbytes = src.numel()
+    h_src = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+    h_dst = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+    h_src.copy_(src.cpu())
+    streams = [torch.cuda.Stream(dev) for _ in range(3)]
+    nchunks = (nb + chunk_blocks - 1) // chunk_blocks
+    cb = chunk_blocks * BLOCK_BYTES
+    d_in = [torch.empty(cb, dtype=torch.uint8, device=dev) for _ in streams]
+    d_out = [torch.empty(cb, dtype=torch.uint8, device=dev) for _ in streams]
+    local_off = (torch.arange(chunk_blocks, device=dev, dtype=torch.int64) * BLOCK_BYTES)
+    local_len = torch.full((chunk_blocks,), BLOCK_BYTES, dtype=torch.int64, device=dev)
+    status = [torch.empty(chunk_blocks, dtype=torch.int32, device=dev) for _ in streams]
+
+    def one_pass():
+        for c in range(nchunks):
+            k = c % len(streams)
+            s = streams[k]
+            b0, b1 = c * chunk_blocks, min(nb, (c + 1) * chunk_blocks)
+            n = (b1 - b0) * BLOCK_BYTES
+            with torch.cuda.stream(s):
+                d_in[k][:n].copy_(h_src[b0 * BLOCK_BYTES:b0 * BLOCK_BYTES + n], non_blocking=True)
+                codec.roundtrip(d_in[k], local_off[: b1 - b0], local_len[: b1 - b0], dst=d_out[k],
+                                status=status[k])
+                h_dst[b0 * BLOCK_BYTES:b0 * BLOCK_BYTES + n].copy_(d_out[k][:n], non_blocking=True)
+        torch.cuda.synchronize()
+
+    one_pass()
+    ok = torch.equal(h_dst, h_src)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        one_pass()
+    el = (time.perf_counter() - t0) / reps
+    return {"value": round(nbytes / el / 2 ** 30, 2), "unit": "GiB/s", "verified": bool(ok),
+            "how": f"pinned host -> H2D -> rt_kernel -> D2H -> pinned host, {nchunks} chunks of "
+                   f"{chunk_blocks} blocks over 3 streams, {nbytes} B input"}
+
+
 def read_traffic(nblocks):
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
@@ -158,6 +201,7 @@ def main():
     ap.add_argument("--blocks", type=int, default=65536, help="blocks per GPU (config 2: 65536)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the host->device->host rate")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -185,10 +229,7 @@ def main():
     if not ok:
         raise SystemExit("round trip output differs from input: timing invalid")
 
-    t = torch.tensor([wall], dtype=torch.float64, device=dev)
-    if dist_on:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    wall_max = float(t.item())
+    wall_max = shard.max_over_ranks(wall, dev)
     in_bytes = nb * BLOCK_BYTES
     total_in = in_bytes * world * args.steps
     value = total_in / wall_max / 2 ** 30
@@ -225,6 +266,8 @@ def main():
         }
         if world == 1:
             out["roofline"]["copy_peak_GBps"] = round(copy_peak(dev), 1)
+            if not args.no_e2e:
+                out["e2e_pcie"] = e2e_rate(codec, src, off, ln, dev)
             if not args.no_cpu_baseline:
                 k = min(nb, 16384)
                 s = src[: k * BLOCK_BYTES].cpu().numpy()
