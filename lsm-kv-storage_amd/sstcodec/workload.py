@@ -122,3 +122,44 @@ def uniform_block_layout(nblocks, per_block=28, key_len=16, val_len=100):
     blen = per_block * (13 + key_len + 4 + val_len + 16) + 16
     off = np.arange(nblocks, dtype=np.uint64) * np.uint64(blen)
     return off, np.full(nblocks, blen, np.uint64)
+
+
+def compaction_inputs(k, n_per, key_space, seed=5, p_delete=0.1, vmin=8, vmax=200, key_width=16,
+                      distinct=True, zipf=None):
+    """k record sets (one per input SST, iterator order), each sorted by key,
+    keys drawn from a shared space of `key_space` keys (overlap across tables),
+    txn ids unique across all tables (the engine's sequence numbers).  zipf:
+    optional exponent for Zipf value sizes clamped to [vmin, vmax]."""
+    rng = np.random.default_rng(seed)
+    total = k * n_per
+    txns = rng.permutation(np.arange(1, total + 1, dtype=np.uint64)) * np.uint64(7) + np.uint64(3)
+    out = []
+    pos = 0
+    for t in range(k):
+        if distinct:
+            idx = np.sort(rng.choice(key_space, size=min(n_per, key_space), replace=False)).astype(np.uint64)
+        else:
+            idx = np.sort(rng.integers(0, key_space, n_per)).astype(np.uint64)
+        n = idx.size
+        key_src = fixed_keys(idx, key_width)
+        if zipf:
+            v = rng.zipf(zipf, n).astype(np.float64)
+            vlen = np.clip(v * vmin, vmin, vmax).astype(np.uint32)
+        else:
+            vlen = rng.integers(vmin, vmax + 1, n).astype(np.uint32)
+        typ = (rng.random(n) < p_delete).astype(np.uint8)
+        vlen[typ == TYPE_DELETED] = NO_VALUE
+        vb = np.where(vlen == NO_VALUE, 0, vlen).astype(np.uint64)
+        val_off = np.zeros(n, np.uint64)
+        val_off[1:] = np.cumsum(vb[:-1])
+        val_src = random_bytes(seed * 1000 + t, int(vb.sum()) + 8)
+        tx = txns[pos:pos + n].copy()
+        pos += n
+        if not distinct:  # duplicates inside one table: newest first (skiplist order)
+            order = np.lexsort((-tx.astype(np.float64), idx))
+            tx = tx[order]
+        out.append({"type": typ, "key_len": np.full(n, key_width, np.uint32), "val_len": vlen, "txn": tx,
+                    "key_off": np.arange(n, dtype=np.uint64) * np.uint64(key_width),
+                    "val_off": np.where(typ == TYPE_DELETED, 0, val_off).astype(np.uint64),
+                    "key_src": key_src, "val_src": val_src})
+    return out

@@ -81,6 +81,8 @@ class Oracle:
         lib.orc_table_build.argtypes = [_u64] + [_vp] * 8 + [_u64, _vp]
         lib.orc_table_index.restype = _u64
         lib.orc_table_index.argtypes = [_vp, _u64, _u64] + [_vp] * 8
+        lib.orc_compact.restype = _u64
+        lib.orc_compact.argtypes = [ctypes.c_uint32, _vp, _vp, _u64, _u64, ctypes.c_int, _vp, _u64, _vp, _u64, _vp]
 
     def encode_block(self, rec, lo=0, hi=None):
         hi = len(rec["type"]) if hi is None else hi
@@ -166,6 +168,48 @@ class Oracle:
         res["min_txn"] = mn.value
         res["max_txn"] = mx.value
         return res
+
+
+def _compact_oracle(self, files, block_threshold=4096, table_limit=32 << 20, base_level=1):
+    """files: list of SST images (numpy u8) in iterator order.  Returns the list
+    of output SST images and the kept-record count."""
+    k = len(files)
+    arrs = [np.ascontiguousarray(f, np.uint8) for f in files]
+    ptrs = (ctypes.c_void_p * max(k, 1))(*[a.ctypes.data for a in arrs])
+    sizes = np.array([a.size for a in arrs] or [0], np.uint64)
+    cap = int(sum(a.size for a in arrs)) * 2 + 4096
+    out = np.zeros(cap, np.uint8)
+    max_t = cap // 40 + 1
+    osz = np.zeros(max_t, np.uint64)
+    kept = _u64()
+    nt = self.lib.orc_compact(k, ptrs, _ptr(sizes), block_threshold, table_limit, base_level, _ptr(out), cap,
+                              _ptr(osz), max_t, ctypes.byref(kept))
+    if nt == 2 ** 64 - 1:
+        raise ValueError("orc_compact failed")
+    res, pos = [], 0
+    for t in range(nt):
+        res.append(out[pos:pos + int(osz[t])].copy())
+        pos += int(osz[t])
+    return res, kept.value
+
+
+Oracle.compact = _compact_oracle
+
+REF_COMPACT = os.path.join(HERE, "_ref", "ref_compact")
+
+
+def ref_compact(paths_and_sizes, out_dir, block_threshold=4096, table_limit=32 << 20, base_level=1):
+    """Run the reference-code compaction driver (oracle/_ref/ref_compact).
+    Returns [(path, GetFileSize())]."""
+    args = [REF_COMPACT, out_dir, str(block_threshold), str(table_limit), str(base_level)]
+    for p, s in paths_and_sizes:
+        args += [p, str(int(s))]
+    r = subprocess.run(args, check=True, capture_output=True, text=True)
+    out = []
+    for line in r.stdout.strip().splitlines():
+        p, s = line.rsplit(" ", 1)
+        out.append((p, int(s)))
+    return out
 
 
 class RefLib:

@@ -5,6 +5,7 @@
  */
 #include "sst_oracle.h"
 
+#include <stdlib.h>
 #include <string.h>
 
 static uint32_t rd32(const uint8_t *p) {
@@ -264,4 +265,198 @@ uint64_t orc_table_index(const uint8_t *file, uint64_t bytes, uint64_t cap,
     p += 24 + (uint64_t)fkl + lkl;
   }
   return nb;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Compaction (db/compact.cc:232-363), records reached through the reference  */
+/* reader (COMPAT txn), merged in MergeIterator order (db/merge_iterator.h:   */
+/* 91-95: key ascending, txn descending; equal (key, txn) -> lower input       */
+/* table first, which the reference's std::priority_queue leaves unspecified). */
+/* ------------------------------------------------------------------------ */
+typedef struct {
+  uint64_t n;
+  uint8_t *type;
+  uint32_t *kl, *vl;
+  uint64_t *tx, *ko, *vo; /* offsets into the table's file image */
+  const uint8_t *file;
+} orc_run;
+
+static int key_cmp(const uint8_t *a, uint32_t al, const uint8_t *b, uint32_t bl) {
+  const uint32_t m = al < bl ? al : bl;
+  const int c = m ? memcmp(a, b, m) : 0;
+  if (c) return c < 0 ? -1 : 1;
+  return al < bl ? -1 : (al > bl ? 1 : 0);
+}
+
+static void run_free(orc_run *r) {
+  free(r->type); free(r->kl); free(r->vl); free(r->tx); free(r->ko); free(r->vo);
+}
+
+static int run_load(orc_run *r, const uint8_t *file, uint64_t bytes) {
+  memset(r, 0, sizeof(*r));
+  r->file = file;
+  uint64_t mn, mx;
+  const uint64_t nb = orc_table_index(file, bytes, 0, NULL, NULL, NULL, NULL, NULL, NULL, &mn, &mx);
+  if (nb == UINT64_MAX) return -1;
+  uint64_t *bo = malloc((nb + 1) * 8), *bl = malloc((nb + 1) * 8), *fo = malloc((nb + 1) * 8), *lo = malloc((nb + 1) * 8);
+  uint32_t *fl = malloc((nb + 1) * 4), *ll = malloc((nb + 1) * 4);
+  orc_table_index(file, bytes, nb, bo, bl, fo, fl, lo, ll, &mn, &mx);
+  uint64_t cap = 0;
+  for (uint64_t b = 0; b < nb; b++) cap += bl[b] / 29 + 1;
+  r->type = malloc(cap + 1); r->kl = malloc(4 * cap + 4); r->vl = malloc(4 * cap + 4);
+  r->tx = malloc(8 * cap + 8); r->ko = malloc(8 * cap + 8); r->vo = malloc(8 * cap + 8);
+  int rc = 0;
+  for (uint64_t b = 0; b < nb && !rc; b++) {
+    uint64_t n = 0;
+    if (bo[b] > bytes || bl[b] > bytes - bo[b]) { rc = -1; break; }
+    if (orc_block_decode(file + bo[b], bl[b], bo[b], ORC_TXN_COMPAT, r->type + r->n, r->kl + r->n, r->vl + r->n,
+                         r->tx + r->n, r->ko + r->n, r->vo + r->n, &n) != ORC_BLK_OK) rc = -1;
+    r->n += n;
+  }
+  free(bo); free(bl); free(fo); free(lo); free(fl); free(ll);
+  return rc;
+}
+
+/* one output table under construction */
+typedef struct {
+  uint64_t n, cap;
+  uint8_t *type;
+  uint32_t *kl, *vl;
+  uint64_t *tx;
+  const uint8_t **kp, **vp;
+} orc_pending;
+
+static void pend_push(orc_pending *p, uint8_t t, uint32_t kl, uint32_t vl, uint64_t tx, const uint8_t *kp,
+                      const uint8_t *vp) {
+  if (p->n == p->cap) {
+    p->cap = p->cap ? 2 * p->cap : 1024;
+    p->type = realloc(p->type, p->cap); p->kl = realloc(p->kl, 4 * p->cap); p->vl = realloc(p->vl, 4 * p->cap);
+    p->tx = realloc(p->tx, 8 * p->cap); p->kp = realloc(p->kp, sizeof(void *) * p->cap);
+    p->vp = realloc(p->vp, sizeof(void *) * p->cap);
+  }
+  p->type[p->n] = t; p->kl[p->n] = kl; p->vl[p->n] = vl; p->tx[p->n] = tx; p->kp[p->n] = kp; p->vp[p->n] = vp;
+  p->n++;
+}
+
+/* TableBuilder AddEntry... Finish over pointer-addressed records */
+static uint64_t pend_build(const orc_pending *p, uint64_t threshold, uint8_t *out) {
+  uint64_t pos = 0, nb = 0, start = 0, acc = 0, mn = UINT64_MAX, mx = 0;
+  uint64_t *bstart = malloc(8 * (p->n + 1)), *bend = malloc(8 * (p->n + 1)), *blen = malloc(8 * (p->n + 1));
+  for (uint64_t i = 0; i < p->n; i++) {
+    if (p->tx[i] < mn) mn = p->tx[i];
+    if (p->tx[i] > mx) mx = p->tx[i];
+    acc += orc_entry_size(p->kl[i], p->vl[i]) + 16;
+    if (acc >= threshold || i + 1 == p->n) {
+      uint64_t q = pos;
+      for (uint64_t j = start; j <= i; j++) {
+        out[q] = p->type[j]; wr32(out + q + 1, p->kl[j]); memcpy(out + q + 5, p->kp[j], p->kl[j]);
+        q += 5 + (uint64_t)p->kl[j];
+        if (p->vl[j] != ORC_NO_VALUE) {
+          wr32(out + q, p->vl[j]);
+          if (p->vl[j]) memcpy(out + q + 4, p->vp[j], p->vl[j]);
+          q += 4 + (uint64_t)p->vl[j];
+        }
+        wr64(out + q, p->tx[j]); q += 8;
+      }
+      const uint64_t data = q - pos;
+      uint64_t st = 0;
+      for (uint64_t j = start; j <= i; j++) {
+        const uint64_t sz = orc_entry_size(p->kl[j], p->vl[j]);
+        wr64(out + q, st); wr64(out + q + 8, sz); q += 16; st += sz;
+      }
+      wr64(out + q, i + 1 - start); wr64(out + q + 8, data); q += 16;
+      bstart[nb] = start; bend[nb] = i; blen[nb] = q - pos;
+      nb++; pos = q; start = i + 1; acc = 0;
+    }
+  }
+  const uint64_t moff = pos;
+  uint64_t boff = 0;
+  for (uint64_t b = 0; b < nb; b++) {
+    const uint64_t f = bstart[b], l = bend[b];
+    pos += meta_entry(out + pos, p->kp[f], p->kl[f], p->kp[l], p->kl[l], boff, blen[b]);
+    boff += blen[b];
+  }
+  wr64(out + pos, nb); wr64(out + pos + 8, moff); wr64(out + pos + 16, pos - moff);
+  wr64(out + pos + 24, mn); wr64(out + pos + 32, mx);
+  free(bstart); free(bend); free(blen);
+  return pos + 40;
+}
+
+uint64_t orc_compact(uint32_t k, const uint8_t *const *files, const uint64_t *bytes, uint64_t block_threshold,
+                     uint64_t table_limit, int base_level, uint8_t *out, uint64_t out_cap, uint64_t *out_size,
+                     uint64_t max_tables, uint64_t *kept_records) {
+  orc_run *runs = calloc(k ? k : 1, sizeof(orc_run));
+  uint64_t *head = calloc(k ? k : 1, 8);
+  uint64_t ntab = 0, pos = 0, kept = 0;
+  int bad = 0;
+  for (uint32_t t = 0; t < k; t++)
+    if (run_load(&runs[t], files[t], bytes[t])) bad = 1;
+  orc_pending cur = {0};
+  uint64_t data_size = 0;
+  const uint8_t *last_key = NULL;
+  uint32_t last_kl = 0;
+  uint64_t last_txn = UINT64_MAX; /* INVALID_TXN_ID */
+  int first = 1;
+  while (!bad) {
+    int best = -1;
+    for (uint32_t t = 0; t < k; t++) {
+      if (head[t] >= runs[t].n) continue;
+      if (best < 0) { best = (int)t; continue; }
+      const orc_run *a = &runs[t], *b = &runs[best];
+      const uint64_t i = head[t], j = head[best];
+      const int c = key_cmp(a->file + a->ko[i], a->kl[i], b->file + b->ko[j], b->kl[j]);
+      if (c < 0 || (c == 0 && a->tx[i] > b->tx[j])) best = (int)t;
+    }
+    if (best < 0) break;
+    const orc_run *r = &runs[best];
+    const uint64_t i = head[best]++;
+    const uint8_t *key = r->file + r->ko[i];
+    const uint32_t kl = r->kl[i];
+    const uint64_t txn = r->tx[i];
+    const uint8_t type = r->type[i];
+    /* ShouldKeepEntry, db/compact.cc:324-363 */
+    int keep;
+    const int new_key = first || key_cmp(key, kl, last_key, last_kl) != 0;
+    if (first) keep = 1;
+    else if (new_key) keep = type == ORC_TYPE_PUT ? 1 : (base_level ? 0 : 1);
+    else keep = !(last_txn > txn);
+    if (new_key) { last_key = key; last_kl = kl; last_txn = txn; }
+    first = 0;
+    if (!keep) continue;
+    kept++;
+    pend_push(&cur, type, kl, r->vl[i], txn, key, r->vl[i] != ORC_NO_VALUE ? r->file + r->vo[i] : NULL);
+    data_size += kl + (r->vl[i] != ORC_NO_VALUE ? r->vl[i] : 0); /* table_builder.cc:55 */
+    if (data_size >= table_limit) {                               /* compact.cc:290 */
+      uint64_t need = 40;
+      for (uint64_t j = 0; j < cur.n; j++) need += orc_entry_size(cur.kl[j], cur.vl[j]) + 16 + 16 + 24 + 2 * cur.kl[j];
+      if (pos + need > out_cap || ntab >= max_tables) { bad = 1; break; }
+      out_size[ntab++] = pend_build(&cur, block_threshold, out + pos);
+      pos += out_size[ntab - 1];
+      cur.n = 0;
+      data_size = 0;
+    }
+  }
+  /* DoCompactJob opens its first output before the loop and finishes it even
+   * when nothing was added (compact.cc:236-240, 304-310) */
+  if (!bad && cur.n == 0 && ntab == 0) {
+    if (out_cap < 40 || max_tables < 1) bad = 1;
+    else {
+      out_size[ntab++] = pend_build(&cur, block_threshold, out + pos);
+      pos += out_size[ntab - 1];
+    }
+  }
+  if (!bad && cur.n) {
+    uint64_t need = 40;
+    for (uint64_t j = 0; j < cur.n; j++) need += orc_entry_size(cur.kl[j], cur.vl[j]) + 16 + 16 + 24 + 2 * cur.kl[j];
+    if (pos + need > out_cap || ntab >= max_tables) bad = 1;
+    else {
+      out_size[ntab++] = pend_build(&cur, block_threshold, out + pos);
+      pos += out_size[ntab - 1];
+    }
+  }
+  free(cur.type); free(cur.kl); free(cur.vl); free(cur.tx); free(cur.kp); free(cur.vp);
+  for (uint32_t t = 0; t < k; t++) run_free(&runs[t]);
+  free(runs); free(head);
+  if (kept_records) *kept_records = kept;
+  return bad ? UINT64_MAX : ntab;
 }

@@ -110,6 +110,20 @@ uint64_t orc_table_index(const uint8_t *file, uint64_t bytes, uint64_t cap,
                          uint64_t *last_key_off, uint32_t *last_key_len,
                          uint64_t *min_txn, uint64_t *max_txn);
 
+/* Compaction job of db/compact.cc:232-363 over k input SST images given in
+ * iterator order (files_need_compaction_[0] then [1], compact.cc:186-230).
+ * Records are read through the reference reader semantics (COMPAT txn),
+ * merged in MergeIterator order (key asc, txn desc; db/merge_iterator.h:91-95),
+ * filtered by ShouldKeepEntry (base_level = IsBaseLevelForKey() for every key,
+ * i.e. a new-key tombstone is dropped), and written to output tables that are
+ * finished once their key+value bytes reach table_limit (compact.cc:290).  The
+ * output tables go back to back into out; out_size[t] = bytes of table t
+ * (GetFileSize() = out_size[t] + 1).  Returns the table count or UINT64_MAX. */
+uint64_t orc_compact(uint32_t k, const uint8_t *const *files, const uint64_t *bytes,
+                     uint64_t block_threshold, uint64_t table_limit, int base_level,
+                     uint8_t *out, uint64_t out_cap, uint64_t *out_size, uint64_t max_tables,
+                     uint64_t *kept_records);
+
 #ifdef __cplusplus
 }
 #endif

@@ -20,7 +20,10 @@ ROOT = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
 sys.path.insert(0, os.path.join(ROOT, "lsm-kv-storage_amd"))
 
-from oracle import RefLib  # noqa: E402
+import hashlib  # noqa: E402
+import json  # noqa: E402
+
+from oracle import RefLib, ref_compact  # noqa: E402
 from sstcodec import workload as W  # noqa: E402
 
 REC_KEYS = ("type", "key_len", "val_len", "txn", "key_off", "val_off")
@@ -151,6 +154,52 @@ def main():
             save(f"table_mixed_{T}.npz", sst=f, file_size=np.array([fs], np.uint64),
                  idx_blk_off=idx["blk_off"], idx_blk_len=idx["blk_len"],
                  idx_first_key_len=idx["first_key_len"], idx_last_key_len=idx["last_key_len"])
+
+    # 6. compaction (db/compact.cc) through the reference merge + table code
+    compaction_fixtures(ref)
+
+
+COMPACTION_CASES = [
+    # name, k, n_per, key_space, vmax, table_limit, distinct
+    ("small", 4, 300, 500, 200, 32 << 20, True),
+    ("split", 8, 2000, 5000, 600, 200_000, True),
+    ("dups", 3, 1000, 800, 100, 50_000, False),
+]
+
+
+def compaction_fixtures(ref):
+    """Inputs are built by the reference TableBuilder from seeded records
+    (sstcodec.workload.compaction_inputs); outputs by oracle/_ref/ref_compact
+    (reference MergeIterator + TableReaderIterator + TableBuilder).  The small
+    case is stored byte for byte, the others as SHA-256 + GetFileSize()."""
+    manifest = {}
+    for name, k, n, ks, vmax, limit, distinct in COMPACTION_CASES:
+        sets = W.compaction_inputs(k, n, ks, vmax=vmax, distinct=distinct)
+        with tempfile.TemporaryDirectory() as td:
+            ins = []
+            for i, rec in enumerate(sets):
+                p = os.path.join(td, f"in{i}.sst")
+                fs = ref.table_build(p, rec, 4096)
+                ins.append((p, fs))
+            case = {"k": k, "n_per": n, "key_space": ks, "vmax": vmax, "table_limit": limit,
+                    "distinct": distinct, "block_threshold": 4096,
+                    "inputs": [{"sha256": hashlib.sha256(open(p, "rb").read()).hexdigest(), "file_size": fs}
+                               for p, fs in ins]}
+            for base in (1, 0):
+                od = os.path.join(td, f"out{base}")
+                os.makedirs(od)
+                outs = ref_compact(ins, od, 4096, limit, base)
+                case[f"outputs_base{base}"] = [
+                    {"sha256": hashlib.sha256(open(p, "rb").read()).hexdigest(), "file_size": fs}
+                    for p, fs in outs]
+                if name == "small":
+                    arrays = {f"in{i}": np.fromfile(p, np.uint8) for i, (p, _) in enumerate(ins)}
+                    arrays.update({f"out{j}": np.fromfile(p, np.uint8) for j, (p, _) in enumerate(outs)})
+                    save(f"compact_small_base{base}.npz", **arrays)
+            manifest[name] = case
+    with open(os.path.join(HERE, "compaction.json"), "w") as f:
+        json.dump(manifest, f, indent=1)
+    print("compaction.json written")
 
 
 if __name__ == "__main__":
