@@ -160,6 +160,40 @@ int sstc_roundtrip_blocks(sstc_ctx *ctx, const uint8_t *d_src, uint8_t *d_dst,
                           uint64_t nblocks, uint32_t txn_mode, uint64_t *d_out_blk_len,
                           uint32_t *d_block_status);
 
+/* ---- compaction job (replaces Compact::DoCompactJob, db/compact.cc:232-363,
+ *      with its MergeIterator, db/merge_iterator.cc) ------------------------ */
+
+typedef struct sstc_compact_params {
+  uint64_t block_threshold; /* Config::GetSSTBlockSize() (4096)                 */
+  uint64_t table_limit;     /* Config::GetPerMemTableSizeLimit() (32 MiB): an   */
+                            /* output SST is finished once its key+value bytes */
+                            /* reach it (compact.cc:290)                       */
+  uint32_t base_level;      /* 1: IsBaseLevelForKey() holds for every key, so a */
+                            /* tombstone that starts a key group is dropped    */
+  uint32_t txn_mode;        /* SSTC_TXN_COMPAT = the reference iterator's txn   */
+} sstc_compact_params;
+
+typedef struct sstc_compact_result {
+  uint64_t records_in, records_kept, blocks_out, tables_out, bytes_out;
+} sstc_compact_result;
+
+/* Compact `ntables` input SSTs given in iterator order (compact.cc:186-230).
+ * Their data blocks are listed table by table in d_blk_off/d_blk_len (block
+ * index order); table t owns blocks [h_table_first_block[t],
+ * h_table_first_block[t+1]) (HOST array, ntables+1 elements).  Every input
+ * table must be sorted (key ascending, equal keys txn descending), as
+ * TableBuilder requires.  Records merge in MergeIterator order (key asc, txn
+ * desc; equal (key, txn): lower input table first), ShouldKeepEntry filters
+ * them, and the survivors are written as complete SST images (blocks, meta
+ * section, 40 B footer) back to back into d_dst: table t at d_table_off[t]
+ * with d_table_len[t] bytes (TableBuilder::GetFileSize() = d_table_len[t] + 1).
+ * d_table_off needs max_tables+1 elements.  This call allocates its own
+ * workspace and synchronises the stream (output sizes are data dependent). */
+int sstc_compact(sstc_ctx *ctx, const uint8_t *d_src, const uint64_t *d_blk_off, const uint64_t *d_blk_len,
+                 uint64_t nblocks, const uint64_t *h_table_first_block, uint32_t ntables,
+                 const sstc_compact_params *params, uint8_t *d_dst, uint64_t dst_cap, uint64_t *d_table_off,
+                 uint64_t *d_table_len, uint64_t max_tables, sstc_compact_result *result);
+
 #ifdef __cplusplus
 }
 #endif

@@ -255,4 +255,34 @@ int sstc_roundtrip_blocks(sstc_ctx *c, const uint8_t *d_src, uint8_t *d_dst,
   return SSTC_OK;
 }
 
+int sstc_compact(sstc_ctx *c, const uint8_t *d_src, const uint64_t *d_blk_off, const uint64_t *d_blk_len,
+                 uint64_t nblocks, const uint64_t *h_table_first_block, uint32_t ntables,
+                 const sstc_compact_params *params, uint8_t *d_dst, uint64_t dst_cap, uint64_t *d_table_off,
+                 uint64_t *d_table_len, uint64_t max_tables, sstc_compact_result *result) {
+  if (!c || !h_table_first_block || !params || !d_dst || !d_table_off || !d_table_len || !result ||
+      (nblocks && (!d_src || !d_blk_off || !d_blk_len)))
+    return fail(SSTC_E_INVALID_ARG, "sstc_compact: NULL argument");
+  if (params->block_threshold == 0 || params->table_limit == 0 || params->txn_mode > SSTC_TXN_CORRECT)
+    return fail(SSTC_E_INVALID_ARG, "sstc_compact: bad parameters");
+  if (h_table_first_block[0] != 0 || h_table_first_block[ntables] != nblocks)
+    return fail(SSTC_E_INVALID_ARG, "sstc_compact: table ranges must cover the block list");
+  for (uint32_t t = 0; t < ntables; t++)
+    if (h_table_first_block[t] > h_table_first_block[t + 1])
+      return fail(SSTC_E_INVALID_ARG, "sstc_compact: table ranges must be ascending");
+  if (int r = bind_device(c)) return r;
+  uint64_t res[5] = {0, 0, 0, 0, 0};
+  std::string err;
+  const int rc = sstc::compact_impl(c->stream, c->err_count, d_src, d_blk_off, d_blk_len, nblocks,
+                                    h_table_first_block, ntables, params->block_threshold, params->table_limit,
+                                    params->base_level, params->txn_mode, d_dst, dst_cap, d_table_off, d_table_len,
+                                    max_tables, res, err);
+  result->records_in = res[0];
+  result->records_kept = res[1];
+  result->blocks_out = res[2];
+  result->tables_out = res[3];
+  result->bytes_out = res[4];
+  if (rc != SSTC_OK) return fail(rc, ("sstc_compact: " + err).c_str());
+  return SSTC_OK;
+}
+
 } // extern "C"

@@ -1,0 +1,538 @@
+// sstc_compact.hip — device-resident compaction job (reference db/compact.cc:
+// 232-363 with MergeIterator, db/merge_iterator.{h,cc}).
+//
+//   decode every input block (sstc decode kernels, COMPAT txn = what the
+//   reference iterator reads)
+//   -> merge the per-table sorted runs: log2(k) rounds of stable merge-path
+//      merges on a 16 B big-endian key prefix + length + txn (full key bytes
+//      compared only when two prefixes tie and both keys are longer than 16 B);
+//      order = key ascending, txn descending, then input table order
+//   -> ShouldKeepEntry as flags (group head = key differs from the previous
+//      merged record, group head txn by a scatter of group heads)
+//   -> stream compaction of the survivors
+//   -> output-table split (key+value bytes >= table_limit, compact.cc:290) and
+//      block split (entry_size+16 >= block_threshold, table_builder.cc:57),
+//      both greedy, both by the pointer-doubling segmentation, blocks clamped
+//      at their table's end
+//   -> layout scans, block encode (enc_emit_kernel), meta entries and footers
+//      (table_builder.cc:101-211) written on the device.
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "sstc_device.h"
+#include "sstc_launch.h"
+
+namespace sstc {
+
+namespace {
+
+// ------------------------------------------------------------------ kernels
+struct KeyView {
+  const uint8_t *src;
+  const uint64_t *koff; // by record id
+};
+
+__device__ __forceinline__ uint64_t be_prefix(const uint8_t *p, uint32_t len, uint32_t from) {
+  uint64_t v = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < 8; j++) {
+    const uint32_t b = from + j < len ? p[from + j] : 0u;
+    v = (v << 8) | b;
+  }
+  return v;
+}
+
+__global__ void ck_prefix_kernel(const uint8_t *src, const uint64_t *koff, const uint32_t *klen,
+                                 const uint64_t *txn, uint64_t n, uint64_t *p0, uint64_t *p1, uint64_t *tx,
+                                 uint32_t *kl, uint32_t *id) {
+  const uint64_t r = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (r >= n) return;
+  const uint8_t *k = src + koff[r];
+  const uint32_t l = klen[r];
+  p0[r] = be_prefix(k, l, 0);
+  p1[r] = be_prefix(k, l, 8);
+  tx[r] = txn[r];
+  kl[r] = l;
+  id[r] = static_cast<uint32_t>(r);
+}
+
+// three-way key compare: prefix, then (only when both are longer than 16 B and
+// the prefixes tie) the remaining bytes, then the length (std::string_view <)
+__device__ __forceinline__ int key_cmp(uint64_t a0, uint64_t a1, uint32_t al, uint32_t aid, uint64_t b0,
+                                       uint64_t b1, uint32_t bl, uint32_t bid, const KeyView &kv) {
+  if (a0 != b0) return a0 < b0 ? -1 : 1;
+  if (a1 != b1) return a1 < b1 ? -1 : 1;
+  if (al > 16 && bl > 16) {
+    const uint8_t *pa = kv.src + kv.koff[aid];
+    const uint8_t *pb = kv.src + kv.koff[bid];
+    const uint32_t m = al < bl ? al : bl;
+    for (uint32_t j = 16; j < m; j++) {
+      const uint32_t x = pa[j], y = pb[j];
+      if (x != y) return x < y ? -1 : 1;
+    }
+  }
+  return al < bl ? -1 : (al > bl ? 1 : 0);
+}
+
+struct Soa {
+  uint64_t *p0, *p1, *tx;
+  uint32_t *kl, *id;
+};
+
+// merge order: key asc, then txn desc (db/merge_iterator.h:91-95)
+__device__ __forceinline__ bool rec_less(const Soa &s, uint64_t a, uint64_t b, const KeyView &kv) {
+  const int c = key_cmp(s.p0[a], s.p1[a], s.kl[a], s.id[a], s.p0[b], s.p1[b], s.kl[b], s.id[b], kv);
+  return c < 0 || (c == 0 && s.tx[a] > s.tx[b]);
+}
+
+// Sortedness of every input run (TableBuilder requires sorted input,
+// table_builder.h:77): a record may not sort before its predecessor.
+__global__ void ck_check_sorted_kernel(Soa s, const uint64_t *run_start, uint64_t nruns, uint64_t n, KeyView kv,
+                                       unsigned long long *bad) {
+  const uint64_t r = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (r == 0 || r >= n) return;
+  uint64_t lo = 0, hi = nruns; // run containing r: last run_start <= r
+  while (lo + 1 < hi) {
+    const uint64_t mid = (lo + hi) >> 1;
+    if (run_start[mid] <= r) lo = mid;
+    else hi = mid;
+  }
+  if (run_start[lo] == r) return; // first record of its run
+  if (rec_less(s, r, r - 1, kv)) atomicAdd(bad, 1ull);
+}
+
+constexpr uint32_t kMergeItems = 8;
+
+// One round of pairwise stable merges: runs [rb[2j], rb[2j+1]) and
+// [rb[2j+1], rb[2j+2]) -> [rb[2j], rb[2j+2]) (ties: left run first).
+__global__ void ck_merge_kernel(Soa in, Soa out, const uint64_t *rb, uint64_t nruns, uint64_t n, KeyView kv) {
+  const uint64_t k0 = (static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x) * kMergeItems;
+  if (k0 >= n) return;
+  const uint64_t npairs = (nruns + 1) / 2;
+  uint64_t k = k0;
+  const uint64_t kend = k0 + kMergeItems < n ? k0 + kMergeItems : n;
+  // pair holding k
+  uint64_t lo = 0, hi = npairs;
+  while (lo + 1 < hi) {
+    const uint64_t mid = (lo + hi) >> 1;
+    if (rb[2 * mid] <= k) lo = mid;
+    else hi = mid;
+  }
+  uint64_t j = lo;
+  while (k < kend) {
+    const uint64_t a0 = rb[2 * j];
+    const uint64_t a1 = 2 * j + 1 <= nruns ? rb[2 * j + 1] : a0;
+    const uint64_t b1 = 2 * j + 2 <= nruns ? rb[2 * j + 2] : a1;
+    const uint64_t na = a1 - a0, nb = b1 - a1;
+    const uint64_t kk = k - a0;
+    uint64_t l = kk > nb ? kk - nb : 0, h = kk < na ? kk : na;
+    while (l < h) { // smallest i with B[kk-i-1] < A[i]
+      const uint64_t mid = (l + h) >> 1;
+      if (rec_less(in, a1 + (kk - mid - 1), a0 + mid, kv)) h = mid;
+      else l = mid + 1;
+    }
+    uint64_t ia = a0 + l, ib = a1 + (kk - l);
+    const uint64_t stop = kend < b1 ? kend : b1;
+    for (; k < stop; k++) {
+      const bool take_a = ia < a1 && (ib >= b1 || !rec_less(in, ib, ia, kv));
+      const uint64_t src = take_a ? ia++ : ib++;
+      out.p0[k] = in.p0[src];
+      out.p1[k] = in.p1[src];
+      out.tx[k] = in.tx[src];
+      out.kl[k] = in.kl[src];
+      out.id[k] = in.id[src];
+    }
+    j++;
+  }
+}
+
+__global__ void ck_runs_next_kernel(const uint64_t *rb, uint64_t nruns, uint64_t *rb2) {
+  const uint64_t j = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  const uint64_t nr2 = (nruns + 1) / 2;
+  if (j <= nr2) rb2[j] = rb[2 * j <= nruns ? 2 * j : nruns];
+}
+
+// head[i] = 1 if merged record i starts a key group (ShouldKeepEntry's
+// last_current_key != key, compact.cc:266-268)
+__global__ void ck_head_kernel(Soa s, uint64_t n, KeyView kv, uint64_t *head) {
+  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint64_t h = 1;
+  if (i > 0)
+    h = key_cmp(s.p0[i - 1], s.p1[i - 1], s.kl[i - 1], s.id[i - 1], s.p0[i], s.p1[i], s.kl[i], s.id[i], kv) != 0;
+  head[i] = h;
+}
+
+// gid = inclusive group count - 1 (from the exclusive scan G of head: gid = G[i] + head[i] - 1)
+__global__ void ck_headpos_kernel(const uint64_t *head, const uint64_t *G, uint64_t n, uint64_t *hp) {
+  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i < n && head[i]) hp[G[i]] = i;
+}
+
+// ShouldKeepEntry (compact.cc:324-363)
+__global__ void ck_keep_kernel(Soa s, const uint64_t *head, const uint64_t *G, const uint64_t *hp,
+                               const uint8_t *type, uint64_t n, uint32_t base_level, uint64_t *keep) {
+  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint64_t k;
+  if (i == 0) {
+    k = 1; // first record of the merge is always kept
+  } else if (head[i]) {
+    k = type[s.id[i]] == kTypePut ? 1 : (base_level ? 0 : 1);
+  } else {
+    const uint64_t h = hp[G[i] - 1]; // this group's head
+    k = s.tx[h] > s.tx[i] ? 0 : 1;   // drop if last_txn > txn
+  }
+  keep[i] = k;
+}
+
+struct Rec {
+  uint8_t *type;
+  uint32_t *kl, *vl;
+  uint64_t *tx, *ko, *vo;
+};
+
+__global__ void ck_gather_kernel(Soa s, const uint64_t *keep, const uint64_t *K, Rec R, uint64_t n, Rec out,
+                                 uint64_t *dw, uint64_t *ew) {
+  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= n || !keep[i]) return;
+  const uint64_t o = K[i];
+  const uint32_t r = s.id[i];
+  const uint32_t vl = R.vl[r];
+  out.type[o] = R.type[r];
+  out.kl[o] = R.kl[r];
+  out.vl[o] = vl;
+  out.tx[o] = R.tx[r];
+  out.ko[o] = R.ko[r];
+  out.vo[o] = R.vo[r];
+  // data_size increment (table_builder.cc:55) and block weight (entry + offset entry)
+  dw[o] = static_cast<uint64_t>(R.kl[r]) + (vl != kNoValue ? vl : 0u);
+  ew[o] = entry_size(R.kl[r], vl);
+}
+
+// per record: end of its output table (clamp for block segmentation)
+__global__ void ck_table_end_kernel(const uint64_t *tf, uint64_t nt, uint64_t m, uint32_t *clamp) {
+  const uint64_t r = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (r > m) return;
+  if (r == m) {
+    clamp[r] = static_cast<uint32_t>(m);
+    return;
+  }
+  uint64_t lo = 0, hi = nt; // last tf <= r
+  while (lo + 1 < hi) {
+    const uint64_t mid = (lo + hi) >> 1;
+    if (tf[mid] <= r) lo = mid;
+    else hi = mid;
+  }
+  clamp[r] = static_cast<uint32_t>(tf[lo + 1]);
+}
+
+// block b: length, meta entry size, table index
+__global__ void ck_block_info_kernel(const uint64_t *bf, uint64_t nb, const uint64_t *Pe, const uint32_t *kl,
+                                     const uint64_t *tf, uint64_t nt, uint64_t *blen, uint64_t *msz,
+                                     uint32_t *btab) {
+  const uint64_t b = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (b >= nb) return;
+  const uint64_t f0 = bf[b], f1 = bf[b + 1];
+  blen[b] = (Pe[f1] - Pe[f0]) + 16 * (f1 - f0) + 16;
+  msz[b] = 24ull + kl[f0] + kl[f1 - 1]; // AddIndexBlockEntry, table_builder.cc:101-145
+  uint64_t lo = 0, hi = nt;
+  while (lo + 1 < hi) {
+    const uint64_t mid = (lo + hi) >> 1;
+    if (tf[mid] <= f0) lo = mid;
+    else hi = mid;
+  }
+  btab[b] = static_cast<uint32_t>(lo);
+}
+
+// table t: first block index, data / meta bytes, total
+__global__ void ck_table_info_kernel(const uint64_t *tf, uint64_t nt, const uint64_t *bf, uint64_t nb,
+                                     const uint64_t *BL, const uint64_t *MS, uint64_t *tbf, uint64_t *tdata,
+                                     uint64_t *tmeta, uint64_t *tlen) {
+  const uint64_t t = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (t > nt) return;
+  // block starting at record tf[t] (every table start is a block start)
+  uint64_t lo = 0, hi = nb + 1;
+  const uint64_t r = tf[t];
+  while (lo + 1 < hi) {
+    const uint64_t mid = (lo + hi) >> 1;
+    if (bf[mid] <= r) lo = mid;
+    else hi = mid;
+  }
+  tbf[t] = lo;
+  if (t == nt) return;
+  // tbf[t+1] computed by its own thread; recompute here for the sizes
+  uint64_t lo2 = 0, hi2 = nb + 1;
+  const uint64_t r2 = tf[t + 1];
+  while (lo2 + 1 < hi2) {
+    const uint64_t mid = (lo2 + hi2) >> 1;
+    if (bf[mid] <= r2) lo2 = mid;
+    else hi2 = mid;
+  }
+  tdata[t] = BL[lo2] - BL[lo];
+  tmeta[t] = MS[lo2] - MS[lo];
+  tlen[t] = tdata[t] + tmeta[t] + 40;
+}
+
+__global__ void ck_block_off_kernel(const uint32_t *btab, uint64_t nb, const uint64_t *BL, const uint64_t *tbf,
+                                    const uint64_t *toff, uint64_t *bo) {
+  const uint64_t b = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (b >= nb) return;
+  const uint32_t t = btab[b];
+  bo[b] = toff[t] + (BL[b] - BL[tbf[t]]);
+}
+
+__device__ __forceinline__ void put_le(uint8_t *p, uint64_t v, int n) {
+  for (int j = 0; j < n; j++) p[j] = static_cast<uint8_t>(v >> (8 * j));
+}
+
+// meta entry of block b (table_builder.cc:101-145)
+__global__ void ck_meta_kernel(const uint64_t *bf, uint64_t nb, const uint32_t *btab, const uint64_t *BL,
+                               const uint64_t *MS, const uint64_t *blen, const uint64_t *tbf, const uint64_t *toff,
+                               const uint64_t *tdata, Rec K, const uint8_t *src, uint8_t *dst) {
+  const uint64_t b = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (b >= nb) return;
+  const uint32_t t = btab[b];
+  uint8_t *p = dst + toff[t] + tdata[t] + (MS[b] - MS[tbf[t]]);
+  const uint64_t f = bf[b], l = bf[b + 1] - 1;
+  const uint32_t fk = K.kl[f], lk = K.kl[l];
+  put_le(p, fk, 4);
+  for (uint32_t j = 0; j < fk; j++) p[4 + j] = src[K.ko[f] + j];
+  put_le(p + 4 + fk, lk, 4);
+  for (uint32_t j = 0; j < lk; j++) p[8 + fk + j] = src[K.ko[l] + j];
+  put_le(p + 8 + fk + lk, BL[b] - BL[tbf[t]], 8);
+  put_le(p + 16 + fk + lk, blen[b], 8);
+}
+
+// footer of table t (table_builder.cc:179-211); one workgroup per table also
+// reduces min/max txn over the table's records
+__global__ __launch_bounds__(256) void ck_footer_kernel(const uint64_t *tf, const uint64_t *tbf,
+                                                        const uint64_t *toff, const uint64_t *tdata,
+                                                        const uint64_t *tmeta, Rec K, uint8_t *dst) {
+  __shared__ uint64_t smn[256], smx[256];
+  const uint64_t t = blockIdx.x;
+  uint64_t mn = ~0ull, mx = 0;
+  for (uint64_t r = tf[t] + threadIdx.x; r < tf[t + 1]; r += 256) {
+    const uint64_t x = K.tx[r];
+    mn = x < mn ? x : mn;
+    mx = x > mx ? x : mx;
+  }
+  smn[threadIdx.x] = mn;
+  smx[threadIdx.x] = mx;
+  __syncthreads();
+  for (uint32_t d = 128; d > 0; d >>= 1) {
+    if (threadIdx.x < d) {
+      smn[threadIdx.x] = smn[threadIdx.x + d] < smn[threadIdx.x] ? smn[threadIdx.x + d] : smn[threadIdx.x];
+      smx[threadIdx.x] = smx[threadIdx.x + d] > smx[threadIdx.x] ? smx[threadIdx.x + d] : smx[threadIdx.x];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    uint8_t *p = dst + toff[t] + tdata[t] + tmeta[t];
+    put_le(p, tbf[t + 1] - tbf[t], 8);
+    put_le(p + 8, tdata[t], 8);
+    put_le(p + 16, tmeta[t], 8);
+    put_le(p + 24, smn[0], 8);
+    put_le(p + 32, smx[0], 8);
+  }
+}
+
+// ------------------------------------------------------------------ host side
+inline uint32_t grid(uint64_t n, uint32_t per = 256) { return static_cast<uint32_t>((n + per - 1) / per); }
+
+struct Pool {
+  std::vector<void *> ptrs;
+  ~Pool() {
+    for (void *p : ptrs) (void)hipFree(p);
+  }
+  template <class T> T *get(uint64_t n) {
+    void *p = nullptr;
+    if (hipMalloc(&p, (n ? n : 1) * sizeof(T)) != hipSuccess) throw std::runtime_error("compaction workspace");
+    ptrs.push_back(p);
+    return static_cast<T *>(p);
+  }
+};
+
+#define CK(x)                                                                                                  \
+  do {                                                                                                         \
+    hipError_t e_ = (x);                                                                                       \
+    if (e_ != hipSuccess) throw std::runtime_error(std::string(#x) + ": " + hipGetErrorString(e_));           \
+  } while (0)
+
+uint32_t bitlen(uint64_t v) {
+  uint32_t b = 0;
+  while (v) {
+    b++;
+    v >>= 1;
+  }
+  return b ? b : 1;
+}
+
+template <class T> T read1(const T *d, hipStream_t s) {
+  T v{};
+  CK(hipMemcpyAsync(&v, d, sizeof(T), hipMemcpyDeviceToHost, s));
+  CK(hipStreamSynchronize(s));
+  return v;
+}
+
+// greedy segmentation of [0, m) by weights w (>= threshold closes), optional clamp
+uint64_t segment(Pool &pool, const uint64_t *w, uint64_t m, uint64_t threshold, const uint32_t *clamp,
+                 uint64_t *first, uint64_t *ws, hipStream_t s) {
+  uint64_t *Pw = pool.get<uint64_t>(m + 1);
+  CK(launch_scan(w, m, 0, Pw, ws, s));
+  const uint32_t levels = bitlen(m);
+  uint32_t *J = pool.get<uint32_t>(static_cast<uint64_t>(levels) * (m + 1));
+  uint64_t *dn = pool.get<uint64_t>(1);
+  CK(launch_segment(Pw, m, threshold, J, levels, dn, first, s, clamp));
+  return read1(dn, s);
+}
+
+} // namespace
+
+int compact_impl(hipStream_t s, unsigned long long *err_count, const uint8_t *d_src, const uint64_t *d_blk_off,
+                 const uint64_t *d_blk_len, uint64_t nblocks, const uint64_t *h_tfb, uint32_t ntables,
+                 uint64_t block_threshold, uint64_t table_limit, uint32_t base_level, uint32_t txn_mode,
+                 uint8_t *d_dst, uint64_t dst_cap, uint64_t *d_table_off, uint64_t *d_table_len, uint64_t max_tables,
+                 uint64_t *res, std::string &err) {
+  try {
+    Pool pool;
+    const uint64_t nws = scan_workspace_elems(nblocks + 1) + 64;
+    // 1. decode every block
+    uint64_t *rb_all = pool.get<uint64_t>(nblocks + 1);
+    uint64_t *ws = pool.get<uint64_t>(nws);
+    CK(launch_count(d_src, d_blk_off, d_blk_len, nblocks, rb_all, s));
+    CK(launch_scan(rb_all, nblocks, 0, rb_all, ws, s));
+    std::vector<uint64_t> h_rb(nblocks + 1);
+    CK(hipMemcpyAsync(h_rb.data(), rb_all, (nblocks + 1) * 8, hipMemcpyDeviceToHost, s));
+    CK(hipStreamSynchronize(s));
+    const uint64_t n = h_rb[nblocks];
+    std::vector<uint64_t> run_start;
+    for (uint32_t t = 0; t <= ntables; t++) run_start.push_back(h_rb[h_tfb[t]]);
+    res[0] = n;
+    if (n >= 0xFFFFFFFFull) {
+      err = "too many records";
+      return SSTC_E_INVALID_ARG;
+    }
+    const uint64_t wsn = scan_workspace_elems(n + 1) + 64;
+    uint64_t *ws2 = pool.get<uint64_t>(wsn);
+    Rec R{pool.get<uint8_t>(n), pool.get<uint32_t>(n), pool.get<uint32_t>(n), pool.get<uint64_t>(n),
+          pool.get<uint64_t>(n), pool.get<uint64_t>(n)};
+    uint32_t *status = pool.get<uint32_t>(nblocks);
+    DecArgs da{d_src, d_blk_off, d_blk_len, nblocks, rb_all,
+               sstc_records{R.type, R.kl, R.vl, R.tx, R.ko, R.vo}, txn_mode, status, err_count};
+    const unsigned long long errs0 = read1(err_count, s);
+    CK(launch_decode(da, s));
+    if (read1(err_count, s) != errs0) {
+      err = "an input block failed to decode";
+      return SSTC_E_INVALID_ARG;
+    }
+    if (n == 0) { // DoCompactJob still finishes its first (empty) output table
+      if (max_tables < 1 || dst_cap < 40) {
+        err = "output capacity";
+        return SSTC_E_CAPACITY;
+      }
+      uint8_t foot[40] = {0};
+      const uint64_t mn = ~0ull;
+      memcpy(foot + 24, &mn, 8);
+      const uint64_t zero = 0, forty = 40;
+      CK(hipMemcpyAsync(d_dst, foot, 40, hipMemcpyHostToDevice, s));
+      CK(hipMemcpyAsync(d_table_off, &zero, 8, hipMemcpyHostToDevice, s));
+      CK(hipMemcpyAsync(d_table_len, &forty, 8, hipMemcpyHostToDevice, s));
+      CK(hipStreamSynchronize(s));
+      res[1] = 0; res[2] = 0; res[3] = 1; res[4] = 40;
+      return SSTC_OK;
+    }
+    // 2. sort keys + merge
+    Soa A{pool.get<uint64_t>(n), pool.get<uint64_t>(n), pool.get<uint64_t>(n), pool.get<uint32_t>(n),
+          pool.get<uint32_t>(n)};
+    Soa B{pool.get<uint64_t>(n), pool.get<uint64_t>(n), pool.get<uint64_t>(n), pool.get<uint32_t>(n),
+          pool.get<uint32_t>(n)};
+    const KeyView kv{d_src, R.ko};
+    ck_prefix_kernel<<<grid(n), 256, 0, s>>>(d_src, R.ko, R.kl, R.tx, n, A.p0, A.p1, A.tx, A.kl, A.id);
+    uint64_t nruns = ntables;
+    uint64_t *rb = pool.get<uint64_t>(nruns + 2);
+    uint64_t *rb2 = pool.get<uint64_t>(nruns + 2);
+    CK(hipMemcpyAsync(rb, run_start.data(), (nruns + 1) * 8, hipMemcpyHostToDevice, s));
+    unsigned long long *bad = reinterpret_cast<unsigned long long *>(pool.get<uint64_t>(1));
+    CK(hipMemsetAsync(bad, 0, 8, s));
+    ck_check_sorted_kernel<<<grid(n), 256, 0, s>>>(A, rb, nruns, n, kv, bad);
+    if (read1(bad, s)) {
+      err = "input SST records are not sorted (key asc, txn desc)";
+      return SSTC_E_INVALID_ARG;
+    }
+    while (nruns > 1) {
+      ck_merge_kernel<<<grid((n + kMergeItems - 1) / kMergeItems), 256, 0, s>>>(A, B, rb, nruns, n, kv);
+      ck_runs_next_kernel<<<grid(nruns + 2), 256, 0, s>>>(rb, nruns, rb2);
+      std::swap(A, B);
+      std::swap(rb, rb2);
+      nruns = (nruns + 1) / 2;
+    }
+    // 3. keep / drop
+    uint64_t *head = pool.get<uint64_t>(n), *G = pool.get<uint64_t>(n + 1), *hp = pool.get<uint64_t>(n);
+    uint64_t *keep = pool.get<uint64_t>(n), *K = pool.get<uint64_t>(n + 1);
+    ck_head_kernel<<<grid(n), 256, 0, s>>>(A, n, kv, head);
+    CK(launch_scan(head, n, 0, G, ws2, s));
+    ck_headpos_kernel<<<grid(n), 256, 0, s>>>(head, G, n, hp);
+    // G[i] (exclusive) + head[i] - 1 = group id; for a non-head i the group id is G[i] - 1
+    ck_keep_kernel<<<grid(n), 256, 0, s>>>(A, head, G, hp, R.type, n, base_level, keep);
+    CK(launch_scan(keep, n, 0, K, ws2, s));
+    const uint64_t m = read1(K + n, s);
+    res[1] = m;
+    Rec KR{pool.get<uint8_t>(m), pool.get<uint32_t>(m), pool.get<uint32_t>(m), pool.get<uint64_t>(m),
+           pool.get<uint64_t>(m), pool.get<uint64_t>(m)};
+    uint64_t *dw = pool.get<uint64_t>(m), *ew = pool.get<uint64_t>(m);
+    ck_gather_kernel<<<grid(n), 256, 0, s>>>(A, keep, K, R, n, KR, dw, ew);
+    // 4. table split then block split (clamped at table ends)
+    uint64_t *tf = pool.get<uint64_t>(m + 1);
+    const uint64_t nt = segment(pool, dw, m, table_limit, nullptr, tf, ws2, s);
+    if (nt > max_tables) {
+      err = "more output tables than max_tables";
+      return SSTC_E_CAPACITY;
+    }
+    uint32_t *clamp = pool.get<uint32_t>(m + 1);
+    ck_table_end_kernel<<<grid(m + 1), 256, 0, s>>>(tf, nt, m, clamp);
+    uint64_t *ew16 = pool.get<uint64_t>(m);
+    CK(launch_enc_sizes(KR.kl, KR.vl, m, 16, ew16, s)); // block weight: entry + offset entry
+    uint64_t *bf = pool.get<uint64_t>(m + 1);
+    const uint64_t nb = segment(pool, ew16, m, block_threshold, clamp, bf, ws2, s);
+    // 5. layout
+    uint64_t *Pe = pool.get<uint64_t>(m + 1);
+    CK(launch_scan(ew, m, 0, Pe, ws2, s));
+    uint64_t *blen = pool.get<uint64_t>(nb), *msz = pool.get<uint64_t>(nb);
+    uint32_t *btab = pool.get<uint32_t>(nb);
+    ck_block_info_kernel<<<grid(nb), 256, 0, s>>>(bf, nb, Pe, KR.kl, tf, nt, blen, msz, btab);
+    uint64_t *BL = pool.get<uint64_t>(nb + 1), *MS = pool.get<uint64_t>(nb + 1);
+    CK(launch_scan(blen, nb, 0, BL, ws2, s));
+    CK(launch_scan(msz, nb, 0, MS, ws2, s));
+    uint64_t *tbf = pool.get<uint64_t>(nt + 1), *tdata = pool.get<uint64_t>(nt), *tmeta = pool.get<uint64_t>(nt);
+    ck_table_info_kernel<<<grid(nt + 1), 256, 0, s>>>(tf, nt, bf, nb, BL, MS, tbf, tdata, tmeta, d_table_len);
+    CK(launch_scan(d_table_len, nt, 0, d_table_off, ws2, s)); // d_table_off needs nt + 1 elements
+    const uint64_t total = read1(d_table_off + nt, s);
+    res[2] = nb;
+    res[3] = nt;
+    res[4] = total;
+    if (total > dst_cap) {
+      err = "output buffer too small";
+      return SSTC_E_CAPACITY;
+    }
+    uint64_t *bo = pool.get<uint64_t>(nb);
+    ck_block_off_kernel<<<grid(nb), 256, 0, s>>>(btab, nb, BL, tbf, d_table_off, bo);
+    // 6. encode blocks, meta entries, footers
+    EncArgs ea{d_src, d_src, sstc_records{KR.type, KR.kl, KR.vl, KR.tx, KR.ko, KR.vo}, bf, nb, Pe, bo, blen, d_dst};
+    CK(launch_enc_emit(ea, s));
+    ck_meta_kernel<<<grid(nb), 256, 0, s>>>(bf, nb, btab, BL, MS, blen, tbf, d_table_off, tdata, KR, d_src, d_dst);
+    ck_footer_kernel<<<static_cast<uint32_t>(nt), 256, 0, s>>>(tf, tbf, d_table_off, tdata, tmeta, KR, d_dst);
+    CK(hipGetLastError());
+    CK(hipStreamSynchronize(s));
+    return SSTC_OK;
+  } catch (const std::exception &e) {
+    err = e.what();
+    return SSTC_E_HIP;
+  }
+}
+
+} // namespace sstc

@@ -620,7 +620,7 @@ __global__ __launch_bounds__(kEncThreads) void enc_emit_kernel(EncArgs a) {
 // nxt[i] = one past the last record of a block that starts at record i;
 // chain from 0 = block starts.  J_{k+1} = J_k o J_k.
 // ---------------------------------------------------------------------------
-__global__ void seg_next_kernel(const uint64_t *Pw, uint64_t nrec, uint64_t threshold,
+__global__ void seg_next_kernel(const uint64_t *Pw, uint64_t nrec, uint64_t threshold, const uint32_t *clamp,
                                 uint32_t *J0) {
   const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (i > nrec) return;
@@ -628,12 +628,15 @@ __global__ void seg_next_kernel(const uint64_t *Pw, uint64_t nrec, uint64_t thre
     J0[i] = static_cast<uint32_t>(nrec);
     return;
   }
+  // clamp[i]: one past the last record the block starting at i may hold (the
+  // end of its output table); nrec when null
+  const uint64_t lim = clamp ? clamp[i] : nrec;
   const uint64_t target = Pw[i] + threshold; // first e >= i with Pw[e+1] >= target
-  if (Pw[nrec] < target) {
-    J0[i] = static_cast<uint32_t>(nrec);
+  if (Pw[lim] < target) {
+    J0[i] = static_cast<uint32_t>(lim);
     return;
   }
-  uint64_t lo = i, hi = nrec - 1;
+  uint64_t lo = i, hi = lim - 1;
   while (lo < hi) {
     const uint64_t mid = (lo + hi) >> 1;
     if (Pw[mid + 1] >= target) hi = mid;
@@ -801,9 +804,10 @@ hipError_t launch_enc_emit(const EncArgs &a, hipStream_t s) {
 }
 
 hipError_t launch_segment(const uint64_t *Pw, uint64_t nrec, uint64_t threshold, uint32_t *J,
-                          uint32_t levels, uint64_t *d_nblocks, uint64_t *blk_first, hipStream_t s) {
+                          uint32_t levels, uint64_t *d_nblocks, uint64_t *blk_first, hipStream_t s,
+                          const uint32_t *clamp) {
   const uint64_t stride = nrec + 1;
-  seg_next_kernel<<<grid_for(nrec + 1, 256), 256, 0, s>>>(Pw, nrec, threshold, J);
+  seg_next_kernel<<<grid_for(nrec + 1, 256), 256, 0, s>>>(Pw, nrec, threshold, clamp, J);
   for (uint32_t k = 0; k + 1 < levels; k++)
     seg_double_kernel<<<grid_for(nrec + 1, 256), 256, 0, s>>>(J + k * stride, J + (k + 1) * stride, nrec);
   seg_depth_kernel<<<1, 64, 0, s>>>(J, levels, stride, nrec, d_nblocks, blk_first);

@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <string>
+
 #include "../../include/sstcodec.h"
 
 namespace sstc {
@@ -60,6 +62,13 @@ hipError_t launch_enc_blk_len(const uint64_t *P, const uint64_t *blk_first, uint
                               uint64_t *blk_len, hipStream_t s);
 hipError_t launch_enc_emit(const EncArgs &a, hipStream_t s);
 hipError_t launch_segment(const uint64_t *Pw, uint64_t nrec, uint64_t threshold, uint32_t *J,
-                          uint32_t levels, uint64_t *d_nblocks, uint64_t *blk_first, hipStream_t s);
+                          uint32_t levels, uint64_t *d_nblocks, uint64_t *blk_first, hipStream_t s,
+                          const uint32_t *clamp = nullptr);
+
+int compact_impl(hipStream_t s, unsigned long long *err_count, const uint8_t *d_src, const uint64_t *d_blk_off,
+                 const uint64_t *d_blk_len, uint64_t nblocks, const uint64_t *h_tfb, uint32_t ntables,
+                 uint64_t block_threshold, uint64_t table_limit, uint32_t base_level, uint32_t txn_mode,
+                 uint8_t *d_dst, uint64_t dst_cap, uint64_t *d_table_off, uint64_t *d_table_len, uint64_t max_tables,
+                 uint64_t *res, std::string &err);
 
 } // namespace sstc

@@ -31,6 +31,16 @@ class Records(ctypes.Structure):
                 ("key_off", c_vp), ("val_off", c_vp)]
 
 
+class CompactParams(ctypes.Structure):
+    _fields_ = [("block_threshold", ctypes.c_uint64), ("table_limit", ctypes.c_uint64),
+                ("base_level", ctypes.c_uint32), ("txn_mode", ctypes.c_uint32)]
+
+
+class CompactResult(ctypes.Structure):
+    _fields_ = [("records_in", ctypes.c_uint64), ("records_kept", ctypes.c_uint64),
+                ("blocks_out", ctypes.c_uint64), ("tables_out", ctypes.c_uint64), ("bytes_out", ctypes.c_uint64)]
+
+
 class SstcError(RuntimeError):
     pass
 
@@ -63,6 +73,8 @@ def load():
         "sstc_encode_blocks": (ctypes.c_int, [c_vp, c_vp, c_vp, Records, c_u64, c_vp, c_u64, c_u64,
                                               c_vp, c_vp, c_vp]),
         "sstc_roundtrip_blocks": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_u64, c_u32, c_vp, c_vp]),
+        "sstc_compact": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_u64, c_vp, c_u32, P(CompactParams), c_vp, c_u64,
+                                        c_vp, c_vp, c_u64, P(CompactResult)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

@@ -165,3 +165,66 @@ class Codec:
                                           nb, int(out_base), _p(dst), _p(out_off), _p(out_len)),
               "sstc_encode_blocks")
         return dst, out_off, out_len[:nb]
+
+    # ---- compaction ----------------------------------------------------------
+    def compact(self, tables, block_threshold=4096, table_limit=32 << 20, base_level=1,
+                txn_mode=_lib.SSTC_TXN_COMPAT):
+        """Compact SST images (list of numpy u8 arrays, iterator order) on the
+        GPU.  Returns (list of output SST images as numpy arrays, result)."""
+        import numpy as np
+        from ._lib import CompactParams, CompactResult
+        if isinstance(tables, (list, tuple)):
+            files = [np.ascontiguousarray(t, np.uint8) for t in tables]
+        else:
+            files = list(tables)
+        # block index of every table (host parse of footer + meta section)
+        offs, lens, tfb, bases = [], [], [0], []
+        base = 0
+        for f in files:
+            idx = _table_index(f)
+            offs.append(idx[0] + base)
+            lens.append(idx[1])
+            tfb.append(tfb[-1] + len(idx[0]))
+            bases.append(base)
+            base += f.size
+        src = torch.from_numpy(np.concatenate(files) if files else np.zeros(1, np.uint8)).to(self.device)
+        blk_off = torch.from_numpy(np.concatenate(offs).astype(np.uint64).view(np.int64) if offs else
+                                   np.zeros(0, np.int64)).to(self.device)
+        blk_len = torch.from_numpy(np.concatenate(lens).astype(np.uint64).view(np.int64) if lens else
+                                   np.zeros(0, np.int64)).to(self.device)
+        h_tfb = np.asarray(tfb, np.uint64)
+        cap = int(src.numel()) * 2 + 4096
+        dst = torch.zeros(cap, dtype=torch.uint8, device=self.device)
+        max_t = cap // 40 + 1
+        toff = torch.zeros(max_t + 1, dtype=torch.int64, device=self.device)
+        tlen = torch.zeros(max_t, dtype=torch.int64, device=self.device)
+        prm = CompactParams(block_threshold, table_limit, base_level, txn_mode)
+        res = CompactResult()
+        self._stream()
+        check(self.lib.sstc_compact(self.h, _p(src), _p(blk_off), _p(blk_len), int(blk_off.numel()),
+                                    h_tfb.ctypes.data_as(ctypes.c_void_p), len(files), ctypes.byref(prm), _p(dst),
+                                    cap, _p(toff), _p(tlen), max_t, ctypes.byref(res)), "sstc_compact")
+        nt = res.tables_out
+        o = toff[: nt + 1].cpu().numpy()
+        d = dst[: int(o[nt])].cpu().numpy()
+        return [d[int(o[t]):int(o[t + 1])] for t in range(nt)], res
+
+
+def _table_index(f):
+    """(block offsets, block sizes) of an SST image: footer + meta section walk
+    (reference table_reader.cc:52-156)."""
+    import numpy as np
+    b = f.size
+    foot = f[b - 40:].view(np.uint64)
+    nb, moff, mlen = int(foot[0]), int(foot[1]), int(foot[2])
+    meta = f[moff:moff + mlen].tobytes()
+    offs, lens = [], []
+    p = 0
+    for _ in range(nb):
+        fk = int.from_bytes(meta[p:p + 4], "little")
+        lk = int.from_bytes(meta[p + 4 + fk:p + 8 + fk], "little")
+        q = p + 8 + fk + lk
+        offs.append(int.from_bytes(meta[q:q + 8], "little"))
+        lens.append(int.from_bytes(meta[q + 8:q + 16], "little"))
+        p = q + 16
+    return np.asarray(offs, np.uint64), np.asarray(lens, np.uint64)

@@ -1,0 +1,100 @@
+"""GPU compaction job (sstc_compact) against the oracle and the outputs of the
+reference's own MergeIterator + TableBuilder (tests/golden/compaction.json)."""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+from conftest import GOLDEN, load_golden
+from sstcodec import workload as W
+
+pytestmark = pytest.mark.gpu
+CASES = json.load(open(os.path.join(GOLDEN, "compaction.json")))
+
+
+@pytest.fixture(scope="module")
+def codec():
+    import sstcodec
+    return sstcodec.Codec(0)
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a, np.uint8).tobytes()).hexdigest()
+
+
+@pytest.mark.parametrize("base", [1, 0])
+def test_compact_small_reference_bytes(codec, base):
+    g = load_golden(f"compact_small_base{base}.npz")
+    ins = [g[f"in{i}"] for i in range(4)]
+    outs, res = codec.compact(ins, 4096, 32 << 20, base)
+    want = [g[k] for k in sorted((k for k in g if k.startswith("out")), key=lambda x: int(x[3:]))]
+    assert len(outs) == len(want)
+    for o, w in zip(outs, want):
+        assert np.array_equal(o, w)
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+@pytest.mark.parametrize("base", [1, 0])
+def test_compact_reference_hashes(codec, oracle, name, base):
+    case = CASES[name]
+    sets = W.compaction_inputs(case["k"], case["n_per"], case["key_space"], vmax=case["vmax"],
+                               distinct=case["distinct"])
+    ins = [oracle.table_build(r, case["block_threshold"]) for r in sets]
+    outs, res = codec.compact(ins, case["block_threshold"], case["table_limit"], base)
+    want = case[f"outputs_base{base}"]
+    assert len(outs) == len(want)
+    for o, w in zip(outs, want):
+        assert o.size + 1 == w["file_size"] and sha(o) == w["sha256"]
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_compact_random_vs_oracle(codec, oracle, seed):
+    k = [2, 5, 8, 13][seed]
+    sets = W.compaction_inputs(k, 1500, 2500, seed=seed + 40, vmax=[50, 400, 900, 120][seed],
+                               p_delete=[0.0, 0.1, 0.5, 0.2][seed], distinct=seed != 3)
+    ins = [oracle.table_build(r, 4096) for r in sets]
+    limit = [1 << 30, 60_000, 150_000, 9_000][seed]
+    for base in (1, 0):
+        want, kept = oracle.compact(ins, 4096, limit, base)
+        outs, res = codec.compact(ins, 4096, limit, base)
+        assert res.records_kept == kept
+        assert len(outs) == len(want)
+        for o, w in zip(outs, want):
+            assert np.array_equal(o, w)
+
+
+def test_compact_long_keys_and_quirk(codec, oracle):
+    """Keys longer than the 16 B sort prefix sharing it, empty values (the
+    compat txn quirk changes merge order input), and a single input table."""
+    rng = np.random.default_rng(1)
+    sets = []
+    for t in range(3):
+        n = 400
+        idx = np.sort(rng.choice(600, n, replace=False))
+        keys = [b"PREFIX-0123456789-" + b"%06d" % i for i in idx]  # 24 B, common 16 B prefix
+        vals = [b"" if rng.random() < 0.2 else bytes(rng.integers(0, 256, int(rng.integers(1, 60)),
+                                                                  dtype=np.uint8)) for _ in range(n)]
+        ks = b"".join(keys)
+        vs = b"".join(vals)
+        rec = {"type": np.zeros(n, np.uint8), "key_len": np.array([len(k) for k in keys], np.uint32),
+               "val_len": np.array([len(v) for v in vals], np.uint32),
+               "txn": rng.permutation(np.arange(1, n + 1, dtype=np.uint64)) + np.uint64(t * 10000),
+               "key_off": np.cumsum([0] + [len(k) for k in keys[:-1]]).astype(np.uint64),
+               "val_off": np.cumsum([0] + [len(v) for v in vals[:-1]]).astype(np.uint64),
+               "key_src": np.frombuffer(ks, np.uint8).copy(), "val_src": np.frombuffer(vs + b"\0", np.uint8).copy()}
+        sets.append(rec)
+    ins = [oracle.table_build(r, 4096) for r in sets]
+    for tables in (ins, ins[:1]):
+        want, _ = oracle.compact(tables, 4096, 20_000, 1)
+        outs, _ = codec.compact(tables, 4096, 20_000, 1)
+        assert len(outs) == len(want)
+        for o, w in zip(outs, want):
+            assert np.array_equal(o, w)
+
+
+def test_compact_rejects_unsorted(codec, oracle):
+    rec = W.mixed_records(300, seed=2)  # random keys: not sorted
+    f = oracle.table_build(rec, 4096)
+    with pytest.raises(Exception):
+        codec.compact([f], 4096, 1 << 20, 1)
