@@ -36,28 +36,35 @@ struct KeyView {
   const uint64_t *koff; // by record id
 };
 
-__device__ __forceinline__ uint64_t be_prefix(const uint8_t *p, uint32_t len, uint32_t from) {
-  uint64_t v = 0;
-#pragma unroll
-  for (uint32_t j = 0; j < 8; j++) {
-    const uint32_t b = from + j < len ? p[from + j] : 0u;
-    v = (v << 8) | b;
-  }
+// 16 B big-endian key prefix, zero padded.  Every key is followed in its block
+// by at least the 8 B txn + 16 B offset entry + 16 B extra, so the 16 B read is
+// inside the block.
+__device__ __forceinline__ uint64_t be_prefix8(const uint8_t *p, uint32_t len, uint32_t from) {
+  if (len <= from) return 0;
+  uint64_t v = __builtin_bswap64(g_u64u(p + from)); // first byte most significant
+  const uint32_t keep = len - from;
+  if (keep < 8) v &= ~0ull << (8 * (8 - keep));
   return v;
 }
 
+struct __attribute__((aligned(16))) SK {
+  uint64_t p0, p1, tx;
+  uint32_t kl, id;
+};
+
 __global__ void ck_prefix_kernel(const uint8_t *src, const uint64_t *koff, const uint32_t *klen,
-                                 const uint64_t *txn, uint64_t n, uint64_t *p0, uint64_t *p1, uint64_t *tx,
-                                 uint32_t *kl, uint32_t *id) {
+                                 const uint64_t *txn, uint64_t n, SK *out) {
   const uint64_t r = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (r >= n) return;
   const uint8_t *k = src + koff[r];
   const uint32_t l = klen[r];
-  p0[r] = be_prefix(k, l, 0);
-  p1[r] = be_prefix(k, l, 8);
-  tx[r] = txn[r];
-  kl[r] = l;
-  id[r] = static_cast<uint32_t>(r);
+  SK v;
+  v.p0 = be_prefix8(k, l, 0);
+  v.p1 = be_prefix8(k, l, 8);
+  v.tx = txn[r];
+  v.kl = l;
+  v.id = static_cast<uint32_t>(r);
+  out[r] = v;
 }
 
 // three-way key compare: prefix, then (only when both are longer than 16 B and
@@ -78,21 +85,16 @@ __device__ __forceinline__ int key_cmp(uint64_t a0, uint64_t a1, uint32_t al, ui
   return al < bl ? -1 : (al > bl ? 1 : 0);
 }
 
-struct Soa {
-  uint64_t *p0, *p1, *tx;
-  uint32_t *kl, *id;
-};
-
 // merge order: key asc, then txn desc (db/merge_iterator.h:91-95)
-__device__ __forceinline__ bool rec_less(const Soa &s, uint64_t a, uint64_t b, const KeyView &kv) {
-  const int c = key_cmp(s.p0[a], s.p1[a], s.kl[a], s.id[a], s.p0[b], s.p1[b], s.kl[b], s.id[b], kv);
-  return c < 0 || (c == 0 && s.tx[a] > s.tx[b]);
+__device__ __forceinline__ bool sk_less(const SK &a, const SK &b, const KeyView &kv) {
+  const int c = key_cmp(a.p0, a.p1, a.kl, a.id, b.p0, b.p1, b.kl, b.id, kv);
+  return c < 0 || (c == 0 && a.tx > b.tx);
 }
 
 // Sortedness of every input run (TableBuilder requires sorted input,
 // table_builder.h:77): a record may not sort before its predecessor.
-__global__ void ck_check_sorted_kernel(Soa s, const uint64_t *run_start, uint64_t nruns, uint64_t n, KeyView kv,
-                                       unsigned long long *bad) {
+__global__ void ck_check_sorted_kernel(const SK *s, const uint64_t *run_start, uint64_t nruns, uint64_t n,
+                                       KeyView kv, unsigned long long *bad) {
   const uint64_t r = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (r == 0 || r >= n) return;
   uint64_t lo = 0, hi = nruns; // run containing r: last run_start <= r
@@ -102,21 +104,21 @@ __global__ void ck_check_sorted_kernel(Soa s, const uint64_t *run_start, uint64_
     else hi = mid;
   }
   if (run_start[lo] == r) return; // first record of its run
-  if (rec_less(s, r, r - 1, kv)) atomicAdd(bad, 1ull);
+  if (sk_less(s[r], s[r - 1], kv)) atomicAdd(bad, 1ull);
 }
 
-constexpr uint32_t kMergeItems = 8;
+constexpr uint32_t kMergeItems = 16;
 
 // One round of pairwise stable merges: runs [rb[2j], rb[2j+1]) and
-// [rb[2j+1], rb[2j+2]) -> [rb[2j], rb[2j+2]) (ties: left run first).
-__global__ void ck_merge_kernel(Soa in, Soa out, const uint64_t *rb, uint64_t nruns, uint64_t n, KeyView kv) {
+// [rb[2j+1], rb[2j+2]) -> [rb[2j], rb[2j+2]) (ties: left run first).  Each
+// thread co-ranks its first output (merge path) then merges kMergeItems.
+__global__ void ck_merge_kernel(const SK *in, SK *out, const uint64_t *rb, uint64_t nruns, uint64_t n, KeyView kv) {
   const uint64_t k0 = (static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x) * kMergeItems;
   if (k0 >= n) return;
   const uint64_t npairs = (nruns + 1) / 2;
   uint64_t k = k0;
   const uint64_t kend = k0 + kMergeItems < n ? k0 + kMergeItems : n;
-  // pair holding k
-  uint64_t lo = 0, hi = npairs;
+  uint64_t lo = 0, hi = npairs; // pair holding k
   while (lo + 1 < hi) {
     const uint64_t mid = (lo + hi) >> 1;
     if (rb[2 * mid] <= k) lo = mid;
@@ -132,19 +134,23 @@ __global__ void ck_merge_kernel(Soa in, Soa out, const uint64_t *rb, uint64_t nr
     uint64_t l = kk > nb ? kk - nb : 0, h = kk < na ? kk : na;
     while (l < h) { // smallest i with B[kk-i-1] < A[i]
       const uint64_t mid = (l + h) >> 1;
-      if (rec_less(in, a1 + (kk - mid - 1), a0 + mid, kv)) h = mid;
+      if (sk_less(in[a1 + (kk - mid - 1)], in[a0 + mid], kv)) h = mid;
       else l = mid + 1;
     }
     uint64_t ia = a0 + l, ib = a1 + (kk - l);
     const uint64_t stop = kend < b1 ? kend : b1;
+    SK va, vb;
+    if (ia < a1) va = in[ia];
+    if (ib < b1) vb = in[ib];
     for (; k < stop; k++) {
-      const bool take_a = ia < a1 && (ib >= b1 || !rec_less(in, ib, ia, kv));
-      const uint64_t src = take_a ? ia++ : ib++;
-      out.p0[k] = in.p0[src];
-      out.p1[k] = in.p1[src];
-      out.tx[k] = in.tx[src];
-      out.kl[k] = in.kl[src];
-      out.id[k] = in.id[src];
+      const bool take_a = ia < a1 && (ib >= b1 || !sk_less(vb, va, kv));
+      if (take_a) {
+        out[k] = va;
+        if (++ia < a1) va = in[ia];
+      } else {
+        out[k] = vb;
+        if (++ib < b1) vb = in[ib];
+      }
     }
     j++;
   }
@@ -158,12 +164,14 @@ __global__ void ck_runs_next_kernel(const uint64_t *rb, uint64_t nruns, uint64_t
 
 // head[i] = 1 if merged record i starts a key group (ShouldKeepEntry's
 // last_current_key != key, compact.cc:266-268)
-__global__ void ck_head_kernel(Soa s, uint64_t n, KeyView kv, uint64_t *head) {
+__global__ void ck_head_kernel(const SK *s, uint64_t n, KeyView kv, uint64_t *head) {
   const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint64_t h = 1;
-  if (i > 0)
-    h = key_cmp(s.p0[i - 1], s.p1[i - 1], s.kl[i - 1], s.id[i - 1], s.p0[i], s.p1[i], s.kl[i], s.id[i], kv) != 0;
+  if (i > 0) {
+    const SK a = s[i - 1], b = s[i];
+    h = key_cmp(a.p0, a.p1, a.kl, a.id, b.p0, b.p1, b.kl, b.id, kv) != 0;
+  }
   head[i] = h;
 }
 
@@ -174,7 +182,7 @@ __global__ void ck_headpos_kernel(const uint64_t *head, const uint64_t *G, uint6
 }
 
 // ShouldKeepEntry (compact.cc:324-363)
-__global__ void ck_keep_kernel(Soa s, const uint64_t *head, const uint64_t *G, const uint64_t *hp,
+__global__ void ck_keep_kernel(const SK *s, const uint64_t *head, const uint64_t *G, const uint64_t *hp,
                                const uint8_t *type, uint64_t n, uint32_t base_level, uint64_t *keep) {
   const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -182,10 +190,10 @@ __global__ void ck_keep_kernel(Soa s, const uint64_t *head, const uint64_t *G, c
   if (i == 0) {
     k = 1; // first record of the merge is always kept
   } else if (head[i]) {
-    k = type[s.id[i]] == kTypePut ? 1 : (base_level ? 0 : 1);
+    k = type[s[i].id] == kTypePut ? 1 : (base_level ? 0 : 1);
   } else {
     const uint64_t h = hp[G[i] - 1]; // this group's head
-    k = s.tx[h] > s.tx[i] ? 0 : 1;   // drop if last_txn > txn
+    k = s[h].tx > s[i].tx ? 0 : 1;   // drop if last_txn > txn
   }
   keep[i] = k;
 }
@@ -196,12 +204,12 @@ struct Rec {
   uint64_t *tx, *ko, *vo;
 };
 
-__global__ void ck_gather_kernel(Soa s, const uint64_t *keep, const uint64_t *K, Rec R, uint64_t n, Rec out,
+__global__ void ck_gather_kernel(const SK *s, const uint64_t *keep, const uint64_t *K, Rec R, uint64_t n, Rec out,
                                  uint64_t *dw, uint64_t *ew) {
   const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (i >= n || !keep[i]) return;
   const uint64_t o = K[i];
-  const uint32_t r = s.id[i];
+  const uint32_t r = s[i].id;
   const uint32_t vl = R.vl[r];
   out.type[o] = R.type[r];
   out.kl[o] = R.kl[r];
@@ -308,37 +316,42 @@ __global__ void ck_meta_kernel(const uint64_t *bf, uint64_t nb, const uint32_t *
   put_le(p + 16 + fk + lk, blen[b], 8);
 }
 
-// footer of table t (table_builder.cc:179-211); one workgroup per table also
-// reduces min/max txn over the table's records
-__global__ __launch_bounds__(256) void ck_footer_kernel(const uint64_t *tf, const uint64_t *tbf,
-                                                        const uint64_t *toff, const uint64_t *tdata,
-                                                        const uint64_t *tmeta, Rec K, uint8_t *dst) {
-  __shared__ uint64_t smn[256], smx[256];
-  const uint64_t t = blockIdx.x;
+// min / max txn of every output table: one wave per block, one atomic per
+// block and table (table_builder.cc:47-49 tracks them per AddEntry)
+__global__ void ck_minmax_kernel(const uint64_t *bf, uint64_t nb, const uint32_t *btab, Rec K,
+                                 unsigned long long *tmin, unsigned long long *tmax) {
+  const uint64_t b = (static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x) / kWave;
+  if (b >= nb) return;
+  const uint32_t lane = lane_id();
   uint64_t mn = ~0ull, mx = 0;
-  for (uint64_t r = tf[t] + threadIdx.x; r < tf[t + 1]; r += 256) {
+  for (uint64_t r = bf[b] + lane; r < bf[b + 1]; r += kWave) {
     const uint64_t x = K.tx[r];
     mn = x < mn ? x : mn;
     mx = x > mx ? x : mx;
   }
-  smn[threadIdx.x] = mn;
-  smx[threadIdx.x] = mx;
-  __syncthreads();
-  for (uint32_t d = 128; d > 0; d >>= 1) {
-    if (threadIdx.x < d) {
-      smn[threadIdx.x] = smn[threadIdx.x + d] < smn[threadIdx.x] ? smn[threadIdx.x + d] : smn[threadIdx.x];
-      smx[threadIdx.x] = smx[threadIdx.x + d] > smx[threadIdx.x] ? smx[threadIdx.x + d] : smx[threadIdx.x];
-    }
-    __syncthreads();
+  for (uint32_t d = kWave / 2; d > 0; d >>= 1) {
+    const uint64_t a = __shfl_xor(mn, d, kWave), c = __shfl_xor(mx, d, kWave);
+    mn = a < mn ? a : mn;
+    mx = c > mx ? c : mx;
   }
-  if (threadIdx.x == 0) {
-    uint8_t *p = dst + toff[t] + tdata[t] + tmeta[t];
-    put_le(p, tbf[t + 1] - tbf[t], 8);
-    put_le(p + 8, tdata[t], 8);
-    put_le(p + 16, tmeta[t], 8);
-    put_le(p + 24, smn[0], 8);
-    put_le(p + 32, smx[0], 8);
+  if (lane == 0) {
+    atomicMin(tmin + btab[b], static_cast<unsigned long long>(mn));
+    atomicMax(tmax + btab[b], static_cast<unsigned long long>(mx));
   }
+}
+
+// footer of table t (table_builder.cc:179-211)
+__global__ void ck_footer_kernel(uint64_t nt, const uint64_t *tbf, const uint64_t *toff, const uint64_t *tdata,
+                                 const uint64_t *tmeta, const unsigned long long *tmin,
+                                 const unsigned long long *tmax, uint8_t *dst) {
+  const uint64_t t = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (t >= nt) return;
+  uint8_t *p = dst + toff[t] + tdata[t] + tmeta[t];
+  put_le(p, tbf[t + 1] - tbf[t], 8);
+  put_le(p + 8, tdata[t], 8);
+  put_le(p + 16, tmeta[t], 8);
+  put_le(p + 24, tmin[t], 8);
+  put_le(p + 32, tmax[t], 8);
 }
 
 // ------------------------------------------------------------------ host side
@@ -381,10 +394,15 @@ template <class T> T read1(const T *d, hipStream_t s) {
 
 // greedy segmentation of [0, m) by weights w (>= threshold closes), optional clamp
 uint64_t segment(Pool &pool, const uint64_t *w, uint64_t m, uint64_t threshold, const uint32_t *clamp,
-                 uint64_t *first, uint64_t *ws, hipStream_t s) {
+                 uint64_t nclamps, uint64_t *first, uint64_t *ws, hipStream_t s) {
   uint64_t *Pw = pool.get<uint64_t>(m + 1);
   CK(launch_scan(w, m, 0, Pw, ws, s));
-  const uint32_t levels = bitlen(m);
+  // every segment but the last one of each clamp range reaches the threshold,
+  // so the chain from record 0 has at most total / threshold + nclamps + 1
+  // nodes: that many doubling levels suffice
+  const uint64_t total = read1(Pw + m, s);
+  const uint64_t chain = total / threshold + nclamps + 1;
+  const uint32_t levels = bitlen(chain < m ? chain : m);
   uint32_t *J = pool.get<uint32_t>(static_cast<uint64_t>(levels) * (m + 1));
   uint64_t *dn = pool.get<uint64_t>(1);
   CK(launch_segment(Pw, m, threshold, J, levels, dn, first, s, clamp));
@@ -447,12 +465,9 @@ int compact_impl(hipStream_t s, unsigned long long *err_count, const uint8_t *d_
       return SSTC_OK;
     }
     // 2. sort keys + merge
-    Soa A{pool.get<uint64_t>(n), pool.get<uint64_t>(n), pool.get<uint64_t>(n), pool.get<uint32_t>(n),
-          pool.get<uint32_t>(n)};
-    Soa B{pool.get<uint64_t>(n), pool.get<uint64_t>(n), pool.get<uint64_t>(n), pool.get<uint32_t>(n),
-          pool.get<uint32_t>(n)};
+    SK *A = pool.get<SK>(n), *B = pool.get<SK>(n);
     const KeyView kv{d_src, R.ko};
-    ck_prefix_kernel<<<grid(n), 256, 0, s>>>(d_src, R.ko, R.kl, R.tx, n, A.p0, A.p1, A.tx, A.kl, A.id);
+    ck_prefix_kernel<<<grid(n), 256, 0, s>>>(d_src, R.ko, R.kl, R.tx, n, A);
     uint64_t nruns = ntables;
     uint64_t *rb = pool.get<uint64_t>(nruns + 2);
     uint64_t *rb2 = pool.get<uint64_t>(nruns + 2);
@@ -488,7 +503,7 @@ int compact_impl(hipStream_t s, unsigned long long *err_count, const uint8_t *d_
     ck_gather_kernel<<<grid(n), 256, 0, s>>>(A, keep, K, R, n, KR, dw, ew);
     // 4. table split then block split (clamped at table ends)
     uint64_t *tf = pool.get<uint64_t>(m + 1);
-    const uint64_t nt = segment(pool, dw, m, table_limit, nullptr, tf, ws2, s);
+    const uint64_t nt = segment(pool, dw, m, table_limit, nullptr, 0, tf, ws2, s);
     if (nt > max_tables) {
       err = "more output tables than max_tables";
       return SSTC_E_CAPACITY;
@@ -498,7 +513,7 @@ int compact_impl(hipStream_t s, unsigned long long *err_count, const uint8_t *d_
     uint64_t *ew16 = pool.get<uint64_t>(m);
     CK(launch_enc_sizes(KR.kl, KR.vl, m, 16, ew16, s)); // block weight: entry + offset entry
     uint64_t *bf = pool.get<uint64_t>(m + 1);
-    const uint64_t nb = segment(pool, ew16, m, block_threshold, clamp, bf, ws2, s);
+    const uint64_t nb = segment(pool, ew16, m, block_threshold, clamp, nt, bf, ws2, s);
     // 5. layout
     uint64_t *Pe = pool.get<uint64_t>(m + 1);
     CK(launch_scan(ew, m, 0, Pe, ws2, s));
@@ -525,7 +540,12 @@ int compact_impl(hipStream_t s, unsigned long long *err_count, const uint8_t *d_
     EncArgs ea{d_src, d_src, sstc_records{KR.type, KR.kl, KR.vl, KR.tx, KR.ko, KR.vo}, bf, nb, Pe, bo, blen, d_dst};
     CK(launch_enc_emit(ea, s));
     ck_meta_kernel<<<grid(nb), 256, 0, s>>>(bf, nb, btab, BL, MS, blen, tbf, d_table_off, tdata, KR, d_src, d_dst);
-    ck_footer_kernel<<<static_cast<uint32_t>(nt), 256, 0, s>>>(tf, tbf, d_table_off, tdata, tmeta, KR, d_dst);
+    unsigned long long *tmin = reinterpret_cast<unsigned long long *>(pool.get<uint64_t>(nt));
+    unsigned long long *tmax = reinterpret_cast<unsigned long long *>(pool.get<uint64_t>(nt));
+    CK(hipMemsetAsync(tmin, 0xFF, nt * 8, s));
+    CK(hipMemsetAsync(tmax, 0, nt * 8, s));
+    ck_minmax_kernel<<<grid(nb * kWave), 256, 0, s>>>(bf, nb, btab, KR, tmin, tmax);
+    ck_footer_kernel<<<grid(nt), 256, 0, s>>>(nt, tbf, d_table_off, tdata, tmeta, tmin, tmax, d_dst);
     CK(hipGetLastError());
     CK(hipStreamSynchronize(s));
     return SSTC_OK;

@@ -522,6 +522,9 @@ __global__ void enc_blk_len_kernel(const uint64_t *P, const uint64_t *blk_first,
 // is funnel-shifted from five source dwords; any other chunk is assembled byte
 // by byte through a per-thread LDS slot.
 constexpr uint32_t kEncThreads = 256;
+constexpr uint32_t kEncWaves = 4;
+constexpr uint32_t kEncSlot = 4608;       // LDS image bytes per wave (enc_lds_kernel)
+constexpr uint32_t kEncMaxRec = 160;      // > (4608 - 16) / 29 entries
 
 __device__ __forceinline__ u32x4 load16_unaligned(const uint8_t *p) {
   const uintptr_t a = reinterpret_cast<uintptr_t>(p);
@@ -537,9 +540,7 @@ __device__ __forceinline__ u32x4 load16_unaligned(const uint8_t *p) {
   return v;
 }
 
-__global__ __launch_bounds__(kEncThreads) void enc_emit_kernel(EncArgs a) {
-  __shared__ __attribute__((aligned(16))) uint8_t slot[kEncThreads * 16];
-  const uint64_t b = blockIdx.x;
+__device__ void enc_emit_block(const EncArgs &a, uint64_t b, uint8_t *slot) {
   const uint32_t tid = threadIdx.x;
   const uint64_t f0 = a.blk_first[b], f1 = a.blk_first[b + 1];
   const uint64_t n = f1 - f0;
@@ -547,6 +548,7 @@ __global__ __launch_bounds__(kEncThreads) void enc_emit_kernel(EncArgs a) {
   const uint64_t D = a.P[f1] - P0;
   const uint64_t bo = a.out_blk_off[b];
   const uint64_t L = a.out_blk_len[b];
+  if ((bo & 15) + L + 16 <= kEncSlot) return; // encoded by enc_lds_kernel
   uint8_t *dst = a.dst;
   uint8_t *my = slot + 16 * tid;
 
@@ -613,6 +615,106 @@ __global__ __launch_bounds__(kEncThreads) void enc_emit_kernel(EncArgs a) {
                                   reinterpret_cast<u32x4 *>(dst + 16 * c));
     }
   }
+}
+
+
+__global__ __launch_bounds__(kEncThreads) void enc_emit_kernel(EncArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t slot[kEncThreads * 16];
+  for (uint64_t b = blockIdx.x; b < a.nblocks; b += gridDim.x) enc_emit_block(a, b, slot);
+}
+
+
+// Small-block encode: one wave per block, the block is assembled in an LDS
+// image then written with 16 B stores (as rt_kernel).  Phase 1, lane per
+// record: type, key_len, val_len, txn, offset entry (start, size), extra.
+// Phase 2, lane per image dword: the key / value bytes it holds (a dword
+// overlaps at most one span: spans of one record are 4 B apart and records are
+// >= 13 B), a whole dword from an unaligned 4-byte global read, a partial one
+// byte by byte.  Phases write disjoint bytes.
+__global__ __launch_bounds__(kEncWaves *kWave) void enc_lds_kernel(EncArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kEncWaves * kEncSlot];
+  __shared__ uint32_t starts_all[kEncWaves * kEncMaxRec];
+  const uint32_t wave = uniform(threadIdx.x / kWave);
+  const uint32_t lane = lane_id();
+  const uint64_t b = static_cast<uint64_t>(blockIdx.x) * kEncWaves + wave;
+  if (b >= a.nblocks) return;
+  uint8_t *img = lds + wave * kEncSlot;
+  uint32_t *starts = starts_all + wave * kEncMaxRec;
+  const uint64_t bo = uniform64(a.out_blk_off[b]);
+  const uint64_t L64 = uniform64(a.out_blk_len[b]);
+  const uint32_t pad = static_cast<uint32_t>(bo & 15u);
+  if (pad + L64 + 16 > kEncSlot) return; // large block: enc_emit_kernel
+  const uint32_t L = static_cast<uint32_t>(L64);
+  const uint64_t f0 = uniform64(a.blk_first[b]);
+  const uint32_t n = static_cast<uint32_t>(uniform64(a.blk_first[b + 1]) - f0);
+  const uint64_t P0 = uniform64(a.P[f0]);
+  const uint32_t D = static_cast<uint32_t>(uniform64(a.P[f0 + n]) - P0);
+  uint8_t *im = img + pad; // image byte 0 == block byte 0
+
+  // phase 1
+  for (uint32_t i = lane; i < n; i += kWave) {
+    const uint64_t r = f0 + i;
+    const uint32_t o = static_cast<uint32_t>(a.P[r] - P0);
+    const uint32_t sz = static_cast<uint32_t>(a.P[r + 1] - a.P[r]);
+    const uint32_t kl = a.in.key_len[r], vl = a.in.val_len[r];
+    starts[i] = o;
+    im[o] = a.in.type[r];
+    for (int j = 0; j < 4; j++) im[o + 1 + j] = static_cast<uint8_t>(kl >> (8 * j));
+    uint32_t t = o + 5 + kl;
+    if (vl != kNoValue) {
+      for (int j = 0; j < 4; j++) im[t + j] = static_cast<uint8_t>(vl >> (8 * j));
+      t += 4 + vl;
+    }
+    const uint64_t tx = a.in.txn[r];
+    for (int j = 0; j < 8; j++) im[t + j] = static_cast<uint8_t>(tx >> (8 * j));
+    lds_st_u64u(im, D + 16 * i, o);
+    lds_st_u64u(im, D + 16 * i + 8, sz);
+  }
+  if (lane == 0) {
+    lds_st_u64u(im, D + 16 * n, n);
+    lds_st_u64u(im, D + 16 * n + 8, D);
+  }
+  wave_lds_sync();
+
+  // phase 2: image dwords covering the data section [pad, pad + D)
+  const uint32_t w_lo = pad >> 2, w_hi = (pad + D + 3) >> 2;
+  for (uint32_t w = w_lo + lane; w < w_hi; w += kWave) {
+    const int32_t x = static_cast<int32_t>(4 * w) - static_cast<int32_t>(pad); // block byte of the dword
+    const uint32_t xs = x < 0 ? 0u : static_cast<uint32_t>(x);
+    // record holding byte xs: last start <= xs
+    uint32_t lo = 0, hi = n;
+    while (lo + 1 < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (starts[mid] <= xs) lo = mid;
+      else hi = mid;
+    }
+    const uint64_t r = f0 + lo;
+    const uint32_t o = starts[lo];
+    const uint32_t kl = a.in.key_len[r], vl = a.in.val_len[r];
+    uint32_t s_lo, s_hi;
+    const uint8_t *sp;
+    const int32_t d0 = x, d1 = x + 4;
+    if (d0 < static_cast<int32_t>(o + 5 + kl) && d1 > static_cast<int32_t>(o + 5)) {
+      s_lo = o + 5;
+      s_hi = o + 5 + kl;
+      sp = a.key_src + a.in.key_off[r];
+    } else if (vl != kNoValue && d0 < static_cast<int32_t>(o + 9 + kl + vl) && d1 > static_cast<int32_t>(o + 9 + kl)) {
+      s_lo = o + 9 + kl;
+      s_hi = o + 9 + kl + vl;
+      sp = a.val_src + a.in.val_off[r];
+    } else {
+      continue; // header / txn bytes only (phase 1)
+    }
+    if (d0 >= static_cast<int32_t>(s_lo) && d1 <= static_cast<int32_t>(s_hi)) {
+      *reinterpret_cast<uint32_t *>(img + 4 * w) = g_u32u(sp + (d0 - s_lo));
+    } else {
+      const int32_t b0 = d0 > static_cast<int32_t>(s_lo) ? d0 : static_cast<int32_t>(s_lo);
+      const int32_t b1 = d1 < static_cast<int32_t>(s_hi) ? d1 : static_cast<int32_t>(s_hi);
+      for (int32_t y = b0; y < b1; y++) im[y] = sp[y - s_lo];
+    }
+  }
+  wave_lds_sync();
+  store_window(img, a.dst + (bo - pad), (pad + L + 15u) >> 4, 0, pad, pad + L);
 }
 
 // ---------------------------------------------------------------------------
@@ -799,7 +901,9 @@ hipError_t launch_enc_blk_len(const uint64_t *P, const uint64_t *blk_first, uint
 }
 
 hipError_t launch_enc_emit(const EncArgs &a, hipStream_t s) {
-  if (a.nblocks) enc_emit_kernel<<<static_cast<uint32_t>(a.nblocks), kEncThreads, 0, s>>>(a);
+  if (!a.nblocks) return hipSuccess;
+  enc_lds_kernel<<<grid_for(a.nblocks, kEncWaves), kEncWaves * kWave, 0, s>>>(a);
+  enc_emit_kernel<<<static_cast<uint32_t>(a.nblocks < 2048 ? a.nblocks : 2048), kEncThreads, 0, s>>>(a);
   return hipGetLastError();
 }
 
