@@ -36,36 +36,7 @@ struct KeyView {
   const uint64_t *koff; // by record id
 };
 
-// 16 B big-endian key prefix, zero padded.  Every key is followed in its block
-// by at least the 8 B txn + 16 B offset entry + 16 B extra, so the 16 B read is
-// inside the block.
-__device__ __forceinline__ uint64_t be_prefix8(const uint8_t *p, uint32_t len, uint32_t from) {
-  if (len <= from) return 0;
-  uint64_t v = __builtin_bswap64(g_u64u(p + from)); // first byte most significant
-  const uint32_t keep = len - from;
-  if (keep < 8) v &= ~0ull << (8 * (8 - keep));
-  return v;
-}
-
-struct __attribute__((aligned(16))) SK {
-  uint64_t p0, p1, tx;
-  uint32_t kl, id;
-};
-
-__global__ void ck_prefix_kernel(const uint8_t *src, const uint64_t *koff, const uint32_t *klen,
-                                 const uint64_t *txn, uint64_t n, SK *out) {
-  const uint64_t r = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (r >= n) return;
-  const uint8_t *k = src + koff[r];
-  const uint32_t l = klen[r];
-  SK v;
-  v.p0 = be_prefix8(k, l, 0);
-  v.p1 = be_prefix8(k, l, 8);
-  v.tx = txn[r];
-  v.kl = l;
-  v.id = static_cast<uint32_t>(r);
-  out[r] = v;
-}
+using SK = SortKey;
 
 // three-way key compare: prefix, then (only when both are longer than 16 B and
 // the prefixes tie) the remaining bytes, then the length (std::string_view <)
@@ -316,10 +287,10 @@ __global__ void ck_meta_kernel(const uint64_t *bf, uint64_t nb, const uint32_t *
   put_le(p + 16 + fk + lk, blen[b], 8);
 }
 
-// min / max txn of every output table: one wave per block, one atomic per
-// block and table (table_builder.cc:47-49 tracks them per AddEntry)
-__global__ void ck_minmax_kernel(const uint64_t *bf, uint64_t nb, const uint32_t *btab, Rec K,
-                                 unsigned long long *tmin, unsigned long long *tmax) {
+// min / max txn of every output table (table_builder.cc:47-49): one wave per
+// block reduces its records, then one workgroup per table reduces its blocks
+// (atomics on ~30 table words from 10^5 blocks would serialise)
+__global__ void ck_blk_minmax_kernel(const uint64_t *bf, uint64_t nb, Rec K, uint64_t *bmin, uint64_t *bmax) {
   const uint64_t b = (static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x) / kWave;
   if (b >= nb) return;
   const uint32_t lane = lane_id();
@@ -335,15 +306,43 @@ __global__ void ck_minmax_kernel(const uint64_t *bf, uint64_t nb, const uint32_t
     mx = c > mx ? c : mx;
   }
   if (lane == 0) {
-    atomicMin(tmin + btab[b], static_cast<unsigned long long>(mn));
-    atomicMax(tmax + btab[b], static_cast<unsigned long long>(mx));
+    bmin[b] = mn;
+    bmax[b] = mx;
+  }
+}
+
+__global__ __launch_bounds__(256) void ck_tab_minmax_kernel(const uint64_t *tbf, const uint64_t *bmin,
+                                                            const uint64_t *bmax, uint64_t *tmin, uint64_t *tmax) {
+  __shared__ uint64_t smn[256 / kWave], smx[256 / kWave];
+  const uint64_t t = blockIdx.x;
+  uint64_t mn = ~0ull, mx = 0;
+  for (uint64_t b = tbf[t] + threadIdx.x; b < tbf[t + 1]; b += 256) {
+    mn = bmin[b] < mn ? bmin[b] : mn;
+    mx = bmax[b] > mx ? bmax[b] : mx;
+  }
+  for (uint32_t d = kWave / 2; d > 0; d >>= 1) {
+    const uint64_t a = __shfl_xor(mn, d, kWave), c = __shfl_xor(mx, d, kWave);
+    mn = a < mn ? a : mn;
+    mx = c > mx ? c : mx;
+  }
+  if (lane_id() == 0) {
+    smn[threadIdx.x / kWave] = mn;
+    smx[threadIdx.x / kWave] = mx;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (uint32_t w = 1; w < 256 / kWave; w++) {
+      mn = smn[w] < mn ? smn[w] : mn;
+      mx = smx[w] > mx ? smx[w] : mx;
+    }
+    tmin[t] = mn;
+    tmax[t] = mx;
   }
 }
 
 // footer of table t (table_builder.cc:179-211)
 __global__ void ck_footer_kernel(uint64_t nt, const uint64_t *tbf, const uint64_t *toff, const uint64_t *tdata,
-                                 const uint64_t *tmeta, const unsigned long long *tmin,
-                                 const unsigned long long *tmax, uint8_t *dst) {
+                                 const uint64_t *tmeta, const uint64_t *tmin, const uint64_t *tmax, uint8_t *dst) {
   const uint64_t t = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (t >= nt) return;
   uint8_t *p = dst + toff[t] + tdata[t] + tmeta[t];
@@ -440,8 +439,9 @@ int compact_impl(hipStream_t s, unsigned long long *err_count, const uint8_t *d_
     Rec R{pool.get<uint8_t>(n), pool.get<uint32_t>(n), pool.get<uint32_t>(n), pool.get<uint64_t>(n),
           pool.get<uint64_t>(n), pool.get<uint64_t>(n)};
     uint32_t *status = pool.get<uint32_t>(nblocks);
+    SK *A = pool.get<SK>(n ? n : 1), *B = pool.get<SK>(n ? n : 1);
     DecArgs da{d_src, d_blk_off, d_blk_len, nblocks, rb_all,
-               sstc_records{R.type, R.kl, R.vl, R.tx, R.ko, R.vo}, txn_mode, status, err_count};
+               sstc_records{R.type, R.kl, R.vl, R.tx, R.ko, R.vo}, txn_mode, status, err_count, A};
     const unsigned long long errs0 = read1(err_count, s);
     CK(launch_decode(da, s));
     if (read1(err_count, s) != errs0) {
@@ -465,9 +465,7 @@ int compact_impl(hipStream_t s, unsigned long long *err_count, const uint8_t *d_
       return SSTC_OK;
     }
     // 2. sort keys + merge
-    SK *A = pool.get<SK>(n), *B = pool.get<SK>(n);
     const KeyView kv{d_src, R.ko};
-    ck_prefix_kernel<<<grid(n), 256, 0, s>>>(d_src, R.ko, R.kl, R.tx, n, A);
     uint64_t nruns = ntables;
     uint64_t *rb = pool.get<uint64_t>(nruns + 2);
     uint64_t *rb2 = pool.get<uint64_t>(nruns + 2);
@@ -540,11 +538,10 @@ int compact_impl(hipStream_t s, unsigned long long *err_count, const uint8_t *d_
     EncArgs ea{d_src, d_src, sstc_records{KR.type, KR.kl, KR.vl, KR.tx, KR.ko, KR.vo}, bf, nb, Pe, bo, blen, d_dst};
     CK(launch_enc_emit(ea, s));
     ck_meta_kernel<<<grid(nb), 256, 0, s>>>(bf, nb, btab, BL, MS, blen, tbf, d_table_off, tdata, KR, d_src, d_dst);
-    unsigned long long *tmin = reinterpret_cast<unsigned long long *>(pool.get<uint64_t>(nt));
-    unsigned long long *tmax = reinterpret_cast<unsigned long long *>(pool.get<uint64_t>(nt));
-    CK(hipMemsetAsync(tmin, 0xFF, nt * 8, s));
-    CK(hipMemsetAsync(tmax, 0, nt * 8, s));
-    ck_minmax_kernel<<<grid(nb * kWave), 256, 0, s>>>(bf, nb, btab, KR, tmin, tmax);
+    uint64_t *bmin = pool.get<uint64_t>(nb), *bmax = pool.get<uint64_t>(nb);
+    uint64_t *tmin = pool.get<uint64_t>(nt), *tmax = pool.get<uint64_t>(nt);
+    ck_blk_minmax_kernel<<<grid(nb * kWave), 256, 0, s>>>(bf, nb, KR, bmin, bmax);
+    ck_tab_minmax_kernel<<<static_cast<uint32_t>(nt), 256, 0, s>>>(tbf, bmin, bmax, tmin, tmax);
     ck_footer_kernel<<<grid(nt), 256, 0, s>>>(nt, tbf, d_table_off, tdata, tmeta, tmin, tmax, d_dst);
     CK(hipGetLastError());
     CK(hipStreamSynchronize(s));

@@ -133,6 +133,12 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Big-endian key bytes (first byte most significant) masked to the first
+// `keep` bytes (keep >= 8 keeps all 8).
+__device__ __forceinline__ uint64_t key_prefix8(uint64_t be, uint32_t keep) {
+  return keep >= 8 ? be : (be & (~0ull << (8 * (8 - keep))));
+}
+
 // One record's entry size (reference sstable/block_builder.cc:19-21).
 __device__ __forceinline__ uint64_t entry_size(uint32_t key_len, uint32_t val_len) {
   return 13ull + key_len + (val_len != kNoValue ? 4ull + val_len : 0ull);

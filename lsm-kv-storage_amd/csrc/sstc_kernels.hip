@@ -449,52 +449,74 @@ __global__ void count_kernel(const uint8_t *src, const uint64_t *blk_off, const 
 
 constexpr uint32_t kDecWaves = 4;
 
-__global__ __launch_bounds__(kDecWaves *kWave) void decode_kernel(DecArgs a) {
-  const uint32_t wave = uniform(threadIdx.x / kWave);
+// Parse one block into the record table (and, when asked, the 32 B sort keys
+// of the compaction merge).  R reads block bytes (LDS image or HBM).
+template <class R>
+__device__ __forceinline__ uint32_t decode_block(const DecArgs &a, const R &rd, uint64_t b, uint64_t off,
+                                                 uint64_t len) {
   const uint32_t lane = lane_id();
-  const uint64_t b = static_cast<uint64_t>(blockIdx.x) * kDecWaves + wave;
-  if (b >= a.nblocks) return;
-  const uint64_t off = uniform64(a.blk_off[b]);
-  const uint64_t len = uniform64(a.blk_len[b]);
   const uint64_t base = uniform64(a.rec_base[b]);
-  const uint8_t *blk = a.src + off;
-  const GlobalReader rd{blk};
-  uint32_t st = kBlkOk;
-  uint64_t n = 0, doff = 0;
-  if (len < 16) {
-    st = kBlkTooSmall;
-  } else {
-    n = rd.u64(len - 16);
-    doff = rd.u64(len - 8);
-    st = check_extra(len, n, doff);
-  }
+  const uint64_t n = uniform64(rd.u64(len - 16));
+  const uint64_t doff = uniform64(rd.u64(len - 8));
+  uint32_t st = check_extra(len, n, doff);
   if (st == kBlkOk && n != uniform64(a.rec_base[b + 1]) - base) st = kBlkCountMismatch;
-  if (st == kBlkOk) {
-    for (uint64_t i0 = 0; i0 < n; i0 += kWave) {
-      const uint64_t i = i0 + lane;
-      Entry e{};
-      uint64_t s = 0;
-      if (i < n) {
-        s = rd.u64(doff + 16 * i);
-        e = parse_entry(rd, s, doff, a.txn_mode);
-      }
-      const uint64_t bad = __ballot(e.code != kBlkOk);
-      if (bad) {
-        st = __shfl(e.code, __ffsll(static_cast<long long>(bad)) - 1, kWave);
-        break;
-      }
-      if (i < n) {
-        const uint64_t r = base + i;
-        a.out.type[r] = static_cast<uint8_t>(e.type);
-        a.out.key_len[r] = e.klen;
-        a.out.val_len[r] = e.vlen;
-        a.out.txn[r] = e.txn;
-        a.out.key_off[r] = off + s + 5;
-        a.out.val_off[r] = e.type != kTypeDeleted ? off + s + 9 + e.klen : 0;
+  if (st != kBlkOk) return st;
+  for (uint64_t i0 = 0; i0 < n; i0 += kWave) {
+    const uint64_t i = i0 + lane;
+    Entry e{};
+    uint64_t s = 0;
+    if (i < n) {
+      s = rd.u64(doff + 16 * i);
+      e = parse_entry(rd, s, doff, a.txn_mode);
+    }
+    const uint64_t bad = __ballot(e.code != kBlkOk);
+    if (bad) return __shfl(e.code, __ffsll(static_cast<long long>(bad)) - 1, kWave);
+    if (i < n) {
+      const uint64_t r = base + i;
+      a.out.type[r] = static_cast<uint8_t>(e.type);
+      a.out.key_len[r] = e.klen;
+      a.out.val_len[r] = e.vlen;
+      a.out.txn[r] = e.txn;
+      a.out.key_off[r] = off + s + 5;
+      a.out.val_off[r] = e.type != kTypeDeleted ? off + s + 9 + e.klen : 0;
+      if (a.sk) {
+        // 16 B big-endian key prefix (a key is followed by >= 40 B of block)
+        SortKey k;
+        k.p0 = e.klen ? key_prefix8(__builtin_bswap64(rd.u64(s + 5)), e.klen) : 0;
+        k.p1 = e.klen > 8 ? key_prefix8(__builtin_bswap64(rd.u64(s + 13)), e.klen - 8) : 0;
+        k.tx = e.txn;
+        k.kl = e.klen;
+        k.id = static_cast<uint32_t>(r);
+        a.sk[r] = k;
       }
     }
   }
-  if (lane == 0) {
+  return kBlkOk;
+}
+
+// One wave per block; a block that fits the LDS slot is staged by LDS-DMA and
+// parsed from LDS (the lane-per-entry header reads would otherwise be
+// dependent HBM round trips), a larger one is parsed from HBM.
+__global__ __launch_bounds__(kDecWaves *kWave) void decode_kernel(DecArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kDecWaves * kRtSlot];
+  const uint32_t wave = uniform(threadIdx.x / kWave);
+  const uint64_t b = static_cast<uint64_t>(blockIdx.x) * kDecWaves + wave;
+  if (b >= a.nblocks) return;
+  uint8_t *img = lds + wave * kRtSlot;
+  const uint64_t off = uniform64(a.blk_off[b]);
+  const uint64_t len = uniform64(a.blk_len[b]);
+  const uint32_t pad = static_cast<uint32_t>(off & 15u);
+  uint32_t st;
+  if (len < 16) {
+    st = kBlkTooSmall;
+  } else if (pad + len + 16 <= kRtSlot) {
+    rt_stage<1>(a.src + (off - pad), img, static_cast<uint32_t>((pad + len + 15) >> 4));
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    st = decode_block(a, LdsReader{img + pad}, b, off, len);
+  } else {
+    st = decode_block(a, GlobalReader{a.src + off}, b, off, len);
+  }
+  if (lane_id() == 0) {
     if (a.status) a.status[b] = st;
     if (st != kBlkOk) atomicAdd(a.err_count, 1ull);
   }
@@ -524,7 +546,7 @@ __global__ void enc_blk_len_kernel(const uint64_t *P, const uint64_t *blk_first,
 constexpr uint32_t kEncThreads = 256;
 constexpr uint32_t kEncWaves = 4;
 constexpr uint32_t kEncSlot = 4608;       // LDS image bytes per wave (enc_lds_kernel)
-constexpr uint32_t kEncMaxRec = 160;      // > (4608 - 16) / 29 entries
+constexpr uint32_t kEncMaxRec = 160;      // > (4608 - 16) / 29 entries per small block
 
 __device__ __forceinline__ u32x4 load16_unaligned(const uint8_t *p) {
   const uintptr_t a = reinterpret_cast<uintptr_t>(p);
@@ -626,20 +648,33 @@ __global__ __launch_bounds__(kEncThreads) void enc_emit_kernel(EncArgs a) {
 
 // Small-block encode: one wave per block, the block is assembled in an LDS
 // image then written with 16 B stores (as rt_kernel).  Phase 1, lane per
-// record: type, key_len, val_len, txn, offset entry (start, size), extra.
-// Phase 2, lane per image dword: the key / value bytes it holds (a dword
-// overlaps at most one span: spans of one record are 4 B apart and records are
-// >= 13 B), a whole dword from an unaligned 4-byte global read, a partial one
-// byte by byte.  Phases write disjoint bytes.
+// record: type, key_len, val_len, txn, offset entry (start, size), extra, and
+// the record's two copy spans (LDS-resident metadata).  Phase 2, lane per image
+// dword: the key / value bytes it holds (a dword overlaps at most one span:
+// spans of one record are 4 B apart, records are >= 13 B); the source reads of
+// kEncBatch dwords per lane are issued before any of them is consumed, so a
+// wave keeps ~128 loads in flight instead of one dependent chain.  Phases write
+// disjoint bytes.
+constexpr uint32_t kEncBatch = 16;
+
+struct EncMeta {
+  uint32_t *start;   // record start in the block
+  uint32_t *kspan;   // key span: dst (low 16) | len (high 16)
+  uint32_t *vspan;   // value span: dst | len (len 0 for no value)
+  const uint8_t **ksrc;
+  const uint8_t **vsrc;
+};
+
 __global__ __launch_bounds__(kEncWaves *kWave) void enc_lds_kernel(EncArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kEncWaves * kEncSlot];
-  __shared__ uint32_t starts_all[kEncWaves * kEncMaxRec];
+  __shared__ uint32_t m32[kEncWaves][3][kEncMaxRec];
+  __shared__ const uint8_t *m64[kEncWaves][2][kEncMaxRec];
   const uint32_t wave = uniform(threadIdx.x / kWave);
   const uint32_t lane = lane_id();
   const uint64_t b = static_cast<uint64_t>(blockIdx.x) * kEncWaves + wave;
   if (b >= a.nblocks) return;
   uint8_t *img = lds + wave * kEncSlot;
-  uint32_t *starts = starts_all + wave * kEncMaxRec;
+  const EncMeta M{m32[wave][0], m32[wave][1], m32[wave][2], m64[wave][0], m64[wave][1]};
   const uint64_t bo = uniform64(a.out_blk_off[b]);
   const uint64_t L64 = uniform64(a.out_blk_len[b]);
   const uint32_t pad = static_cast<uint32_t>(bo & 15u);
@@ -657,13 +692,20 @@ __global__ __launch_bounds__(kEncWaves *kWave) void enc_lds_kernel(EncArgs a) {
     const uint32_t o = static_cast<uint32_t>(a.P[r] - P0);
     const uint32_t sz = static_cast<uint32_t>(a.P[r + 1] - a.P[r]);
     const uint32_t kl = a.in.key_len[r], vl = a.in.val_len[r];
-    starts[i] = o;
+    M.start[i] = o;
+    M.kspan[i] = (o + 5) | (kl << 16);
+    M.ksrc[i] = a.key_src + a.in.key_off[r];
     im[o] = a.in.type[r];
     for (int j = 0; j < 4; j++) im[o + 1 + j] = static_cast<uint8_t>(kl >> (8 * j));
     uint32_t t = o + 5 + kl;
     if (vl != kNoValue) {
       for (int j = 0; j < 4; j++) im[t + j] = static_cast<uint8_t>(vl >> (8 * j));
+      M.vspan[i] = (t + 4) | (vl << 16);
+      M.vsrc[i] = a.val_src + a.in.val_off[r];
       t += 4 + vl;
+    } else {
+      M.vspan[i] = 0;
+      M.vsrc[i] = nullptr;
     }
     const uint64_t tx = a.in.txn[r];
     for (int j = 0; j < 8; j++) im[t + j] = static_cast<uint8_t>(tx >> (8 * j));
@@ -678,39 +720,60 @@ __global__ __launch_bounds__(kEncWaves *kWave) void enc_lds_kernel(EncArgs a) {
 
   // phase 2: image dwords covering the data section [pad, pad + D)
   const uint32_t w_lo = pad >> 2, w_hi = (pad + D + 3) >> 2;
-  for (uint32_t w = w_lo + lane; w < w_hi; w += kWave) {
-    const int32_t x = static_cast<int32_t>(4 * w) - static_cast<int32_t>(pad); // block byte of the dword
-    const uint32_t xs = x < 0 ? 0u : static_cast<uint32_t>(x);
-    // record holding byte xs: last start <= xs
-    uint32_t lo = 0, hi = n;
-    while (lo + 1 < hi) {
-      const uint32_t mid = (lo + hi) >> 1;
-      if (starts[mid] <= xs) lo = mid;
-      else hi = mid;
+  for (uint32_t wb = w_lo; wb < w_hi; wb += kWave * kEncBatch) {
+    uint32_t val[kEncBatch];
+    uint32_t full = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < kEncBatch; j++) {
+      const uint32_t w = wb + lane + kWave * j;
+      val[j] = 0;
+      if (w >= w_hi) continue;
+      const int32_t d0 = static_cast<int32_t>(4 * w) - static_cast<int32_t>(pad);
+      const uint32_t xs = d0 < 0 ? 0u : static_cast<uint32_t>(d0);
+      uint32_t lo = 0, hi = n;
+      while (lo + 1 < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (M.start[mid] <= xs) lo = mid;
+        else hi = mid;
+      }
+      const uint32_t ks = M.kspan[lo], vs = M.vspan[lo];
+      int32_t s0 = static_cast<int32_t>(ks & 0xFFFFu), s1 = s0 + static_cast<int32_t>(ks >> 16);
+      const uint8_t *sp = M.ksrc[lo];
+      if (!(d0 < s1 && d0 + 4 > s0)) {
+        s0 = static_cast<int32_t>(vs & 0xFFFFu);
+        s1 = s0 + static_cast<int32_t>(vs >> 16);
+        sp = M.vsrc[lo];
+      }
+      if (d0 >= s0 && d0 + 4 <= s1 && s1 > s0) {
+        val[j] = g_u32u(sp + (d0 - s0));
+        full |= 1u << j;
+      }
     }
-    const uint64_t r = f0 + lo;
-    const uint32_t o = starts[lo];
-    const uint32_t kl = a.in.key_len[r], vl = a.in.val_len[r];
-    uint32_t s_lo, s_hi;
-    const uint8_t *sp;
-    const int32_t d0 = x, d1 = x + 4;
-    if (d0 < static_cast<int32_t>(o + 5 + kl) && d1 > static_cast<int32_t>(o + 5)) {
-      s_lo = o + 5;
-      s_hi = o + 5 + kl;
-      sp = a.key_src + a.in.key_off[r];
-    } else if (vl != kNoValue && d0 < static_cast<int32_t>(o + 9 + kl + vl) && d1 > static_cast<int32_t>(o + 9 + kl)) {
-      s_lo = o + 9 + kl;
-      s_hi = o + 9 + kl + vl;
-      sp = a.val_src + a.in.val_off[r];
-    } else {
-      continue; // header / txn bytes only (phase 1)
-    }
-    if (d0 >= static_cast<int32_t>(s_lo) && d1 <= static_cast<int32_t>(s_hi)) {
-      *reinterpret_cast<uint32_t *>(img + 4 * w) = g_u32u(sp + (d0 - s_lo));
-    } else {
-      const int32_t b0 = d0 > static_cast<int32_t>(s_lo) ? d0 : static_cast<int32_t>(s_lo);
-      const int32_t b1 = d1 < static_cast<int32_t>(s_hi) ? d1 : static_cast<int32_t>(s_hi);
-      for (int32_t y = b0; y < b1; y++) im[y] = sp[y - s_lo];
+#pragma unroll
+    for (uint32_t j = 0; j < kEncBatch; j++) {
+      const uint32_t w = wb + lane + kWave * j;
+      if (w >= w_hi) continue;
+      if (full & (1u << j)) {
+        *reinterpret_cast<uint32_t *>(img + 4 * w) = val[j];
+        continue;
+      }
+      // partial dword at a span edge (or no span): byte copy of the span part
+      const int32_t d0 = static_cast<int32_t>(4 * w) - static_cast<int32_t>(pad);
+      const uint32_t xs = d0 < 0 ? 0u : static_cast<uint32_t>(d0);
+      uint32_t lo = 0, hi = n;
+      while (lo + 1 < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (M.start[mid] <= xs) lo = mid;
+        else hi = mid;
+      }
+      const uint32_t spans[2] = {M.kspan[lo], M.vspan[lo]};
+      const uint8_t *srcs[2] = {M.ksrc[lo], M.vsrc[lo]};
+#pragma unroll
+      for (int q = 0; q < 2; q++) {
+        const int32_t s0 = static_cast<int32_t>(spans[q] & 0xFFFFu), s1 = s0 + static_cast<int32_t>(spans[q] >> 16);
+        const int32_t b0 = d0 > s0 ? d0 : s0, b1 = d0 + 4 < s1 ? d0 + 4 : s1;
+        for (int32_t y = b0; y < b1; y++) im[y] = srcs[q][y - s0];
+      }
     }
   }
   wave_lds_sync();

@@ -25,6 +25,13 @@ struct RtArgs {
   uint32_t num_cus;
 };
 
+// 32 B merge key of one record (compaction): 16 B big-endian key prefix (zero
+// padded), txn, key length, record id.
+struct __attribute__((aligned(16))) SortKey {
+  uint64_t p0, p1, tx;
+  uint32_t kl, id;
+};
+
 struct DecArgs {
   const uint8_t *src;
   const uint64_t *blk_off;
@@ -35,6 +42,7 @@ struct DecArgs {
   uint32_t txn_mode;
   uint32_t *status; // may be null
   unsigned long long *err_count;
+  SortKey *sk = nullptr; // optional merge keys (compaction)
 };
 
 struct EncArgs {
