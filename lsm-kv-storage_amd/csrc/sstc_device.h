@@ -74,22 +74,28 @@ __device__ __forceinline__ void lds_st_u64u(uint8_t *img, uint32_t off, uint64_t
 
 // ---- global reads at arbitrary byte offsets ---------------------------------
 // Only dwords that hold a requested byte are touched, so a field that ends at
-// the last byte of an allocation never reads past it.
+// the last byte of an allocation never reads past it.  The aligned pointer is
+// derived by pointer arithmetic (not an integer round trip), so the compiler
+// keeps the global address space and emits global_load, not flat_load (a flat
+// load is waited for with vmcnt(0) lgkmcnt(0)).
 __device__ __forceinline__ uint32_t g_u8(const uint8_t *p) { return *p; }
 
+__device__ __forceinline__ const uint32_t *align4_down(const uint8_t *p, uint32_t &sh) {
+  sh = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(p) & 3u);
+  return reinterpret_cast<const uint32_t *>(p - sh);
+}
+
 __device__ __forceinline__ uint32_t g_u32u(const uint8_t *p) {
-  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
-  const uint32_t *w = reinterpret_cast<const uint32_t *>(a & ~uintptr_t(3));
-  const uint32_t sh = a & 3u;
+  uint32_t sh;
+  const uint32_t *w = align4_down(p, sh);
   const uint32_t lo = w[0];
   const uint32_t hi = sh ? w[1] : 0u;
   return __builtin_amdgcn_alignbyte(hi, lo, sh);
 }
 
 __device__ __forceinline__ uint64_t g_u64u(const uint8_t *p) {
-  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
-  const uint32_t *w = reinterpret_cast<const uint32_t *>(a & ~uintptr_t(3));
-  const uint32_t sh = a & 3u;
+  uint32_t sh;
+  const uint32_t *w = align4_down(p, sh);
   const uint32_t x = w[0], y = w[1];
   const uint32_t z = sh ? w[2] : 0u;
   const uint32_t lo = __builtin_amdgcn_alignbyte(y, x, sh);

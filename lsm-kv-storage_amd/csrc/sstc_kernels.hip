@@ -546,12 +546,10 @@ __global__ void enc_blk_len_kernel(const uint64_t *P, const uint64_t *blk_first,
 constexpr uint32_t kEncThreads = 256;
 constexpr uint32_t kEncWaves = 4;
 constexpr uint32_t kEncSlot = 4608;       // LDS image bytes per wave (enc_lds_kernel)
-constexpr uint32_t kEncMaxRec = 160;      // > (4608 - 16) / 29 entries per small block
 
 __device__ __forceinline__ u32x4 load16_unaligned(const uint8_t *p) {
-  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
-  const uint32_t *w = reinterpret_cast<const uint32_t *>(a & ~uintptr_t(3));
-  const uint32_t sh = a & 3u;
+  uint32_t sh;
+  const uint32_t *w = align4_down(p, sh);
   const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3];
   const uint32_t w4 = sh ? w[4] : 0u;
   u32x4 v;
@@ -646,35 +644,51 @@ __global__ __launch_bounds__(kEncThreads) void enc_emit_kernel(EncArgs a) {
 }
 
 
-// Small-block encode: one wave per block, the block is assembled in an LDS
-// image then written with 16 B stores (as rt_kernel).  Phase 1, lane per
-// record: type, key_len, val_len, txn, offset entry (start, size), extra, and
-// the record's two copy spans (LDS-resident metadata).  Phase 2, lane per image
-// dword: the key / value bytes it holds (a dword overlaps at most one span:
-// spans of one record are 4 B apart, records are >= 13 B); the source reads of
-// kEncBatch dwords per lane are issued before any of them is consumed, so a
-// wave keeps ~128 loads in flight instead of one dependent chain.  Phases write
-// disjoint bytes.
-constexpr uint32_t kEncBatch = 16;
+// One lane copies len bytes from global src to LDS dst, both at arbitrary
+// alignment: head bytes until dst is 4-aligned, then one aligned source dword
+// per destination dword through a funnel shift (the source / destination byte
+// skew is constant along a span), then tail bytes.
+__device__ __forceinline__ void lane_copy(uint8_t *dst, const uint8_t *src, uint32_t len) {
+  uint32_t i = 0;
+  uint32_t head = (4u - static_cast<uint32_t>(reinterpret_cast<uintptr_t>(dst) & 3u)) & 3u;
+  head = head < len ? head : len;
+  for (; i < head; i++) dst[i] = src[i];
+  const uint32_t nw = (len - i) >> 2;
+  if (nw) {
+    uint32_t sh;
+    const uint32_t *w = align4_down(src + i, sh);
+    uint32_t *d = reinterpret_cast<uint32_t *>(dst + i);
+    if (sh == 0) {
+      for (uint32_t k = 0; k < nw; k++) d[k] = w[k];
+    } else {
+      uint32_t lo = w[0];
+      for (uint32_t k = 0; k < nw; k++) {
+        const uint32_t hi = w[k + 1];
+        d[k] = __builtin_amdgcn_alignbyte(hi, lo, sh);
+        lo = hi;
+      }
+    }
+    i += 4 * nw;
+  }
+  for (; i < len; i++) dst[i] = src[i];
+}
 
-struct EncMeta {
-  uint32_t *start;   // record start in the block
-  uint32_t *kspan;   // key span: dst (low 16) | len (high 16)
-  uint32_t *vspan;   // value span: dst | len (len 0 for no value)
-  const uint8_t **ksrc;
-  const uint8_t **vsrc;
-};
+// Small-block encode: one wave per block, the block is assembled in an LDS
+// image then written with 16 B stores (as rt_kernel).  Lane per record: its
+// header fields, key and value bytes (lane_copy), txn and offset entry; lane 0
+// the extra.  When the records were decoded from blocks held in key_src
+// (a.entries_in_src, the compaction path) each record's whole entry is one
+// contiguous source range at key_off - 5 and is copied as one span (txn then
+// rewritten from the record: the compat reader may have changed it).
+constexpr uint32_t kEncSlotWaves = kEncWaves;
 
 __global__ __launch_bounds__(kEncWaves *kWave) void enc_lds_kernel(EncArgs a) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds[kEncWaves * kEncSlot];
-  __shared__ uint32_t m32[kEncWaves][3][kEncMaxRec];
-  __shared__ const uint8_t *m64[kEncWaves][2][kEncMaxRec];
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kEncSlotWaves * kEncSlot];
   const uint32_t wave = uniform(threadIdx.x / kWave);
   const uint32_t lane = lane_id();
   const uint64_t b = static_cast<uint64_t>(blockIdx.x) * kEncWaves + wave;
   if (b >= a.nblocks) return;
   uint8_t *img = lds + wave * kEncSlot;
-  const EncMeta M{m32[wave][0], m32[wave][1], m32[wave][2], m64[wave][0], m64[wave][1]};
   const uint64_t bo = uniform64(a.out_blk_off[b]);
   const uint64_t L64 = uniform64(a.out_blk_len[b]);
   const uint32_t pad = static_cast<uint32_t>(bo & 15u);
@@ -686,95 +700,31 @@ __global__ __launch_bounds__(kEncWaves *kWave) void enc_lds_kernel(EncArgs a) {
   const uint32_t D = static_cast<uint32_t>(uniform64(a.P[f0 + n]) - P0);
   uint8_t *im = img + pad; // image byte 0 == block byte 0
 
-  // phase 1
   for (uint32_t i = lane; i < n; i += kWave) {
     const uint64_t r = f0 + i;
     const uint32_t o = static_cast<uint32_t>(a.P[r] - P0);
     const uint32_t sz = static_cast<uint32_t>(a.P[r + 1] - a.P[r]);
     const uint32_t kl = a.in.key_len[r], vl = a.in.val_len[r];
-    M.start[i] = o;
-    M.kspan[i] = (o + 5) | (kl << 16);
-    M.ksrc[i] = a.key_src + a.in.key_off[r];
-    im[o] = a.in.type[r];
-    for (int j = 0; j < 4; j++) im[o + 1 + j] = static_cast<uint8_t>(kl >> (8 * j));
-    uint32_t t = o + 5 + kl;
-    if (vl != kNoValue) {
-      for (int j = 0; j < 4; j++) im[t + j] = static_cast<uint8_t>(vl >> (8 * j));
-      M.vspan[i] = (t + 4) | (vl << 16);
-      M.vsrc[i] = a.val_src + a.in.val_off[r];
-      t += 4 + vl;
-    } else {
-      M.vspan[i] = 0;
-      M.vsrc[i] = nullptr;
-    }
     const uint64_t tx = a.in.txn[r];
-    for (int j = 0; j < 8; j++) im[t + j] = static_cast<uint8_t>(tx >> (8 * j));
+    const uint32_t t = sz - 8; // txn position in the entry
+    if (a.entries_in_src) {
+      lane_copy(im + o, a.key_src + a.in.key_off[r] - 5, sz - 8);
+    } else {
+      im[o] = a.in.type[r];
+      for (int j = 0; j < 4; j++) im[o + 1 + j] = static_cast<uint8_t>(kl >> (8 * j));
+      lane_copy(im + o + 5, a.key_src + a.in.key_off[r], kl);
+      if (vl != kNoValue) {
+        for (int j = 0; j < 4; j++) im[o + 5 + kl + j] = static_cast<uint8_t>(vl >> (8 * j));
+        lane_copy(im + o + 9 + kl, a.val_src + a.in.val_off[r], vl);
+      }
+    }
+    for (int j = 0; j < 8; j++) im[o + t + j] = static_cast<uint8_t>(tx >> (8 * j));
     lds_st_u64u(im, D + 16 * i, o);
     lds_st_u64u(im, D + 16 * i + 8, sz);
   }
   if (lane == 0) {
     lds_st_u64u(im, D + 16 * n, n);
     lds_st_u64u(im, D + 16 * n + 8, D);
-  }
-  wave_lds_sync();
-
-  // phase 2: image dwords covering the data section [pad, pad + D)
-  const uint32_t w_lo = pad >> 2, w_hi = (pad + D + 3) >> 2;
-  for (uint32_t wb = w_lo; wb < w_hi; wb += kWave * kEncBatch) {
-    uint32_t val[kEncBatch];
-    uint32_t full = 0;
-#pragma unroll
-    for (uint32_t j = 0; j < kEncBatch; j++) {
-      const uint32_t w = wb + lane + kWave * j;
-      val[j] = 0;
-      if (w >= w_hi) continue;
-      const int32_t d0 = static_cast<int32_t>(4 * w) - static_cast<int32_t>(pad);
-      const uint32_t xs = d0 < 0 ? 0u : static_cast<uint32_t>(d0);
-      uint32_t lo = 0, hi = n;
-      while (lo + 1 < hi) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (M.start[mid] <= xs) lo = mid;
-        else hi = mid;
-      }
-      const uint32_t ks = M.kspan[lo], vs = M.vspan[lo];
-      int32_t s0 = static_cast<int32_t>(ks & 0xFFFFu), s1 = s0 + static_cast<int32_t>(ks >> 16);
-      const uint8_t *sp = M.ksrc[lo];
-      if (!(d0 < s1 && d0 + 4 > s0)) {
-        s0 = static_cast<int32_t>(vs & 0xFFFFu);
-        s1 = s0 + static_cast<int32_t>(vs >> 16);
-        sp = M.vsrc[lo];
-      }
-      if (d0 >= s0 && d0 + 4 <= s1 && s1 > s0) {
-        val[j] = g_u32u(sp + (d0 - s0));
-        full |= 1u << j;
-      }
-    }
-#pragma unroll
-    for (uint32_t j = 0; j < kEncBatch; j++) {
-      const uint32_t w = wb + lane + kWave * j;
-      if (w >= w_hi) continue;
-      if (full & (1u << j)) {
-        *reinterpret_cast<uint32_t *>(img + 4 * w) = val[j];
-        continue;
-      }
-      // partial dword at a span edge (or no span): byte copy of the span part
-      const int32_t d0 = static_cast<int32_t>(4 * w) - static_cast<int32_t>(pad);
-      const uint32_t xs = d0 < 0 ? 0u : static_cast<uint32_t>(d0);
-      uint32_t lo = 0, hi = n;
-      while (lo + 1 < hi) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (M.start[mid] <= xs) lo = mid;
-        else hi = mid;
-      }
-      const uint32_t spans[2] = {M.kspan[lo], M.vspan[lo]};
-      const uint8_t *srcs[2] = {M.ksrc[lo], M.vsrc[lo]};
-#pragma unroll
-      for (int q = 0; q < 2; q++) {
-        const int32_t s0 = static_cast<int32_t>(spans[q] & 0xFFFFu), s1 = s0 + static_cast<int32_t>(spans[q] >> 16);
-        const int32_t b0 = d0 > s0 ? d0 : s0, b1 = d0 + 4 < s1 ? d0 + 4 : s1;
-        for (int32_t y = b0; y < b1; y++) im[y] = srcs[q][y - s0];
-      }
-    }
   }
   wave_lds_sync();
   store_window(img, a.dst + (bo - pad), (pad + L + 15u) >> 4, 0, pad, pad + L);

@@ -55,6 +55,7 @@ struct EncArgs {
   const uint64_t *out_blk_off;
   const uint64_t *out_blk_len;
   uint8_t *dst;
+  uint32_t entries_in_src = 0; // records decoded from blocks in key_src (== val_src)
 };
 
 hipError_t launch_roundtrip(const RtArgs &a, hipStream_t s);

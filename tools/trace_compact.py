@@ -1,0 +1,24 @@
+"""Print the per-kernel timeline of the last sstc_compact call in a rocprofv3
+kernel trace (tools/profile of tools/bench_compact.py)."""
+import csv
+import sys
+
+rows = list(csv.DictReader(open(sys.argv[1])))
+rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+idx = [i for i, r in enumerate(rows) if r["Kernel_Name"].startswith("sstc::decode_kernel")]
+start = idx[-1] - 2
+t0 = int(rows[start]["Start_Timestamp"])
+last = t0
+agg = {}
+for r in rows[start:]:
+    n = r["Kernel_Name"].split("(")[0].replace("sstc::(anonymous namespace)::", "").replace("sstc::", "")
+    st, en = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+    if n.startswith("__amd_rocclr_copyBuffer") and (en - st) > 100_000:
+        break
+    agg.setdefault(n, [0, 0.0])
+    agg[n][0] += 1
+    agg[n][1] += (en - st) / 1e3
+    last = en
+for n, (c, us) in sorted(agg.items(), key=lambda x: -x[1][1]):
+    print(f"{n[:32]:32s} calls={c:4d} total_us={us:9.1f}")
+print(f"span us {(last - t0) / 1e3:.1f}  kernel sum us {sum(v[1] for v in agg.values()):.1f}")
