@@ -23,6 +23,7 @@ struct sstc_ctx {
   uint64_t *sizes = nullptr;                // cap_records + 1
   uint64_t *P = nullptr;                    // cap_records + 1
   uint32_t *jump = nullptr;                 // cap_jump
+  sstc::Arena arena;                        // compaction workspace
 };
 
 namespace {
@@ -140,7 +141,7 @@ int sstc_ctx_destroy(sstc_ctx *c) {
   if (!c) return SSTC_OK;
   bind_device(c);
   (void)hipStreamSynchronize(c->stream);
-  for (void *p : {c->counters,
+  for (void *p : {c->counters, c->arena.base,
                   static_cast<void *>(c->scan_ws), static_cast<void *>(c->sizes),
                   static_cast<void *>(c->P), static_cast<void *>(c->jump)})
     if (p) (void)hipFree(p);
@@ -272,7 +273,7 @@ int sstc_compact(sstc_ctx *c, const uint8_t *d_src, const uint64_t *d_blk_off, c
   if (int r = bind_device(c)) return r;
   uint64_t res[5] = {0, 0, 0, 0, 0};
   std::string err;
-  const int rc = sstc::compact_impl(c->stream, c->err_count, d_src, d_blk_off, d_blk_len, nblocks,
+  const int rc = sstc::compact_impl(c->arena, c->stream, c->err_count, d_src, d_blk_off, d_blk_len, nblocks,
                                     h_table_first_block, ntables, params->block_threshold, params->table_limit,
                                     params->base_level, params->txn_mode, d_dst, dst_cap, d_table_off, d_table_len,
                                     max_tables, res, err);

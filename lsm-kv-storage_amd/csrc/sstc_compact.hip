@@ -356,15 +356,32 @@ __global__ void ck_footer_kernel(uint64_t nt, const uint64_t *tbf, const uint64_
 // ------------------------------------------------------------------ host side
 inline uint32_t grid(uint64_t n, uint32_t per = 256) { return static_cast<uint32_t>((n + per - 1) / per); }
 
+// Bump allocator over the context's persistent compaction arena; requests
+// beyond it fall back to hipMalloc and the arena is regrown to the high-water
+// mark for the next call (a steady-state call then allocates nothing).
 struct Pool {
-  std::vector<void *> ptrs;
+  Arena &arena;
+  uint64_t used = 0;
+  std::vector<void *> extra;
+  explicit Pool(Arena &a) : arena(a) {}
   ~Pool() {
-    for (void *p : ptrs) (void)hipFree(p);
+    for (void *p : extra) (void)hipFree(p);
+    if (used > arena.cap) {
+      if (arena.base) (void)hipFree(arena.base);
+      arena.base = nullptr;
+      arena.cap = 0;
+      const uint64_t want = used + used / 8;
+      if (hipMalloc(&arena.base, want) == hipSuccess) arena.cap = want;
+    }
   }
   template <class T> T *get(uint64_t n) {
+    const uint64_t bytes = ((n ? n : 1) * sizeof(T) + 255) & ~uint64_t(255);
+    const uint64_t at = used;
+    used += bytes;
+    if (arena.base && used <= arena.cap) return reinterpret_cast<T *>(static_cast<char *>(arena.base) + at);
     void *p = nullptr;
-    if (hipMalloc(&p, (n ? n : 1) * sizeof(T)) != hipSuccess) throw std::runtime_error("compaction workspace");
-    ptrs.push_back(p);
+    if (hipMalloc(&p, bytes) != hipSuccess) throw std::runtime_error("compaction workspace");
+    extra.push_back(p);
     return static_cast<T *>(p);
   }
 };
@@ -410,13 +427,14 @@ uint64_t segment(Pool &pool, const uint64_t *w, uint64_t m, uint64_t threshold, 
 
 } // namespace
 
-int compact_impl(hipStream_t s, unsigned long long *err_count, const uint8_t *d_src, const uint64_t *d_blk_off,
+int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, const uint8_t *d_src,
+                 const uint64_t *d_blk_off,
                  const uint64_t *d_blk_len, uint64_t nblocks, const uint64_t *h_tfb, uint32_t ntables,
                  uint64_t block_threshold, uint64_t table_limit, uint32_t base_level, uint32_t txn_mode,
                  uint8_t *d_dst, uint64_t dst_cap, uint64_t *d_table_off, uint64_t *d_table_len, uint64_t max_tables,
                  uint64_t *res, std::string &err) {
   try {
-    Pool pool;
+    Pool pool(arena);
     const uint64_t nws = scan_workspace_elems(nblocks + 1) + 64;
     // 1. decode every block
     uint64_t *rb_all = pool.get<uint64_t>(nblocks + 1);

@@ -74,7 +74,14 @@ hipError_t launch_segment(const uint64_t *Pw, uint64_t nrec, uint64_t threshold,
                           uint32_t levels, uint64_t *d_nblocks, uint64_t *blk_first, hipStream_t s,
                           const uint32_t *clamp = nullptr);
 
-int compact_impl(hipStream_t s, unsigned long long *err_count, const uint8_t *d_src, const uint64_t *d_blk_off,
+// persistent device workspace of one context (compaction)
+struct Arena {
+  void *base = nullptr;
+  uint64_t cap = 0;
+};
+
+int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, const uint8_t *d_src,
+                 const uint64_t *d_blk_off,
                  const uint64_t *d_blk_len, uint64_t nblocks, const uint64_t *h_tfb, uint32_t ntables,
                  uint64_t block_threshold, uint64_t table_limit, uint32_t base_level, uint32_t txn_mode,
                  uint8_t *d_dst, uint64_t dst_cap, uint64_t *d_table_off, uint64_t *d_table_len, uint64_t max_tables,

@@ -11,7 +11,7 @@ t0 = int(rows[start]["Start_Timestamp"])
 last = t0
 agg = {}
 for r in rows[start:]:
-    n = r["Kernel_Name"].split("(")[0].replace("sstc::(anonymous namespace)::", "").replace("sstc::", "")
+    n = r["Kernel_Name"].replace("sstc::(anonymous namespace)::", "").replace("sstc::", "").split("(")[0]
     st, en = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
     if n.startswith("__amd_rocclr_copyBuffer") and (en - st) > 100_000:
         break
