@@ -78,59 +78,71 @@ __global__ void ck_check_sorted_kernel(const SK *s, const uint64_t *run_start, u
   if (sk_less(s[r], s[r - 1], kv)) atomicAdd(bad, 1ull);
 }
 
-constexpr uint32_t kMergeItems = 16;
+// Pairwise stable merge of sorted runs, tiled through LDS (merge path): one
+// 256-thread workgroup per kMergeTile outputs of one run pair.  Two threads
+// co-rank the tile's ends against HBM; the tile's slices of A and B are loaded
+// coalesced into LDS; every thread co-ranks its kMergeIt outputs inside LDS
+// and merges them.  Ties go to A (the earlier input table): stable.
+constexpr uint32_t kMergeIt = 4;
+constexpr uint32_t kMergeThreads = 256;
+constexpr uint32_t kMergeTile = kMergeIt * kMergeThreads;
 
-// One round of pairwise stable merges: runs [rb[2j], rb[2j+1]) and
-// [rb[2j+1], rb[2j+2]) -> [rb[2j], rb[2j+2]) (ties: left run first).  Each
-// thread co-ranks its first output (merge path) then merges kMergeItems.
-__global__ void ck_merge_kernel(const SK *in, SK *out, const uint64_t *rb, uint64_t nruns, uint64_t n, KeyView kv) {
-  const uint64_t k0 = (static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x) * kMergeItems;
-  if (k0 >= n) return;
-  const uint64_t npairs = (nruns + 1) / 2;
-  uint64_t k = k0;
-  const uint64_t kend = k0 + kMergeItems < n ? k0 + kMergeItems : n;
-  uint64_t lo = 0, hi = npairs; // pair holding k
+struct MergePair {
+  uint64_t a0, a1, b1; // A = [a0, a1), B = [a1, b1)
+  uint64_t tile0;      // first tile of this pair
+};
+
+__global__ __launch_bounds__(kMergeThreads) void ck_merge_tile_kernel(const SK *in, SK *out, const MergePair *pairs,
+                                                                      uint32_t npairs, KeyView kv) {
+  __shared__ SK tile[kMergeTile];
+  __shared__ uint64_t corank[2];
+  const uint64_t g = blockIdx.x;
+  uint32_t lo = 0, hi = npairs; // pair of this tile: last tile0 <= g
   while (lo + 1 < hi) {
-    const uint64_t mid = (lo + hi) >> 1;
-    if (rb[2 * mid] <= k) lo = mid;
+    const uint32_t mid = (lo + hi) >> 1;
+    if (pairs[mid].tile0 <= g) lo = mid;
     else hi = mid;
   }
-  uint64_t j = lo;
-  while (k < kend) {
-    const uint64_t a0 = rb[2 * j];
-    const uint64_t a1 = 2 * j + 1 <= nruns ? rb[2 * j + 1] : a0;
-    const uint64_t b1 = 2 * j + 2 <= nruns ? rb[2 * j + 2] : a1;
-    const uint64_t na = a1 - a0, nb = b1 - a1;
-    const uint64_t kk = k - a0;
-    uint64_t l = kk > nb ? kk - nb : 0, h = kk < na ? kk : na;
+  const MergePair P = pairs[lo];
+  const uint64_t na_all = P.a1 - P.a0, nb_all = P.b1 - P.a1;
+  const uint64_t seg = na_all + nb_all;
+  const uint64_t k0 = (g - P.tile0) * kMergeTile;
+  const uint64_t k1 = k0 + kMergeTile < seg ? k0 + kMergeTile : seg;
+  if (threadIdx.x < 2) {
+    const uint64_t kk = threadIdx.x ? k1 : k0;
+    uint64_t l = kk > nb_all ? kk - nb_all : 0, h = kk < na_all ? kk : na_all;
     while (l < h) { // smallest i with B[kk-i-1] < A[i]
       const uint64_t mid = (l + h) >> 1;
-      if (sk_less(in[a1 + (kk - mid - 1)], in[a0 + mid], kv)) h = mid;
+      if (sk_less(in[P.a1 + (kk - mid - 1)], in[P.a0 + mid], kv)) h = mid;
       else l = mid + 1;
     }
-    uint64_t ia = a0 + l, ib = a1 + (kk - l);
-    const uint64_t stop = kend < b1 ? kend : b1;
-    SK va, vb;
-    if (ia < a1) va = in[ia];
-    if (ib < b1) vb = in[ib];
-    for (; k < stop; k++) {
-      const bool take_a = ia < a1 && (ib >= b1 || !sk_less(vb, va, kv));
-      if (take_a) {
-        out[k] = va;
-        if (++ia < a1) va = in[ia];
-      } else {
-        out[k] = vb;
-        if (++ib < b1) vb = in[ib];
-      }
-    }
-    j++;
+    corank[threadIdx.x] = l;
   }
-}
-
-__global__ void ck_runs_next_kernel(const uint64_t *rb, uint64_t nruns, uint64_t *rb2) {
-  const uint64_t j = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  const uint64_t nr2 = (nruns + 1) / 2;
-  if (j <= nr2) rb2[j] = rb[2 * j <= nruns ? 2 * j : nruns];
+  __syncthreads();
+  const uint64_t ia0 = corank[0], ia1 = corank[1];
+  const uint32_t na = static_cast<uint32_t>(ia1 - ia0);
+  const uint32_t nt = static_cast<uint32_t>(k1 - k0);
+  const uint32_t nb = nt - na;
+  const uint64_t ib0 = k0 - ia0;
+  for (uint32_t t = threadIdx.x; t < nt; t += kMergeThreads)
+    tile[t] = t < na ? in[P.a0 + ia0 + t] : in[P.a1 + ib0 + (t - na)];
+  __syncthreads();
+  const SK *A = tile, *B = tile + na;
+  const uint32_t k = threadIdx.x * kMergeIt;
+  if (k >= nt) return;
+  uint32_t l = k > nb ? k - nb : 0, h = k < na ? k : na;
+  while (l < h) {
+    const uint32_t mid = (l + h) >> 1;
+    if (sk_less(B[k - mid - 1], A[mid], kv)) h = mid;
+    else l = mid + 1;
+  }
+  uint32_t ia = l, ib = k - l;
+  const uint32_t stop = k + kMergeIt < nt ? k + kMergeIt : nt;
+  SK *o = out + P.a0 + k0;
+  for (uint32_t q = k; q < stop; q++) {
+    const bool take_a = ia < na && (ib >= nb || !sk_less(B[ib], A[ia], kv));
+    o[q] = take_a ? A[ia++] : B[ib++];
+  }
 }
 
 // head[i] = 1 if merged record i starts a key group (ShouldKeepEntry's
@@ -486,7 +498,6 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     const KeyView kv{d_src, R.ko};
     uint64_t nruns = ntables;
     uint64_t *rb = pool.get<uint64_t>(nruns + 2);
-    uint64_t *rb2 = pool.get<uint64_t>(nruns + 2);
     CK(hipMemcpyAsync(rb, run_start.data(), (nruns + 1) * 8, hipMemcpyHostToDevice, s));
     unsigned long long *bad = reinterpret_cast<unsigned long long *>(pool.get<uint64_t>(1));
     CK(hipMemsetAsync(bad, 0, 8, s));
@@ -495,12 +506,44 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
       err = "input SST records are not sorted (key asc, txn desc)";
       return SSTC_E_INVALID_ARG;
     }
-    while (nruns > 1) {
-      ck_merge_kernel<<<grid((n + kMergeItems - 1) / kMergeItems), 256, 0, s>>>(A, B, rb, nruns, n, kv);
-      ck_runs_next_kernel<<<grid(nruns + 2), 256, 0, s>>>(rb, nruns, rb2);
-      std::swap(A, B);
-      std::swap(rb, rb2);
-      nruns = (nruns + 1) / 2;
+    {
+      // run boundaries of every round are known on the host (input table
+      // sizes): one descriptor upload for all rounds
+      std::vector<std::vector<MergePair>> rounds;
+      std::vector<uint64_t> cur = run_start;
+      while (cur.size() > 2) {
+        std::vector<MergePair> ps;
+        std::vector<uint64_t> next;
+        uint64_t tiles = 0;
+        for (size_t j = 0; 2 * j + 1 < cur.size(); j++) {
+          const uint64_t a0 = cur[2 * j];
+          const uint64_t a1 = 2 * j + 1 < cur.size() ? cur[2 * j + 1] : a0;
+          const uint64_t b1 = 2 * j + 2 < cur.size() ? cur[2 * j + 2] : a1;
+          ps.push_back(MergePair{a0, a1, b1, tiles});
+          tiles += (b1 - a0 + kMergeTile - 1) / kMergeTile;
+          next.push_back(a0);
+        }
+        next.push_back(cur.back());
+        ps.push_back(MergePair{0, 0, 0, tiles}); // sentinel: total tiles
+        rounds.push_back(std::move(ps));
+        cur = std::move(next);
+      }
+      size_t total = 0;
+      for (auto &r : rounds) total += r.size();
+      std::vector<MergePair> flat;
+      for (auto &r : rounds) flat.insert(flat.end(), r.begin(), r.end());
+      MergePair *d_pairs = pool.get<MergePair>(total ? total : 1);
+      if (total) CK(hipMemcpyAsync(d_pairs, flat.data(), total * sizeof(MergePair), hipMemcpyHostToDevice, s));
+      size_t at = 0;
+      for (auto &r : rounds) {
+        const uint32_t np = static_cast<uint32_t>(r.size() - 1);
+        const uint64_t tiles = r.back().tile0;
+        if (tiles)
+          ck_merge_tile_kernel<<<static_cast<uint32_t>(tiles), kMergeThreads, 0, s>>>(A, B, d_pairs + at, np, kv);
+        std::swap(A, B);
+        at += r.size();
+      }
+      CK(hipStreamSynchronize(s)); // flat (host) must outlive the upload
     }
     // 3. keep / drop
     uint64_t *head = pool.get<uint64_t>(n), *G = pool.get<uint64_t>(n + 1), *hp = pool.get<uint64_t>(n);
