@@ -281,14 +281,16 @@ __device__ __forceinline__ void put_le(uint8_t *p, uint64_t v, int n) {
   for (int j = 0; j < n; j++) p[j] = static_cast<uint8_t>(v >> (8 * j));
 }
 
-// meta entry of block b (table_builder.cc:101-145)
-__global__ void ck_meta_kernel(const uint64_t *bf, uint64_t nb, const uint32_t *btab, const uint64_t *BL,
-                               const uint64_t *MS, const uint64_t *blen, const uint64_t *tbf, const uint64_t *toff,
-                               const uint64_t *tdata, Rec K, const uint8_t *src, uint8_t *dst) {
-  const uint64_t b = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (b >= nb) return;
+// meta entry of block b (table_builder.cc:101-145): u32 first-key length,
+// first key, u32 last-key length, last key, u64 block offset, u64 block size.
+// Entries are assembled in LDS by a thread per block, then every table run of
+// the workgroup's 256 blocks is written with aligned 16 B stores (byte stores
+// straight to HBM from 256 threads at a 56 B stride cost ~10x more).
+constexpr uint32_t kMetaLds = 32768;
+__device__ __forceinline__ void meta_entry(uint8_t *p, uint64_t b, const uint64_t *bf, const uint32_t *btab,
+                                           const uint64_t *BL, const uint64_t *blen, const uint64_t *tbf, Rec K,
+                                           const uint8_t *src) {
   const uint32_t t = btab[b];
-  uint8_t *p = dst + toff[t] + tdata[t] + (MS[b] - MS[tbf[t]]);
   const uint64_t f = bf[b], l = bf[b + 1] - 1;
   const uint32_t fk = K.kl[f], lk = K.kl[l];
   put_le(p, fk, 4);
@@ -297,6 +299,52 @@ __global__ void ck_meta_kernel(const uint64_t *bf, uint64_t nb, const uint32_t *
   for (uint32_t j = 0; j < lk; j++) p[8 + fk + j] = src[K.ko[l] + j];
   put_le(p + 8 + fk + lk, BL[b] - BL[tbf[t]], 8);
   put_le(p + 16 + fk + lk, blen[b], 8);
+}
+
+__global__ __launch_bounds__(256) void ck_meta_kernel(const uint64_t *bf, uint64_t nb, const uint32_t *btab,
+                                                      const uint64_t *BL, const uint64_t *MS, const uint64_t *blen,
+                                                      const uint64_t *tbf, const uint64_t *toff,
+                                                      const uint64_t *tdata, Rec K, const uint8_t *src,
+                                                      uint8_t *dst) {
+  __shared__ __attribute__((aligned(16))) uint8_t img[kMetaLds + 16];
+  const uint64_t b0 = static_cast<uint64_t>(blockIdx.x) * 256u;
+  const uint64_t bend = b0 + 256u < nb ? b0 + 256u : nb;
+  const uint64_t b = b0 + threadIdx.x;
+  const uint64_t m0 = MS[b0];
+  if (MS[bend] - m0 > kMetaLds) {  // long keys: direct per-thread writes
+    if (b < bend) {
+      const uint32_t t = btab[b];
+      meta_entry(dst + toff[t] + tdata[t] + (MS[b] - MS[tbf[t]]), b, bf, btab, BL, blen, tbf, K, src);
+    }
+    return;
+  }
+  if (b < bend) meta_entry(img + (MS[b] - m0), b, bf, btab, BL, blen, tbf, K, src);
+  __syncthreads();
+  for (uint64_t bs = b0; bs < bend;) {  // one run per output table touched
+    const uint32_t t = btab[bs];
+    const uint64_t be = tbf[t + 1] < bend ? tbf[t + 1] : bend;
+    const uint32_t l0 = static_cast<uint32_t>(MS[bs] - m0);
+    const int64_t len = static_cast<int64_t>(MS[be] - MS[bs]);
+    uint8_t *g = dst + toff[t] + tdata[t] + (MS[bs] - MS[tbf[t]]);
+    const uint32_t pad = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(g) & 15u);
+    const uint32_t nchunk = static_cast<uint32_t>((pad + len + 15) >> 4);
+    for (uint32_t c = threadIdx.x; c < nchunk; c += 256u) {
+      const int64_t lo = 16 * static_cast<int64_t>(c) - pad;
+      if (lo >= 0 && lo + 16 <= len) {
+        const uint32_t o = l0 + static_cast<uint32_t>(lo);
+        u32x4 v;
+        v.x = lds_u32u(img, o);
+        v.y = lds_u32u(img, o + 4);
+        v.z = lds_u32u(img, o + 8);
+        v.w = lds_u32u(img, o + 12);
+        *reinterpret_cast<u32x4 *>(g + lo) = v;
+      } else {
+        const int64_t x1 = lo + 16 < len ? lo + 16 : len;
+        for (int64_t x = lo < 0 ? 0 : lo; x < x1; x++) g[x] = img[l0 + x];
+      }
+    }
+    bs = be;
+  }
 }
 
 // min / max txn of every output table (table_builder.cc:47-49): one wave per
@@ -420,20 +468,19 @@ template <class T> T read1(const T *d, hipStream_t s) {
   return v;
 }
 
-// greedy segmentation of [0, m) by weights w (>= threshold closes), optional clamp
-uint64_t segment(Pool &pool, const uint64_t *w, uint64_t m, uint64_t threshold, const uint32_t *clamp,
-                 uint64_t nclamps, uint64_t *first, uint64_t *ws, hipStream_t s) {
-  uint64_t *Pw = pool.get<uint64_t>(m + 1);
-  CK(launch_scan(w, m, 0, Pw, ws, s));
+// greedy segmentation of [0, m) by weights whose prefix sums are
+// Pw[i] + add * i (>= threshold closes), optional clamp
+uint64_t segment(Pool &pool, const uint64_t *Pw, uint64_t add, uint64_t m, uint64_t threshold,
+                 const uint32_t *clamp, uint64_t nclamps, uint64_t *first, hipStream_t s) {
   // every segment but the last one of each clamp range reaches the threshold,
   // so the chain from record 0 has at most total / threshold + nclamps + 1
   // nodes: that many doubling levels suffice
-  const uint64_t total = read1(Pw + m, s);
+  const uint64_t total = read1(Pw + m, s) + add * m;
   const uint64_t chain = total / threshold + nclamps + 1;
   const uint32_t levels = bitlen(chain < m ? chain : m);
   uint32_t *J = pool.get<uint32_t>(static_cast<uint64_t>(levels) * (m + 1));
   uint64_t *dn = pool.get<uint64_t>(1);
-  CK(launch_segment(Pw, m, threshold, J, levels, dn, first, s, clamp));
+  CK(launch_segment(Pw, m, threshold, J, levels, dn, first, s, clamp, add));
   return read1(dn, s);
 }
 
@@ -560,22 +607,22 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
            pool.get<uint64_t>(m), pool.get<uint64_t>(m)};
     uint64_t *dw = pool.get<uint64_t>(m), *ew = pool.get<uint64_t>(m);
     ck_gather_kernel<<<grid(n), 256, 0, s>>>(A, keep, K, R, n, KR, dw, ew);
-    // 4. table split then block split (clamped at table ends)
+    // 4. table split then block split (clamped at table ends); block weight =
+    // entry + offset entry, i.e. the prefix sums of the entry sizes + 16 i
+    uint64_t *Pd = pool.get<uint64_t>(m + 1), *Pe = pool.get<uint64_t>(m + 1);
+    CK(launch_scan(dw, m, 0, Pd, ws2, s));
+    CK(launch_scan(ew, m, 0, Pe, ws2, s));
     uint64_t *tf = pool.get<uint64_t>(m + 1);
-    const uint64_t nt = segment(pool, dw, m, table_limit, nullptr, 0, tf, ws2, s);
+    const uint64_t nt = segment(pool, Pd, 0, m, table_limit, nullptr, 0, tf, s);
     if (nt > max_tables) {
       err = "more output tables than max_tables";
       return SSTC_E_CAPACITY;
     }
     uint32_t *clamp = pool.get<uint32_t>(m + 1);
     ck_table_end_kernel<<<grid(m + 1), 256, 0, s>>>(tf, nt, m, clamp);
-    uint64_t *ew16 = pool.get<uint64_t>(m);
-    CK(launch_enc_sizes(KR.kl, KR.vl, m, 16, ew16, s)); // block weight: entry + offset entry
     uint64_t *bf = pool.get<uint64_t>(m + 1);
-    const uint64_t nb = segment(pool, ew16, m, block_threshold, clamp, nt, bf, ws2, s);
+    const uint64_t nb = segment(pool, Pe, 16, m, block_threshold, clamp, nt, bf, s);
     // 5. layout
-    uint64_t *Pe = pool.get<uint64_t>(m + 1);
-    CK(launch_scan(ew, m, 0, Pe, ws2, s));
     uint64_t *blen = pool.get<uint64_t>(nb), *msz = pool.get<uint64_t>(nb);
     uint32_t *btab = pool.get<uint32_t>(nb);
     ck_block_info_kernel<<<grid(nb), 256, 0, s>>>(bf, nb, Pe, KR.kl, tf, nt, blen, msz, btab);
@@ -598,7 +645,7 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     // 6. encode blocks, meta entries, footers
     EncArgs ea{d_src, d_src, sstc_records{KR.type, KR.kl, KR.vl, KR.tx, KR.ko, KR.vo}, bf, nb, Pe, bo, blen, d_dst, 1};
     CK(launch_enc_emit(ea, s));
-    ck_meta_kernel<<<grid(nb), 256, 0, s>>>(bf, nb, btab, BL, MS, blen, tbf, d_table_off, tdata, KR, d_src, d_dst);
+    ck_meta_kernel<<<static_cast<uint32_t>((nb + 255) / 256), 256, 0, s>>>(bf, nb, btab, BL, MS, blen, tbf, d_table_off, tdata, KR, d_src, d_dst);
     uint64_t *bmin = pool.get<uint64_t>(nb), *bmax = pool.get<uint64_t>(nb);
     uint64_t *tmin = pool.get<uint64_t>(nt), *tmax = pool.get<uint64_t>(nt);
     ck_blk_minmax_kernel<<<grid(nb * kWave), 256, 0, s>>>(bf, nb, KR, bmin, bmax);

@@ -700,16 +700,70 @@ __global__ __launch_bounds__(kEncWaves *kWave) void enc_lds_kernel(EncArgs a) {
   const uint32_t D = static_cast<uint32_t>(uniform64(a.P[f0 + n]) - P0);
   uint8_t *im = img + pad; // image byte 0 == block byte 0
 
-  for (uint32_t i = lane; i < n; i += kWave) {
+  if (a.entries_in_src) {
+    // 8 lanes per record: lane g copies interior dwords g, g+8, ... of the
+    // entry span (dword-aligned in LDS, funnel-shifted from the source), lane 0
+    // of the group the unaligned head / tail bytes, lane 1 the txn and the
+    // offset entry.  Every load of a pass is issued before the first use, so a
+    // pass costs one memory latency (the lane-serial copy cost one per dword).
+    const uint32_t g = lane & 7u;
+    constexpr uint32_t kU = 5; // interior dwords per lane held in registers (spans <= 163 B)
+    for (uint32_t i0 = 0; i0 < n; i0 += kWave / 8) {
+      const uint32_t i = i0 + (lane >> 3);
+      if (i >= n) continue;
+      const uint64_t r = f0 + i;
+      const uint64_t pr = a.P[r], pr1 = a.P[r + 1];
+      const uint64_t ko = a.in.key_off[r];
+      const uint32_t o = static_cast<uint32_t>(pr - P0);
+      const uint32_t sz = static_cast<uint32_t>(pr1 - pr);
+      const uint32_t len = sz - 8;
+      const uint8_t *sp = a.key_src + ko - 5;
+      uint8_t *d = im + o;
+      uint32_t head = (4u - (o + pad) % 4u) % 4u; // img is 16-aligned: d's alignment
+      head = head < len ? head : len;
+      const uint32_t nw = (len - head) >> 2;
+      uint32_t sh;
+      const uint32_t *w = align4_down(sp + head, sh);
+      uint32_t *d32 = reinterpret_cast<uint32_t *>(d + head);
+      uint32_t lo[kU], hi[kU];
+#pragma unroll
+      for (uint32_t j = 0; j < kU; j++) {
+        const uint32_t k = g + 8 * j;
+        lo[j] = k < nw ? w[k] : 0u;
+        hi[j] = k < nw && sh ? w[k + 1] : 0u;
+      }
+      uint32_t hd = 0, tl = 0;
+      uint64_t tx = 0;
+      const uint32_t t0 = head + 4 * nw;
+      if (g == 0) {
+        hd = head ? g_u32u(sp) : 0u;
+        tl = t0 < len ? g_u32u(sp + t0) : 0u; // < 4 bytes; the txn field follows in the source
+      } else if (g == 1) {
+        tx = a.in.txn[r];
+      }
+#pragma unroll
+      for (uint32_t j = 0; j < kU; j++) {
+        const uint32_t k = g + 8 * j;
+        if (k < nw) d32[k] = __builtin_amdgcn_alignbyte(hi[j], lo[j], sh);
+      }
+      for (uint32_t k = g + 8 * kU; k < nw; k += 8) d32[k] = __builtin_amdgcn_alignbyte(sh ? w[k + 1] : 0u, w[k], sh);
+      if (g == 0) {
+        for (uint32_t j = 0; j < head; j++) d[j] = static_cast<uint8_t>(hd >> (8 * j));
+        for (uint32_t j = t0; j < len; j++) d[j] = static_cast<uint8_t>(tl >> (8 * (j - t0)));
+      } else if (g == 1) {
+        for (int j = 0; j < 8; j++) d[len + j] = static_cast<uint8_t>(tx >> (8 * j));
+        lds_st_u64u(im, D + 16 * i, o);
+        lds_st_u64u(im, D + 16 * i + 8, sz);
+      }
+    }
+  } else for (uint32_t i = lane; i < n; i += kWave) {
     const uint64_t r = f0 + i;
     const uint32_t o = static_cast<uint32_t>(a.P[r] - P0);
     const uint32_t sz = static_cast<uint32_t>(a.P[r + 1] - a.P[r]);
     const uint32_t kl = a.in.key_len[r], vl = a.in.val_len[r];
     const uint64_t tx = a.in.txn[r];
     const uint32_t t = sz - 8; // txn position in the entry
-    if (a.entries_in_src) {
-      lane_copy(im + o, a.key_src + a.in.key_off[r] - 5, sz - 8);
-    } else {
+    {
       im[o] = a.in.type[r];
       for (int j = 0; j < 4; j++) im[o + 1 + j] = static_cast<uint8_t>(kl >> (8 * j));
       lane_copy(im + o + 5, a.key_src + a.in.key_off[r], kl);
@@ -731,12 +785,19 @@ __global__ __launch_bounds__(kEncWaves *kWave) void enc_lds_kernel(EncArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// Greedy segmentation by pointer doubling.
-// nxt[i] = one past the last record of a block that starts at record i;
-// chain from 0 = block starts.  J_{k+1} = J_k o J_k.
+// Greedy segmentation by radix-8 pointer jumping.
+// J_0[i] = one past the last record of a block that starts at record i (the
+// chain from 0 visits the block starts); level k holds J_0^(8^k), computed as
+// J_k = J_{k-1}^8.  A chain of h blocks needs ceil(log8(h + 1)) levels instead
+// of log2 squarings: each level is one bandwidth-bound pass over the records,
+// so this is ~3x fewer passes.  The weights' prefix sums are Pw[i] + add * i
+// (add = the per-record offset entry for block weights, so the entry-size scan
+// is reused).
 // ---------------------------------------------------------------------------
-__global__ void seg_next_kernel(const uint64_t *Pw, uint64_t nrec, uint64_t threshold, const uint32_t *clamp,
-                                uint32_t *J0) {
+constexpr uint32_t kSegRadix = 8;
+
+__global__ void seg_next_kernel(const uint64_t *Pw, uint64_t add, uint64_t nrec, uint64_t threshold,
+                                const uint32_t *clamp, uint32_t *J0) {
   const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (i > nrec) return;
   if (i == nrec) {
@@ -746,35 +807,55 @@ __global__ void seg_next_kernel(const uint64_t *Pw, uint64_t nrec, uint64_t thre
   // clamp[i]: one past the last record the block starting at i may hold (the
   // end of its output table); nrec when null
   const uint64_t lim = clamp ? clamp[i] : nrec;
-  const uint64_t target = Pw[i] + threshold; // first e >= i with Pw[e+1] >= target
-  if (Pw[lim] < target) {
+  // first e >= i with W(e + 1) >= target, W(x) = Pw[x] + add * x
+  const uint64_t target = Pw[i] + add * i + threshold;
+  if (Pw[lim] + add * lim < target) {
     J0[i] = static_cast<uint32_t>(lim);
     return;
   }
+  // gallop (blocks are short: ~2 log2(len) reads, all in nearby lines), then bisect
   uint64_t lo = i, hi = lim - 1;
+  for (uint64_t span = 1;; span <<= 1) {
+    const uint64_t e = i + span - 1;
+    if (e >= lim - 1) break;
+    if (Pw[e + 1] + add * (e + 1) >= target) {
+      hi = e;
+      break;
+    }
+    lo = e + 1;
+  }
   while (lo < hi) {
     const uint64_t mid = (lo + hi) >> 1;
-    if (Pw[mid + 1] >= target) hi = mid;
+    if (Pw[mid + 1] + add * (mid + 1) >= target) hi = mid;
     else lo = mid + 1;
   }
   J0[i] = static_cast<uint32_t>(lo + 1);
 }
 
-__global__ void seg_double_kernel(const uint32_t *Jk, uint32_t *Jk1, uint64_t nrec) {
+__global__ void seg_pow_kernel(const uint32_t *Jk, uint32_t *Jk1, uint64_t nrec) {
   const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (i <= nrec) Jk1[i] = Jk[Jk[i]];
+  if (i > nrec) return;
+  uint32_t x = static_cast<uint32_t>(i);
+#pragma unroll
+  for (uint32_t j = 0; j < kSegRadix; j++) x = Jk[x];
+  Jk1[i] = x;
 }
 
+// number of blocks: hops of the chain from 0 that stay below nrec, + 1
 __global__ void seg_depth_kernel(const uint32_t *J, uint32_t levels, uint64_t stride, uint64_t nrec,
                                  uint64_t *d_nblocks, uint64_t *blk_first) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   uint64_t pos = 0, cnt = 0;
   if (nrec > 0) {
-    for (int k = static_cast<int>(levels) - 1; k >= 0; k--) {
-      const uint32_t nx = J[static_cast<uint64_t>(k) * stride + pos];
-      if (nx < nrec) {
+    uint64_t w = 1;
+    for (uint32_t k = 1; k < levels; k++) w *= kSegRadix;
+    for (int k = static_cast<int>(levels) - 1; k >= 0; k--, w /= kSegRadix) {
+      const uint32_t *Jk = J + static_cast<uint64_t>(k) * stride;
+      for (uint32_t d = 1; d < kSegRadix; d++) {
+        const uint32_t nx = Jk[pos];
+        if (nx >= nrec) break;
         pos = nx;
-        cnt += 1ull << k;
+        cnt += w;
       }
     }
     cnt += 1;
@@ -787,14 +868,20 @@ __global__ void seg_emit_kernel(const uint32_t *J, uint32_t levels, uint64_t str
                                 const uint64_t *d_nblocks, uint64_t *blk_first) {
   const uint64_t t = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (t >= *d_nblocks) return;
-  uint64_t pos = 0;
-  for (uint32_t k = 0; k < levels; k++)
-    if ((t >> k) & 1) pos = J[static_cast<uint64_t>(k) * stride + pos];
+  uint32_t pos = 0;
+  uint64_t q = t;
+  for (uint32_t k = 0; k < levels && q; k++, q /= kSegRadix) {
+    const uint32_t *Jk = J + static_cast<uint64_t>(k) * stride;
+    for (uint32_t d = static_cast<uint32_t>(q % kSegRadix); d; d--) pos = Jk[pos];
+  }
   blk_first[t] = pos;
 }
 
 // ---------------------------------------------------------------------------
-// Device-wide exclusive scan of u64: reduce-then-scan, 2048 items per tile.
+// Device-wide exclusive scan of u64.  Up to 2048 items: one workgroup
+// (scan_apply_kernel).  Beyond: single pass with decoupled look-back
+// (scan_lookback_kernel, 4096 items per tile): read n, write n, instead of
+// reduce-then-scan's 2 reads + 1 write and its extra launches.
 // ---------------------------------------------------------------------------
 constexpr uint32_t kScanThreads = 256, kScanItems = 8, kScanTile = kScanThreads * kScanItems;
 
@@ -814,18 +901,6 @@ __device__ __forceinline__ uint64_t wg_excl_scan_u64(uint64_t v, uint64_t &total
   __syncthreads();
   total = tot;
   return base + incl - v;
-}
-
-__global__ __launch_bounds__(kScanThreads) void scan_reduce_kernel(const uint64_t *in, uint64_t n,
-                                                                   uint64_t *partials) {
-  const uint64_t t0 = static_cast<uint64_t>(blockIdx.x) * kScanTile + threadIdx.x * kScanItems;
-  uint64_t s = 0;
-#pragma unroll
-  for (uint32_t j = 0; j < kScanItems; j++)
-    if (t0 + j < n) s += in[t0 + j];
-  uint64_t tot;
-  wg_excl_scan_u64(s, tot);
-  if (threadIdx.x == 0) partials[blockIdx.x] = tot;
 }
 
 // out[i] = carry_in + sum(in[0..i)), out[n] = carry_in + total.  in may alias out.
@@ -854,6 +929,97 @@ __global__ __launch_bounds__(kScanThreads) void scan_apply_kernel(const uint64_t
   }
 }
 
+// Tile status word: 2 flag bits + 62 value bits in ONE u64, published and
+// polled with agent-scope atomics (per-XCD L2s are not coherent; an sc1 store
+// / sc1 load pair on a single word needs no separate fence).  Totals must stay
+// below 2^62.  Tiles are numbered by a ticket counter so every tile a
+// workgroup waits on is already resident.  ws = [ticket, status[tiles]],
+// zeroed by the launcher.
+constexpr uint32_t kLbItems = 16, kLbTile = kScanThreads * kLbItems;
+constexpr uint64_t kLbAgg = 1ull << 62, kLbInc = 2ull << 62, kLbVal = kLbAgg - 1;
+constexpr uint64_t kLbSpinLimit = 1ull << 24; // never reached unless a tile died
+
+__device__ __forceinline__ uint32_t lb_idx(uint32_t i) { return i + (i >> 4); } // 1 pad per 16
+
+__global__ __launch_bounds__(kScanThreads) void scan_lookback_kernel(const uint64_t *in, uint64_t n,
+                                                                     uint64_t carry_in, uint64_t *out,
+                                                                     uint64_t *ws) {
+  __shared__ uint64_t sm[kLbTile + kLbTile / 16];
+  __shared__ uint64_t s_wsum[kScanThreads / kWave];
+  __shared__ uint64_t s_tile, s_prefix;
+  const uint32_t tid = threadIdx.x, lane = lane_id(), w = tid / kWave;
+  if (tid == 0) s_tile = __hip_atomic_fetch_add(ws, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  const uint64_t tile = s_tile;
+  const uint64_t base = tile * kLbTile;
+  uint64_t *status = ws + 1;
+#pragma unroll
+  for (uint32_t j = 0; j < kLbItems; j++) {
+    const uint32_t i = j * kScanThreads + tid;
+    sm[lb_idx(i)] = base + i < n ? in[base + i] : 0;
+  }
+  __syncthreads();
+  uint64_t v[kLbItems], sum = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < kLbItems; j++) {
+    v[j] = sm[lb_idx(tid * kLbItems + j)];
+    sum += v[j];
+  }
+  const uint64_t incl = wave_incl_scan_u64(sum);
+  if (lane == kWave - 1) s_wsum[w] = incl;
+  __syncthreads();
+  uint64_t wbase = 0, total = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < kScanThreads / kWave; k++) {
+    const uint64_t x = s_wsum[k];
+    if (k < w) wbase += x;
+    total += x;
+  }
+  if (w == 0) {
+    uint64_t prefix = 0;
+    if (tile == 0) {
+      if (lane == 0) __hip_atomic_store(&status[0], kLbInc | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      if (lane == 0) __hip_atomic_store(&status[tile], kLbAgg | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      int64_t p = static_cast<int64_t>(tile) - 1; // window [p - 63, p]
+      uint64_t spins = 0;
+      for (;;) {
+        const int64_t q = p - static_cast<int64_t>(lane);
+        const uint64_t st = q >= 0 ? __hip_atomic_load(&status[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                   : kLbInc;
+        const uint64_t inc = __ballot((st >> 62) == 2);
+        const uint32_t need = inc ? static_cast<uint32_t>(__ffsll(static_cast<long long>(inc))) : kWave;
+        const uint64_t zero = __ballot((st >> 62) == 0 && lane < need);
+        if (zero) {
+          if (++spins > kLbSpinLimit) break; // a predecessor never published: give up (wrong sums, no hang)
+          __builtin_amdgcn_s_sleep(1);
+          continue;
+        }
+        prefix += wave_sum_u64(lane < need ? (st & kLbVal) : 0);
+        if (inc) break;
+        p -= kWave;
+      }
+      if (lane == 0)
+        __hip_atomic_store(&status[tile], kLbInc | (prefix + total), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (lane == 0) s_prefix = prefix;
+  }
+  __syncthreads();
+  uint64_t run = carry_in + s_prefix + wbase + incl - sum;
+#pragma unroll
+  for (uint32_t j = 0; j < kLbItems; j++) {
+    sm[lb_idx(tid * kLbItems + j)] = run;
+    run += v[j];
+  }
+  __syncthreads();
+#pragma unroll
+  for (uint32_t j = 0; j < kLbItems; j++) {
+    const uint32_t i = j * kScanThreads + tid;
+    if (base + i < n) out[base + i] = sm[lb_idx(i)];
+  }
+  if (tid == 0 && base < n && n <= base + kLbTile) out[n] = carry_in + s_prefix + total;
+}
+
 // ---------------------------------------------------------------------------
 // Launch wrappers
 // ---------------------------------------------------------------------------
@@ -875,29 +1041,18 @@ hipError_t launch_decode(const DecArgs &a, hipStream_t s) {
   return hipGetLastError();
 }
 
-uint64_t scan_workspace_elems(uint64_t n) {
-  uint64_t tot = 0;
-  uint64_t m = (n + kScanTile - 1) / kScanTile;
-  while (m > 1) {
-    tot += m + 1;
-    m = (m + kScanTile - 1) / kScanTile;
-  }
-  return tot + 2;
-}
+uint64_t scan_workspace_elems(uint64_t n) { return (n + kLbTile - 1) / kLbTile + 2; }
 
 hipError_t launch_scan(const uint64_t *in, uint64_t n, uint64_t carry_in, uint64_t *out, uint64_t *ws,
                        hipStream_t s) {
-  const uint64_t tiles = (n + kScanTile - 1) / kScanTile;
-  if (tiles <= 1) {
+  if (n <= kScanTile) {
     scan_apply_kernel<<<1, kScanThreads, 0, s>>>(in, n, nullptr, carry_in, out);
     return hipGetLastError();
   }
-  uint64_t *partials = ws;           // tiles elements
-  uint64_t *tile_base = ws;          // scanned in place (tiles + 1 elements)
-  scan_reduce_kernel<<<static_cast<uint32_t>(tiles), kScanThreads, 0, s>>>(in, n, partials);
-  hipError_t e = launch_scan(partials, tiles, 0, tile_base, ws + tiles + 1, s);
+  const uint64_t tiles = (n + kLbTile - 1) / kLbTile;
+  hipError_t e = hipMemsetAsync(ws, 0, (tiles + 1) * sizeof(uint64_t), s);
   if (e != hipSuccess) return e;
-  scan_apply_kernel<<<static_cast<uint32_t>(tiles), kScanThreads, 0, s>>>(in, n, tile_base, carry_in, out);
+  scan_lookback_kernel<<<static_cast<uint32_t>(tiles), kScanThreads, 0, s>>>(in, n, carry_in, out, ws);
   return hipGetLastError();
 }
 
@@ -922,13 +1077,16 @@ hipError_t launch_enc_emit(const EncArgs &a, hipStream_t s) {
 
 hipError_t launch_segment(const uint64_t *Pw, uint64_t nrec, uint64_t threshold, uint32_t *J,
                           uint32_t levels, uint64_t *d_nblocks, uint64_t *blk_first, hipStream_t s,
-                          const uint32_t *clamp) {
+                          const uint32_t *clamp, uint64_t add) {
+  // levels = binary levels the caller provisioned (J holds levels * (nrec + 1));
+  // radix-8 needs ceil(levels / 3) of them
+  const uint32_t lv = (levels + 2) / 3;
   const uint64_t stride = nrec + 1;
-  seg_next_kernel<<<grid_for(nrec + 1, 256), 256, 0, s>>>(Pw, nrec, threshold, clamp, J);
-  for (uint32_t k = 0; k + 1 < levels; k++)
-    seg_double_kernel<<<grid_for(nrec + 1, 256), 256, 0, s>>>(J + k * stride, J + (k + 1) * stride, nrec);
-  seg_depth_kernel<<<1, 64, 0, s>>>(J, levels, stride, nrec, d_nblocks, blk_first);
-  if (nrec) seg_emit_kernel<<<grid_for(nrec, 256), 256, 0, s>>>(J, levels, stride, d_nblocks, blk_first);
+  seg_next_kernel<<<grid_for(nrec + 1, 256), 256, 0, s>>>(Pw, add, nrec, threshold, clamp, J);
+  for (uint32_t k = 0; k + 1 < lv; k++)
+    seg_pow_kernel<<<grid_for(nrec + 1, 256), 256, 0, s>>>(J + k * stride, J + (k + 1) * stride, nrec);
+  seg_depth_kernel<<<1, 64, 0, s>>>(J, lv, stride, nrec, d_nblocks, blk_first);
+  if (nrec) seg_emit_kernel<<<grid_for(nrec, 256), 256, 0, s>>>(J, lv, stride, d_nblocks, blk_first);
   return hipGetLastError();
 }
 

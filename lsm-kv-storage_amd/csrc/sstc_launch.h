@@ -72,7 +72,7 @@ hipError_t launch_enc_blk_len(const uint64_t *P, const uint64_t *blk_first, uint
 hipError_t launch_enc_emit(const EncArgs &a, hipStream_t s);
 hipError_t launch_segment(const uint64_t *Pw, uint64_t nrec, uint64_t threshold, uint32_t *J,
                           uint32_t levels, uint64_t *d_nblocks, uint64_t *blk_first, hipStream_t s,
-                          const uint32_t *clamp = nullptr);
+                          const uint32_t *clamp = nullptr, uint64_t add = 0);
 
 // persistent device workspace of one context (compaction)
 struct Arena {
