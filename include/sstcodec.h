@@ -194,6 +194,45 @@ int sstc_compact(sstc_ctx *ctx, const uint8_t *d_src, const uint64_t *d_blk_off,
                  const sstc_compact_params *params, uint8_t *d_dst, uint64_t dst_cap, uint64_t *d_table_off,
                  uint64_t *d_table_len, uint64_t max_tables, sstc_compact_result *result);
 
+
+/* ---- file-to-file compaction (Compact::DoCompactJob end to end: the input
+ *      SST files are read, compacted on the device and the output SSTs written
+ *      and fsync'ed, db/compact.cc:232-322 with io/linux_file.cc:138-195) --- */
+
+typedef struct sstc_pipe sstc_pipe; /* pinned host + device staging, grow-only */
+
+typedef struct sstc_file_out {
+  uint64_t sst_id;           /* output file = out_prefix + sst_id + ".sst"      */
+  uint64_t file_size;        /* TableBuilder::GetFileSize(): bytes + 1          */
+  uint64_t smallest_key_off; /* GetSmallestKey() bytes in key_arena             */
+  uint64_t largest_key_off;  /* GetLargestKey() bytes in key_arena              */
+  uint32_t smallest_key_len, largest_key_len;
+} sstc_file_out;
+
+typedef struct sstc_files_timing {
+  double index_s;   /* footer + meta section read and parse (host, per file) */
+  double load_s;    /* data sections: pread into pinned memory + H2D, overlapped */
+  double compact_s; /* sstc_compact on the device                               */
+  double store_s;   /* D2H + pwrite + fsync of the outputs, overlapped          */
+  double total_s;
+} sstc_files_timing;
+
+int sstc_pipe_create(sstc_ctx *ctx, uint32_t io_threads, sstc_pipe **out);
+int sstc_pipe_destroy(sstc_pipe *pipe);
+
+/* Compact the SST files in_paths[0..n_in) (iterator order, each with its
+ * GetFileSize() value in in_file_sizes = bytes + 1) into out_prefix + id +
+ * ".sst", ids first_sst_id, first_sst_id + 1, ... (Compact::DoCompactJob's
+ * GetNextSSTId() sequence).  Output files are created or truncated; fsync when
+ * do_fsync (TableBuilder::Finish does).  Per output: id, GetFileSize() and the
+ * smallest / largest key copied into key_arena (what VersionEdit::AddNewFiles
+ * records).  timing may be NULL. */
+int sstc_compact_files(sstc_pipe *pipe, const char *const *in_paths, const uint64_t *in_file_sizes,
+                       uint32_t n_in, const char *out_prefix, uint64_t first_sst_id,
+                       const sstc_compact_params *params, uint32_t do_fsync, sstc_file_out *outs,
+                       uint32_t max_outs, uint32_t *n_out, uint8_t *key_arena, uint64_t key_arena_cap,
+                       sstc_files_timing *timing);
+
 #ifdef __cplusplus
 }
 #endif

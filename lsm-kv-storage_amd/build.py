@@ -17,7 +17,7 @@ LIB = os.path.join(HERE, "lib")
 ARCH = os.environ.get("SSTC_OFFLOAD_ARCH", "gfx950")
 
 HIP_SOURCES = ["sstc_kernels.hip", "sstc_compact.hip", "sstc_api.hip"]
-HOST_SOURCES = ["host/sst_table.cpp"]
+HOST_SOURCES = ["host/sst_table.cpp", "host/compact_files.cpp"]
 
 
 def _hipcc():

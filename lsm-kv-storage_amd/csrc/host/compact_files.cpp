@@ -1,0 +1,405 @@
+// compact_files.cpp — file-to-file compaction (include/sstcodec.h
+// sstc_compact_files): the I/O half of Compact::DoCompactJob
+// (db/compact.cc:232-322, io/linux_file.cc:138-195) around the device job
+// sstc_compact.
+//
+//   index   one thread per input file preads the 40 B footer and the meta
+//           section and walks it (TableReader, table_reader.cc:52-156);
+//   load    the data sections are read in 16 MiB chunks by io_threads into
+//           pinned memory and every finished chunk is copied H2D at once, so
+//           file reads overlap PCIe;
+//   compact sstc_compact (device; synchronous);
+//   store   every output SST is copied D2H as one async copy with an event;
+//           writer threads wait for their table's event, pwrite, fsync.
+//
+// The reference writes each block with three pwrite64 and fsyncs per output
+// SST (table_builder.cc:62-99,147-211); here each output SST is one pwrite.
+#include <fcntl.h>
+#include <hip/hip_runtime_api.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cerrno>
+#include <chrono>
+#include <condition_variable>
+#include <cstring>
+#include <deque>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "sstcodec.h"
+
+extern "C" int sstc__fail(int code, const char *what); // sstc_api.hip: sets sstc_last_error_string
+
+struct sstc_pipe {
+  sstc_ctx *ctx = nullptr;
+  int device = 0;
+  uint32_t io_threads = 8;
+  hipStream_t stream = nullptr;
+  uint8_t *h_in = nullptr, *h_out = nullptr, *d_src = nullptr, *d_dst = nullptr;
+  uint64_t *d_idx = nullptr;
+  uint64_t cap_h_in = 0, cap_h_out = 0, cap_d_src = 0, cap_d_dst = 0, cap_d_idx = 0;
+};
+
+namespace {
+
+using clk = std::chrono::steady_clock;
+constexpr uint64_t kChunk = 16ull << 20;
+
+double secs(clk::time_point a, clk::time_point b) { return std::chrono::duration<double>(b - a).count(); }
+
+uint32_t get32(const uint8_t *p) {
+  uint32_t v;
+  std::memcpy(&v, p, 4);
+  return v;
+}
+uint64_t get64(const uint8_t *p) {
+  uint64_t v;
+  std::memcpy(&v, p, 8);
+  return v;
+}
+
+bool pread_full(int fd, uint8_t *buf, uint64_t size, uint64_t off) {
+  while (size > 0) {
+    const ssize_t r = ::pread(fd, buf, size, static_cast<off_t>(off));
+    if (r < 0 && errno == EINTR) continue;
+    if (r <= 0) return false;
+    buf += r;
+    size -= static_cast<uint64_t>(r);
+    off += static_cast<uint64_t>(r);
+  }
+  return true;
+}
+
+bool pwrite_full(int fd, const uint8_t *buf, uint64_t size, uint64_t off) {
+  while (size > 0) {
+    const ssize_t w = ::pwrite(fd, buf, size, static_cast<off_t>(off));
+    if (w < 0 && errno == EINTR) continue;
+    if (w <= 0) return false;
+    buf += w;
+    size -= static_cast<uint64_t>(w);
+    off += static_cast<uint64_t>(w);
+  }
+  return true;
+}
+
+int grow_pinned(uint8_t *&p, uint64_t &cap, uint64_t need) {
+  if (p && need <= cap) return 0;
+  if (p) (void)hipHostFree(p);
+  p = nullptr;
+  cap = 0;
+  const uint64_t n = need + need / 8 + 4096;
+  if (hipHostMalloc(reinterpret_cast<void **>(&p), n, hipHostMallocDefault) != hipSuccess) {
+    p = nullptr;
+    return -1;
+  }
+  cap = n;
+  return 0;
+}
+
+template <class T> int grow_dev(T *&p, uint64_t &cap, uint64_t need_elems) {
+  if (p && need_elems <= cap) return 0;
+  if (p) (void)hipFree(p);
+  p = nullptr;
+  cap = 0;
+  const uint64_t n = need_elems + need_elems / 8 + 1024;
+  if (hipMalloc(reinterpret_cast<void **>(&p), n * sizeof(T)) != hipSuccess) {
+    p = nullptr;
+    return -1;
+  }
+  cap = n;
+  return 0;
+}
+
+struct InFile {
+  int fd = -1;
+  uint64_t bytes = 0, meta_off = 0, base = 0;
+  std::vector<uint64_t> off, len;
+  bool ok = false;
+};
+
+// DecodeExtraInfo + FetchBlockIndexInfo (table_reader.cc:52-156)
+void index_file(InFile &f) {
+  uint8_t foot[40];
+  if (f.bytes < 40 || !pread_full(f.fd, foot, 40, f.bytes - 40)) return;
+  const uint64_t nb = get64(foot), moff = get64(foot + 8), mlen = get64(foot + 16);
+  if (moff > f.bytes - 40 || mlen > f.bytes - 40 - moff) return;
+  std::vector<uint8_t> meta(mlen);
+  if (mlen && !pread_full(f.fd, meta.data(), mlen, moff)) return;
+  f.off.reserve(nb);
+  f.len.reserve(nb);
+  uint64_t p = 0;
+  for (uint64_t i = 0; i < nb; i++) {
+    if (p + 4 > mlen) return;
+    const uint64_t fk = get32(&meta[p]);
+    if (p + 8 + fk > mlen) return;
+    const uint64_t lk = get32(&meta[p + 4 + fk]);
+    if (p + 24 + fk + lk > mlen) return;
+    const uint64_t bo = get64(&meta[p + 8 + fk + lk]), bl = get64(&meta[p + 16 + fk + lk]);
+    if (bo > moff || bl > moff - bo) return;
+    f.off.push_back(bo);
+    f.len.push_back(bl);
+    p += 24 + fk + lk;
+  }
+  f.meta_off = moff;
+  f.ok = true;
+}
+
+// smallest / largest key of a finished table image (its first and last meta
+// entries: TableBuilder::GetSmallestKey/GetLargestKey, table_builder.h:118-125)
+void table_keys(const uint8_t *img, uint64_t bytes, std::string &lo, std::string &hi) {
+  lo.clear();
+  hi.clear();
+  if (bytes < 40) return;
+  const uint8_t *foot = img + bytes - 40;
+  const uint64_t nb = get64(foot), moff = get64(foot + 8);
+  const uint8_t *m = img + moff;
+  for (uint64_t i = 0; i < nb; i++) {
+    const uint32_t fk = get32(m);
+    const uint32_t lk = get32(m + 4 + fk);
+    if (i == 0) lo.assign(reinterpret_cast<const char *>(m + 4), fk);
+    if (i + 1 == nb) hi.assign(reinterpret_cast<const char *>(m + 8 + fk), lk);
+    m += 24ull + fk + lk;
+  }
+}
+
+struct FdGuard {
+  std::vector<InFile> &files;
+  ~FdGuard() {
+    for (auto &f : files)
+      if (f.fd >= 0) ::close(f.fd);
+  }
+};
+
+} // namespace
+
+extern "C" {
+
+int sstc_pipe_create(sstc_ctx *ctx, uint32_t io_threads, sstc_pipe **out) {
+  if (!ctx || !out) return sstc__fail(SSTC_E_INVALID_ARG, "sstc_pipe_create: NULL argument");
+  *out = nullptr;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return sstc__fail(SSTC_E_NO_DEVICE, "no HIP device");
+  sstc_pipe *p = new sstc_pipe();
+  p->ctx = ctx;
+  p->device = dev;
+  p->io_threads = io_threads ? io_threads : 8;
+  if (hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete p;
+    return sstc__fail(SSTC_E_HIP, "sstc_pipe_create: hipStreamCreate");
+  }
+  *out = p;
+  return SSTC_OK;
+}
+
+int sstc_pipe_destroy(sstc_pipe *p) {
+  if (!p) return SSTC_OK;
+  (void)hipSetDevice(p->device);
+  (void)hipStreamSynchronize(p->stream);
+  if (p->h_in) (void)hipHostFree(p->h_in);
+  if (p->h_out) (void)hipHostFree(p->h_out);
+  for (void *d : {static_cast<void *>(p->d_src), static_cast<void *>(p->d_dst), static_cast<void *>(p->d_idx)})
+    if (d) (void)hipFree(d);
+  (void)hipStreamDestroy(p->stream);
+  delete p;
+  return SSTC_OK;
+}
+
+int sstc_compact_files(sstc_pipe *pipe, const char *const *in_paths, const uint64_t *in_file_sizes,
+                       uint32_t n_in, const char *out_prefix, uint64_t first_sst_id,
+                       const sstc_compact_params *params, uint32_t do_fsync, sstc_file_out *outs,
+                       uint32_t max_outs, uint32_t *n_out, uint8_t *key_arena, uint64_t key_arena_cap,
+                       sstc_files_timing *timing) {
+  if (!pipe || (n_in && (!in_paths || !in_file_sizes)) || !out_prefix || !params || !outs || !n_out)
+    return sstc__fail(SSTC_E_INVALID_ARG, "sstc_compact_files: NULL argument");
+  if (params->table_limit == 0 || params->block_threshold == 0)
+    return sstc__fail(SSTC_E_INVALID_ARG, "sstc_compact_files: bad parameters");
+  *n_out = 0;
+  if (hipSetDevice(pipe->device) != hipSuccess) return sstc__fail(SSTC_E_HIP, "hipSetDevice");
+  const auto t0 = clk::now();
+  hipStream_t s = pipe->stream;
+
+  // ---- index: footers + meta sections, one thread per file
+  std::vector<InFile> files(n_in);
+  FdGuard guard{files};
+  for (uint32_t i = 0; i < n_in; i++) {
+    files[i].fd = ::open(in_paths[i], O_RDONLY);
+    if (files[i].fd < 0 || in_file_sizes[i] < 41)
+      return sstc__fail(SSTC_E_INVALID_ARG, (std::string("cannot open SST ") + in_paths[i]).c_str());
+    files[i].bytes = in_file_sizes[i] - 1; // GetFileSize() = bytes + 1
+  }
+  {
+    std::vector<std::thread> th;
+    for (auto &f : files) th.emplace_back(index_file, std::ref(f));
+    for (auto &t : th) t.join();
+  }
+  uint64_t total = 0, nblocks = 0;
+  std::vector<uint64_t> tfb(1, 0);
+  for (uint32_t i = 0; i < n_in; i++) {
+    if (!files[i].ok) return sstc__fail(SSTC_E_INVALID_ARG, (std::string("bad SST index: ") + in_paths[i]).c_str());
+    files[i].base = total;
+    total += (files[i].meta_off + 255) & ~uint64_t(255);
+    nblocks += files[i].off.size();
+    tfb.push_back(nblocks);
+  }
+  const auto t1 = clk::now();
+
+  // ---- load: chunked preads into pinned memory, each chunk copied H2D when done
+  const uint64_t idx_at = (total + 255) & ~uint64_t(255);
+  if (grow_pinned(pipe->h_in, pipe->cap_h_in, idx_at + 16 * nblocks + 16) ||
+      grow_dev(pipe->d_src, pipe->cap_d_src, total + 16))
+    return sstc__fail(SSTC_E_NOMEM, "sstc_compact_files: input staging");
+  struct Chunk {
+    uint32_t file;
+    uint64_t off, len;
+  };
+  std::vector<Chunk> chunks;
+  for (uint32_t i = 0; i < n_in; i++)
+    for (uint64_t o = 0; o < files[i].meta_off; o += kChunk)
+      chunks.push_back({i, o, std::min(kChunk, files[i].meta_off - o)});
+  std::mutex mu;
+  std::condition_variable cv;
+  std::deque<int64_t> done; // chunk index, or -1 - index on a read failure
+  std::atomic<size_t> next{0};
+  const uint32_t nth = std::max<uint32_t>(1, std::min<uint32_t>(pipe->io_threads, chunks.size()));
+  std::vector<std::thread> readers;
+  for (uint32_t w = 0; w < nth && !chunks.empty(); w++)
+    readers.emplace_back([&] {
+      for (size_t c; (c = next.fetch_add(1)) < chunks.size();) {
+        const Chunk &k = chunks[c];
+        const bool ok = pread_full(files[k.file].fd, pipe->h_in + files[k.file].base + k.off, k.len, k.off);
+        std::lock_guard<std::mutex> lk(mu);
+        done.push_back(ok ? static_cast<int64_t>(c) : -1 - static_cast<int64_t>(c));
+        cv.notify_one();
+      }
+    });
+  bool read_ok = true;
+  hipError_t herr = hipSuccess;
+  for (size_t got = 0; got < chunks.size(); got++) {
+    int64_t c;
+    {
+      std::unique_lock<std::mutex> lk(mu);
+      cv.wait(lk, [&] { return !done.empty(); });
+      c = done.front();
+      done.pop_front();
+    }
+    if (c < 0) {
+      read_ok = false;
+      continue;
+    }
+    const Chunk &k = chunks[c];
+    const uint64_t at = files[k.file].base + k.off;
+    if (herr == hipSuccess) herr = hipMemcpyAsync(pipe->d_src + at, pipe->h_in + at, k.len, hipMemcpyHostToDevice, s);
+  }
+  for (auto &t : readers) t.join();
+  if (!read_ok) return sstc__fail(SSTC_E_INVALID_ARG, "sstc_compact_files: input read failed");
+  // block index (absolute offsets into the staged data sections)
+  uint64_t *h_off = reinterpret_cast<uint64_t *>(pipe->h_in + idx_at), *h_len = h_off + nblocks;
+  for (uint32_t i = 0, b = 0; i < n_in; i++)
+    for (size_t j = 0; j < files[i].off.size(); j++, b++) {
+      h_off[b] = files[i].base + files[i].off[j];
+      h_len[b] = files[i].len[j];
+    }
+  const uint64_t max_tables = std::min(total / params->table_limit + 2, total / 13 + 2);
+  if (grow_dev(pipe->d_idx, pipe->cap_d_idx, 2 * nblocks + 2 * max_tables + 2))
+    return sstc__fail(SSTC_E_NOMEM, "sstc_compact_files: index staging");
+  uint64_t *d_off = pipe->d_idx, *d_len = d_off + nblocks, *d_toff = d_len + nblocks, *d_tlen = d_toff + max_tables + 1;
+  if (herr == hipSuccess && nblocks)
+    herr = hipMemcpyAsync(d_off, h_off, 16 * nblocks, hipMemcpyHostToDevice, s);
+  if (herr == hipSuccess) herr = hipStreamSynchronize(s);
+  if (herr != hipSuccess) return sstc__fail(SSTC_E_HIP, "sstc_compact_files: H2D");
+  const auto t2 = clk::now();
+
+  // ---- compact on the device
+  sstc_compact_result res{};
+  uint64_t cap = total + total / 2 + (1u << 20);
+  int rc = SSTC_E_CAPACITY;
+  for (int attempt = 0; attempt < 2 && rc == SSTC_E_CAPACITY; attempt++) {
+    if (grow_dev(pipe->d_dst, pipe->cap_d_dst, cap)) return sstc__fail(SSTC_E_NOMEM, "sstc_compact_files: output");
+    rc = sstc_compact(pipe->ctx, pipe->d_src, d_off, d_len, nblocks, tfb.data(), n_in, params, pipe->d_dst,
+                      pipe->cap_d_dst, d_toff, d_tlen, max_tables, &res);
+    cap = res.bytes_out; // exact size known after a capacity miss
+  }
+  if (rc != SSTC_OK) return rc; // sstc_compact set the error string
+  const auto t3 = clk::now();
+
+  // ---- store: per-table D2H with an event, writer threads pwrite + fsync
+  const uint64_t nt = res.tables_out;
+  if (nt > max_outs) return sstc__fail(SSTC_E_CAPACITY, "sstc_compact_files: more output tables than max_outs");
+  std::vector<uint64_t> toff(nt + 1);
+  if (hipMemcpy(toff.data(), d_toff, 8 * (nt + 1), hipMemcpyDeviceToHost) != hipSuccess)
+    return sstc__fail(SSTC_E_HIP, "sstc_compact_files: table offsets");
+  if (grow_pinned(pipe->h_out, pipe->cap_h_out, toff[nt] + 16))
+    return sstc__fail(SSTC_E_NOMEM, "sstc_compact_files: output staging");
+  std::vector<hipEvent_t> ev(nt);
+  for (uint64_t t = 0; t < nt; t++) {
+    if (hipEventCreateWithFlags(&ev[t], hipEventDisableTiming) != hipSuccess ||
+        hipMemcpyAsync(pipe->h_out + toff[t], pipe->d_dst + toff[t], toff[t + 1] - toff[t], hipMemcpyDeviceToHost,
+                       s) != hipSuccess ||
+        hipEventRecord(ev[t], s) != hipSuccess) {
+      (void)hipStreamSynchronize(s);
+      for (uint64_t u = 0; u <= t && u < nt; u++)
+        if (ev[u]) (void)hipEventDestroy(ev[u]);
+      return sstc__fail(SSTC_E_HIP, "sstc_compact_files: D2H");
+    }
+  }
+  std::vector<std::string> lo(nt), hi(nt);
+  std::atomic<uint64_t> tnext{0};
+  std::atomic<int> werr{0};
+  std::vector<std::thread> writers;
+  const std::string prefix(out_prefix);
+  const uint32_t nw = static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>(pipe->io_threads, nt)));
+  for (uint32_t w = 0; w < nw; w++)
+    writers.emplace_back([&] {
+      (void)hipSetDevice(pipe->device);
+      for (uint64_t t; (t = tnext.fetch_add(1)) < nt;) {
+        if (hipEventSynchronize(ev[t]) != hipSuccess) {
+          werr = 1;
+          continue;
+        }
+        const uint8_t *img = pipe->h_out + toff[t];
+        const uint64_t bytes = toff[t + 1] - toff[t];
+        const std::string path = prefix + std::to_string(first_sst_id + t) + ".sst";
+        const int fd = ::open(path.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
+        if (fd < 0 || !pwrite_full(fd, img, bytes, 0) || (do_fsync && ::fsync(fd) < 0)) werr = 2;
+        if (fd >= 0) ::close(fd);
+        table_keys(img, bytes, lo[t], hi[t]);
+      }
+    });
+  for (auto &t : writers) t.join();
+  for (auto &e : ev) (void)hipEventDestroy(e);
+  if (werr) return sstc__fail(werr == 1 ? SSTC_E_HIP : SSTC_E_INVALID_ARG, "sstc_compact_files: output write failed");
+  uint64_t kat = 0;
+  for (uint64_t t = 0; t < nt; t++) {
+    sstc_file_out &o = outs[t];
+    o.sst_id = first_sst_id + t;
+    o.file_size = toff[t + 1] - toff[t] + 1;
+    o.smallest_key_len = static_cast<uint32_t>(lo[t].size());
+    o.largest_key_len = static_cast<uint32_t>(hi[t].size());
+    o.smallest_key_off = kat;
+    o.largest_key_off = kat + lo[t].size();
+    if (key_arena) {
+      if (kat + lo[t].size() + hi[t].size() > key_arena_cap)
+        return sstc__fail(SSTC_E_CAPACITY, "sstc_compact_files: key_arena too small");
+      std::memcpy(key_arena + kat, lo[t].data(), lo[t].size());
+      std::memcpy(key_arena + kat + lo[t].size(), hi[t].data(), hi[t].size());
+    }
+    kat += lo[t].size() + hi[t].size();
+  }
+  *n_out = static_cast<uint32_t>(nt);
+  const auto t4 = clk::now();
+  if (timing) {
+    timing->index_s = secs(t0, t1);
+    timing->load_s = secs(t1, t2);
+    timing->compact_s = secs(t2, t3);
+    timing->store_s = secs(t3, t4);
+    timing->total_s = secs(t0, t4);
+  }
+  return SSTC_OK;
+}
+
+} // extern "C"

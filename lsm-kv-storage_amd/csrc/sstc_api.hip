@@ -104,6 +104,10 @@ extern "C" {
 
 uint32_t sstc_version(void) { return SSTC_ABI_VERSION; }
 
+// internal: lets the host-only translation units (host/*.cpp) report errors
+// through sstc_last_error_string
+int sstc__fail(int code, const char *what) { return fail(code, what); }
+
 const char *sstc_last_error_string(void) { return g_last_error.c_str(); }
 
 int sstc_ctx_create(int device, void *stream, sstc_ctx **out) {

@@ -533,9 +533,9 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
       uint8_t foot[40] = {0};
       const uint64_t mn = ~0ull;
       memcpy(foot + 24, &mn, 8);
-      const uint64_t zero = 0, forty = 40;
+      const uint64_t offs[2] = {0, 40}, forty = 40;
       CK(hipMemcpyAsync(d_dst, foot, 40, hipMemcpyHostToDevice, s));
-      CK(hipMemcpyAsync(d_table_off, &zero, 8, hipMemcpyHostToDevice, s));
+      CK(hipMemcpyAsync(d_table_off, offs, 16, hipMemcpyHostToDevice, s)); // nt + 1 entries
       CK(hipMemcpyAsync(d_table_len, &forty, 8, hipMemcpyHostToDevice, s));
       CK(hipStreamSynchronize(s));
       res[1] = 0; res[2] = 0; res[3] = 1; res[4] = 40;

@@ -41,6 +41,17 @@ class CompactResult(ctypes.Structure):
                 ("blocks_out", ctypes.c_uint64), ("tables_out", ctypes.c_uint64), ("bytes_out", ctypes.c_uint64)]
 
 
+class FileOut(ctypes.Structure):
+    _fields_ = [("sst_id", ctypes.c_uint64), ("file_size", ctypes.c_uint64), ("smallest_key_off", ctypes.c_uint64),
+                ("largest_key_off", ctypes.c_uint64), ("smallest_key_len", ctypes.c_uint32),
+                ("largest_key_len", ctypes.c_uint32)]
+
+
+class FilesTiming(ctypes.Structure):
+    _fields_ = [("index_s", ctypes.c_double), ("load_s", ctypes.c_double), ("compact_s", ctypes.c_double),
+                ("store_s", ctypes.c_double), ("total_s", ctypes.c_double)]
+
+
 class SstcError(RuntimeError):
     pass
 
@@ -75,6 +86,10 @@ def load():
         "sstc_roundtrip_blocks": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_u64, c_u32, c_vp, c_vp]),
         "sstc_compact": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_u64, c_vp, c_u32, P(CompactParams), c_vp, c_u64,
                                         c_vp, c_vp, c_u64, P(CompactResult)]),
+        "sstc_pipe_create": (ctypes.c_int, [c_vp, c_u32, P(c_vp)]),
+        "sstc_pipe_destroy": (ctypes.c_int, [c_vp]),
+        "sstc_compact_files": (ctypes.c_int, [c_vp, c_vp, c_vp, c_u32, ctypes.c_char_p, c_u64, P(CompactParams),
+                                              c_u32, c_vp, c_u32, P(c_u32), c_vp, c_u64, P(FilesTiming)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

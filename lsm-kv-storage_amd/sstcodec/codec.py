@@ -210,6 +210,56 @@ class Codec:
         return [d[int(o[t]):int(o[t + 1])] for t in range(nt)], res
 
 
+class FilePipe:
+    """sstc_pipe: file-to-file compaction (input SST files -> output SST files)
+    with pinned staging kept across calls."""
+
+    def __init__(self, codec, io_threads=8):
+        self.codec = codec
+        self.lib = codec.lib
+        h = ctypes.c_void_p()
+        check(self.lib.sstc_pipe_create(codec.h, int(io_threads), ctypes.byref(h)), "sstc_pipe_create")
+        self.h = h
+
+    def close(self):
+        if self.h:
+            self.lib.sstc_pipe_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def compact_files(self, paths, file_sizes, out_prefix, first_sst_id, block_threshold=4096,
+                      table_limit=32 << 20, base_level=1, txn_mode=_lib.SSTC_TXN_COMPAT, fsync=True,
+                      max_outs=4096):
+        """Returns ([(sst_id, file_size, smallest_key, largest_key)], timing dict)."""
+        from ._lib import CompactParams, FileOut, FilesTiming
+        n = len(paths)
+        arr = (ctypes.c_char_p * max(n, 1))(*[p.encode() for p in paths])
+        sizes = (ctypes.c_uint64 * max(n, 1))(*[int(x) for x in file_sizes])
+        outs = (FileOut * max_outs)()
+        arena = ctypes.create_string_buffer(max_outs * 2 * 4096)
+        nout = ctypes.c_uint32()
+        tm = FilesTiming()
+        prm = CompactParams(block_threshold, table_limit, base_level, txn_mode)
+        self.codec._stream()
+        check(self.lib.sstc_compact_files(self.h, ctypes.cast(arr, ctypes.c_void_p), ctypes.cast(sizes, ctypes.c_void_p),
+                                          n, out_prefix.encode(), int(first_sst_id), ctypes.byref(prm),
+                                          1 if fsync else 0, ctypes.cast(outs, ctypes.c_void_p), max_outs,
+                                          ctypes.byref(nout), ctypes.cast(arena, ctypes.c_void_p),
+                                          len(arena), ctypes.byref(tm)), "sstc_compact_files")
+        raw = arena.raw
+        res = []
+        for o in outs[: nout.value]:
+            lo = raw[o.smallest_key_off:o.smallest_key_off + o.smallest_key_len]
+            hi = raw[o.largest_key_off:o.largest_key_off + o.largest_key_len]
+            res.append((o.sst_id, o.file_size, lo, hi))
+        return res, {k: getattr(tm, k) for k, _ in FilesTiming._fields_}
+
+
 def _table_index(f):
     """(block offsets, block sizes) of an SST image: footer + meta section walk
     (reference table_reader.cc:52-156)."""

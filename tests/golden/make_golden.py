@@ -160,10 +160,13 @@ def main():
 
 
 COMPACTION_CASES = [
-    # name, k, n_per, key_space, vmax, table_limit, distinct
-    ("small", 4, 300, 500, 200, 32 << 20, True),
-    ("split", 8, 2000, 5000, 600, 200_000, True),
-    ("dups", 3, 1000, 800, 100, 50_000, False),
+    # name, k, n_per, key_space, vmax, table_limit, distinct, extra generator args
+    ("small", 4, 300, 500, 200, 32 << 20, True, {}),
+    ("split", 8, 2000, 5000, 600, 200_000, True, {}),
+    ("dups", 3, 1000, 800, 100, 50_000, False, {}),
+    # config 5 shape: Zipf(1.1) values clamped to [8 B, 64 KiB]
+    # (entries far above the 4 KiB block threshold), ~50 % key overlap, 10 % DELETE
+    ("zipf", 4, 600, 1200, 65536, 4 << 20, True, {"vmin": 8, "zipf": 1.1, "p_delete": 0.1}),
 ]
 
 
@@ -173,8 +176,8 @@ def compaction_fixtures(ref):
     (reference MergeIterator + TableReaderIterator + TableBuilder).  The small
     case is stored byte for byte, the others as SHA-256 + GetFileSize()."""
     manifest = {}
-    for name, k, n, ks, vmax, limit, distinct in COMPACTION_CASES:
-        sets = W.compaction_inputs(k, n, ks, vmax=vmax, distinct=distinct)
+    for name, k, n, ks, vmax, limit, distinct, gen in COMPACTION_CASES:
+        sets = W.compaction_inputs(k, n, ks, vmax=vmax, distinct=distinct, **gen)
         with tempfile.TemporaryDirectory() as td:
             ins = []
             for i, rec in enumerate(sets):
@@ -182,7 +185,7 @@ def compaction_fixtures(ref):
                 fs = ref.table_build(p, rec, 4096)
                 ins.append((p, fs))
             case = {"k": k, "n_per": n, "key_space": ks, "vmax": vmax, "table_limit": limit,
-                    "distinct": distinct, "block_threshold": 4096,
+                    "distinct": distinct, "block_threshold": 4096, "gen": gen,
                     "inputs": [{"sha256": hashlib.sha256(open(p, "rb").read()).hexdigest(), "file_size": fs}
                                for p, fs in ins]}
             for base in (1, 0):

@@ -332,3 +332,29 @@ def _records(items):
     sys.path.insert(0, __import__("os").path.join(__import__("conftest").ROOT, "tests", "golden"))
     from make_golden import records_from_list
     return records_from_list(items)
+
+
+def test_config5_zipf_blocks(codec, oracle):
+    """Config 5 shape: Zipf(1.1) values clamped to [8 B, 64 KiB],
+    10 % DELETE.  Most blocks hold one entry far above the 4 KiB threshold
+    (streamed paths of rt_kernel and enc_emit_kernel), the rest pack small
+    entries: segmentation, encode and the compat / correct round trips against
+    the oracle."""
+    rec = W.compaction_inputs(1, 1500, 3000, seed=11, vmin=8, vmax=65536, zipf=1.1, p_delete=0.1)[0]
+    first = oracle.segment(rec, 4096)
+    got_first = cpu_u64(codec.segment(records_table(rec), 4096))
+    assert np.array_equal(got_first, first)
+    want, woff, wlen = oracle.encode_blocks(rec, first, base=5)
+    assert wlen.max() > 60000 and wlen.min() < 4608
+    dst, off, ln = codec.encode(records_table(rec), t8(rec["key_src"]), t8(rec["val_src"]), t64(first),
+                                out_base=5)
+    torch.cuda.synchronize()
+    assert np.array_equal(cpu_u64(off)[:-1], woff) and np.array_equal(cpu_u64(ln), wlen)
+    img = dst.cpu().numpy()
+    assert np.array_equal(img[5:5 + want.size], want)
+    src = np.concatenate([np.zeros(5, np.uint8), want, np.zeros(3, np.uint8)])
+    for mode in (0, 1):
+        got = run_roundtrip(codec, src, woff, wlen, mode, dst_fill=0xA7)
+        ref = oracle_rt(oracle, src, woff, wlen, mode, dst_fill=0xA7)
+        assert (got[2] == 0).all()
+        assert np.array_equal(got[1], ref[1]) and np.array_equal(got[0], ref[0])

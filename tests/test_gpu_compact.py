@@ -39,7 +39,7 @@ def test_compact_small_reference_bytes(codec, base):
 def test_compact_reference_hashes(codec, oracle, name, base):
     case = CASES[name]
     sets = W.compaction_inputs(case["k"], case["n_per"], case["key_space"], vmax=case["vmax"],
-                               distinct=case["distinct"])
+                               distinct=case["distinct"], **case.get("gen", {}))
     ins = [oracle.table_build(r, case["block_threshold"]) for r in sets]
     outs, res = codec.compact(ins, case["block_threshold"], case["table_limit"], base)
     want = case[f"outputs_base{base}"]
@@ -98,3 +98,15 @@ def test_compact_rejects_unsorted(codec, oracle):
     f = oracle.table_build(rec, 4096)
     with pytest.raises(Exception):
         codec.compact([f], 4096, 1 << 20, 1)
+
+
+def test_compact_no_records(codec, oracle):
+    """No input records (no tables, or only empty 40 B SSTs): one empty output
+    table, as DoCompactJob's first TableBuilder (compact.cc:234-243)."""
+    empty = oracle.table_build(W.compaction_inputs(1, 0, 10)[0], 4096)
+    assert empty.size == 40
+    for tables in ([], [empty], [empty, empty]):
+        want, kept = oracle.compact(tables, 4096, 1 << 20, 1)
+        outs, res = codec.compact(tables, 4096, 1 << 20, 1)
+        assert res.records_kept == kept == 0 and res.tables_out == 1
+        assert len(outs) == len(want) == 1 and np.array_equal(outs[0], want[0])

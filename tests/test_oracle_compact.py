@@ -20,7 +20,7 @@ def sha(a):
 
 def build_inputs(oracle, case):
     sets = W.compaction_inputs(case["k"], case["n_per"], case["key_space"], vmax=case["vmax"],
-                               distinct=case["distinct"])
+                               distinct=case["distinct"], **case.get("gen", {}))
     return [oracle.table_build(rec, case["block_threshold"]) for rec in sets]
 
 

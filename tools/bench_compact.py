@@ -1,22 +1,33 @@
-"""Config 3 (BASELINE.json): full L0->L1 compaction re-encode of 8 input SSTs x
-1 M keys (16 B keys, 100 B values) on one GPU, device-resident.
+"""Compaction benchmarks of BASELINE.json configs 3-5.
 
-    python tools/bench_compact.py [--keys 1000000] [--ssts 8] [--overlap] [--steps 3]
+    python tools/bench_compact.py [--config 3|4|5] [--steps 3] [--no-ref] [--no-files]
+    torchrun --nproc-per-node N tools/bench_compact.py --config 4     # sharded
 
-Inputs: SST s holds keys k%015d of i*8+s (disjoint interleave),
-or with --overlap the same key set in every SST with distinct txns (exercises
-the drop path).  They are written by this framework's TableBuilder (bit-exact
-with the reference's, tests/test_gpu_table.py).  Timed: sstc_compact on the
-resident input (decode, merge, filter, split, encode, meta, footers).
-Baseline: the reference's own MergeIterator + TableBuilder driver
-(oracle/_ref/ref_compact, includes its file I/O), when present; outputs are
-compared by SHA-256.
+config 3  8 SSTs x 1 M keys (16 B keys, 100 B values); SST s holds k%015d of
+          i*8+s (disjoint interleave); --overlap: the same key set in every SST
+          with distinct txns (exercises the drop path).
+config 4  1024 SSTs x 100 k keys sharded 128 per GPU: each rank compacts its
+          own key-range-disjoint 128 SSTs (no collective).
+config 5  8 SSTs x 5000 keys from a shared space of 20000 (overlap across
+          SSTs), Zipf(1.1) values clamped to [8 B, 64 KiB], 10 % DELETE.
+
+Inputs are written by this framework's TableBuilder (bit-exact with the
+reference's, tests/test_gpu_table.py).  Legs:
+  device  sstc_compact on the resident input (decode, merge, filter, split,
+          encode, meta, footers), median of --steps;
+  files   sstc_compact_files: input SST files -> output SST files (footer/meta
+          parse, pread, H2D, device job, D2H, pwrite, fsync), median of --steps;
+  ref     the reference's own MergeIterator + TableReaderIterator +
+          TableBuilder (oracle/_ref/ref_compact, 1 thread, files incl. fsync),
+          rank 0 only, once.
+Outputs of all legs are compared by SHA-256.
 """
 import argparse
 import ctypes
 import hashlib
 import json
 import os
+import shutil
 import subprocess
 import sys
 import tempfile
@@ -28,31 +39,85 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "lsm-kv-storage_amd"))
 import sstcodec  # noqa: E402
+from sstcodec import shard as SH  # noqa: E402
 from sstcodec import workload as W  # noqa: E402
 from sstcodec._lib import CompactParams, CompactResult, check  # noqa: E402
 from sstcodec.codec import _table_index  # noqa: E402
 from sstcodec.table import build_table  # noqa: E402
 
 
+def record_sets(args, rank):
+    """Input record sets of this rank (iterator order)."""
+    if args.config == 3:
+        out = []
+        for s in range(args.ssts):
+            i = np.arange(args.keys, dtype=np.uint64)
+            keys = i if args.overlap else i * np.uint64(args.ssts) + np.uint64(s)
+            out.append(W.uniform_records(args.keys, key_index=keys, seed=s + 1, txn_start=1 + s * args.keys))
+        return out
+    if args.config == 4:
+        # rank r owns keys [r * K, (r + 1) * K), K = ssts * keys; SST s of the shard
+        # holds base + i * ssts + s (the config-3 interleave inside each shard)
+        K = args.ssts * args.keys
+        base = np.uint64(rank * K)
+        out = []
+        for s in range(args.ssts):
+            i = np.arange(args.keys, dtype=np.uint64)
+            keys = base + i * np.uint64(args.ssts) + np.uint64(s)
+            g = rank * args.ssts + s
+            out.append(W.uniform_records(args.keys, key_index=keys, seed=g + 1, txn_start=1 + g * args.keys))
+        return out
+    return W.compaction_inputs(args.ssts, args.keys, args.key_space, seed=55 + rank, vmin=8, vmax=65536,
+                               zipf=1.1, p_delete=0.1)
+
+
+def barrier(world):
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+
+
+def sha(b):
+    return hashlib.sha256(b).hexdigest()
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--keys", type=int, default=1_000_000)
-    ap.add_argument("--ssts", type=int, default=8)
+    ap.add_argument("--config", type=int, default=3, choices=(3, 4, 5))
+    ap.add_argument("--keys", type=int, default=None)
+    ap.add_argument("--ssts", type=int, default=None)
+    ap.add_argument("--key-space", type=int, default=20000)
     ap.add_argument("--overlap", action="store_true")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--no-ref", action="store_true")
+    ap.add_argument("--no-files", action="store_true")
+    ap.add_argument("--tmp", default=None, help="directory for the SST files (default: system temp)")
     args = ap.parse_args()
-    dev = torch.device("cuda", 0)
-    codec = sstcodec.Codec(0)
-    td = tempfile.mkdtemp(prefix="sstc_c3_")
+    defaults = {3: (8, 1_000_000), 4: (128, 100_000), 5: (8, 5000)}[args.config]
+    args.ssts = args.ssts or defaults[0]
+    args.keys = args.keys or defaults[1]
+
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl" if torch.cuda.is_available() else "gloo")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    codec = sstcodec.Codec(local)
+    td = tempfile.mkdtemp(prefix=f"sstc_c{args.config}_r{rank}_", dir=args.tmp)
+    try:
+        run_bench(args, rank, world, dev, codec, td)
+    finally:
+        shutil.rmtree(td, ignore_errors=True)
+
+
+def run_bench(args, rank, world, dev, codec, td):
     files, paths = [], []
     t0 = time.perf_counter()
-    for s in range(args.ssts):
-        i = np.arange(args.keys, dtype=np.uint64)
-        keys = i if args.overlap else i * np.uint64(args.ssts) + np.uint64(s)
-        rec = W.uniform_records(args.keys, key_index=keys, seed=s + 1,
-                                txn_start=1 + s * args.keys)
-        p = os.path.join(td, f"{s}.sst")
+    for s, rec in enumerate(record_sets(args, rank)):
+        p = os.path.join(td, f"in{s}.sst")
         fs, _ = build_table(codec, p, rec, 4096)
         files.append(np.fromfile(p, np.uint8))
         paths.append((p, fs))
@@ -70,7 +135,7 @@ def main():
     h_tfb = np.asarray(tfb, np.uint64)
     cap = int(src.numel()) + (1 << 20)
     dst = torch.empty(cap, dtype=torch.uint8, device=dev)
-    max_t = 4096
+    max_t = 1 << 16
     toff = torch.zeros(max_t + 1, dtype=torch.int64, device=dev)
     tlen = torch.zeros(max_t, dtype=torch.int64, device=dev)
     prm = CompactParams(4096, 32 << 20, 1, 0)
@@ -87,23 +152,53 @@ def main():
     torch.cuda.synchronize()
     times = []
     for _ in range(args.steps):
+        barrier(world)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         run()
         torch.cuda.synchronize()
-        times.append(time.perf_counter() - t0)
+        times.append(SH.max_over_ranks(time.perf_counter() - t0, dev))
     nt = res.tables_out
     o = toff[: nt + 1].cpu().numpy()
     d = dst[: int(o[nt])].cpu().numpy()
-    gpu_hash = [hashlib.sha256(d[int(o[t]):int(o[t + 1])].tobytes()).hexdigest() for t in range(nt)]
+    gpu_hash = [sha(d[int(o[t]):int(o[t + 1])].tobytes()) for t in range(nt)]
     in_bytes = int(src.numel())
-    out = {"workload": "config3" + ("-overlap" if args.overlap else ""), "ssts": args.ssts, "keys_per_sst": args.keys,
-           "input_bytes": in_bytes, "records_in": res.records_in, "records_kept": res.records_kept,
+    all_in = SH.sum_over_ranks(in_bytes, dev)
+    med = float(np.median(times))
+    name = {3: "config3" + ("-overlap" if args.overlap else ""), 4: "config4", 5: "config5"}[args.config]
+    out = {"workload": name, "ranks": world, "ssts_per_rank": args.ssts, "keys_per_sst": args.keys,
+           "input_bytes_per_rank": in_bytes, "records_in": res.records_in, "records_kept": res.records_kept,
            "tables_out": nt, "blocks_out": res.blocks_out, "bytes_out": res.bytes_out,
-           "gpu_s_median": float(np.median(times)), "gpu_GiBps_in": in_bytes / np.median(times) / 2 ** 30,
+           "device_s_median": med, "device_GiBps_in_all_ranks": all_in / med / 2 ** 30,
            "input_build_s": gen_s, "output_sizes_head": [int(x) + 1 for x in tlen[:min(nt, 4)].cpu().tolist()]}
+    del dst, src
+    torch.cuda.empty_cache()
+
+    if not args.no_files:
+        pipe = sstcodec.FilePipe(codec, io_threads=8)
+        od = os.path.join(td, "gpu_out")
+        os.makedirs(od)
+        ftimes, tms = [], []
+        for step in range(args.steps + 1):  # first call sizes the pinned staging
+            barrier(world)
+            t0 = time.perf_counter()
+            outs, tm = pipe.compact_files([p for p, _ in paths], [fs for _, fs in paths], od + "/", 1)
+            dt = SH.max_over_ranks(time.perf_counter() - t0, dev)
+            if step:
+                ftimes.append(dt)
+                tms.append(tm)
+        fhash = [sha(open(os.path.join(od, f"{sid}.sst"), "rb").read()) for sid, _, _, _ in outs]
+        fmed = float(np.median(ftimes))
+        k = int(np.argsort(ftimes)[len(ftimes) // 2])
+        out["files"] = {"seconds_median": fmed, "GiBps_in_all_ranks": all_in / fmed / 2 ** 30,
+                        "breakdown_s": {a: round(b, 5) for a, b in tms[k].items()},
+                        "what": "sstc_compact_files: footer/meta parse, pread -> pinned -> H2D (8 threads, "
+                                "16 MiB chunks), device job, D2H -> pwrite + fsync per output SST",
+                        "identical_to_device_leg": fhash == gpu_hash}
+        pipe.close()
+
     ref = os.path.join(ROOT, "oracle", "_ref", "ref_compact")
-    if not args.no_ref and os.path.exists(ref):
+    if rank == 0 and not args.no_ref and os.path.exists(ref):
         od = os.path.join(td, "ref_out")
         os.makedirs(od)
         cmd = [ref, od, "4096", str(32 << 20), "1"]
@@ -113,13 +208,15 @@ def main():
         r = subprocess.run(cmd, check=True, capture_output=True, text=True)
         ref_s = time.perf_counter() - t0
         lines = [ln.rsplit(" ", 1) for ln in r.stdout.strip().splitlines()]
-        ref_hash = [hashlib.sha256(open(p, "rb").read()).hexdigest() for p, _ in lines]
+        ref_hash = [sha(open(p, "rb").read()) for p, _ in lines]
         out["cpu_baseline"] = {"kind": "reference", "seconds": ref_s, "GiBps_in": in_bytes / ref_s / 2 ** 30,
-                               "cores": 1, "what": "reference MergeIterator + TableReaderIterator + TableBuilder "
-                                                   "(oracle/_ref/ref_compact), files on local disk incl. fsync"}
+                               "cores": 1, "sample": f"rank 0's {len(paths)} SSTs",
+                               "what": "reference MergeIterator + TableReaderIterator + TableBuilder "
+                                       "(oracle/_ref/ref_compact), files on local disk incl. fsync"}
         out["bit_exact_vs_reference"] = ref_hash == gpu_hash
         out["ref_tables"] = len(ref_hash)
-    print(json.dumps(out))
+    if rank == 0:
+        print(json.dumps(out), flush=True)
 
 
 if __name__ == "__main__":
