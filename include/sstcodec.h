@@ -195,6 +195,41 @@ int sstc_compact(sstc_ctx *ctx, const uint8_t *d_src, const uint64_t *d_blk_off,
                  uint64_t *d_table_len, uint64_t max_tables, sstc_compact_result *result);
 
 
+/* ---- point lookups (replaces TableReader::GetValue without a block cache,
+ *      sstable/table_reader.cc:168-210, with BlockReader::GetValue,
+ *      sstable/block_reader.cc:20-57, for a batch of keys) ------------------ */
+
+#define SSTC_GET_PUT 0u       /* db::ValueType::PUT                          */
+#define SSTC_GET_DELETED 1u   /* db::ValueType::DELETED                      */
+#define SSTC_GET_NOT_FOUND 2u /* db::ValueType::NOT_FOUND                    */
+#define SSTC_GET_BAD_BLOCK 4u /* a probed entry / trailer is out of range    */
+
+/* Block indexes of one or many SSTs (device arrays; what TableReader holds
+ * after FetchBlockIndexInfo, table_reader.cc:86-156). */
+typedef struct sstc_block_index {
+  const uint64_t *blk_off;           /* block b = d_src[blk_off[b] .. + blk_len[b])     */
+  const uint64_t *blk_len;
+  const uint64_t *last_key_off;      /* GetLargestKey() of block b = keys[off .. + len) */
+  const uint32_t *last_key_len;
+  const uint8_t *keys;
+  const uint64_t *table_first_block; /* table t owns blocks [tfb[t], tfb[t+1])          */
+  uint32_t ntables;
+} sstc_block_index;
+
+/* Query q looks key d_q_keys[d_q_key_off[q] .. + d_q_key_len[q]) up in table
+ * d_q_table[q]: the block is the first whose largest key >= key (the table's
+ * last block when none is: GetBlockOffsetAndSize), then the block's entries
+ * are binary-searched exactly as BlockReader::GetValue does (the first probed
+ * equal key wins; the txn is not consulted).  Outputs per query: SSTC_GET_*
+ * type, for PUT the value at d_src[d_out_val_off .. + d_out_val_len), and the
+ * probed block (UINT64_MAX when the table has no block).  d_out_block may be
+ * NULL.  A table without blocks answers NOT_FOUND (the reference reads
+ * block_index_[-1] there). */
+int sstc_get_batch(sstc_ctx *ctx, const uint8_t *d_src, const sstc_block_index *index,
+                   const uint32_t *d_q_table, const uint8_t *d_q_keys, const uint64_t *d_q_key_off,
+                   const uint32_t *d_q_key_len, uint64_t nq, uint32_t *d_out_type, uint64_t *d_out_val_off,
+                   uint32_t *d_out_val_len, uint64_t *d_out_block);
+
 /* ---- file-to-file compaction (Compact::DoCompactJob end to end: the input
  *      SST files are read, compacted on the device and the output SSTs written
  *      and fsync'ed, db/compact.cc:232-322 with io/linux_file.cc:138-195) --- */

@@ -16,7 +16,7 @@ CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "lib")
 ARCH = os.environ.get("SSTC_OFFLOAD_ARCH", "gfx950")
 
-HIP_SOURCES = ["sstc_kernels.hip", "sstc_compact.hip", "sstc_api.hip"]
+HIP_SOURCES = ["sstc_kernels.hip", "sstc_compact.hip", "sstc_get.hip", "sstc_api.hip"]
 HOST_SOURCES = ["host/sst_table.cpp", "host/compact_files.cpp"]
 
 

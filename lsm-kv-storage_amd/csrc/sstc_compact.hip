@@ -644,6 +644,9 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     ck_block_off_kernel<<<grid(nb), 256, 0, s>>>(btab, nb, BL, tbf, d_table_off, bo);
     // 6. encode blocks, meta entries, footers
     EncArgs ea{d_src, d_src, sstc_records{KR.type, KR.kl, KR.vl, KR.tx, KR.ko, KR.vo}, bf, nb, Pe, bo, blen, d_dst, 1};
+    ea.big = pool.get<uint32_t>(nb + 1);
+    ea.nbig = ea.big + nb;
+    CK(hipMemsetAsync(ea.nbig, 0, sizeof(uint32_t), s));
     CK(launch_enc_emit(ea, s));
     ck_meta_kernel<<<static_cast<uint32_t>((nb + 255) / 256), 256, 0, s>>>(bf, nb, btab, BL, MS, blen, tbf, d_table_off, tdata, KR, d_src, d_dst);
     uint64_t *bmin = pool.get<uint64_t>(nb), *bmax = pool.get<uint64_t>(nb);

@@ -44,6 +44,17 @@ __device__ __forceinline__ uint64_t uniform64(uint64_t v) {
   return (static_cast<uint64_t>(hi) << 32) | lo;
 }
 
+// ---- XCD-aware workgroup order ---------------------------------------------
+// Workgroups are dispatched round-robin over the 8 XCDs (WG i runs on XCD
+// i % 8), each with its own L2.  Remapping so that XCD x owns one contiguous
+// range of logical workgroups keeps neighbouring blocks -- which share the
+// cache lines at their boundaries -- inside one L2.  Bijective for any grid.
+constexpr uint32_t kNumXcd = 8;
+__device__ __forceinline__ uint32_t xcd_logical_block(uint32_t i, uint32_t n) {
+  const uint32_t q = n / kNumXcd, r = n % kNumXcd, x = i % kNumXcd, k = i / kNumXcd;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + k;
+}
+
 // ---- LDS image reads (image is padded by >= 16 bytes past its last byte) ----
 __device__ __forceinline__ uint32_t lds_u8(const uint8_t *img, uint32_t off) { return img[off]; }
 

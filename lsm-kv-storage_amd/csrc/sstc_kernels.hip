@@ -415,7 +415,8 @@ __device__ __forceinline__ uint32_t rt_classify(const RtArgs &a, uint64_t b, uin
 __global__ __launch_bounds__(kRtWaves *kWave, 8) void rt_kernel(RtArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kRtWaves * kRtSlot];
   const uint32_t wave = uniform(threadIdx.x / kWave);
-  const uint64_t b = static_cast<uint64_t>(blockIdx.x) * kRtWaves + wave;
+  const uint32_t wg = a.xcd ? xcd_logical_block(blockIdx.x, gridDim.x) : blockIdx.x;
+  const uint64_t b = static_cast<uint64_t>(wg) * kRtWaves + wave;
   if (b >= a.nblocks) return;
   uint8_t *img = lds + wave * kRtSlot;
   uint64_t off;
@@ -500,7 +501,8 @@ __device__ __forceinline__ uint32_t decode_block(const DecArgs &a, const R &rd, 
 __global__ __launch_bounds__(kDecWaves *kWave) void decode_kernel(DecArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kDecWaves * kRtSlot];
   const uint32_t wave = uniform(threadIdx.x / kWave);
-  const uint64_t b = static_cast<uint64_t>(blockIdx.x) * kDecWaves + wave;
+  const uint32_t wg = a.xcd ? xcd_logical_block(blockIdx.x, gridDim.x) : blockIdx.x;
+  const uint64_t b = static_cast<uint64_t>(wg) * kDecWaves + wave;
   if (b >= a.nblocks) return;
   uint8_t *img = lds + wave * kRtSlot;
   const uint64_t off = uniform64(a.blk_off[b]);
@@ -640,6 +642,11 @@ __device__ void enc_emit_block(const EncArgs &a, uint64_t b, uint8_t *slot) {
 
 __global__ __launch_bounds__(kEncThreads) void enc_emit_kernel(EncArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t slot[kEncThreads * 16];
+  if (a.big) {
+    const uint32_t cnt = *a.nbig;
+    for (uint32_t i = blockIdx.x; i < cnt; i += gridDim.x) enc_emit_block(a, a.big[i], slot);
+    return;
+  }
   for (uint64_t b = blockIdx.x; b < a.nblocks; b += gridDim.x) enc_emit_block(a, b, slot);
 }
 
@@ -686,13 +693,17 @@ __global__ __launch_bounds__(kEncWaves *kWave) void enc_lds_kernel(EncArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kEncSlotWaves * kEncSlot];
   const uint32_t wave = uniform(threadIdx.x / kWave);
   const uint32_t lane = lane_id();
-  const uint64_t b = static_cast<uint64_t>(blockIdx.x) * kEncWaves + wave;
+  const uint32_t wg = a.xcd ? xcd_logical_block(blockIdx.x, gridDim.x) : blockIdx.x;
+  const uint64_t b = static_cast<uint64_t>(wg) * kEncWaves + wave;
   if (b >= a.nblocks) return;
   uint8_t *img = lds + wave * kEncSlot;
   const uint64_t bo = uniform64(a.out_blk_off[b]);
   const uint64_t L64 = uniform64(a.out_blk_len[b]);
   const uint32_t pad = static_cast<uint32_t>(bo & 15u);
-  if (pad + L64 + 16 > kEncSlot) return; // large block: enc_emit_kernel
+  if (pad + L64 + 16 > kEncSlot) {       // large block: enc_emit_kernel
+    if (a.big && lane == 0) a.big[atomicAdd(a.nbig, 1u)] = static_cast<uint32_t>(b);
+    return;
+  }
   const uint32_t L = static_cast<uint32_t>(L64);
   const uint64_t f0 = uniform64(a.blk_first[b]);
   const uint32_t n = static_cast<uint32_t>(uniform64(a.blk_first[b + 1]) - f0);
@@ -701,59 +712,87 @@ __global__ __launch_bounds__(kEncWaves *kWave) void enc_lds_kernel(EncArgs a) {
   uint8_t *im = img + pad; // image byte 0 == block byte 0
 
   if (a.entries_in_src) {
-    // 8 lanes per record: lane g copies interior dwords g, g+8, ... of the
-    // entry span (dword-aligned in LDS, funnel-shifted from the source), lane 0
-    // of the group the unaligned head / tail bytes, lane 1 the txn and the
-    // offset entry.  Every load of a pass is issued before the first use, so a
-    // pass costs one memory latency (the lane-serial copy cost one per dword).
-    const uint32_t g = lane & 7u;
-    constexpr uint32_t kU = 5; // interior dwords per lane held in registers (spans <= 163 B)
-    for (uint32_t i0 = 0; i0 < n; i0 += kWave / 8) {
-      const uint32_t i = i0 + (lane >> 3);
-      if (i >= n) continue;
-      const uint64_t r = f0 + i;
-      const uint64_t pr = a.P[r], pr1 = a.P[r + 1];
-      const uint64_t ko = a.in.key_off[r];
-      const uint32_t o = static_cast<uint32_t>(pr - P0);
-      const uint32_t sz = static_cast<uint32_t>(pr1 - pr);
-      const uint32_t len = sz - 8;
-      const uint8_t *sp = a.key_src + ko - 5;
-      uint8_t *d = im + o;
-      uint32_t head = (4u - (o + pad) % 4u) % 4u; // img is 16-aligned: d's alignment
-      head = head < len ? head : len;
-      const uint32_t nw = (len - head) >> 2;
-      uint32_t sh;
-      const uint32_t *w = align4_down(sp + head, sh);
-      uint32_t *d32 = reinterpret_cast<uint32_t *>(d + head);
-      uint32_t lo[kU], hi[kU];
+    // Records in chunks of 64.  Lane per record: metadata, txn and offset
+    // entry.  Then 8 lanes per record copy the entry span (type .. value,
+    // contiguous in the source block) as 16 B pieces: lane g owns interior
+    // dwords [4g, 4g + 4) (+32t), dword-aligned in LDS and funnel-shifted from
+    // 5 source dwords; lane 0 of a group also the < 4 head / tail bytes.  Four
+    // record groups are unrolled so one wave has ~20 independent loads in
+    // flight per lane (the copy is latency-bound, not bandwidth-bound).
+    const uint32_t g = lane & 7u, sub = lane >> 3;
+    for (uint32_t c0 = 0; c0 < n; c0 += kWave) {
+      const uint32_t nc = n - c0 < kWave ? n - c0 : kWave;
+      uint32_t my_o = 0, my_sz = 0;
+      uint64_t my_ko = 0;
+      if (lane < nc) {
+        const uint64_t r = f0 + c0 + lane;
+        const uint64_t pr = a.P[r], pr1 = a.P[r + 1];
+        my_ko = a.in.key_off[r];
+        const uint64_t tx = a.in.txn[r];
+        my_o = static_cast<uint32_t>(pr - P0);
+        my_sz = static_cast<uint32_t>(pr1 - pr);
+        lds_st_u64u(img, pad + my_o + my_sz - 8, tx);
+        lds_st_u64u(img, pad + D + 16 * (c0 + lane), my_o);
+        lds_st_u64u(img, pad + D + 16 * (c0 + lane) + 8, my_sz);
+      }
+      for (uint32_t p0 = 0; p0 < nc; p0 += 32) {
+        constexpr uint32_t kQ = 4;
+        uint32_t x[kQ][5], hd[kQ], tl[kQ], o_[kQ], len_[kQ], head_[kQ], nw_[kQ], sh_[kQ];
+        const uint8_t *sp_[kQ];
 #pragma unroll
-      for (uint32_t j = 0; j < kU; j++) {
-        const uint32_t k = g + 8 * j;
-        lo[j] = k < nw ? w[k] : 0u;
-        hi[j] = k < nw && sh ? w[k + 1] : 0u;
-      }
-      uint32_t hd = 0, tl = 0;
-      uint64_t tx = 0;
-      const uint32_t t0 = head + 4 * nw;
-      if (g == 0) {
-        hd = head ? g_u32u(sp) : 0u;
-        tl = t0 < len ? g_u32u(sp + t0) : 0u; // < 4 bytes; the txn field follows in the source
-      } else if (g == 1) {
-        tx = a.in.txn[r];
-      }
+        for (uint32_t q = 0; q < kQ; q++) {
+          const uint32_t i = p0 + 8 * q + sub; // record of this lane's group
+          const uint32_t o = __shfl(my_o, static_cast<int>(i & 63u), kWave);
+          const uint32_t sz = __shfl(my_sz, static_cast<int>(i & 63u), kWave);
+          const uint32_t klo = __shfl(static_cast<uint32_t>(my_ko), static_cast<int>(i & 63u), kWave);
+          const uint32_t khi = __shfl(static_cast<uint32_t>(my_ko >> 32), static_cast<int>(i & 63u), kWave);
+          const bool act = i < nc;
+          const uint32_t len = act ? sz - 8 : 0u;
+          const uint8_t *sp = a.key_src + ((static_cast<uint64_t>(khi) << 32) | klo) - 5;
+          uint32_t head = (4u - ((o + pad) & 3u)) & 3u;
+          head = head < len ? head : len;
+          const uint32_t nw = (len - head) >> 2;
+          uint32_t sh;
+          const uint32_t *w = align4_down(sp + head, sh);
+          const uint32_t k0 = 4 * g;
+          // a shifted dword also needs the next one (inside the entry: the txn
+          // follows the span); an idle group (no record) loads nothing
+          const uint32_t lim = act ? nw + (sh ? 1u : 0u) : 0u;
 #pragma unroll
-      for (uint32_t j = 0; j < kU; j++) {
-        const uint32_t k = g + 8 * j;
-        if (k < nw) d32[k] = __builtin_amdgcn_alignbyte(hi[j], lo[j], sh);
-      }
-      for (uint32_t k = g + 8 * kU; k < nw; k += 8) d32[k] = __builtin_amdgcn_alignbyte(sh ? w[k + 1] : 0u, w[k], sh);
-      if (g == 0) {
-        for (uint32_t j = 0; j < head; j++) d[j] = static_cast<uint8_t>(hd >> (8 * j));
-        for (uint32_t j = t0; j < len; j++) d[j] = static_cast<uint8_t>(tl >> (8 * (j - t0)));
-      } else if (g == 1) {
-        for (int j = 0; j < 8; j++) d[len + j] = static_cast<uint8_t>(tx >> (8 * j));
-        lds_st_u64u(im, D + 16 * i, o);
-        lds_st_u64u(im, D + 16 * i + 8, sz);
+          for (uint32_t j = 0; j < 5; j++) x[q][j] = k0 + j < lim ? w[k0 + j] : 0u;
+          const uint32_t t0 = head + 4 * nw;
+          hd[q] = (g == 0 && head) ? g_u32u(sp) : 0u;
+          tl[q] = (g == 0 && t0 < len) ? g_u32u(sp + t0) : 0u; // < 4 bytes; the txn follows in the source
+          o_[q] = o;
+          len_[q] = len;
+          head_[q] = head;
+          nw_[q] = nw;
+          sh_[q] = sh;
+          sp_[q] = sp;
+        }
+#pragma unroll
+        for (uint32_t q = 0; q < kQ; q++) {
+          if (len_[q] == 0) continue;
+          uint8_t *d = im + o_[q];
+          uint32_t *d32 = reinterpret_cast<uint32_t *>(d + head_[q]);
+          const uint32_t k0 = 4 * g, sh = sh_[q], nw = nw_[q];
+#pragma unroll
+          for (uint32_t j = 0; j < 4; j++)
+            if (k0 + j < nw) d32[k0 + j] = __builtin_amdgcn_alignbyte(x[q][j + 1], x[q][j], sh);
+          // spans longer than 128 B: the rest, 32 dwords per round
+          uint32_t sh2;
+          const uint32_t *w = align4_down(sp_[q] + head_[q], sh2);
+          for (uint32_t k = k0 + 32; k < nw; k += 32) {
+#pragma unroll
+            for (uint32_t j = 0; j < 4; j++)
+              if (k + j < nw) d32[k + j] = __builtin_amdgcn_alignbyte(sh ? w[k + j + 1] : 0u, w[k + j], sh);
+          }
+          if (g == 0) {
+            const uint32_t t0 = head_[q] + 4 * nw;
+            for (uint32_t j = 0; j < head_[q]; j++) d[j] = static_cast<uint8_t>(hd[q] >> (8 * j));
+            for (uint32_t j = t0; j < len_[q]; j++) d[j] = static_cast<uint8_t>(tl[q] >> (8 * (j - t0)));
+          }
+        }
       }
     }
   } else for (uint32_t i = lane; i < n; i += kWave) {
@@ -1025,8 +1064,20 @@ __global__ __launch_bounds__(kScanThreads) void scan_lookback_kernel(const uint6
 // ---------------------------------------------------------------------------
 static inline uint32_t grid_for(uint64_t n, uint32_t per) { return static_cast<uint32_t>((n + per - 1) / per); }
 
+// A/B switch for the XCD-aware block order (SSTC_XCD=0/1/2/3: bit 0 rt_kernel,
+// bit 1 decode/encode); temporary while it is measured
+static uint32_t xcd_mode() {
+  static const uint32_t m = [] {
+    const char *e = getenv("SSTC_XCD");
+    return e ? static_cast<uint32_t>(atoi(e)) : 0u;
+  }();
+  return m;
+}
+
 hipError_t launch_roundtrip(const RtArgs &a, hipStream_t s) {
-  if (a.nblocks) rt_kernel<<<grid_for(a.nblocks, kRtWaves), kRtWaves * kWave, 0, s>>>(a);
+  RtArgs b = a;
+  b.xcd = xcd_mode() & 1u;
+  if (a.nblocks) rt_kernel<<<grid_for(a.nblocks, kRtWaves), kRtWaves * kWave, 0, s>>>(b);
   return hipGetLastError();
 }
 
@@ -1037,7 +1088,9 @@ hipError_t launch_count(const uint8_t *src, const uint64_t *blk_off, const uint6
 }
 
 hipError_t launch_decode(const DecArgs &a, hipStream_t s) {
-  if (a.nblocks) decode_kernel<<<grid_for(a.nblocks, kDecWaves), kDecWaves * kWave, 0, s>>>(a);
+  DecArgs b = a;
+  b.xcd = (xcd_mode() >> 1) & 1u;
+  if (a.nblocks) decode_kernel<<<grid_for(a.nblocks, kDecWaves), kDecWaves * kWave, 0, s>>>(b);
   return hipGetLastError();
 }
 
@@ -1070,7 +1123,9 @@ hipError_t launch_enc_blk_len(const uint64_t *P, const uint64_t *blk_first, uint
 
 hipError_t launch_enc_emit(const EncArgs &a, hipStream_t s) {
   if (!a.nblocks) return hipSuccess;
-  enc_lds_kernel<<<grid_for(a.nblocks, kEncWaves), kEncWaves * kWave, 0, s>>>(a);
+  EncArgs b = a;
+  b.xcd = (xcd_mode() >> 1) & 1u;
+  enc_lds_kernel<<<grid_for(a.nblocks, kEncWaves), kEncWaves * kWave, 0, s>>>(b);
   enc_emit_kernel<<<static_cast<uint32_t>(a.nblocks < 2048 ? a.nblocks : 2048), kEncThreads, 0, s>>>(a);
   return hipGetLastError();
 }

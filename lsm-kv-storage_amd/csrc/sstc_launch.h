@@ -23,6 +23,7 @@ struct RtArgs {
   uint32_t *status;    // may be null
   unsigned long long *err_count;
   uint32_t num_cus;
+  uint32_t xcd = 0; // XCD-aware block order (set by the launcher)
 };
 
 // 32 B merge key of one record (compaction): 16 B big-endian key prefix (zero
@@ -43,6 +44,7 @@ struct DecArgs {
   uint32_t *status; // may be null
   unsigned long long *err_count;
   SortKey *sk = nullptr; // optional merge keys (compaction)
+  uint32_t xcd = 0;
 };
 
 struct EncArgs {
@@ -56,7 +58,32 @@ struct EncArgs {
   const uint64_t *out_blk_len;
   uint8_t *dst;
   uint32_t entries_in_src = 0; // records decoded from blocks in key_src (== val_src)
+  uint32_t xcd = 0;
+  // optional: blocks too large for an LDS slot are listed here by enc_lds_kernel
+  // (*nbig zeroed by the caller) so enc_emit_kernel visits only them
+  uint32_t *big = nullptr, *nbig = nullptr;
 };
+
+// point lookups (sstc_get.hip)
+struct GetArgs {
+  const uint8_t *src;
+  const uint64_t *blk_off, *blk_len, *lk_off;
+  const uint32_t *lk_len;
+  const uint8_t *keys;
+  const uint64_t *tfb;
+  uint32_t ntables;
+  const uint32_t *q_table;
+  const uint8_t *q_keys;
+  const uint64_t *q_key_off;
+  const uint32_t *q_key_len;
+  uint64_t nq;
+  uint32_t *out_type;
+  uint64_t *out_val_off;
+  uint32_t *out_val_len;
+  uint64_t *out_block; // may be null
+  unsigned long long *err_count;
+};
+hipError_t launch_get(const GetArgs &a, hipStream_t s);
 
 hipError_t launch_roundtrip(const RtArgs &a, hipStream_t s);
 hipError_t launch_count(const uint8_t *src, const uint64_t *blk_off, const uint64_t *blk_len,

@@ -14,7 +14,7 @@ from ._lib import (BLK_STATUS, LIB_PATH, SSTC_NO_VALUE, SSTC_TXN_COMPAT, SSTC_TX
 def __getattr__(name):
     # torch-facing classes are imported lazily so that CPU-only tooling can use
     # the workload generator without importing torch.
-    if name in ("Codec", "RecordTable", "FilePipe"):
+    if name in ("Codec", "RecordTable", "FilePipe", "Lookup"):
         from . import codec
         return getattr(codec, name)
     raise AttributeError(name)

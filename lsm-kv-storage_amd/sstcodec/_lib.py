@@ -41,6 +41,15 @@ class CompactResult(ctypes.Structure):
                 ("blocks_out", ctypes.c_uint64), ("tables_out", ctypes.c_uint64), ("bytes_out", ctypes.c_uint64)]
 
 
+class BlockIndex(ctypes.Structure):
+    """sstc_block_index (device pointers)."""
+    _fields_ = [("blk_off", c_vp), ("blk_len", c_vp), ("last_key_off", c_vp), ("last_key_len", c_vp),
+                ("keys", c_vp), ("table_first_block", c_vp), ("ntables", ctypes.c_uint32)]
+
+
+GET_TYPES = {0: "PUT", 1: "DELETED", 2: "NOT_FOUND", 4: "BAD_BLOCK"}
+
+
 class FileOut(ctypes.Structure):
     _fields_ = [("sst_id", ctypes.c_uint64), ("file_size", ctypes.c_uint64), ("smallest_key_off", ctypes.c_uint64),
                 ("largest_key_off", ctypes.c_uint64), ("smallest_key_len", ctypes.c_uint32),
@@ -86,6 +95,8 @@ def load():
         "sstc_roundtrip_blocks": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_u64, c_u32, c_vp, c_vp]),
         "sstc_compact": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_u64, c_vp, c_u32, P(CompactParams), c_vp, c_u64,
                                         c_vp, c_vp, c_u64, P(CompactResult)]),
+        "sstc_get_batch": (ctypes.c_int, [c_vp, c_vp, P(BlockIndex), c_vp, c_vp, c_vp, c_vp, c_u64, c_vp, c_vp, c_vp,
+                                          c_vp]),
         "sstc_pipe_create": (ctypes.c_int, [c_vp, c_u32, P(c_vp)]),
         "sstc_pipe_destroy": (ctypes.c_int, [c_vp]),
         "sstc_compact_files": (ctypes.c_int, [c_vp, c_vp, c_vp, c_u32, ctypes.c_char_p, c_u64, P(CompactParams),

@@ -210,6 +210,76 @@ class Codec:
         return [d[int(o[t]):int(o[t + 1])] for t in range(nt)], res
 
 
+def _queries(keys):
+    import numpy as np
+    lens = np.array([len(k) for k in keys], np.uint32)
+    off = np.zeros(len(keys), np.uint64)
+    if len(keys) > 1:
+        off[1:] = np.cumsum(lens[:-1].astype(np.uint64))
+    arena = np.frombuffer(b"".join(keys) + b"\0" * 8, np.uint8).copy()
+    return arena, off, lens
+
+
+class Lookup:
+    """Device-resident SSTs + block indexes for batched point lookups
+    (sstc_get_batch): TableReader::GetValue over many tables and keys."""
+
+    def __init__(self, codec, tables):
+        import numpy as np
+        self.codec = codec
+        dev = codec.device
+        offs, lens, lko, lkl, tfb, base = [], [], [], [], [0], 0
+        for f in tables:
+            o, ln, ko, kl = _table_index(f, keys=True)
+            offs.append(o + np.uint64(base))
+            lens.append(ln)
+            lko.append(ko + np.uint64(base))
+            lkl.append(kl)
+            tfb.append(tfb[-1] + len(o))
+            base += f.size
+        cat = lambda xs, dt: np.concatenate(xs).astype(dt) if xs and sum(len(x) for x in xs) else np.zeros(1, dt)  # noqa: E731
+        self.src = torch.from_numpy(np.concatenate(tables) if tables else np.zeros(1, np.uint8)).to(dev)
+        self.blk_off = torch.from_numpy(cat(offs, np.uint64).view(np.int64)).to(dev)
+        self.blk_len = torch.from_numpy(cat(lens, np.uint64).view(np.int64)).to(dev)
+        self.lk_off = torch.from_numpy(cat(lko, np.uint64).view(np.int64)).to(dev)
+        self.lk_len = torch.from_numpy(cat(lkl, np.uint32).view(np.int32)).to(dev)
+        self.tfb = torch.from_numpy(np.asarray(tfb, np.uint64).view(np.int64)).to(dev)
+        self.ntables = len(tables)
+        self.base = [0]
+        for f in tables:
+            self.base.append(self.base[-1] + f.size)
+
+    def index(self):
+        from ._lib import BlockIndex
+        return BlockIndex(self.blk_off.data_ptr(), self.blk_len.data_ptr(), self.lk_off.data_ptr(),
+                          self.lk_len.data_ptr(), self.src.data_ptr(), self.tfb.data_ptr(), self.ntables)
+
+    def get(self, q_table, keys, raw=False):
+        """q_table: table index per query; keys: list of bytes.  Returns numpy
+        (type, val_off (absolute, into the concatenated tables), val_len, block)."""
+        import numpy as np
+        dev = self.codec.device
+        arena, off, lens = _queries(keys)
+        n = len(keys)
+        qt = torch.from_numpy(np.asarray(q_table, np.uint32).view(np.int32)).to(dev) if n else \
+            torch.zeros(1, dtype=torch.int32, device=dev)
+        qk = torch.from_numpy(arena).to(dev)
+        qo = torch.from_numpy(off.view(np.int64) if n else np.zeros(1, np.int64)).to(dev)
+        ql = torch.from_numpy(lens.view(np.int32) if n else np.zeros(1, np.int32)).to(dev)
+        ot = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+        ov = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
+        ol = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+        ob = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
+        idx = self.index()
+        self.codec._stream()
+        check(self.codec.lib.sstc_get_batch(self.codec.h, _p(self.src), ctypes.byref(idx), _p(qt), _p(qk), _p(qo),
+                                            _p(ql), n, _p(ot), _p(ov), _p(ol), _p(ob)), "sstc_get_batch")
+        if raw:
+            return ot, ov, ol, ob
+        return (ot[:n].cpu().numpy().view(np.uint32), ov[:n].cpu().numpy().view(np.uint64),
+                ol[:n].cpu().numpy().view(np.uint32), ob[:n].cpu().numpy().view(np.uint64))
+
+
 class FilePipe:
     """sstc_pipe: file-to-file compaction (input SST files -> output SST files)
     with pinned staging kept across calls."""
@@ -260,21 +330,27 @@ class FilePipe:
         return res, {k: getattr(tm, k) for k, _ in FilesTiming._fields_}
 
 
-def _table_index(f):
-    """(block offsets, block sizes) of an SST image: footer + meta section walk
-    (reference table_reader.cc:52-156)."""
+def _table_index(f, keys=False):
+    """(block offsets, block sizes[, last-key offsets, last-key lengths]) of an
+    SST image: footer + meta section walk (reference table_reader.cc:52-156).
+    Key offsets point into the image."""
     import numpy as np
     b = f.size
     foot = f[b - 40:].view(np.uint64)
     nb, moff, mlen = int(foot[0]), int(foot[1]), int(foot[2])
     meta = f[moff:moff + mlen].tobytes()
-    offs, lens = [], []
+    offs, lens, lko, lkl = [], [], [], []
     p = 0
     for _ in range(nb):
         fk = int.from_bytes(meta[p:p + 4], "little")
         lk = int.from_bytes(meta[p + 4 + fk:p + 8 + fk], "little")
         q = p + 8 + fk + lk
+        lko.append(moff + p + 8 + fk)
+        lkl.append(lk)
         offs.append(int.from_bytes(meta[q:q + 8], "little"))
         lens.append(int.from_bytes(meta[q + 8:q + 16], "little"))
         p = q + 16
+    if keys:
+        return (np.asarray(offs, np.uint64), np.asarray(lens, np.uint64), np.asarray(lko, np.uint64),
+                np.asarray(lkl, np.uint32))
     return np.asarray(offs, np.uint64), np.asarray(lens, np.uint64)

@@ -83,6 +83,8 @@ class Oracle:
         lib.orc_table_index.argtypes = [_vp, _u64, _u64] + [_vp] * 8
         lib.orc_compact.restype = _u64
         lib.orc_compact.argtypes = [ctypes.c_uint32, _vp, _vp, _u64, _u64, ctypes.c_int, _vp, _u64, _vp, _u64, _vp]
+        lib.orc_table_get.restype = ctypes.c_int
+        lib.orc_table_get.argtypes = [_vp, _u64, _u64] + [_vp] * 7
 
     def encode_block(self, rec, lo=0, hi=None):
         hi = len(rec["type"]) if hi is None else hi
@@ -170,6 +172,36 @@ class Oracle:
         return res
 
 
+def queries_arena(keys):
+    """list of bytes -> (arena u8, off u64, len u32)"""
+    lens = np.array([len(k) for k in keys], np.uint32)
+    off = np.zeros(len(keys), np.uint64)
+    if len(keys) > 1:
+        off[1:] = np.cumsum(lens[:-1].astype(np.uint64))
+    arena = np.frombuffer(b"".join(keys) + b"\0" * 8, np.uint8).copy()
+    return arena, off, lens
+
+
+def _table_get_oracle(self, file_bytes, keys):
+    """Point lookups of TableReader::GetValue on one SST image.  Returns
+    (type u32[], val_off u64[] into the image, val_len u32[], block u64[])."""
+    f = np.ascontiguousarray(file_bytes, np.uint8)
+    arena, off, lens = queries_arena(keys)
+    n = len(keys)
+    t = np.zeros(max(n, 1), np.uint32)
+    vo = np.zeros(max(n, 1), np.uint64)
+    vl = np.zeros(max(n, 1), np.uint32)
+    blk = np.zeros(max(n, 1), np.uint64)
+    rc = self.lib.orc_table_get(_ptr(f), f.size, n, _ptr(arena), _ptr(off), _ptr(lens), _ptr(t), _ptr(vo),
+                                _ptr(vl), _ptr(blk))
+    if rc != 0:
+        return None
+    return t[:n], vo[:n], vl[:n], blk[:n]
+
+
+Oracle.table_get = _table_get_oracle
+
+
 def _compact_oracle(self, files, block_threshold=4096, table_limit=32 << 20, base_level=1):
     """files: list of SST images (numpy u8) in iterator order.  Returns the list
     of output SST images and the kept-record count."""
@@ -229,6 +261,8 @@ class RefLib:
         lib.ref_table_build.argtypes = [ctypes.c_char_p, _u64, _u64] + [_vp] * 8
         lib.ref_table_index.restype = _u64
         lib.ref_table_index.argtypes = [ctypes.c_char_p, _u64, _u64] + [_vp] * 6
+        lib.ref_table_get.restype = _u64
+        lib.ref_table_get.argtypes = [ctypes.c_char_p, _u64, _u64] + [_vp] * 7 + [_u64]
 
     def encode_block(self, rec, lo=0, hi=None):
         hi = len(rec["type"]) if hi is None else hi
@@ -284,3 +318,23 @@ class RefLib:
         res["first_key"] = bytes(fk[: int(res["first_key_len"][0])]) if nb else b""
         res["last_key"] = bytes(lk[: int(res["last_key_len"][-1])]) if nb else b""
         return res
+
+
+def _ref_table_get(self, path, file_size, keys, val_cap=1 << 26):
+    """The reference's TableReader::GetValue (no cache) on an SST file.  Returns
+    (type u32[], list of value bytes or None)."""
+    arena, off, lens = queries_arena(keys)
+    n = len(keys)
+    t = np.zeros(max(n, 1), np.uint32)
+    vo = np.zeros(max(n, 1), np.uint64)
+    vl = np.zeros(max(n, 1), np.uint32)
+    out = np.zeros(val_cap, np.uint8)
+    used = self.lib.ref_table_get(path.encode(), file_size, n, _ptr(arena), _ptr(off), _ptr(lens), _ptr(t),
+                                  _ptr(vo), _ptr(vl), _ptr(out), val_cap)
+    if used == 2 ** 64 - 1:
+        return None
+    vals = [bytes(out[int(vo[i]):int(vo[i]) + int(vl[i])]) if t[i] == 0 else None for i in range(n)]
+    return t[:n], vals
+
+
+RefLib.table_get = _ref_table_get

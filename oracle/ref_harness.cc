@@ -213,4 +213,32 @@ uint64_t ref_table_index(const char *path, uint64_t file_size, uint64_t cap, uin
   return idx.size();
 }
 
+
+// TableReader::GetValue without a block cache (table_reader.cc:168-189 ->
+// BlockReader::GetValue, block_reader.cc:20-57), on the SST file itself.
+// Per query: type (db::ValueType) and, for PUT, the value bytes appended to
+// val_out (val_off / val_len).  Returns the bytes used in val_out, or
+// UINT64_MAX on open failure / capacity.
+uint64_t ref_table_get(const char *path, uint64_t file_size, uint64_t nq, const uint8_t *keys,
+                       const uint64_t *key_off, const uint32_t *key_len, uint32_t *out_type,
+                       uint64_t *val_off, uint32_t *val_len, uint8_t *val_out, uint64_t val_cap) {
+  auto tr = kvs::sstable::CreateAndSetupDataForTableReader(std::string(path), 1, file_size);
+  if (!tr) return UINT64_MAX;
+  uint64_t used = 0;
+  for (uint64_t q = 0; q < nq; q++) {
+    const std::string_view key(reinterpret_cast<const char *>(keys + key_off[q]), key_len[q]);
+    const kvs::db::GetStatus st = tr->GetValue(key, 1, nullptr, tr.get());
+    out_type[q] = static_cast<uint32_t>(st.type);
+    val_off[q] = used;
+    val_len[q] = 0;
+    if (st.value) {
+      if (used + st.value->size() > val_cap) return UINT64_MAX;
+      std::memcpy(val_out + used, st.value->data(), st.value->size());
+      val_len[q] = static_cast<uint32_t>(st.value->size());
+      used += st.value->size();
+    }
+  }
+  return used;
+}
+
 } // extern "C"

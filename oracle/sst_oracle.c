@@ -460,3 +460,81 @@ uint64_t orc_compact(uint32_t k, const uint8_t *const *files, const uint64_t *by
   if (kept_records) *kept_records = kept;
   return bad ? UINT64_MAX : ntab;
 }
+
+/* ------------------------------------------------------------------------ */
+/* Point lookup (sstable/table_reader.cc:168-210, block_reader.cc:20-57)      */
+/* ------------------------------------------------------------------------ */
+
+/* std::string_view::compare: unsigned bytes, then length */
+static int sv_cmp(const uint8_t *a, uint64_t la, const uint8_t *b, uint64_t lb) {
+  const uint64_t m = la < lb ? la : lb;
+  for (uint64_t i = 0; i < m; i++)
+    if (a[i] != b[i]) return a[i] < b[i] ? -1 : 1;
+  return la < lb ? -1 : (la > lb ? 1 : 0);
+}
+
+int orc_table_get(const uint8_t *file, uint64_t bytes, uint64_t nq, const uint8_t *keys,
+                  const uint64_t *key_off, const uint32_t *key_len, uint32_t *out_type,
+                  uint64_t *out_val_off, uint32_t *out_val_len, uint64_t *out_block) {
+  uint64_t mn, mx;
+  const uint64_t nb = orc_table_index(file, bytes, 0, NULL, NULL, NULL, NULL, NULL, NULL, &mn, &mx);
+  if (nb == UINT64_MAX) return -1;
+  uint64_t *bo = (uint64_t *)malloc(sizeof(uint64_t) * (nb + 1)), *bl = (uint64_t *)malloc(sizeof(uint64_t) * (nb + 1));
+  uint64_t *fo = (uint64_t *)malloc(sizeof(uint64_t) * (nb + 1)), *lo = (uint64_t *)malloc(sizeof(uint64_t) * (nb + 1));
+  uint32_t *fl = (uint32_t *)malloc(sizeof(uint32_t) * (nb + 1)), *ll = (uint32_t *)malloc(sizeof(uint32_t) * (nb + 1));
+  orc_table_index(file, bytes, nb, bo, bl, fo, fl, lo, ll, &mn, &mx);
+  for (uint64_t q = 0; q < nq; q++) {
+    const uint8_t *key = keys + key_off[q];
+    const uint64_t kl = key_len[q];
+    out_type[q] = ORC_GET_NOT_FOUND;
+    out_val_off[q] = 0;
+    out_val_len[q] = 0;
+    out_block[q] = UINT64_MAX;
+    if (nb == 0) continue; /* the reference indexes block_index_[-1] here */
+    /* GetBlockOffsetAndSize :191-210 */
+    int64_t left = 0, right = (int64_t)nb - 1;
+    while (left < right) {
+      const int64_t mid = left + (right - left) / 2;
+      if (sv_cmp(file + lo[mid], ll[mid], key, kl) >= 0) right = mid;
+      else left = mid + 1;
+    }
+    const uint64_t b = (uint64_t)right;
+    out_block[q] = b;
+    /* CreateAndSetupDataForBlockReader :212-241 (trailer + entry starts) */
+    const uint64_t L = bl[b];
+    if (bo[b] > bytes || L > bytes - bo[b] || L < 16) { out_type[q] = ORC_GET_BAD; continue; }
+    const uint8_t *blk = file + bo[b];
+    const uint64_t n = rd64(blk + L - 16), offs = rd64(blk + L - 8);
+    if (offs > L - 16 || n > (L - 16 - offs) / 16) { out_type[q] = ORC_GET_BAD; continue; }
+    /* BlockReader::GetValue :20-57 */
+    int64_t l2 = 0, r2 = (int64_t)n - 1;
+    while (l2 <= r2) {
+      const int64_t mid = l2 + (r2 - l2) / 2;
+      const uint64_t s = rd64(blk + offs + 16 * (uint64_t)mid);
+      if (s > offs || offs - s < 5) { out_type[q] = ORC_GET_BAD; break; }
+      const uint8_t t = blk[s];
+      const uint32_t ekl = rd32(blk + s + 1);
+      if ((uint64_t)ekl > offs - s - 5 || t > 1) { out_type[q] = ORC_GET_BAD; break; }
+      const int c = sv_cmp(blk + s + 5, ekl, key, kl);
+      if (c == 0) {
+        if (t == 1) {
+          out_type[q] = ORC_GET_DELETED;
+        } else {
+          if (offs - s - 5 - ekl < 4) { out_type[q] = ORC_GET_BAD; break; }
+          const uint32_t vl = rd32(blk + s + 5 + ekl);
+          if ((uint64_t)vl > offs - s - 9 - ekl) { out_type[q] = ORC_GET_BAD; break; }
+          out_type[q] = ORC_GET_PUT;
+          out_val_off[q] = bo[b] + s + 9 + ekl;
+          out_val_len[q] = vl;
+        }
+        break;
+      } else if (c < 0) {
+        l2 = mid + 1;
+      } else {
+        r2 = mid - 1;
+      }
+    }
+  }
+  free(bo); free(bl); free(fo); free(lo); free(fl); free(ll);
+  return 0;
+}

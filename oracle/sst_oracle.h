@@ -124,6 +124,24 @@ uint64_t orc_compact(uint32_t k, const uint8_t *const *files, const uint64_t *by
                      uint8_t *out, uint64_t out_cap, uint64_t *out_size, uint64_t max_tables,
                      uint64_t *kept_records);
 
+
+/* Point lookup of TableReader::GetValue without a block cache
+ * (sstable/table_reader.cc:168-210): GetBlockOffsetAndSize picks the first
+ * block whose largest key >= key (the last block when none is), then
+ * BlockReader::GetValue (sstable/block_reader.cc:20-57) binary-searches the
+ * block's entry starts exactly as the reference does (the first probed equal
+ * key wins, the txn is ignored).  Per query: out_type = 0 PUT, 1 DELETED,
+ * 2 NOT_FOUND (db/status.h:11-19), 4 = malformed block; for PUT the value is
+ * file[out_val_off .. + out_val_len).  file = one SST image (bytes on disk).
+ * Returns 0, or -1 on a malformed footer / meta section. */
+#define ORC_GET_PUT 0u
+#define ORC_GET_DELETED 1u
+#define ORC_GET_NOT_FOUND 2u
+#define ORC_GET_BAD 4u
+int orc_table_get(const uint8_t *file, uint64_t bytes, uint64_t nq, const uint8_t *keys,
+                  const uint64_t *key_off, const uint32_t *key_len, uint32_t *out_type,
+                  uint64_t *out_val_off, uint32_t *out_val_len, uint64_t *out_block);
+
 #ifdef __cplusplus
 }
 #endif

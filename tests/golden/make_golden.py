@@ -23,7 +23,7 @@ sys.path.insert(0, os.path.join(ROOT, "lsm-kv-storage_amd"))
 import hashlib  # noqa: E402
 import json  # noqa: E402
 
-from oracle import RefLib, ref_compact  # noqa: E402
+from oracle import RefLib, queries_arena, ref_compact  # noqa: E402
 from sstcodec import workload as W  # noqa: E402
 
 REC_KEYS = ("type", "key_len", "val_len", "txn", "key_off", "val_off")
@@ -158,6 +158,9 @@ def main():
     # 6. compaction (db/compact.cc) through the reference merge + table code
     compaction_fixtures(ref)
 
+    # 7. point lookups (TableReader::GetValue -> BlockReader::GetValue)
+    lookup_fixtures(ref)
+
 
 COMPACTION_CASES = [
     # name, k, n_per, key_space, vmax, table_limit, distinct, extra generator args
@@ -203,6 +206,48 @@ def compaction_fixtures(ref):
     with open(os.path.join(HERE, "compaction.json"), "w") as f:
         json.dump(manifest, f, indent=1)
     print("compaction.json written")
+
+
+def sorted_ragged(n, seed):
+    """ragged records (empty keys, DELETEs, empty values) sorted by key bytes,
+    equal keys newest first: a valid SST key order with repeated keys."""
+    rec = W.mixed_records(n, seed=seed, max_key=24, max_val=120, p_delete=0.15, p_empty_val=0.1,
+                          p_empty_key=0.02)
+    key = [bytes(rec["key_src"][int(o):int(o) + int(k)]) for o, k in zip(rec["key_off"], rec["key_len"])]
+    key = [k[:int(1 + (i % 5))] if i % 3 == 0 else k for i, k in enumerate(key)]  # short keys -> repeats
+    order = sorted(range(n), key=lambda i: (key[i], -int(rec["txn"][i])))
+    items = []
+    for i in order:
+        vl = int(rec["val_len"][i])
+        v = None if vl == W.NO_VALUE else bytes(rec["val_src"][int(rec["val_off"][i]):int(rec["val_off"][i]) + vl])
+        items.append((int(rec["type"][i]), key[i], v, int(rec["txn"][i])))
+    return records_from_list(items), sorted(set(key))
+
+
+def lookup_fixtures(ref):
+    """Two SSTs written by the reference TableBuilder (one with repeated keys
+    inside blocks, one ragged with empty keys / values) and a query set looked
+    up by the reference's own TableReader::GetValue: present keys, absent keys,
+    keys before the first / after the last, prefixes, empty key."""
+    dups = W.compaction_inputs(1, 3000, 6000, seed=4, vmax=300, p_delete=0.2, distinct=False)[0]
+    rag, rag_keys = sorted_ragged(2500, 21)
+    arrays = {}
+    with tempfile.TemporaryDirectory() as td:
+        for t, (rec, T) in enumerate(((dups, 4096), (rag, 4096))):
+            p = os.path.join(td, f"{t}.sst")
+            fs = ref.table_build(p, rec, T)
+            if t == 0:
+                keys = [b"k%015d" % i for i in range(0, 6000, 2)]
+            else:
+                keys = rag_keys[::2] + [k + b"\x00" for k in rag_keys[1::7]] + [k[:-1] for k in rag_keys[2::9] if k]
+            keys += [b"", b"\x00", b"a", b"zzzz", b"\xff" * 5, b"k00000000000000", b"k0000000000000000"]
+            types, vals = ref.table_get(p, fs, keys)
+            ka, ko, kl = queries_arena(keys)
+            va, vo, vlen = queries_arena([v if v is not None else b"" for v in vals])
+            arrays.update({f"sst{t}": np.fromfile(p, np.uint8), f"q{t}_keys": ka, f"q{t}_key_off": ko,
+                           f"q{t}_key_len": kl, f"q{t}_type": types, f"q{t}_val": va, f"q{t}_val_off": vo,
+                           f"q{t}_val_len": vlen})
+    save("lookup.npz", **arrays)
 
 
 if __name__ == "__main__":

@@ -52,7 +52,12 @@ def record_sets(args, rank):
         out = []
         for s in range(args.ssts):
             i = np.arange(args.keys, dtype=np.uint64)
-            keys = i if args.overlap else i * np.uint64(args.ssts) + np.uint64(s)
+            if args.overlap:
+                keys = i
+            elif args.ranges:  # SST s holds one contiguous key range (merge = concatenation)
+                keys = i + np.uint64(s * args.keys)
+            else:
+                keys = i * np.uint64(args.ssts) + np.uint64(s)
             out.append(W.uniform_records(args.keys, key_index=keys, seed=s + 1, txn_start=1 + s * args.keys))
         return out
     if args.config == 4:
@@ -88,6 +93,7 @@ def main():
     ap.add_argument("--ssts", type=int, default=None)
     ap.add_argument("--key-space", type=int, default=20000)
     ap.add_argument("--overlap", action="store_true")
+    ap.add_argument("--ranges", action="store_true", help="config 3 with key-range-disjoint SSTs")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--no-ref", action="store_true")
     ap.add_argument("--no-files", action="store_true")
