@@ -25,7 +25,8 @@ collected for this workload, else null.
 cpu_baseline: the reference's own code (oracle/_ref/libsstref.so: BlockReader +
 BlockReaderIterator -> BlockBuilder), one thread, on a bounded sample of the
 same blocks; falls back to the clean-room oracle ("port") if the reference
-build is absent.
+build is absent.  cpu_baseline_16_threads: the same on 16 host threads (the
+box's CPU share per GPU; generous, the reference compacts on one thread).
 """
 import argparse
 import json
@@ -121,6 +122,43 @@ def cpu_baseline(sample_src, sample_off, sample_len, seconds=10.0):
             "sample": f"{sample_len.size} blocks x {int(sample_len[0])} B (same uniform workload), "
                       f"{passes} passes in {el:.1f} s, 1 thread, decode (BlockReader/Iterator) + "
                       f"re-encode (BlockBuilder) in host memory"}
+
+
+def cpu_baseline_threads(sample_src, sample_off, sample_len, threads=16, seconds=5.0):
+    """The same reference round trip on `threads` host threads (blocks split
+    into contiguous ranges, one per thread; ctypes releases the GIL).  A
+    generous baseline: the reference runs one compaction at a time on one
+    thread (db/db_impl.cc:548).  16 = the GPU box's CPU share per GPU."""
+    import threading
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    try:
+        lib = O.RefLib()
+    except (FileNotFoundError, OSError):
+        return None
+    nb = sample_off.size
+    parts = np.array_split(np.arange(nb), threads)
+    dsts = [np.zeros_like(sample_src) for _ in range(threads)]
+    done = [0] * threads
+    stop = time.perf_counter() + seconds
+
+    def work(k):
+        idx = parts[k]
+        o, ln = sample_off[idx], sample_len[idx]
+        while time.perf_counter() < stop:
+            lib.roundtrip(sample_src, o, ln, dst=dsts[k])
+            done[k] += int(ln.sum())
+
+    t0 = time.perf_counter()
+    th = [threading.Thread(target=work, args=(k,)) for k in range(threads)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    el = time.perf_counter() - t0
+    return {"value": sum(done) / el / 2 ** 30, "unit": "GiB/s", "cores": threads, "kind": "reference",
+            "sample": f"{nb} blocks split over {threads} threads, {el:.1f} s (generous: the reference compacts "
+                      f"on one thread)"}
 
 
 def e2e_rate(codec, src, off, ln, dev, chunk_blocks=8192, reps=3):
@@ -274,6 +312,9 @@ def main():
                 o = off[:k].cpu().numpy().view(np.uint64)
                 l_ = ln[:k].cpu().numpy().view(np.uint64)
                 out["cpu_baseline"] = cpu_baseline(s, o, l_, args.cpu_seconds)
+                all_cores = cpu_baseline_threads(s, o, l_, 16, min(5.0, args.cpu_seconds))
+                if all_cores:
+                    out["cpu_baseline_16_threads"] = all_cores
         print(json.dumps(out), flush=True)
     if dist_on:
         dist.barrier()

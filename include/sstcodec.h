@@ -202,7 +202,7 @@ int sstc_compact(sstc_ctx *ctx, const uint8_t *d_src, const uint64_t *d_blk_off,
 #define SSTC_GET_PUT 0u       /* db::ValueType::PUT                          */
 #define SSTC_GET_DELETED 1u   /* db::ValueType::DELETED                      */
 #define SSTC_GET_NOT_FOUND 2u /* db::ValueType::NOT_FOUND                    */
-#define SSTC_GET_BAD_BLOCK 4u /* a probed entry / trailer is out of range    */
+#define SSTC_GET_BAD_BLOCK 4u /* a probed entry / trailer / index entry is out of range */
 
 /* Block indexes of one or many SSTs (device arrays; what TableReader holds
  * after FetchBlockIndexInfo, table_reader.cc:86-156). */
@@ -214,6 +214,8 @@ typedef struct sstc_block_index {
   const uint8_t *keys;
   const uint64_t *table_first_block; /* table t owns blocks [tfb[t], tfb[t+1])          */
   uint32_t ntables;
+  uint64_t src_bytes;                /* size of d_src: every read is bounds-checked    */
+  uint64_t keys_bytes;               /* size of keys                                   */
 } sstc_block_index;
 
 /* Query q looks key d_q_keys[d_q_key_off[q] .. + d_q_key_len[q]) up in table
@@ -226,9 +228,9 @@ typedef struct sstc_block_index {
  * NULL.  A table without blocks answers NOT_FOUND (the reference reads
  * block_index_[-1] there). */
 int sstc_get_batch(sstc_ctx *ctx, const uint8_t *d_src, const sstc_block_index *index,
-                   const uint32_t *d_q_table, const uint8_t *d_q_keys, const uint64_t *d_q_key_off,
-                   const uint32_t *d_q_key_len, uint64_t nq, uint32_t *d_out_type, uint64_t *d_out_val_off,
-                   uint32_t *d_out_val_len, uint64_t *d_out_block);
+                   const uint32_t *d_q_table, const uint8_t *d_q_keys, uint64_t q_keys_bytes,
+                   const uint64_t *d_q_key_off, const uint32_t *d_q_key_len, uint64_t nq, uint32_t *d_out_type,
+                   uint64_t *d_out_val_off, uint32_t *d_out_val_len, uint64_t *d_out_block);
 
 /* ---- file-to-file compaction (Compact::DoCompactJob end to end: the input
  *      SST files are read, compacted on the device and the output SSTs written

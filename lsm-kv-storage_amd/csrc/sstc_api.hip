@@ -291,17 +291,19 @@ int sstc_compact(sstc_ctx *c, const uint8_t *d_src, const uint64_t *d_blk_off, c
 }
 
 int sstc_get_batch(sstc_ctx *c, const uint8_t *d_src, const sstc_block_index *index, const uint32_t *d_q_table,
-                   const uint8_t *d_q_keys, const uint64_t *d_q_key_off, const uint32_t *d_q_key_len, uint64_t nq,
-                   uint32_t *d_out_type, uint64_t *d_out_val_off, uint32_t *d_out_val_len, uint64_t *d_out_block) {
+                   const uint8_t *d_q_keys, uint64_t q_keys_bytes, const uint64_t *d_q_key_off,
+                   const uint32_t *d_q_key_len, uint64_t nq, uint32_t *d_out_type, uint64_t *d_out_val_off,
+                   uint32_t *d_out_val_len, uint64_t *d_out_block) {
   if (!c || !index) return fail(SSTC_E_INVALID_ARG, "sstc_get_batch: NULL argument");
   if (nq && (!d_src || !index->blk_off || !index->blk_len || !index->last_key_off || !index->last_key_len ||
              !index->keys || !index->table_first_block || !d_q_table || !d_q_keys || !d_q_key_off ||
              !d_q_key_len || !d_out_type || !d_out_val_off || !d_out_val_len))
     return fail(SSTC_E_INVALID_ARG, "sstc_get_batch: NULL argument");
   if (int r = bind_device(c)) return r;
-  const sstc::GetArgs a{d_src, index->blk_off, index->blk_len, index->last_key_off, index->last_key_len,
-                        index->keys, index->table_first_block, index->ntables, d_q_table, d_q_keys, d_q_key_off,
-                        d_q_key_len, nq, d_out_type, d_out_val_off, d_out_val_len, d_out_block, c->err_count};
+  const sstc::GetArgs a{d_src,        index->blk_off,  index->blk_len, index->last_key_off, index->last_key_len,
+                        index->keys,  index->table_first_block, index->ntables, d_q_table, d_q_keys, d_q_key_off,
+                        d_q_key_len,  nq, d_out_type, d_out_val_off, d_out_val_len, d_out_block, c->err_count,
+                        index->src_bytes, index->keys_bytes, q_keys_bytes};
   SSTC_HIP(sstc::launch_get(a, c->stream), "sstc_get_batch launch");
   return SSTC_OK;
 }

@@ -1064,20 +1064,12 @@ __global__ __launch_bounds__(kScanThreads) void scan_lookback_kernel(const uint6
 // ---------------------------------------------------------------------------
 static inline uint32_t grid_for(uint64_t n, uint32_t per) { return static_cast<uint32_t>((n + per - 1) / per); }
 
-// A/B switch for the XCD-aware block order (SSTC_XCD=0/1/2/3: bit 0 rt_kernel,
-// bit 1 decode/encode); temporary while it is measured
-static uint32_t xcd_mode() {
-  static const uint32_t m = [] {
-    const char *e = getenv("SSTC_XCD");
-    return e ? static_cast<uint32_t>(atoi(e)) : 0u;
-  }();
-  return m;
-}
+
 
 hipError_t launch_roundtrip(const RtArgs &a, hipStream_t s) {
-  RtArgs b = a;
-  b.xcd = xcd_mode() & 1u;
-  if (a.nblocks) rt_kernel<<<grid_for(a.nblocks, kRtWaves), kRtWaves * kWave, 0, s>>>(b);
+  // blocks in dispatch order: the XCD-grouped order measured +3 % at config 2
+  // (256 MiB, Infinity-Cache resident) but -2.5 % on 1 GiB (profiles/r01_ab_xcd.log)
+  if (a.nblocks) rt_kernel<<<grid_for(a.nblocks, kRtWaves), kRtWaves * kWave, 0, s>>>(a);
   return hipGetLastError();
 }
 
@@ -1089,7 +1081,7 @@ hipError_t launch_count(const uint8_t *src, const uint64_t *blk_off, const uint6
 
 hipError_t launch_decode(const DecArgs &a, hipStream_t s) {
   DecArgs b = a;
-  b.xcd = (xcd_mode() >> 1) & 1u;
+  b.xcd = 1; // XCD-grouped block order: neighbouring blocks share L2 lines (-5 % time, config 3)
   if (a.nblocks) decode_kernel<<<grid_for(a.nblocks, kDecWaves), kDecWaves * kWave, 0, s>>>(b);
   return hipGetLastError();
 }
@@ -1123,9 +1115,7 @@ hipError_t launch_enc_blk_len(const uint64_t *P, const uint64_t *blk_first, uint
 
 hipError_t launch_enc_emit(const EncArgs &a, hipStream_t s) {
   if (!a.nblocks) return hipSuccess;
-  EncArgs b = a;
-  b.xcd = (xcd_mode() >> 1) & 1u;
-  enc_lds_kernel<<<grid_for(a.nblocks, kEncWaves), kEncWaves * kWave, 0, s>>>(b);
+  enc_lds_kernel<<<grid_for(a.nblocks, kEncWaves), kEncWaves * kWave, 0, s>>>(a);
   enc_emit_kernel<<<static_cast<uint32_t>(a.nblocks < 2048 ? a.nblocks : 2048), kEncThreads, 0, s>>>(a);
   return hipGetLastError();
 }

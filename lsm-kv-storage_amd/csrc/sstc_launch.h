@@ -82,6 +82,7 @@ struct GetArgs {
   uint32_t *out_val_len;
   uint64_t *out_block; // may be null
   unsigned long long *err_count;
+  uint64_t src_bytes, keys_bytes, q_keys_bytes; // read bounds
 };
 hipError_t launch_get(const GetArgs &a, hipStream_t s);
 

@@ -44,7 +44,8 @@ class CompactResult(ctypes.Structure):
 class BlockIndex(ctypes.Structure):
     """sstc_block_index (device pointers)."""
     _fields_ = [("blk_off", c_vp), ("blk_len", c_vp), ("last_key_off", c_vp), ("last_key_len", c_vp),
-                ("keys", c_vp), ("table_first_block", c_vp), ("ntables", ctypes.c_uint32)]
+                ("keys", c_vp), ("table_first_block", c_vp), ("ntables", ctypes.c_uint32),
+                ("src_bytes", ctypes.c_uint64), ("keys_bytes", ctypes.c_uint64)]
 
 
 GET_TYPES = {0: "PUT", 1: "DELETED", 2: "NOT_FOUND", 4: "BAD_BLOCK"}
@@ -95,8 +96,8 @@ def load():
         "sstc_roundtrip_blocks": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_u64, c_u32, c_vp, c_vp]),
         "sstc_compact": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_u64, c_vp, c_u32, P(CompactParams), c_vp, c_u64,
                                         c_vp, c_vp, c_u64, P(CompactResult)]),
-        "sstc_get_batch": (ctypes.c_int, [c_vp, c_vp, P(BlockIndex), c_vp, c_vp, c_vp, c_vp, c_u64, c_vp, c_vp, c_vp,
-                                          c_vp]),
+        "sstc_get_batch": (ctypes.c_int, [c_vp, c_vp, P(BlockIndex), c_vp, c_vp, c_u64, c_vp, c_vp, c_u64, c_vp, c_vp,
+                                          c_vp, c_vp]),
         "sstc_pipe_create": (ctypes.c_int, [c_vp, c_u32, P(c_vp)]),
         "sstc_pipe_destroy": (ctypes.c_int, [c_vp]),
         "sstc_compact_files": (ctypes.c_int, [c_vp, c_vp, c_vp, c_u32, ctypes.c_char_p, c_u64, P(CompactParams),

@@ -251,8 +251,9 @@ class Lookup:
 
     def index(self):
         from ._lib import BlockIndex
+        n = self.src.numel()
         return BlockIndex(self.blk_off.data_ptr(), self.blk_len.data_ptr(), self.lk_off.data_ptr(),
-                          self.lk_len.data_ptr(), self.src.data_ptr(), self.tfb.data_ptr(), self.ntables)
+                          self.lk_len.data_ptr(), self.src.data_ptr(), self.tfb.data_ptr(), self.ntables, n, n)
 
     def get(self, q_table, keys, raw=False):
         """q_table: table index per query; keys: list of bytes.  Returns numpy
@@ -272,8 +273,9 @@ class Lookup:
         ob = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
         idx = self.index()
         self.codec._stream()
-        check(self.codec.lib.sstc_get_batch(self.codec.h, _p(self.src), ctypes.byref(idx), _p(qt), _p(qk), _p(qo),
-                                            _p(ql), n, _p(ot), _p(ov), _p(ol), _p(ob)), "sstc_get_batch")
+        check(self.codec.lib.sstc_get_batch(self.codec.h, _p(self.src), ctypes.byref(idx), _p(qt), _p(qk),
+                                            qk.numel(), _p(qo), _p(ql), n, _p(ot), _p(ov), _p(ol), _p(ob)),
+              "sstc_get_batch")
         if raw:
             return ot, ov, ol, ob
         return (ot[:n].cpu().numpy().view(np.uint32), ov[:n].cpu().numpy().view(np.uint64),

@@ -71,8 +71,8 @@ def main():
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         codec._stream()
         e0.record(stream)
-        check(codec.lib.sstc_get_batch(codec.h, _p(lk.src), ctypes.byref(idx), _p(qt_d), _p(qk), _p(qo), _p(ql), n,
-                                       _p(ot), _p(ov), _p(ol), _p(ob)), "sstc_get_batch")
+        check(codec.lib.sstc_get_batch(codec.h, _p(lk.src), ctypes.byref(idx), _p(qt_d), _p(qk), qk.numel(), _p(qo),
+                                       _p(ql), n, _p(ot), _p(ov), _p(ol), _p(ob)), "sstc_get_batch")
         e1.record(stream)
         e1.synchronize()
         times.append(e0.elapsed_time(e1) / 1e3)
