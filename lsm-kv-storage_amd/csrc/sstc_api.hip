@@ -145,6 +145,7 @@ int sstc_ctx_destroy(sstc_ctx *c) {
   if (!c) return SSTC_OK;
   bind_device(c);
   (void)hipStreamSynchronize(c->stream);
+  if (c->arena.host) (void)hipHostFree(c->arena.host);
   for (void *p : {c->counters, c->arena.base,
                   static_cast<void *>(c->scan_ws), static_cast<void *>(c->sizes),
                   static_cast<void *>(c->P), static_cast<void *>(c->jump)})

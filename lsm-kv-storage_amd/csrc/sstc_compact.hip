@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstring>
+#include <initializer_list>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -206,9 +207,10 @@ __global__ void ck_gather_kernel(const SK *s, const uint64_t *keep, const uint64
 }
 
 // per record: end of its output table (clamp for block segmentation)
-__global__ void ck_table_end_kernel(const uint64_t *tf, uint64_t nt, uint64_t m, uint32_t *clamp) {
+__global__ void ck_table_end_kernel(const uint64_t *tf, const uint64_t *d_nt, uint64_t m, uint32_t *clamp) {
   const uint64_t r = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (r > m) return;
+  const uint64_t nt = *d_nt;
   if (r == m) {
     clamp[r] = static_cast<uint32_t>(m);
     return;
@@ -461,27 +463,27 @@ uint32_t bitlen(uint64_t v) {
   return b ? b : 1;
 }
 
-template <class T> T read1(const T *d, hipStream_t s) {
-  T v{};
-  CK(hipMemcpyAsync(&v, d, sizeof(T), hipMemcpyDeviceToHost, s));
-  CK(hipStreamSynchronize(s));
-  return v;
-}
 
 // greedy segmentation of [0, m) by weights whose prefix sums are
-// Pw[i] + add * i (>= threshold closes), optional clamp
-uint64_t segment(Pool &pool, const uint64_t *Pw, uint64_t add, uint64_t m, uint64_t threshold,
-                 const uint32_t *clamp, uint64_t nclamps, uint64_t *first, hipStream_t s) {
-  // every segment but the last one of each clamp range reaches the threshold,
-  // so the chain from record 0 has at most total / threshold + nclamps + 1
-  // nodes: that many doubling levels suffice
-  const uint64_t total = read1(Pw + m, s) + add * m;
-  const uint64_t chain = total / threshold + nclamps + 1;
-  const uint32_t levels = bitlen(chain < m ? chain : m);
+// Pw[i] + add * i (>= threshold closes), optional clamp.  chain_bound: an
+// upper bound of the number of segments (host-known, so no sync); the count
+// lands in *dn on the device.
+void segment(Pool &pool, const uint64_t *Pw, uint64_t add, uint64_t m, uint64_t threshold, const uint32_t *clamp,
+             uint64_t chain_bound, uint64_t *first, uint64_t *dn, hipStream_t s) {
+  const uint32_t levels = bitlen(chain_bound < m ? chain_bound : m);
   uint32_t *J = pool.get<uint32_t>(static_cast<uint64_t>(levels) * (m + 1));
-  uint64_t *dn = pool.get<uint64_t>(1);
   CK(launch_segment(Pw, m, threshold, J, levels, dn, first, s, clamp, add));
-  return read1(dn, s);
+}
+
+// device -> pinned host words, one sync
+void fetch(Arena &arena, hipStream_t s, std::initializer_list<const uint64_t *> src) {
+  if (!arena.host && hipHostMalloc(reinterpret_cast<void **>(&arena.host), 64 * sizeof(uint64_t)) != hipSuccess) {
+    arena.host = nullptr;
+    throw std::runtime_error("pinned host words");
+  }
+  int i = 0;
+  for (const uint64_t *p : src) CK(hipMemcpyAsync(arena.host + i++, p, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+  CK(hipStreamSynchronize(s));
 }
 
 } // namespace
@@ -495,14 +497,23 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
   try {
     Pool pool(arena);
     const uint64_t nws = scan_workspace_elems(nblocks + 1) + 64;
+    // Host syncs: (1) per-block record counts (they size every array), (2) the
+    // kept count with the sortedness / decode error flags, (3) the table and
+    // block counts, (4) the output size (capacity check before any write),
+    // (5) completion.  Everything else stays on the stream.
     // 1. decode every block
     uint64_t *rb_all = pool.get<uint64_t>(nblocks + 1);
+    uint64_t *inb = pool.get<uint64_t>(nblocks + 1);
     uint64_t *ws = pool.get<uint64_t>(nws);
+    uint64_t *errs = pool.get<uint64_t>(2);
     CK(launch_count(d_src, d_blk_off, d_blk_len, nblocks, rb_all, s));
     CK(launch_scan(rb_all, nblocks, 0, rb_all, ws, s));
+    CK(launch_scan(d_blk_len, nblocks, 0, inb, ws, s)); // input bytes: bounds the split chains
+    CK(hipMemcpyAsync(errs, err_count, 8, hipMemcpyDeviceToDevice, s));
     std::vector<uint64_t> h_rb(nblocks + 1);
     CK(hipMemcpyAsync(h_rb.data(), rb_all, (nblocks + 1) * 8, hipMemcpyDeviceToHost, s));
-    CK(hipStreamSynchronize(s));
+    fetch(arena, s, {inb + nblocks});
+    const uint64_t in_bytes = arena.host[0];
     const uint64_t n = h_rb[nblocks];
     std::vector<uint64_t> run_start;
     for (uint32_t t = 0; t <= ntables; t++) run_start.push_back(h_rb[h_tfb[t]]);
@@ -519,13 +530,13 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     SK *A = pool.get<SK>(n ? n : 1), *B = pool.get<SK>(n ? n : 1);
     DecArgs da{d_src, d_blk_off, d_blk_len, nblocks, rb_all,
                sstc_records{R.type, R.kl, R.vl, R.tx, R.ko, R.vo}, txn_mode, status, err_count, A};
-    const unsigned long long errs0 = read1(err_count, s);
     CK(launch_decode(da, s));
-    if (read1(err_count, s) != errs0) {
-      err = "an input block failed to decode";
-      return SSTC_E_INVALID_ARG;
-    }
     if (n == 0) { // DoCompactJob still finishes its first (empty) output table
+      fetch(arena, s, {reinterpret_cast<const uint64_t *>(err_count), errs});
+      if (arena.host[0] != arena.host[1]) {
+        err = "an input block failed to decode";
+        return SSTC_E_INVALID_ARG;
+      }
       if (max_tables < 1 || dst_cap < 40) {
         err = "output capacity";
         return SSTC_E_CAPACITY;
@@ -549,10 +560,7 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     unsigned long long *bad = reinterpret_cast<unsigned long long *>(pool.get<uint64_t>(1));
     CK(hipMemsetAsync(bad, 0, 8, s));
     ck_check_sorted_kernel<<<grid(n), 256, 0, s>>>(A, rb, nruns, n, kv, bad);
-    if (read1(bad, s)) {
-      err = "input SST records are not sorted (key asc, txn desc)";
-      return SSTC_E_INVALID_ARG;
-    }
+    std::vector<MergePair> flat; // uploaded asynchronously: lives until the next sync
     {
       // run boundaries of every round are known on the host (input table
       // sizes): one descriptor upload for all rounds
@@ -577,7 +585,6 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
       }
       size_t total = 0;
       for (auto &r : rounds) total += r.size();
-      std::vector<MergePair> flat;
       for (auto &r : rounds) flat.insert(flat.end(), r.begin(), r.end());
       MergePair *d_pairs = pool.get<MergePair>(total ? total : 1);
       if (total) CK(hipMemcpyAsync(d_pairs, flat.data(), total * sizeof(MergePair), hipMemcpyHostToDevice, s));
@@ -590,7 +597,6 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
         std::swap(A, B);
         at += r.size();
       }
-      CK(hipStreamSynchronize(s)); // flat (host) must outlive the upload
     }
     // 3. keep / drop
     uint64_t *head = pool.get<uint64_t>(n), *G = pool.get<uint64_t>(n + 1), *hp = pool.get<uint64_t>(n);
@@ -601,27 +607,43 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     // G[i] (exclusive) + head[i] - 1 = group id; for a non-head i the group id is G[i] - 1
     ck_keep_kernel<<<grid(n), 256, 0, s>>>(A, head, G, hp, R.type, n, base_level, keep);
     CK(launch_scan(keep, n, 0, K, ws2, s));
-    const uint64_t m = read1(K + n, s);
+    fetch(arena, s, {K + n, reinterpret_cast<const uint64_t *>(bad), reinterpret_cast<const uint64_t *>(err_count),
+                     errs});
+    if (arena.host[2] != arena.host[3]) {
+      err = "an input block failed to decode";
+      return SSTC_E_INVALID_ARG;
+    }
+    if (arena.host[1]) {
+      err = "input SST records are not sorted (key asc, txn desc)";
+      return SSTC_E_INVALID_ARG;
+    }
+    const uint64_t m = arena.host[0];
     res[1] = m;
     Rec KR{pool.get<uint8_t>(m), pool.get<uint32_t>(m), pool.get<uint32_t>(m), pool.get<uint64_t>(m),
            pool.get<uint64_t>(m), pool.get<uint64_t>(m)};
     uint64_t *dw = pool.get<uint64_t>(m), *ew = pool.get<uint64_t>(m);
     ck_gather_kernel<<<grid(n), 256, 0, s>>>(A, keep, K, R, n, KR, dw, ew);
     // 4. table split then block split (clamped at table ends); block weight =
-    // entry + offset entry, i.e. the prefix sums of the entry sizes + 16 i
+    // entry + offset entry, i.e. the prefix sums of the entry sizes + 16 i.
+    // Chain bounds: kept key+value bytes and entry+offset bytes are at most
+    // the input block bytes, and every table / block but the last of each
+    // clamp range reaches its threshold.
     uint64_t *Pd = pool.get<uint64_t>(m + 1), *Pe = pool.get<uint64_t>(m + 1);
     CK(launch_scan(dw, m, 0, Pd, ws2, s));
     CK(launch_scan(ew, m, 0, Pe, ws2, s));
-    uint64_t *tf = pool.get<uint64_t>(m + 1);
-    const uint64_t nt = segment(pool, Pd, 0, m, table_limit, nullptr, 0, tf, s);
+    uint64_t *tf = pool.get<uint64_t>(m + 1), *dn = pool.get<uint64_t>(2);
+    const uint64_t nt_bound = in_bytes / table_limit + 1;
+    segment(pool, Pd, 0, m, table_limit, nullptr, nt_bound, tf, dn, s);
+    uint32_t *clamp = pool.get<uint32_t>(m + 1);
+    ck_table_end_kernel<<<grid(m + 1), 256, 0, s>>>(tf, dn, m, clamp);
+    uint64_t *bf = pool.get<uint64_t>(m + 1);
+    segment(pool, Pe, 16, m, block_threshold, clamp, in_bytes / block_threshold + nt_bound + 1, bf, dn + 1, s);
+    fetch(arena, s, {dn, dn + 1});
+    const uint64_t nt = arena.host[0], nb = arena.host[1];
     if (nt > max_tables) {
       err = "more output tables than max_tables";
       return SSTC_E_CAPACITY;
     }
-    uint32_t *clamp = pool.get<uint32_t>(m + 1);
-    ck_table_end_kernel<<<grid(m + 1), 256, 0, s>>>(tf, nt, m, clamp);
-    uint64_t *bf = pool.get<uint64_t>(m + 1);
-    const uint64_t nb = segment(pool, Pe, 16, m, block_threshold, clamp, nt, bf, s);
     // 5. layout
     uint64_t *blen = pool.get<uint64_t>(nb), *msz = pool.get<uint64_t>(nb);
     uint32_t *btab = pool.get<uint32_t>(nb);
@@ -632,7 +654,8 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     uint64_t *tbf = pool.get<uint64_t>(nt + 1), *tdata = pool.get<uint64_t>(nt), *tmeta = pool.get<uint64_t>(nt);
     ck_table_info_kernel<<<grid(nt + 1), 256, 0, s>>>(tf, nt, bf, nb, BL, MS, tbf, tdata, tmeta, d_table_len);
     CK(launch_scan(d_table_len, nt, 0, d_table_off, ws2, s)); // d_table_off needs nt + 1 elements
-    const uint64_t total = read1(d_table_off + nt, s);
+    fetch(arena, s, {d_table_off + nt});
+    const uint64_t total = arena.host[0];
     res[2] = nb;
     res[3] = nt;
     res[4] = total;

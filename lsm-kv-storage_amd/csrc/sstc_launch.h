@@ -106,6 +106,7 @@ hipError_t launch_segment(const uint64_t *Pw, uint64_t nrec, uint64_t threshold,
 struct Arena {
   void *base = nullptr;
   uint64_t cap = 0;
+  uint64_t *host = nullptr; // 64 pinned host words: the job's few device -> host reads
 };
 
 int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, const uint8_t *d_src,
