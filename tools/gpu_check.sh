@@ -3,7 +3,7 @@
 # (test failures, exit 1, do not stop the bench).
 cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 2
 mkdir -p gpurun_out
-timeout -k 10 900 python -m pytest tests -m gpu -q -rf > gpurun_out/pytest_gpu.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -v -rf --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
 rc=$?
 echo "pytest rc=$rc"; tail -30 gpurun_out/pytest_gpu.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
