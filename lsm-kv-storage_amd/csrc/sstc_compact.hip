@@ -18,6 +18,7 @@
 //      (table_builder.cc:101-211) written on the device.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <cstring>
 #include <initializer_list>
 #include <stdexcept>

@@ -689,6 +689,101 @@ __device__ __forceinline__ void lane_copy(uint8_t *dst, const uint8_t *src, uint
 // rewritten from the record: the compat reader may have changed it).
 constexpr uint32_t kEncSlotWaves = kEncWaves;
 
+// Four destination dwords of one aligned 16 B source chunk: source bytes
+// r0 + 4j .. r0 + 4j + 3 of (v, nxt) go to the LDS dword at y + 4j when that
+// dword lies inside [lo, hi) (the entry's image bytes).
+__device__ __forceinline__ void emit_chunk(uint8_t *img, u32x4 v, uint32_t nxt, uint32_t r0, int32_t y,
+                                           int32_t lo, int32_t hi) {
+  const uint32_t w[5] = {v.x, v.y, v.z, v.w, nxt};
+#pragma unroll
+  for (uint32_t j = 0; j < 4; j++) {
+    const int32_t yy = y + 4 * static_cast<int32_t>(j);
+    if (yy >= lo && yy + 4 <= hi)
+      *reinterpret_cast<uint32_t *>(img + yy) = __builtin_amdgcn_alignbyte(w[j + 1], w[j], r0);
+  }
+}
+
+// Compaction encode (records decoded from blocks held in key_src): every
+// surviving entry is already its own encoding in its input block, so the block
+// image is assembled by copying whole entries.  16 lanes per entry, each loads
+// one ALIGNED 16 B source chunk (one dwordx4 per lane instead of five dword
+// loads) and funnel-shifts it, with the first dword of its right neighbour's
+// chunk, into the dword-aligned LDS image; kCopyQ entry quads are loaded
+// before any is written so a lane has kCopyQ wide loads in flight.  Dwords
+// that straddle an entry's ends are left to the record pass that follows:
+// lane per record writes type + key length (the first 5 bytes), the txn (the
+// last 8; the compat reader may have changed it) and the offset entry.
+template <uint32_t kCopyQ>
+__device__ __forceinline__ void enc_copy_entries(const EncArgs &a, uint8_t *img, uint32_t pad, uint64_t f0,
+                                                 uint32_t n, uint64_t P0, uint32_t D) {
+  const uint32_t lane = lane_id();
+  const uint32_t g = lane & 15u, sub = lane >> 4;
+  for (uint32_t c0 = 0; c0 < n; c0 += kWave) {
+    const uint32_t nc = n - c0 < kWave ? n - c0 : kWave;
+    uint32_t my_o = 0, my_sz = 0, my_kl = 0, my_ty = 0;
+    uint64_t my_ko = 0, my_tx = 0;
+    if (lane < nc) {
+      const uint64_t r = f0 + c0 + lane;
+      const uint64_t pr = a.P[r];
+      my_o = static_cast<uint32_t>(pr - P0);
+      my_sz = static_cast<uint32_t>(a.P[r + 1] - pr);
+      my_ko = a.in.key_off[r];
+      my_tx = a.in.txn[r];
+      my_kl = a.in.key_len[r];
+      my_ty = a.in.type[r];
+    }
+    for (uint32_t p0 = 0; p0 < nc; p0 += 4 * kCopyQ) {
+      u32x4 v[kCopyQ];
+      uint32_t r0_[kCopyQ], nch_[kCopyQ];
+      int32_t y_[kCopyQ], lo_[kCopyQ], hi_[kCopyQ];
+      const uint8_t *A_[kCopyQ];
+#pragma unroll
+      for (uint32_t q = 0; q < kCopyQ; q++) {
+        const uint32_t i = p0 + 4 * q + sub;
+        const int sl = static_cast<int>(i & 63u);
+        const uint32_t o = __shfl(my_o, sl, kWave), sz = __shfl(my_sz, sl, kWave);
+        const uint32_t klo = __shfl(static_cast<uint32_t>(my_ko), sl, kWave);
+        const uint32_t khi = __shfl(static_cast<uint32_t>(my_ko >> 32), sl, kWave);
+        const uint8_t *sp = a.key_src + ((static_cast<uint64_t>(khi) << 32) | klo) - 5;
+        const uint32_t mis = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(sp) & 15u);
+        const uint8_t *A = sp - mis;
+        const uint32_t nch = i < nc ? (mis + sz + 15u) >> 4 : 0u;
+        const uint32_t ds = pad + o;
+        v[q] = g < nch ? *reinterpret_cast<const u32x4 *>(A + 16 * g) : u32x4{0u, 0u, 0u, 0u};
+        r0_[q] = (mis - ds) & 3u;
+        y_[q] = static_cast<int32_t>(ds) - static_cast<int32_t>(mis) + static_cast<int32_t>(r0_[q]);
+        lo_[q] = static_cast<int32_t>(ds);
+        hi_[q] = static_cast<int32_t>(ds + sz);
+        nch_[q] = nch;
+        A_[q] = A;
+      }
+#pragma unroll
+      for (uint32_t q = 0; q < kCopyQ; q++) {
+        const uint32_t nxt = __shfl_down(v[q].x, 1u, 16);
+        if (g < 15u && g < nch_[q]) emit_chunk(img, v[q], nxt, r0_[q], y_[q] + 16 * static_cast<int32_t>(g), lo_[q], hi_[q]);
+        // entries longer than 15 chunks (~230 B): further rounds of 15 chunks
+        for (uint32_t c = 15u + g; c - g < nch_[q]; c += 15u) {
+          const u32x4 w = c < nch_[q] ? *reinterpret_cast<const u32x4 *>(A_[q] + 16 * c) : u32x4{0u, 0u, 0u, 0u};
+          const uint32_t nx = __shfl_down(w.x, 1u, 16);
+          if (g < 15u && c < nch_[q]) emit_chunk(img, w, nx, r0_[q], y_[q] + 16 * static_cast<int32_t>(c), lo_[q], hi_[q]);
+        }
+      }
+    }
+    wave_lds_sync();
+    if (lane < nc) {
+      uint8_t *e = img + pad + my_o;
+      e[0] = static_cast<uint8_t>(my_ty);
+#pragma unroll
+      for (int j = 0; j < 4; j++) e[1 + j] = static_cast<uint8_t>(my_kl >> (8 * j));
+#pragma unroll
+      for (int j = 0; j < 8; j++) e[my_sz - 8 + j] = static_cast<uint8_t>(my_tx >> (8 * j));
+      lds_st_u64u(img, pad + D + 16 * (c0 + lane), my_o);
+      lds_st_u64u(img, pad + D + 16 * (c0 + lane) + 8, my_sz);
+    }
+  }
+}
+
+template <uint32_t kMode> // 0: lane per record, 1: whole-entry copy (compaction)
 __global__ __launch_bounds__(kEncWaves *kWave) void enc_lds_kernel(EncArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kEncSlotWaves * kEncSlot];
   const uint32_t wave = uniform(threadIdx.x / kWave);
@@ -711,91 +806,10 @@ __global__ __launch_bounds__(kEncWaves *kWave) void enc_lds_kernel(EncArgs a) {
   const uint32_t D = static_cast<uint32_t>(uniform64(a.P[f0 + n]) - P0);
   uint8_t *im = img + pad; // image byte 0 == block byte 0
 
-  if (a.entries_in_src) {
-    // Records in chunks of 64.  Lane per record: metadata, txn and offset
-    // entry.  Then 8 lanes per record copy the entry span (type .. value,
-    // contiguous in the source block) as 16 B pieces: lane g owns interior
-    // dwords [4g, 4g + 4) (+32t), dword-aligned in LDS and funnel-shifted from
-    // 5 source dwords; lane 0 of a group also the < 4 head / tail bytes.  Four
-    // record groups are unrolled so one wave has ~20 independent loads in
-    // flight per lane (the copy is latency-bound, not bandwidth-bound).
-    const uint32_t g = lane & 7u, sub = lane >> 3;
-    for (uint32_t c0 = 0; c0 < n; c0 += kWave) {
-      const uint32_t nc = n - c0 < kWave ? n - c0 : kWave;
-      uint32_t my_o = 0, my_sz = 0;
-      uint64_t my_ko = 0;
-      if (lane < nc) {
-        const uint64_t r = f0 + c0 + lane;
-        const uint64_t pr = a.P[r], pr1 = a.P[r + 1];
-        my_ko = a.in.key_off[r];
-        const uint64_t tx = a.in.txn[r];
-        my_o = static_cast<uint32_t>(pr - P0);
-        my_sz = static_cast<uint32_t>(pr1 - pr);
-        lds_st_u64u(img, pad + my_o + my_sz - 8, tx);
-        lds_st_u64u(img, pad + D + 16 * (c0 + lane), my_o);
-        lds_st_u64u(img, pad + D + 16 * (c0 + lane) + 8, my_sz);
-      }
-      for (uint32_t p0 = 0; p0 < nc; p0 += 32) {
-        constexpr uint32_t kQ = 4;
-        uint32_t x[kQ][5], hd[kQ], tl[kQ], o_[kQ], len_[kQ], head_[kQ], nw_[kQ], sh_[kQ];
-        const uint8_t *sp_[kQ];
-#pragma unroll
-        for (uint32_t q = 0; q < kQ; q++) {
-          const uint32_t i = p0 + 8 * q + sub; // record of this lane's group
-          const uint32_t o = __shfl(my_o, static_cast<int>(i & 63u), kWave);
-          const uint32_t sz = __shfl(my_sz, static_cast<int>(i & 63u), kWave);
-          const uint32_t klo = __shfl(static_cast<uint32_t>(my_ko), static_cast<int>(i & 63u), kWave);
-          const uint32_t khi = __shfl(static_cast<uint32_t>(my_ko >> 32), static_cast<int>(i & 63u), kWave);
-          const bool act = i < nc;
-          const uint32_t len = act ? sz - 8 : 0u;
-          const uint8_t *sp = a.key_src + ((static_cast<uint64_t>(khi) << 32) | klo) - 5;
-          uint32_t head = (4u - ((o + pad) & 3u)) & 3u;
-          head = head < len ? head : len;
-          const uint32_t nw = (len - head) >> 2;
-          uint32_t sh;
-          const uint32_t *w = align4_down(sp + head, sh);
-          const uint32_t k0 = 4 * g;
-          // a shifted dword also needs the next one (inside the entry: the txn
-          // follows the span); an idle group (no record) loads nothing
-          const uint32_t lim = act ? nw + (sh ? 1u : 0u) : 0u;
-#pragma unroll
-          for (uint32_t j = 0; j < 5; j++) x[q][j] = k0 + j < lim ? w[k0 + j] : 0u;
-          const uint32_t t0 = head + 4 * nw;
-          hd[q] = (g == 0 && head) ? g_u32u(sp) : 0u;
-          tl[q] = (g == 0 && t0 < len) ? g_u32u(sp + t0) : 0u; // < 4 bytes; the txn follows in the source
-          o_[q] = o;
-          len_[q] = len;
-          head_[q] = head;
-          nw_[q] = nw;
-          sh_[q] = sh;
-          sp_[q] = sp;
-        }
-#pragma unroll
-        for (uint32_t q = 0; q < kQ; q++) {
-          if (len_[q] == 0) continue;
-          uint8_t *d = im + o_[q];
-          uint32_t *d32 = reinterpret_cast<uint32_t *>(d + head_[q]);
-          const uint32_t k0 = 4 * g, sh = sh_[q], nw = nw_[q];
-#pragma unroll
-          for (uint32_t j = 0; j < 4; j++)
-            if (k0 + j < nw) d32[k0 + j] = __builtin_amdgcn_alignbyte(x[q][j + 1], x[q][j], sh);
-          // spans longer than 128 B: the rest, 32 dwords per round
-          uint32_t sh2;
-          const uint32_t *w = align4_down(sp_[q] + head_[q], sh2);
-          for (uint32_t k = k0 + 32; k < nw; k += 32) {
-#pragma unroll
-            for (uint32_t j = 0; j < 4; j++)
-              if (k + j < nw) d32[k + j] = __builtin_amdgcn_alignbyte(sh ? w[k + j + 1] : 0u, w[k + j], sh);
-          }
-          if (g == 0) {
-            const uint32_t t0 = head_[q] + 4 * nw;
-            for (uint32_t j = 0; j < head_[q]; j++) d[j] = static_cast<uint8_t>(hd[q] >> (8 * j));
-            for (uint32_t j = t0; j < len_[q]; j++) d[j] = static_cast<uint8_t>(tl[q] >> (8 * (j - t0)));
-          }
-        }
-      }
-    }
-  } else for (uint32_t i = lane; i < n; i += kWave) {
+  if constexpr (kMode == 1) {
+    enc_copy_entries<4>(a, img, pad, f0, n, P0, D);
+  } else {
+  for (uint32_t i = lane; i < n; i += kWave) {
     const uint64_t r = f0 + i;
     const uint32_t o = static_cast<uint32_t>(a.P[r] - P0);
     const uint32_t sz = static_cast<uint32_t>(a.P[r + 1] - a.P[r]);
@@ -814,6 +828,7 @@ __global__ __launch_bounds__(kEncWaves *kWave) void enc_lds_kernel(EncArgs a) {
     for (int j = 0; j < 8; j++) im[o + t + j] = static_cast<uint8_t>(tx >> (8 * j));
     lds_st_u64u(im, D + 16 * i, o);
     lds_st_u64u(im, D + 16 * i + 8, sz);
+  }
   }
   if (lane == 0) {
     lds_st_u64u(im, D + 16 * n, n);
@@ -1115,7 +1130,9 @@ hipError_t launch_enc_blk_len(const uint64_t *P, const uint64_t *blk_first, uint
 
 hipError_t launch_enc_emit(const EncArgs &a, hipStream_t s) {
   if (!a.nblocks) return hipSuccess;
-  enc_lds_kernel<<<grid_for(a.nblocks, kEncWaves), kEncWaves * kWave, 0, s>>>(a);
+  const uint32_t g = grid_for(a.nblocks, kEncWaves);
+  if (!a.entries_in_src) enc_lds_kernel<0><<<g, kEncWaves * kWave, 0, s>>>(a);
+  else enc_lds_kernel<1><<<g, kEncWaves * kWave, 0, s>>>(a);
   enc_emit_kernel<<<static_cast<uint32_t>(a.nblocks < 2048 ? a.nblocks : 2048), kEncThreads, 0, s>>>(a);
   return hipGetLastError();
 }
