@@ -3,10 +3,10 @@
 //
 //   decode every input block (sstc decode kernels, COMPAT txn = what the
 //   reference iterator reads)
-//   -> merge the per-table sorted runs: log2(k) rounds of stable merge-path
-//      merges on a 16 B big-endian key prefix + length + txn (full key bytes
-//      compared only when two prefixes tie and both keys are longer than 16 B);
-//      order = key ascending, txn descending, then input table order
+//   -> merge the per-table sorted runs: ceil(log8 k) k-way merge passes on a
+//      16 B big-endian key prefix + length + txn (full key bytes compared only
+//      when two prefixes tie and both keys are longer than 16 B); order = key
+//      ascending, txn descending, then input table order
 //   -> ShouldKeepEntry as flags (group head = key differs from the previous
 //      merged record, group head txn by a scatter of group heads)
 //   -> stream compaction of the survivors
@@ -20,6 +20,7 @@
 
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
 #include <initializer_list>
 #include <stdexcept>
 #include <string>
@@ -80,70 +81,196 @@ __global__ void ck_check_sorted_kernel(const SK *s, const uint64_t *run_start, u
   if (sk_less(s[r], s[r - 1], kv)) atomicAdd(bad, 1ull);
 }
 
-// Pairwise stable merge of sorted runs, tiled through LDS (merge path): one
-// 256-thread workgroup per kMergeTile outputs of one run pair.  Two threads
-// co-rank the tile's ends against HBM; the tile's slices of A and B are loaded
-// coalesced into LDS; every thread co-ranks its kMergeIt outputs inside LDS
-// and merges them.  Ties go to A (the earlier input table): stable.
-constexpr uint32_t kMergeIt = 4;
-constexpr uint32_t kMergeThreads = 256;
-constexpr uint32_t kMergeTile = kMergeIt * kMergeThreads;
+// k-way merge pass: every group of up to kKWay consecutive sorted runs is
+// merged in ONE pass (ceil(log8 k) passes instead of log2 k pairwise rounds).
+//  1. splitters: every S-th record of every run (S = kKWin / runs).  A wave
+//     lane per (splitter, run) binary-searches the splitter's co-rank in that
+//     run (records of the run that precede it in merge order); 8 lanes reduce
+//     them to the splitter's rank among splitters (sum of ceil(c / S)) and
+//     among records (sum of c), and write the co-rank row in sorted order.
+//     Between two consecutive splitter rows a run contributes <= S records.
+//  2. merge: workgroup w takes the records between the first splitter rows
+//     at or after output ranks w * kKWin and (w + 1) * kKWin (< 2 kKWin records),
+//     stages the <= kKWay sub-runs in LDS, and every record's output rank is
+//     its position in its sub-run + its co-ranks in the other sub-runs (LDS
+//     binary searches).  Order = key asc, txn desc, then lower run first, i.e.
+//     the stable pairwise merge of MergeIterator (merge_iterator.cc:34-46).
+constexpr uint32_t kKWay = 8;
+constexpr uint32_t kKWin = 512;
+constexpr uint32_t kKRegion = 2 * kKWin;
+constexpr uint32_t kKThreads = 512;
 
-struct MergePair {
-  uint64_t a0, a1, b1; // A = [a0, a1), B = [a1, b1)
-  uint64_t tile0;      // first tile of this pair
+struct KGroup {
+  uint64_t start[kKWay + 1]; // absolute run starts; start[nruns] = group end
+  uint32_t sbase[kKWay + 1]; // prefix of the runs' splitter counts
+  uint32_t nruns, stride;    // runs, splitter stride S
+  uint32_t base;             // first splitter id == first row (nsamp + 1 of each, the last a sentinel)
+  uint32_t wg0;              // first merge workgroup
 };
 
-__global__ __launch_bounds__(kMergeThreads) void ck_merge_tile_kernel(const SK *in, SK *out, const MergePair *pairs,
-                                                                      uint32_t npairs, KeyView kv) {
-  __shared__ SK tile[kMergeTile];
-  __shared__ uint64_t corank[2];
-  const uint64_t g = blockIdx.x;
-  uint32_t lo = 0, hi = npairs; // pair of this tile: last tile0 <= g
+// y precedes x in merge order, y from run ry, x from run rx != ry
+__device__ __forceinline__ bool kw_before(const SK &y, uint32_t ry, const SK &x, uint32_t rx, const KeyView &kv) {
+  return ry < rx ? !sk_less(x, y, kv) : sk_less(y, x, kv);
+}
+
+template <class T>
+__device__ __forceinline__ uint32_t find_group(const KGroup *g, uint32_t ng, uint32_t v, T field) {
+  uint32_t lo = 0, hi = ng; // last group with field <= v
   while (lo + 1 < hi) {
     const uint32_t mid = (lo + hi) >> 1;
-    if (pairs[mid].tile0 <= g) lo = mid;
+    if (field(g[mid]) <= v) lo = mid;
     else hi = mid;
   }
-  const MergePair P = pairs[lo];
-  const uint64_t na_all = P.a1 - P.a0, nb_all = P.b1 - P.a1;
-  const uint64_t seg = na_all + nb_all;
-  const uint64_t k0 = (g - P.tile0) * kMergeTile;
-  const uint64_t k1 = k0 + kMergeTile < seg ? k0 + kMergeTile : seg;
-  if (threadIdx.x < 2) {
-    const uint64_t kk = threadIdx.x ? k1 : k0;
-    uint64_t l = kk > nb_all ? kk - nb_all : 0, h = kk < na_all ? kk : na_all;
-    while (l < h) { // smallest i with B[kk-i-1] < A[i]
-      const uint64_t mid = (l + h) >> 1;
-      if (sk_less(in[P.a1 + (kk - mid - 1)], in[P.a0 + mid], kv)) h = mid;
-      else l = mid + 1;
+  return lo;
+}
+
+__global__ __launch_bounds__(256) void ck_kw_split_kernel(const SK *in, const KGroup *groups, uint32_t ngroups,
+                                                          uint32_t nids, KeyView kv, uint32_t *C, uint64_t *G) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t u = t >> 3, r = t & 7u;
+  if (u >= nids) return; // whole 8-lane groups leave together
+  const KGroup &gr = groups[find_group(groups, ngroups, u, [](const KGroup &x) { return x.base; })];
+  const uint32_t local = u - gr.base, nsamp = gr.sbase[gr.nruns], S = gr.stride;
+  uint64_t c = 0;
+  if (r < gr.nruns) {
+    const uint64_t rs = gr.start[r], len = gr.start[r + 1] - rs;
+    if (local == nsamp) {
+      c = len; // sentinel row
+    } else {
+      uint32_t q = 0;
+      while (gr.sbase[q + 1] <= local) q++;
+      const uint64_t p = static_cast<uint64_t>(local - gr.sbase[q]) * S;
+      if (r == q) {
+        c = p;
+      } else {
+        const SK x = in[gr.start[q] + p];
+        uint64_t lo = 0, hi = len;
+        while (lo < hi) {
+          const uint64_t mid = (lo + hi) >> 1;
+          if (kw_before(in[rs + mid], r, x, q, kv)) lo = mid + 1;
+          else hi = mid;
+        }
+        c = lo;
+      }
     }
-    corank[threadIdx.x] = l;
+  }
+  uint64_t sr = (c + S - 1) / S, sc = c;
+#pragma unroll
+  for (uint32_t d = 1; d < 8; d <<= 1) {
+    sr += __shfl_xor(sr, d, 8);
+    sc += __shfl_xor(sc, d, 8);
+  }
+  const uint64_t row = gr.base + sr;
+  C[row * kKWay + r] = static_cast<uint32_t>(c);
+  if (r == 0) G[row] = sc;
+}
+
+// LDS slot of staged record i: rows of 8 records (256 B = all 64 banks); the
+// column is XOR-swizzled by the row so that lanes ranking consecutive 8-record
+// runs (one row each) do not all hit the same banks.
+__device__ __forceinline__ uint32_t kw_slot(uint32_t i) { return i ^ ((i >> 3) & 7u); }
+
+// kw_before on a staged record: the 16 B prefix (one 16 B LDS read) decides
+// unless it ties
+__device__ __forceinline__ bool kw_before_lds(const SK *tile, uint32_t i, uint32_t ry, const SK &x, uint32_t rx,
+                                              const KeyView &kv) {
+  const SK *y = tile + kw_slot(i);
+  const uint64_t p0 = y->p0, p1 = y->p1;
+  if (p0 != x.p0) return p0 < x.p0;
+  if (p1 != x.p1) return p1 < x.p1;
+  return kw_before(*y, ry, x, rx, kv);
+}
+
+// first splitter row of every merge window: window w starts at the first row
+// whose record rank G is >= w * kKWin (rows are sorted, G increasing)
+__global__ void ck_kw_bounds_kernel(const KGroup *groups, uint32_t ngroups, uint32_t nids, const uint64_t *G,
+                                    uint32_t *J) {
+  const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= nids) return;
+  const KGroup &gr = groups[find_group(groups, ngroups, u, [](const KGroup &x) { return x.base; })];
+  const uint32_t j = u - gr.base, nsamp = gr.sbase[gr.nruns];
+  const uint64_t N = gr.start[gr.nruns] - gr.start[0];
+  const uint32_t nw = static_cast<uint32_t>((N + kKWin - 1) / kKWin);
+  const uint64_t g = G[u];
+  const uint64_t gp = j ? G[u - 1] : 0;
+  // windows w with gp < w*kKWin <= g start at row j (row 0 also takes w = 0);
+  // the sentinel row (G = N) also takes every window past the last record
+  uint64_t w0 = j ? gp / kKWin + 1 : 0;
+  uint64_t w1 = j == nsamp ? nw : g / kKWin; // inclusive
+  for (uint64_t w = w0; w <= w1 && w <= nw; w++) J[gr.wg0 + gr.base + w] = j;
+}
+
+__global__ __launch_bounds__(kKThreads) void ck_kw_merge_kernel(const SK *in, SK *out, const KGroup *groups,
+                                                               uint32_t ngroups, const uint32_t *C,
+                                                               const uint64_t *G, const uint32_t *J, KeyView kv) {
+  __shared__ SK tile[kKRegion];
+  __shared__ uint32_t s_j[2], s_off[kKWay + 1], s_lo[kKWay];
+  const KGroup &gr = groups[find_group(groups, ngroups, blockIdx.x, [](const KGroup &x) { return x.wg0; })];
+  const uint32_t wl = blockIdx.x - gr.wg0, k = gr.nruns;
+  const uint64_t *Gg = G + gr.base;
+  if (threadIdx.x < 2) s_j[threadIdx.x] = J[gr.wg0 + gr.base + wl + threadIdx.x];
+  __syncthreads();
+  const uint32_t j0 = s_j[0], j1 = s_j[1];
+  if (j0 == j1) return;
+  if (threadIdx.x < k) {
+    const uint32_t lo = C[static_cast<uint64_t>(gr.base + j0) * kKWay + threadIdx.x];
+    s_lo[threadIdx.x] = lo;
+    s_off[threadIdx.x + 1] = C[static_cast<uint64_t>(gr.base + j1) * kKWay + threadIdx.x] - lo;
   }
   __syncthreads();
-  const uint64_t ia0 = corank[0], ia1 = corank[1];
-  const uint32_t na = static_cast<uint32_t>(ia1 - ia0);
-  const uint32_t nt = static_cast<uint32_t>(k1 - k0);
-  const uint32_t nb = nt - na;
-  const uint64_t ib0 = k0 - ia0;
-  for (uint32_t t = threadIdx.x; t < nt; t += kMergeThreads)
-    tile[t] = t < na ? in[P.a0 + ia0 + t] : in[P.a1 + ib0 + (t - na)];
-  __syncthreads();
-  const SK *A = tile, *B = tile + na;
-  const uint32_t k = threadIdx.x * kMergeIt;
-  if (k >= nt) return;
-  uint32_t l = k > nb ? k - nb : 0, h = k < na ? k : na;
-  while (l < h) {
-    const uint32_t mid = (l + h) >> 1;
-    if (sk_less(B[k - mid - 1], A[mid], kv)) h = mid;
-    else l = mid + 1;
+  if (threadIdx.x == 0) {
+    s_off[0] = 0;
+    for (uint32_t q = 0; q < k; q++) s_off[q + 1] += s_off[q];
   }
-  uint32_t ia = l, ib = k - l;
-  const uint32_t stop = k + kMergeIt < nt ? k + kMergeIt : nt;
-  SK *o = out + P.a0 + k0;
-  for (uint32_t q = k; q < stop; q++) {
-    const bool take_a = ia < na && (ib >= nb || !sk_less(B[ib], A[ia], kv));
-    o[q] = take_a ? A[ia++] : B[ib++];
+  __syncthreads();
+  const uint32_t total = s_off[k];
+  for (uint32_t i = threadIdx.x; i < total; i += kKThreads) {
+    uint32_t q = 0;
+    while (s_off[q + 1] <= i) q++;
+    tile[kw_slot(i)] = in[gr.start[q] + s_lo[q] + (i - s_off[q])];
+  }
+  __syncthreads();
+  // every thread ranks kKPer consecutive staged records: along a sub-run the
+  // co-ranks in the other sub-runs are nondecreasing, so after one binary
+  // search per sub-run the cursors gallop forward (interleaved runs: ~2 probes)
+  SK *o = out + gr.start[0] + Gg[j0];
+  constexpr uint32_t kKPer = kKRegion / kKThreads;
+  uint32_t cur[kKWay];
+  uint32_t qprev = kKWay;
+  for (uint32_t e = 0; e < kKPer; e++) {
+    const uint32_t i = threadIdx.x * kKPer + e;
+    if (i >= total) break;
+    uint32_t q = 0;
+    while (s_off[q + 1] <= i) q++;
+    const SK x = tile[kw_slot(i)];
+    uint32_t rank = i - s_off[q];
+#pragma unroll
+    for (uint32_t r = 0; r < kKWay; r++) {
+      if (r >= k || r == q) continue;
+      const uint32_t b1 = s_off[r + 1];
+      uint32_t lo = q == qprev ? cur[r] : s_off[r], hi = b1;
+      if (q == qprev) {
+        uint32_t step = 1;
+        for (uint32_t p = lo; p < b1;) {
+          if (!kw_before_lds(tile, p, r, x, q, kv)) {
+            hi = p;
+            break;
+          }
+          lo = p + 1;
+          p = lo + step - 1;
+          step <<= 1;
+        }
+      }
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (kw_before_lds(tile, mid, r, x, q, kv)) lo = mid + 1;
+        else hi = mid;
+      }
+      cur[r] = lo;
+      rank += lo - s_off[r];
+    }
+    qprev = q;
+    o[rank] = x;
   }
 }
 
@@ -561,42 +688,56 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     unsigned long long *bad = reinterpret_cast<unsigned long long *>(pool.get<uint64_t>(1));
     CK(hipMemsetAsync(bad, 0, 8, s));
     ck_check_sorted_kernel<<<grid(n), 256, 0, s>>>(A, rb, nruns, n, kv, bad);
-    std::vector<MergePair> flat; // uploaded asynchronously: lives until the next sync
+    // k-way merge passes; run boundaries of every pass are known on the host,
+    // so all group descriptors go up in one upload (lives until the next sync)
+    std::vector<KGroup> kg;
+    std::vector<uint32_t> pass_groups, pass_ids, pass_wgs;
     {
-      // run boundaries of every round are known on the host (input table
-      // sizes): one descriptor upload for all rounds
-      std::vector<std::vector<MergePair>> rounds;
       std::vector<uint64_t> cur = run_start;
       while (cur.size() > 2) {
-        std::vector<MergePair> ps;
         std::vector<uint64_t> next;
-        uint64_t tiles = 0;
-        for (size_t j = 0; 2 * j + 1 < cur.size(); j++) {
-          const uint64_t a0 = cur[2 * j];
-          const uint64_t a1 = 2 * j + 1 < cur.size() ? cur[2 * j + 1] : a0;
-          const uint64_t b1 = 2 * j + 2 < cur.size() ? cur[2 * j + 2] : a1;
-          ps.push_back(MergePair{a0, a1, b1, tiles});
-          tiles += (b1 - a0 + kMergeTile - 1) / kMergeTile;
-          next.push_back(a0);
+        uint32_t ids = 0, wgs = 0, ng = 0;
+        for (size_t r0 = 0; r0 + 1 < cur.size(); r0 += kKWay) {
+          const uint32_t k = static_cast<uint32_t>(std::min<size_t>(kKWay, cur.size() - 1 - r0));
+          KGroup g{};
+          g.nruns = k;
+          g.stride = kKWin / k;
+          g.base = ids;
+          g.wg0 = wgs;
+          g.sbase[0] = 0;
+          for (uint32_t q = 0; q <= k; q++) g.start[q] = cur[r0 + q];
+          for (uint32_t q = 0; q < k; q++)
+            g.sbase[q + 1] = g.sbase[q] + static_cast<uint32_t>((g.start[q + 1] - g.start[q] + g.stride - 1) / g.stride);
+          ids += g.sbase[k] + 1;
+          wgs += static_cast<uint32_t>((g.start[k] - g.start[0] + kKWin - 1) / kKWin);
+          kg.push_back(g);
+          ng++;
+          next.push_back(cur[r0]);
         }
         next.push_back(cur.back());
-        ps.push_back(MergePair{0, 0, 0, tiles}); // sentinel: total tiles
-        rounds.push_back(std::move(ps));
+        pass_groups.push_back(ng);
+        pass_ids.push_back(ids);
+        pass_wgs.push_back(wgs);
         cur = std::move(next);
       }
-      size_t total = 0;
-      for (auto &r : rounds) total += r.size();
-      for (auto &r : rounds) flat.insert(flat.end(), r.begin(), r.end());
-      MergePair *d_pairs = pool.get<MergePair>(total ? total : 1);
-      if (total) CK(hipMemcpyAsync(d_pairs, flat.data(), total * sizeof(MergePair), hipMemcpyHostToDevice, s));
-      size_t at = 0;
-      for (auto &r : rounds) {
-        const uint32_t np = static_cast<uint32_t>(r.size() - 1);
-        const uint64_t tiles = r.back().tile0;
-        if (tiles)
-          ck_merge_tile_kernel<<<static_cast<uint32_t>(tiles), kMergeThreads, 0, s>>>(A, B, d_pairs + at, np, kv);
-        std::swap(A, B);
-        at += r.size();
+      if (!kg.empty()) {
+        KGroup *d_kg = pool.get<KGroup>(kg.size());
+        CK(hipMemcpyAsync(d_kg, kg.data(), kg.size() * sizeof(KGroup), hipMemcpyHostToDevice, s));
+        const uint32_t max_ids = *std::max_element(pass_ids.begin(), pass_ids.end());
+        uint32_t *Cm = pool.get<uint32_t>(static_cast<uint64_t>(max_ids) * kKWay);
+        uint64_t *Gm = pool.get<uint64_t>(max_ids);
+        uint32_t max_j = 0;
+        for (size_t p = 0; p < pass_groups.size(); p++) max_j = std::max(max_j, pass_ids[p] + pass_wgs[p] + pass_groups[p]);
+        uint32_t *Jm = pool.get<uint32_t>(max_j);
+        size_t at = 0;
+        for (size_t p = 0; p < pass_groups.size(); p++) {
+          const uint32_t ng = pass_groups[p];
+          ck_kw_split_kernel<<<grid(static_cast<uint64_t>(pass_ids[p]) * 8), 256, 0, s>>>(A, d_kg + at, ng, pass_ids[p], kv, Cm, Gm);
+          ck_kw_bounds_kernel<<<grid(pass_ids[p]), 256, 0, s>>>(d_kg + at, ng, pass_ids[p], Gm, Jm);
+          if (pass_wgs[p]) ck_kw_merge_kernel<<<pass_wgs[p], kKThreads, 0, s>>>(A, B, d_kg + at, ng, Cm, Gm, Jm, kv);
+          std::swap(A, B);
+          at += ng;
+        }
       }
     }
     // 3. keep / drop

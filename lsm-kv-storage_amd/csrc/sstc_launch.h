@@ -45,7 +45,6 @@ struct DecArgs {
   unsigned long long *err_count;
   SortKey *sk = nullptr; // optional merge keys (compaction)
   uint32_t xcd = 0;
-  uint32_t variant = 0; // A/B switch (0 = current encode copy)
 };
 
 struct EncArgs {
