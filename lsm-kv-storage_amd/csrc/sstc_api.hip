@@ -85,14 +85,6 @@ int ensure_records(sstc_ctx *c, uint64_t nr) {
   return ensure_scan(c, nr + 1);
 }
 
-uint32_t bit_length(uint64_t v) {
-  uint32_t b = 0;
-  while (v) {
-    b++;
-    v >>= 1;
-  }
-  return b;
-}
 
 bool bad_records(const sstc_records &r) {
   return !r.type || !r.key_len || !r.val_len || !r.txn || !r.key_off || !r.val_off;
@@ -217,12 +209,11 @@ int sstc_segment_records(sstc_ctx *c, const uint32_t *d_key_len, const uint32_t 
   if (nrec >= 0xFFFFFFFFull) return fail(SSTC_E_INVALID_ARG, "too many records for one call");
   if (int r = bind_device(c)) return r;
   if (int r = ensure_records(c, nrec)) return r;
-  const uint32_t levels = bit_length(nrec) ? bit_length(nrec) : 1;
-  if (int r = grow(c, c->jump, c->cap_jump, static_cast<uint64_t>(levels) * (nrec + 1), "jump tables")) return r;
+  if (int r = grow(c, c->jump, c->cap_jump, sstc::segment_workspace_u32(nrec), "segmentation workspace")) return r;
   // weights = entry_size + 16 (block_builder.cc:33), Pw = exclusive scan
   SSTC_HIP(sstc::launch_enc_sizes(d_key_len, d_val_len, nrec, 16, c->sizes, c->stream), "weights");
   SSTC_HIP(sstc::launch_scan(c->sizes, nrec, 0, c->P, c->scan_ws, c->stream), "scan");
-  SSTC_HIP(sstc::launch_segment(c->P, nrec, block_threshold, c->jump, levels, d_nblocks, d_blk_first, c->stream),
+  SSTC_HIP(sstc::launch_segment(c->P, nrec, block_threshold, c->jump, d_nblocks, d_blk_first, c->stream),
            "segment kernels");
   return SSTC_OK;
 }

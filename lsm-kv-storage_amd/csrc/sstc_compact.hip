@@ -582,35 +582,52 @@ struct Pool {
     if (e_ != hipSuccess) throw std::runtime_error(std::string(#x) + ": " + hipGetErrorString(e_));           \
   } while (0)
 
-uint32_t bitlen(uint64_t v) {
-  uint32_t b = 0;
-  while (v) {
-    b++;
-    v >>= 1;
-  }
-  return b ? b : 1;
-}
 
 
 // greedy segmentation of [0, m) by weights whose prefix sums are
-// Pw[i] + add * i (>= threshold closes), optional clamp.  chain_bound: an
-// upper bound of the number of segments (host-known, so no sync); the count
-// lands in *dn on the device.
+// Pw[i] + add * i (>= threshold closes), optional clamp; the count lands in
+// *dn on the device.
 void segment(Pool &pool, const uint64_t *Pw, uint64_t add, uint64_t m, uint64_t threshold, const uint32_t *clamp,
-             uint64_t chain_bound, uint64_t *first, uint64_t *dn, hipStream_t s) {
-  const uint32_t levels = bitlen(chain_bound < m ? chain_bound : m);
-  uint32_t *J = pool.get<uint32_t>(static_cast<uint64_t>(levels) * (m + 1));
-  CK(launch_segment(Pw, m, threshold, J, levels, dn, first, s, clamp, add));
+             uint64_t *first, uint64_t *dn, hipStream_t s, bool long_segments) {
+  uint32_t *J = pool.get<uint32_t>(segment_workspace_u32(m));
+  CK(launch_segment(Pw, m, threshold, J, dn, first, s, clamp, add, long_segments));
 }
 
-// device -> pinned host words, one sync
-void fetch(Arena &arena, hipStream_t s, std::initializer_list<const uint64_t *> src) {
-  if (!arena.host && hipHostMalloc(reinterpret_cast<void **>(&arena.host), 64 * sizeof(uint64_t)) != hipSuccess) {
+struct Words {
+  const uint64_t *p[8];
+  uint32_t n;
+};
+
+__global__ void ck_pack_kernel(Words w, uint64_t *out) {
+  if (threadIdx.x < w.n) out[threadIdx.x] = *w.p[threadIdx.x];
+}
+
+__global__ void ck_gather_words_kernel(const uint64_t *src, const uint64_t *idx, uint64_t n, uint64_t *out) {
+  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = src[idx[i]];
+}
+
+void ensure_host(Arena &arena, uint64_t words) {
+  if (arena.host && arena.host_cap >= words) return;
+  if (arena.host) (void)hipHostFree(arena.host);
+  arena.host = nullptr;
+  arena.host_cap = 0;
+  const uint64_t cap = words < 64 ? 64 : words;
+  if (hipHostMalloc(reinterpret_cast<void **>(&arena.host), cap * sizeof(uint64_t)) != hipSuccess) {
     arena.host = nullptr;
     throw std::runtime_error("pinned host words");
   }
-  int i = 0;
-  for (const uint64_t *p : src) CK(hipMemcpyAsync(arena.host + i++, p, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+  arena.host_cap = cap;
+}
+
+// device words -> pinned host words: one pack kernel, one copy, one sync
+void fetch(Arena &arena, Pool &pool, hipStream_t s, std::initializer_list<const uint64_t *> src) {
+  ensure_host(arena, 64);
+  Words w{};
+  for (const uint64_t *p : src) w.p[w.n++] = p;
+  uint64_t *stage = pool.get<uint64_t>(8);
+  ck_pack_kernel<<<1, 64, 0, s>>>(w, stage);
+  CK(hipMemcpyAsync(arena.host, stage, w.n * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
   CK(hipStreamSynchronize(s));
 }
 
@@ -631,20 +648,20 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     // (5) completion.  Everything else stays on the stream.
     // 1. decode every block
     uint64_t *rb_all = pool.get<uint64_t>(nblocks + 1);
-    uint64_t *inb = pool.get<uint64_t>(nblocks + 1);
     uint64_t *ws = pool.get<uint64_t>(nws);
     uint64_t *errs = pool.get<uint64_t>(2);
+    uint64_t *d_tfb = pool.get<uint64_t>(ntables + 1), *d_rs = pool.get<uint64_t>(ntables + 1);
     CK(launch_count(d_src, d_blk_off, d_blk_len, nblocks, rb_all, s));
     CK(launch_scan(rb_all, nblocks, 0, rb_all, ws, s));
-    CK(launch_scan(d_blk_len, nblocks, 0, inb, ws, s)); // input bytes: bounds the split chains
     CK(hipMemcpyAsync(errs, err_count, 8, hipMemcpyDeviceToDevice, s));
-    std::vector<uint64_t> h_rb(nblocks + 1);
-    CK(hipMemcpyAsync(h_rb.data(), rb_all, (nblocks + 1) * 8, hipMemcpyDeviceToHost, s));
-    fetch(arena, s, {inb + nblocks});
-    const uint64_t in_bytes = arena.host[0];
-    const uint64_t n = h_rb[nblocks];
-    std::vector<uint64_t> run_start;
-    for (uint32_t t = 0; t <= ntables; t++) run_start.push_back(h_rb[h_tfb[t]]);
+    // record index of every input table's first record (its run start)
+    CK(hipMemcpyAsync(d_tfb, h_tfb, (ntables + 1) * 8, hipMemcpyHostToDevice, s));
+    ck_gather_words_kernel<<<grid(ntables + 1), 256, 0, s>>>(rb_all, d_tfb, ntables + 1, d_rs);
+    ensure_host(arena, ntables + 1);
+    CK(hipMemcpyAsync(arena.host, d_rs, (ntables + 1) * 8, hipMemcpyDeviceToHost, s));
+    CK(hipStreamSynchronize(s));
+    std::vector<uint64_t> run_start(arena.host, arena.host + ntables + 1);
+    const uint64_t n = run_start[ntables];
     res[0] = n;
     if (n >= 0xFFFFFFFFull) {
       err = "too many records";
@@ -660,7 +677,7 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
                sstc_records{R.type, R.kl, R.vl, R.tx, R.ko, R.vo}, txn_mode, status, err_count, A};
     CK(launch_decode(da, s));
     if (n == 0) { // DoCompactJob still finishes its first (empty) output table
-      fetch(arena, s, {reinterpret_cast<const uint64_t *>(err_count), errs});
+      fetch(arena, pool, s, {reinterpret_cast<const uint64_t *>(err_count), errs});
       if (arena.host[0] != arena.host[1]) {
         err = "an input block failed to decode";
         return SSTC_E_INVALID_ARG;
@@ -749,7 +766,7 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     // G[i] (exclusive) + head[i] - 1 = group id; for a non-head i the group id is G[i] - 1
     ck_keep_kernel<<<grid(n), 256, 0, s>>>(A, head, G, hp, R.type, n, base_level, keep);
     CK(launch_scan(keep, n, 0, K, ws2, s));
-    fetch(arena, s, {K + n, reinterpret_cast<const uint64_t *>(bad), reinterpret_cast<const uint64_t *>(err_count),
+    fetch(arena, pool, s, {K + n, reinterpret_cast<const uint64_t *>(bad), reinterpret_cast<const uint64_t *>(err_count),
                      errs});
     if (arena.host[2] != arena.host[3]) {
       err = "an input block failed to decode";
@@ -774,13 +791,12 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     CK(launch_scan(dw, m, 0, Pd, ws2, s));
     CK(launch_scan(ew, m, 0, Pe, ws2, s));
     uint64_t *tf = pool.get<uint64_t>(m + 1), *dn = pool.get<uint64_t>(2);
-    const uint64_t nt_bound = in_bytes / table_limit + 1;
-    segment(pool, Pd, 0, m, table_limit, nullptr, nt_bound, tf, dn, s);
+    segment(pool, Pd, 0, m, table_limit, nullptr, tf, dn, s, true);
     uint32_t *clamp = pool.get<uint32_t>(m + 1);
     ck_table_end_kernel<<<grid(m + 1), 256, 0, s>>>(tf, dn, m, clamp);
     uint64_t *bf = pool.get<uint64_t>(m + 1);
-    segment(pool, Pe, 16, m, block_threshold, clamp, in_bytes / block_threshold + nt_bound + 1, bf, dn + 1, s);
-    fetch(arena, s, {dn, dn + 1});
+    segment(pool, Pe, 16, m, block_threshold, clamp, bf, dn + 1, s, false);
+    fetch(arena, pool, s, {dn, dn + 1});
     const uint64_t nt = arena.host[0], nb = arena.host[1];
     if (nt > max_tables) {
       err = "more output tables than max_tables";
@@ -796,7 +812,7 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     uint64_t *tbf = pool.get<uint64_t>(nt + 1), *tdata = pool.get<uint64_t>(nt), *tmeta = pool.get<uint64_t>(nt);
     ck_table_info_kernel<<<grid(nt + 1), 256, 0, s>>>(tf, nt, bf, nb, BL, MS, tbf, tdata, tmeta, d_table_len);
     CK(launch_scan(d_table_len, nt, 0, d_table_off, ws2, s)); // d_table_off needs nt + 1 elements
-    fetch(arena, s, {d_table_off + nt});
+    fetch(arena, pool, s, {d_table_off + nt});
     const uint64_t total = arena.host[0];
     res[2] = nb;
     res[3] = nt;

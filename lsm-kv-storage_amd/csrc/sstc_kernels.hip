@@ -839,40 +839,48 @@ __global__ __launch_bounds__(kEncWaves *kWave) void enc_lds_kernel(EncArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// Greedy segmentation by radix-8 pointer jumping.
-// J_0[i] = one past the last record of a block that starts at record i (the
-// chain from 0 visits the block starts); level k holds J_0^(8^k), computed as
-// J_k = J_{k-1}^8.  A chain of h blocks needs ceil(log8(h + 1)) levels instead
-// of log2 squarings: each level is one bandwidth-bound pass over the records,
-// so this is ~3x fewer passes.  The weights' prefix sums are Pw[i] + add * i
-// (add = the per-record offset entry for block weights, so the entry-size scan
-// is reused).
+// Greedy segmentation (TableBuilder::AddEntry's flush rule, table_builder.cc:
+// 57-59, and DoCompactJob's output split, compact.cc:290).
+// J0[i] = one past the last record of a segment that starts at record i: the
+// first e >= i with W(e + 1) >= W(i) + threshold, plus one, clamped to the end
+// of i's output table; W(x) = Pw[x] + add * x.  The segments are the chain
+// 0 -> J0[0] -> ...; J0 is nondecreasing.
+//
+// Many short segments (blocks): tiles of kChTile records.
+//  A seg_walk_kernel: J0 of the tile by galloping in an LDS copy of W; a
+//    segment that enters tile k starts in its entry window [c0, J0[c0 - 1]]
+//    (J0 is monotone), and every window position walks the chain inside the
+//    tile: entry -> (exit record, segments started in the tile).
+//  B the window positions of all tiles are the nodes of a much smaller chain
+//    (one node per tile it visits): node -> node of its exit, radix-8 pointer
+//    jumping over nodes (log8 tiles levels) with segment counts.
+//  C every visited tile learns its entry and the segments before it, then
+//    seg_emit_kernel re-walks its part of the chain and writes the starts.
+// Few long segments (output tables): seg_hops_kernel, one workgroup hopping
+// along the chain with a 4096-ary search of W per hop.
 // ---------------------------------------------------------------------------
+constexpr uint32_t kChTile = 2048, kChThreads = 256, kChMargin = 2048;
 constexpr uint32_t kSegRadix = 8;
+constexpr uint32_t kNoNode = 0xFFFFFFFFu;
 
-__global__ void seg_next_kernel(const uint64_t *Pw, uint64_t add, uint64_t nrec, uint64_t threshold,
-                                const uint32_t *clamp, uint32_t *J0) {
-  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (i > nrec) return;
-  if (i == nrec) {
-    J0[i] = static_cast<uint32_t>(nrec);
-    return;
+struct SegW { // W(x) from an LDS window [base, base + n) or from HBM
+  const uint64_t *Pw, *lw;
+  uint64_t add, base, n;
+  __device__ __forceinline__ uint64_t operator()(uint64_t x) const {
+    return x - base < n ? lw[x - base] : Pw[x] + add * x;
   }
-  // clamp[i]: one past the last record the block starting at i may hold (the
-  // end of its output table); nrec when null
+};
+
+__device__ uint64_t seg_next_at(const SegW &W, uint64_t i, uint64_t nrec, uint64_t threshold,
+                                const uint32_t *clamp) {
   const uint64_t lim = clamp ? clamp[i] : nrec;
-  // first e >= i with W(e + 1) >= target, W(x) = Pw[x] + add * x
-  const uint64_t target = Pw[i] + add * i + threshold;
-  if (Pw[lim] + add * lim < target) {
-    J0[i] = static_cast<uint32_t>(lim);
-    return;
-  }
-  // gallop (blocks are short: ~2 log2(len) reads, all in nearby lines), then bisect
-  uint64_t lo = i, hi = lim - 1;
+  const uint64_t target = W(i) + threshold;
+  if (W(lim) < target) return lim;
+  uint64_t lo = i, hi = lim - 1; // smallest e in [i, lim - 1] with W(e + 1) >= target
   for (uint64_t span = 1;; span <<= 1) {
     const uint64_t e = i + span - 1;
     if (e >= lim - 1) break;
-    if (Pw[e + 1] + add * (e + 1) >= target) {
+    if (W(e + 1) >= target) {
       hi = e;
       break;
     }
@@ -880,55 +888,213 @@ __global__ void seg_next_kernel(const uint64_t *Pw, uint64_t add, uint64_t nrec,
   }
   while (lo < hi) {
     const uint64_t mid = (lo + hi) >> 1;
-    if (Pw[mid + 1] + add * (mid + 1) >= target) hi = mid;
+    if (W(mid + 1) >= target) hi = mid;
     else lo = mid + 1;
   }
-  J0[i] = static_cast<uint32_t>(lo + 1);
+  return lo + 1;
 }
 
-__global__ void seg_pow_kernel(const uint32_t *Jk, uint32_t *Jk1, uint64_t nrec) {
-  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (i > nrec) return;
-  uint32_t x = static_cast<uint32_t>(i);
-#pragma unroll
-  for (uint32_t j = 0; j < kSegRadix; j++) x = Jk[x];
-  Jk1[i] = x;
-}
+struct SegArgs {
+  const uint64_t *Pw;
+  uint64_t add, m, threshold;
+  const uint32_t *clamp;
+  uint32_t *J0, *Fx, *Fc; // by record
+  uint64_t *win;          // per tile: entry-window size (scanned into node bases)
+  uint64_t *first, *d_count;
+};
 
-// number of blocks: hops of the chain from 0 that stay below nrec, + 1
-__global__ void seg_depth_kernel(const uint32_t *J, uint32_t levels, uint64_t stride, uint64_t nrec,
-                                 uint64_t *d_nblocks, uint64_t *blk_first) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  uint64_t pos = 0, cnt = 0;
-  if (nrec > 0) {
-    uint64_t w = 1;
-    for (uint32_t k = 1; k < levels; k++) w *= kSegRadix;
-    for (int k = static_cast<int>(levels) - 1; k >= 0; k--, w /= kSegRadix) {
-      const uint32_t *Jk = J + static_cast<uint64_t>(k) * stride;
-      for (uint32_t d = 1; d < kSegRadix; d++) {
-        const uint32_t nx = Jk[pos];
-        if (nx >= nrec) break;
-        pos = nx;
-        cnt += w;
-      }
+__global__ __launch_bounds__(kChThreads) void seg_walk_kernel(SegArgs a) {
+  __shared__ uint64_t lw[kChTile + kChMargin];
+  __shared__ uint32_t js[kChTile];
+  __shared__ uint64_t s_wend;
+  const uint32_t tid = threadIdx.x;
+  const uint64_t c0 = static_cast<uint64_t>(blockIdx.x) * kChTile;
+  const uint64_t c1 = c0 + kChTile < a.m ? c0 + kChTile : a.m;
+  const uint32_t len = static_cast<uint32_t>(c1 - c0);
+  const uint64_t nl = a.m + 1 - c0 < kChTile + kChMargin ? a.m + 1 - c0 : kChTile + kChMargin;
+  for (uint32_t x = tid; x < nl; x += kChThreads) lw[x] = a.Pw[c0 + x] + a.add * (c0 + x);
+  __syncthreads();
+  const SegW W{a.Pw, lw, a.add, c0, nl};
+  for (uint32_t p = tid; p < len; p += kChThreads) {
+    const uint32_t j = static_cast<uint32_t>(seg_next_at(W, c0 + p, a.m, a.threshold, a.clamp));
+    js[p] = j;
+    a.J0[c0 + p] = j;
+  }
+  if (tid == 0) s_wend = blockIdx.x ? seg_next_at(W, c0 - 1, a.m, a.threshold, a.clamp) : c0;
+  __syncthreads();
+  const uint64_t wend = s_wend; // inclusive; >= c0
+  const uint32_t nwin = static_cast<uint32_t>((wend < c1 - 1 ? wend : c1 - 1) - c0 + 1);
+  for (uint32_t p = tid; p < nwin; p += kChThreads) {
+    uint64_t pos = c0 + p;
+    uint32_t cnt = 0;
+    while (pos < c1) {
+      pos = js[pos - c0];
+      cnt++;
     }
-    cnt += 1;
+    a.Fx[c0 + p] = static_cast<uint32_t>(pos);
+    a.Fc[c0 + p] = cnt;
   }
-  *d_nblocks = cnt;
-  blk_first[cnt] = nrec;
+  if (tid == 0) a.win[blockIdx.x] = nwin;
 }
 
-__global__ void seg_emit_kernel(const uint32_t *J, uint32_t levels, uint64_t stride,
-                                const uint64_t *d_nblocks, uint64_t *blk_first) {
-  const uint64_t t = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (t >= *d_nblocks) return;
-  uint32_t pos = 0;
-  uint64_t q = t;
-  for (uint32_t k = 0; k < levels && q; k++, q /= kSegRadix) {
-    const uint32_t *Jk = J + static_cast<uint64_t>(k) * stride;
-    for (uint32_t d = static_cast<uint32_t>(q % kSegRadix); d; d--) pos = Jk[pos];
+struct NodeArgs {
+  const uint32_t *Fx, *Fc;
+  const uint64_t *base; // node base of every tile (exclusive scan of win), tiles + 1
+  uint64_t m, tiles;
+  uint32_t *Nx, *Nc, *Nt; // level 0: next node, segments, tile
+};
+
+__global__ void seg_node_kernel(NodeArgs a) {
+  const uint64_t k = blockIdx.x;
+  const uint64_t b0 = a.base[k], nw = a.base[k + 1] - b0, c0 = k * kChTile;
+  for (uint64_t o = threadIdx.x; o < nw; o += blockDim.x) {
+    const uint64_t x = a.Fx[c0 + o];
+    uint32_t nx = kNoNode;
+    if (x < a.m) {
+      const uint64_t t = x / kChTile;
+      nx = static_cast<uint32_t>(a.base[t] + (x - t * kChTile));
+    }
+    a.Nx[b0 + o] = nx;
+    a.Nc[b0 + o] = a.Fc[c0 + o];
+    a.Nt[b0 + o] = static_cast<uint32_t>(k);
   }
-  blk_first[t] = pos;
+}
+
+// level k + 1 = 8 hops of level k (node count from the device)
+__global__ void seg_npow_kernel(const uint32_t *Nx, const uint32_t *Nc, uint32_t *Nx1, uint32_t *Nc1,
+                                const uint64_t *nnodes) {
+  const uint64_t n = *nnodes;
+  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
+       i += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
+    uint32_t x = static_cast<uint32_t>(i), c = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < kSegRadix; j++) {
+      if (x == kNoNode) break;
+      c += Nc[x];
+      x = Nx[x];
+    }
+    Nx1[i] = x;
+    Nc1[i] = c;
+  }
+}
+
+// visits of the node chain from node 0, total segments, first[total] = m
+__global__ void seg_ndepth_kernel(const uint32_t *Nx, const uint32_t *Nc, uint32_t levels, uint64_t stride,
+                                  uint64_t m, uint64_t *d_visits, uint64_t *first, uint64_t *d_count) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  uint64_t pos = 0, hops = 0, tot = 0, w = 1;
+  for (uint32_t k = 1; k < levels; k++) w *= kSegRadix;
+  for (int k = static_cast<int>(levels) - 1; k >= 0; k--, w /= kSegRadix) {
+    const uint32_t *X = Nx + static_cast<uint64_t>(k) * stride, *C = Nc + static_cast<uint64_t>(k) * stride;
+    for (uint32_t d = 1; d < kSegRadix; d++) {
+      const uint32_t nx = X[pos];
+      if (nx == kNoNode) break;
+      tot += C[pos];
+      pos = nx;
+      hops += w;
+    }
+  }
+  tot += Nc[pos];
+  *d_visits = hops + 1;
+  *d_count = tot;
+  first[tot] = m;
+}
+
+// visit h: its node (tile, entry) and the segments before it
+__global__ void seg_nentry_kernel(const uint32_t *Nx, const uint32_t *Nc, const uint32_t *Nt, const uint64_t *base,
+                                  uint32_t levels, uint64_t stride, const uint64_t *d_visits, uint32_t *tentry,
+                                  uint32_t *tbefore) {
+  const uint64_t h = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (h >= *d_visits) return;
+  uint64_t pos = 0, before = 0, q = h;
+  for (uint32_t k = 0; k < levels && q; k++, q /= kSegRadix) {
+    const uint32_t *X = Nx + static_cast<uint64_t>(k) * stride, *C = Nc + static_cast<uint64_t>(k) * stride;
+    for (uint32_t d = static_cast<uint32_t>(q % kSegRadix); d; d--) {
+      before += C[pos];
+      pos = X[pos];
+    }
+  }
+  const uint32_t t = Nt[pos];
+  tentry[t] = static_cast<uint32_t>(pos - base[t]) + 1; // 0 = not visited
+  tbefore[t] = static_cast<uint32_t>(before);
+}
+
+__global__ __launch_bounds__(kChThreads) void seg_emit_kernel(const uint32_t *J0, uint64_t m, const uint32_t *tentry,
+                                                              const uint32_t *tbefore, uint64_t *first) {
+  __shared__ uint32_t js[kChTile];
+  const uint64_t k = blockIdx.x;
+  const uint32_t e = tentry[k];
+  if (!e) return; // a segment spans the whole tile
+  const uint64_t c0 = k * kChTile, c1 = c0 + kChTile < m ? c0 + kChTile : m;
+  for (uint32_t p = threadIdx.x; p < c1 - c0; p += kChThreads) js[p] = J0[c0 + p];
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t pos = c0 + e - 1, b = tbefore[k];
+    while (pos < c1) {
+      first[b++] = pos;
+      pos = js[pos - c0];
+    }
+  }
+}
+
+// few long segments: one wave follows the chain.  Each hop first probes
+// kHopSpan consecutive records around pos + (previous segment length) --
+// equal-sized tables end there: one coalesced round -- and falls back to a
+// kHopSpan-ary search of W over the rest.  Wave-synchronous: a round is one
+// batch of loads and ballots, no barrier.
+constexpr uint32_t kHopProbe = 8;
+constexpr uint64_t kHopSpan = static_cast<uint64_t>(kWave) * kHopProbe;
+
+// number of x = x0 + j * step (j < kHopSpan, x <= x1) with W(x) < target
+__device__ __forceinline__ uint64_t hop_below(const uint64_t *Pw, uint64_t add, uint64_t x0, uint64_t x1,
+                                              uint64_t step, uint64_t target) {
+  const uint32_t lane = lane_id();
+  bool b[kHopProbe];
+#pragma unroll
+  for (uint32_t r = 0; r < kHopProbe; r++) {
+    const uint64_t x = x0 + (static_cast<uint64_t>(r) * kWave + lane) * step;
+    b[r] = x <= x1 && Pw[x] + add * x < target;
+  }
+  uint64_t nb = 0;
+#pragma unroll
+  for (uint32_t r = 0; r < kHopProbe; r++) nb += __popcll(__ballot(b[r]));
+  return nb;
+}
+
+__global__ __launch_bounds__(kWave) void seg_hops_kernel(const uint64_t *Pw, uint64_t add, uint64_t m,
+                                                         uint64_t threshold, uint64_t *first, uint64_t *d_count) {
+  const uint64_t wm = Pw[m] + add * m;
+  uint64_t pos = 0, nseg = 0, glen = 0;
+  while (pos < m) {
+    if (lane_id() == 0) first[nseg] = pos;
+    nseg++;
+    const uint64_t target = Pw[pos] + add * pos + threshold;
+    if (wm < target) break; // the last segment runs to m
+    // answer: the first x in [pos + 1, m] with W(x) >= target (W(m) >= target)
+    uint64_t lo = pos + 1, hi = m;
+    if (glen) {
+      const uint64_t g0 = pos + glen > pos + 1 + kHopSpan / 2 ? pos + glen - kHopSpan / 2 : pos + 1;
+      const uint64_t g1 = g0 + kHopSpan - 1 < m ? g0 + kHopSpan - 1 : m;
+      const uint64_t nb = hop_below(Pw, add, g0, g1, 1, target);
+      if (nb == 0) hi = g0;
+      else if (g0 + nb <= g1) lo = hi = g0 + nb;
+      else lo = g1 + 1;
+    }
+    while (hi > lo) {
+      const uint64_t step = (hi - lo + kHopSpan) / kHopSpan; // ceil(span / kHopSpan)
+      const uint64_t nb = hop_below(Pw, add, lo, hi, step, target);
+      // probes below target form a prefix (W is monotone): answer in (lo + (nb - 1) step, lo + nb step]
+      const uint64_t h2 = lo + nb * step;
+      if (nb) lo = lo + (nb - 1) * step + 1;
+      hi = h2 < hi ? h2 : hi;
+    }
+    glen = lo - pos;
+    pos = lo;
+  }
+  if (lane_id() == 0) {
+    first[nseg] = m;
+    *d_count = nseg;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1137,18 +1303,74 @@ hipError_t launch_enc_emit(const EncArgs &a, hipStream_t s) {
   return hipGetLastError();
 }
 
+namespace {
+struct SegLayout { // u32 offsets into the segmentation workspace
+  uint64_t tiles, levels, J0, Fx, Fc, Nx, Nc, Nt, tentry, tbefore, u64, total;
+  // u64 region (8-aligned): win[tiles + 1], base[tiles + 1], nn, visits, scan ws
+  uint64_t win, base, nn, visits, sws;
+  explicit SegLayout(uint64_t m) {
+    tiles = (m + kChTile - 1) / kChTile;
+    levels = 1;
+    for (uint64_t r = kSegRadix; r < tiles; r *= kSegRadix) levels++;
+    const uint64_t n1 = m + 1;
+    J0 = 0;
+    Fx = J0 + n1;
+    Fc = Fx + n1;
+    Nx = Fc + n1;
+    Nc = Nx + levels * n1;
+    Nt = Nc + levels * n1;
+    tentry = Nt + n1;
+    tbefore = tentry + tiles + 1;
+    u64 = (tbefore + tiles + 1 + 1) & ~uint64_t(1);
+    win = 0;
+    base = win + tiles + 1;
+    nn = base + tiles + 1;
+    visits = nn + 1;
+    sws = visits + 1;
+    total = u64 + 2 * (sws + scan_workspace_elems(tiles + 1) + 1);
+  }
+};
+} // namespace
+
+uint64_t segment_workspace_u32(uint64_t nrec) { return SegLayout(nrec).total + 2; }
+
 hipError_t launch_segment(const uint64_t *Pw, uint64_t nrec, uint64_t threshold, uint32_t *J,
-                          uint32_t levels, uint64_t *d_nblocks, uint64_t *blk_first, hipStream_t s,
-                          const uint32_t *clamp, uint64_t add) {
-  // levels = binary levels the caller provisioned (J holds levels * (nrec + 1));
-  // radix-8 needs ceil(levels / 3) of them
-  const uint32_t lv = (levels + 2) / 3;
+                          uint64_t *d_nblocks, uint64_t *blk_first, hipStream_t s, const uint32_t *clamp,
+                          uint64_t add, bool long_segments) {
+  if (nrec == 0) { // no records: no segment, first[0] = 0
+    hipError_t e = hipMemsetAsync(d_nblocks, 0, sizeof(uint64_t), s);
+    if (e == hipSuccess) e = hipMemsetAsync(blk_first, 0, sizeof(uint64_t), s);
+    return e;
+  }
+  if (long_segments && !clamp) {
+    seg_hops_kernel<<<1, kWave, 0, s>>>(Pw, add, nrec, threshold, blk_first, d_nblocks);
+    return hipGetLastError();
+  }
+  const SegLayout L(nrec);
+  // u64 region 8-aligned relative to J (J itself is 256-aligned by the callers' allocators)
+  uint64_t *U = reinterpret_cast<uint64_t *>(J + L.u64);
+  uint64_t *win = U + L.win, *base = U + L.base, *nn = U + L.nn, *visits = U + L.visits, *sws = U + L.sws;
+  uint32_t *tentry = J + L.tentry, *tbefore = J + L.tbefore;
   const uint64_t stride = nrec + 1;
-  seg_next_kernel<<<grid_for(nrec + 1, 256), 256, 0, s>>>(Pw, add, nrec, threshold, clamp, J);
-  for (uint32_t k = 0; k + 1 < lv; k++)
-    seg_pow_kernel<<<grid_for(nrec + 1, 256), 256, 0, s>>>(J + k * stride, J + (k + 1) * stride, nrec);
-  seg_depth_kernel<<<1, 64, 0, s>>>(J, lv, stride, nrec, d_nblocks, blk_first);
-  if (nrec) seg_emit_kernel<<<grid_for(nrec, 256), 256, 0, s>>>(J, lv, stride, d_nblocks, blk_first);
+  SegArgs a{Pw, add, nrec, threshold, clamp, J + L.J0, J + L.Fx, J + L.Fc, win, blk_first, d_nblocks};
+  seg_walk_kernel<<<static_cast<uint32_t>(L.tiles), kChThreads, 0, s>>>(a);
+  hipError_t e = launch_scan(win, L.tiles, 0, base, sws, s); // base[tiles] = node count
+  if (e != hipSuccess) return e;
+  e = hipMemcpyAsync(nn, base + L.tiles, sizeof(uint64_t), hipMemcpyDeviceToDevice, s);
+  if (e == hipSuccess) e = hipMemsetAsync(tentry, 0, (L.tiles + 1) * sizeof(uint32_t), s);
+  if (e != hipSuccess) return e;
+  NodeArgs na{J + L.Fx, J + L.Fc, base, nrec, L.tiles, J + L.Nx, J + L.Nc, J + L.Nt};
+  seg_node_kernel<<<static_cast<uint32_t>(L.tiles), 256, 0, s>>>(na);
+  const uint32_t pg = static_cast<uint32_t>(std::min<uint64_t>(grid_for(nrec + 1, 256), 2048));
+  for (uint64_t k = 0; k + 1 < L.levels; k++)
+    seg_npow_kernel<<<pg, 256, 0, s>>>(J + L.Nx + k * stride, J + L.Nc + k * stride, J + L.Nx + (k + 1) * stride,
+                                       J + L.Nc + (k + 1) * stride, nn);
+  seg_ndepth_kernel<<<1, 64, 0, s>>>(J + L.Nx, J + L.Nc, static_cast<uint32_t>(L.levels), stride, nrec, visits,
+                                     blk_first, d_nblocks);
+  seg_nentry_kernel<<<grid_for(L.tiles, 256), 256, 0, s>>>(J + L.Nx, J + L.Nc, J + L.Nt, base,
+                                                           static_cast<uint32_t>(L.levels), stride, visits,
+                                                           tentry, tbefore);
+  seg_emit_kernel<<<static_cast<uint32_t>(L.tiles), kChThreads, 0, s>>>(J + L.J0, nrec, tentry, tbefore, blk_first);
   return hipGetLastError();
 }
 

@@ -98,15 +98,18 @@ hipError_t launch_enc_sizes(const uint32_t *klen, const uint32_t *vlen, uint64_t
 hipError_t launch_enc_blk_len(const uint64_t *P, const uint64_t *blk_first, uint64_t nblocks,
                               uint64_t *blk_len, hipStream_t s);
 hipError_t launch_enc_emit(const EncArgs &a, hipStream_t s);
+// greedy segmentation; J = segment_workspace_u32(nrec) u32 of device workspace
+uint64_t segment_workspace_u32(uint64_t nrec);
 hipError_t launch_segment(const uint64_t *Pw, uint64_t nrec, uint64_t threshold, uint32_t *J,
-                          uint32_t levels, uint64_t *d_nblocks, uint64_t *blk_first, hipStream_t s,
-                          const uint32_t *clamp = nullptr, uint64_t add = 0);
+                          uint64_t *d_nblocks, uint64_t *blk_first, hipStream_t s,
+                          const uint32_t *clamp = nullptr, uint64_t add = 0, bool long_segments = false);
 
 // persistent device workspace of one context (compaction)
 struct Arena {
   void *base = nullptr;
   uint64_t cap = 0;
-  uint64_t *host = nullptr; // 64 pinned host words: the job's few device -> host reads
+  uint64_t *host = nullptr; // pinned host words: the job's few device -> host reads
+  uint64_t host_cap = 0;
 };
 
 int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, const uint8_t *d_src,

@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 var=$1; vals=$2; shift 2
 args=${*:---config 3 --steps 5 --no-ref --no-files}
 mkdir -p gpurun_out/ab
-timeout -k 10 300 python -u -m pytest tests/test_gpu_compact.py tests/test_gpu_files.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/ab/pytest.log 2>&1 || { echo "pytest failed"; tail -30 gpurun_out/ab/pytest.log; exit 3; }
+timeout -k 10 300 python -u -m pytest tests/test_gpu_compact.py tests/test_gpu_files.py tests/test_gpu_codec.py tests/test_gpu_table.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/ab/pytest.log 2>&1 || { echo "pytest failed"; tail -30 gpurun_out/ab/pytest.log; exit 3; }
 tail -1 gpurun_out/ab/pytest.log
 for v in $vals; do
   export $var=$v
