@@ -358,3 +358,36 @@ def test_config5_zipf_blocks(codec, oracle):
         ref = oracle_rt(oracle, src, woff, wlen, mode, dst_fill=0xA7)
         assert (got[2] == 0).all()
         assert np.array_equal(got[1], ref[1]) and np.array_equal(got[0], ref[0])
+
+
+def length_records(klen, vlen):
+    """Records that carry only lengths (segmentation reads nothing else)."""
+    n = len(klen)
+    z = np.zeros(n, np.uint64)
+    return {"type": np.zeros(n, np.uint8), "key_len": np.asarray(klen, np.uint32),
+            "val_len": np.asarray(vlen, np.uint32), "txn": z, "key_off": z, "val_off": z,
+            "key_src": np.zeros(1, np.uint8), "val_src": np.zeros(1, np.uint8)}
+
+
+@pytest.mark.parametrize("case", ["tiny", "huge", "span_tiles", "mixed_runs", "no_value"])
+def test_segment_tiles_vs_oracle(codec, oracle, case):
+    """Block segmentation across many 2048-record tiles: entry windows of
+    ~140 records (tiny entries), 1-record blocks (huge values), blocks that
+    span several tiles (large thresholds), runs alternating between the two,
+    and DELETE-shaped records without value fields."""
+    rng = np.random.default_rng({"tiny": 1, "huge": 2, "span_tiles": 3, "mixed_runs": 4, "no_value": 5}[case])
+    n = {"tiny": 150_000, "huge": 20_000, "span_tiles": 60_000, "mixed_runs": 80_000, "no_value": 50_000}[case]
+    klen = rng.integers(0, 20, n)
+    vlen = rng.integers(0, 12, n)
+    if case == "huge":
+        vlen = rng.integers(4000, 70_000, n)
+    elif case == "mixed_runs":
+        big = (np.arange(n) // 3000) % 2 == 1
+        vlen = np.where(big, rng.integers(3000, 9000, n), vlen)
+    elif case == "no_value":
+        vlen = np.full(n, 0xFFFFFFFF)
+    rec = length_records(klen, vlen)
+    for T in ((4096, 1 << 20) if case == "span_tiles" else (4096, 32768)):
+        want = oracle.segment(rec, T)
+        got = cpu_u64(codec.segment(records_table(rec), T))
+        assert np.array_equal(got, want), (case, T)
