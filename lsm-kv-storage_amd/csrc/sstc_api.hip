@@ -157,6 +157,8 @@ int sstc_ctx_reserve(sstc_ctx *c, uint64_t max_blocks, uint64_t max_records) {
   if (int r = bind_device(c)) return r;
   if (int r = ensure_blocks(c, max_blocks)) return r;
   if (int r = ensure_records(c, max_records)) return r;
+  if (int r = grow(c, c->jump, c->cap_jump, sstc::segment_workspace_u32(max_records), "segmentation workspace"))
+    return r;
   return SSTC_OK;
 }
 

@@ -274,64 +274,167 @@ __global__ __launch_bounds__(kKThreads) void ck_kw_merge_kernel(const SK *in, SK
   }
 }
 
-// head[i] = 1 if merged record i starts a key group (ShouldKeepEntry's
-// last_current_key != key, compact.cc:266-268)
-__global__ void ck_head_kernel(const SK *s, uint64_t n, KeyView kv, uint64_t *head) {
-  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  uint64_t h = 1;
-  if (i > 0) {
-    const SK a = s[i - 1], b = s[i];
-    h = key_cmp(a.p0, a.p1, a.kl, a.id, b.p0, b.p1, b.kl, b.id, kv) != 0;
-  }
-  head[i] = h;
-}
-
-// gid = inclusive group count - 1 (from the exclusive scan G of head: gid = G[i] + head[i] - 1)
-__global__ void ck_headpos_kernel(const uint64_t *head, const uint64_t *G, uint64_t n, uint64_t *hp) {
-  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (i < n && head[i]) hp[G[i]] = i;
-}
-
-// ShouldKeepEntry (compact.cc:324-363)
-__global__ void ck_keep_kernel(const SK *s, const uint64_t *head, const uint64_t *G, const uint64_t *hp,
-                               const uint8_t *type, uint64_t n, uint32_t base_level, uint64_t *keep) {
-  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  uint64_t k;
-  if (i == 0) {
-    k = 1; // first record of the merge is always kept
-  } else if (head[i]) {
-    k = type[s[i].id] == kTypePut ? 1 : (base_level ? 0 : 1);
-  } else {
-    const uint64_t h = hp[G[i] - 1]; // this group's head
-    k = s[h].tx > s[i].tx ? 0 : 1;   // drop if last_txn > txn
-  }
-  keep[i] = k;
-}
-
 struct Rec {
   uint8_t *type;
   uint32_t *kl, *vl;
   uint64_t *tx, *ko, *vo;
 };
 
-__global__ void ck_gather_kernel(const SK *s, const uint64_t *keep, const uint64_t *K, Rec R, uint64_t n, Rec out,
-                                 uint64_t *dw, uint64_t *ew) {
-  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (i >= n || !keep[i]) return;
-  const uint64_t o = K[i];
-  const uint32_t r = s[i].id;
-  const uint32_t vl = R.vl[r];
-  out.type[o] = R.type[r];
-  out.kl[o] = R.kl[r];
-  out.vl[o] = vl;
-  out.tx[o] = R.tx[r];
-  out.ko[o] = R.ko[r];
-  out.vo[o] = R.vo[r];
-  // data_size increment (table_builder.cc:55) and block weight (entry + offset entry)
-  dw[o] = static_cast<uint64_t>(R.kl[r]) + (vl != kNoValue ? vl : 0u);
-  ew[o] = entry_size(R.kl[r], vl);
+// Keep / drop (ShouldKeepEntry, compact.cc:324-363) over the merged records,
+// then stream compaction of the survivors with the prefix sums the splits
+// need, in three kernels: per-tile keep flags + sums, one scan of the tile
+// sums, per-tile compaction.  Tile = kFtItems rows of kFtThreads records;
+// a row's records are lane-consecutive so loads and stores coalesce.
+constexpr uint32_t kFtThreads = 256, kFtItems = 16, kFtTile = kFtThreads * kFtItems;
+
+// exclusive scan of three u64 per thread over the workgroup; tot = totals
+__device__ __forceinline__ void wg_scan3(uint64_t (&v)[3], uint64_t (&tot)[3]) {
+  __shared__ uint64_t sw[3][kFtThreads / kWave];
+  const uint32_t lane = lane_id(), w = threadIdx.x / kWave;
+  uint64_t inc[3];
+#pragma unroll
+  for (int c = 0; c < 3; c++) {
+    inc[c] = wave_incl_scan_u64(v[c]);
+    if (lane == kWave - 1) sw[c][w] = inc[c];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int c = 0; c < 3; c++) {
+    uint64_t base = 0, t = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kFtThreads / kWave; k++) {
+      const uint64_t x = sw[c][k];
+      if (k < w) base += x;
+      t += x;
+    }
+    v[c] = base + inc[c] - v[c];
+    tot[c] = t;
+  }
+  __syncthreads();
+}
+
+// data_size increment (table_builder.cc:55)
+__device__ __forceinline__ uint64_t data_bytes(uint32_t kl, uint32_t vl) {
+  return static_cast<uint64_t>(kl) + (vl != kNoValue ? vl : 0u);
+}
+
+// keep[i]: the first merged record always; a group head (key differs from the
+// previous record, compact.cc:266-268) if PUT, or if DELETED and not the base
+// level; any other record iff its txn equals its group head's (drop if
+// last_txn > txn).  Txns descend within a group, so a non-head whose txn
+// differs from its predecessor's is dropped, and an equal one looks back along
+// its run of equal txns (records duplicated across inputs) to the head.
+// tsum[3 t + {0,1,2}] = kept records, their key+value bytes, their entry bytes.
+__global__ __launch_bounds__(kFtThreads) void ck_keep_tile_kernel(const SK *s, uint64_t n, KeyView kv,
+                                                                  const uint8_t *type, const uint32_t *kl,
+                                                                  const uint32_t *vl, uint32_t base_level,
+                                                                  uint8_t *keep, uint64_t *tsum) {
+  const uint64_t t0 = static_cast<uint64_t>(blockIdx.x) * kFtTile;
+  uint64_t v[3] = {0, 0, 0};
+  for (uint32_t j = 0; j < kFtItems; j++) { // row j: records t0 + 256 j + [0, 256), lane-consecutive
+    const uint64_t i = t0 + static_cast<uint64_t>(j) * kFtThreads + threadIdx.x;
+    if (i >= n) break;
+    const SK x = s[i];
+    uint32_t k;
+    if (i == 0) {
+      k = 1;
+    } else {
+      const SK prev = s[i - 1];
+      if (key_cmp(prev.p0, prev.p1, prev.kl, prev.id, x.p0, x.p1, x.kl, x.id, kv) != 0) {
+        k = type[x.id] == kTypePut ? 1u : (base_level ? 0u : 1u);
+      } else if (x.tx != prev.tx) {
+        k = 0;
+      } else {
+        k = 1;
+        for (uint64_t q = i - 1; q > 0; q--) {
+          const SK y = s[q - 1], z = s[q];
+          if (key_cmp(y.p0, y.p1, y.kl, y.id, z.p0, z.p1, z.kl, z.id, kv) != 0) break; // z is the head
+          if (y.tx != z.tx) {
+            k = 0;
+            break;
+          }
+        }
+      }
+    }
+    keep[i] = static_cast<uint8_t>(k);
+    if (k) {
+      const uint32_t a = kl[x.id], b = vl[x.id];
+      v[0] += 1;
+      v[1] += data_bytes(a, b);
+      v[2] += entry_size(a, b);
+    }
+  }
+  uint64_t tot[3];
+  wg_scan3(v, tot);
+  if (threadIdx.x == 0) {
+    tsum[3 * blockIdx.x] = tot[0];
+    tsum[3 * blockIdx.x + 1] = tot[1];
+    tsum[3 * blockIdx.x + 2] = tot[2];
+  }
+}
+
+// exclusive scan of the tile sums in place (one workgroup); totals[3]
+__global__ __launch_bounds__(kFtThreads) void ck_tile_scan_kernel(uint64_t *tsum, uint64_t tiles, uint64_t *totals) {
+  uint64_t carry[3] = {0, 0, 0};
+  for (uint64_t t0 = 0; t0 < tiles; t0 += kFtThreads) {
+    const uint64_t t = t0 + threadIdx.x;
+    uint64_t v[3];
+#pragma unroll
+    for (int c = 0; c < 3; c++) v[c] = t < tiles ? tsum[3 * t + c] : 0;
+    uint64_t tot[3];
+    wg_scan3(v, tot);
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+      if (t < tiles) tsum[3 * t + c] = carry[c] + v[c];
+      carry[c] += tot[c];
+    }
+  }
+  if (threadIdx.x == 0)
+    for (int c = 0; c < 3; c++) totals[c] = carry[c];
+}
+
+// the survivors in merge order: record table, Pd = prefix sums of key+value
+// bytes (table split), Pe = prefix sums of entry bytes (block split, encode)
+__global__ __launch_bounds__(kFtThreads) void ck_compact_tile_kernel(const SK *s, uint64_t n, const uint8_t *keep,
+                                                                     const uint64_t *tsum, const uint64_t *totals,
+                                                                     Rec R, Rec out, uint64_t *Pd, uint64_t *Pe) {
+  const uint64_t t0 = static_cast<uint64_t>(blockIdx.x) * kFtTile;
+  uint64_t base[3] = {tsum[3 * blockIdx.x], tsum[3 * blockIdx.x + 1], tsum[3 * blockIdx.x + 2]};
+  for (uint32_t j = 0; j < kFtItems; j++) { // row by row: survivors of a row are written lane-consecutively
+    const uint64_t r0 = t0 + static_cast<uint64_t>(j) * kFtThreads;
+    if (r0 >= n) break; // uniform over the workgroup
+    const uint64_t i = r0 + threadIdx.x;
+    const bool k = i < n && keep[i];
+    uint32_t id = 0, a = 0, b = 0;
+    uint64_t v[3] = {0, 0, 0};
+    if (k) {
+      id = s[i].id;
+      a = R.kl[id];
+      b = R.vl[id];
+      v[0] = 1;
+      v[1] = data_bytes(a, b);
+      v[2] = entry_size(a, b);
+    }
+    uint64_t tot[3];
+    wg_scan3(v, tot);
+    if (k) {
+      const uint64_t o = base[0] + v[0];
+      out.type[o] = R.type[id];
+      out.kl[o] = a;
+      out.vl[o] = b;
+      out.tx[o] = R.tx[id];
+      out.ko[o] = R.ko[id];
+      out.vo[o] = R.vo[id];
+      Pd[o] = base[1] + v[1];
+      Pe[o] = base[2] + v[2];
+    }
+#pragma unroll
+    for (int c = 0; c < 3; c++) base[c] += tot[c];
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    Pd[totals[0]] = totals[1];
+    Pe[totals[0]] = totals[2];
+  }
 }
 
 // per record: end of its output table (clamp for block segmentation)
@@ -477,30 +580,8 @@ __global__ __launch_bounds__(256) void ck_meta_kernel(const uint64_t *bf, uint64
   }
 }
 
-// min / max txn of every output table (table_builder.cc:47-49): one wave per
-// block reduces its records, then one workgroup per table reduces its blocks
-// (atomics on ~30 table words from 10^5 blocks would serialise)
-__global__ void ck_blk_minmax_kernel(const uint64_t *bf, uint64_t nb, Rec K, uint64_t *bmin, uint64_t *bmax) {
-  const uint64_t b = (static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x) / kWave;
-  if (b >= nb) return;
-  const uint32_t lane = lane_id();
-  uint64_t mn = ~0ull, mx = 0;
-  for (uint64_t r = bf[b] + lane; r < bf[b + 1]; r += kWave) {
-    const uint64_t x = K.tx[r];
-    mn = x < mn ? x : mn;
-    mx = x > mx ? x : mx;
-  }
-  for (uint32_t d = kWave / 2; d > 0; d >>= 1) {
-    const uint64_t a = __shfl_xor(mn, d, kWave), c = __shfl_xor(mx, d, kWave);
-    mn = a < mn ? a : mn;
-    mx = c > mx ? c : mx;
-  }
-  if (lane == 0) {
-    bmin[b] = mn;
-    bmax[b] = mx;
-  }
-}
-
+// min / max txn of every output table (table_builder.cc:47-49): the encode
+// kernels reduce every block, then one workgroup per table reduces its blocks
 __global__ __launch_bounds__(256) void ck_tab_minmax_kernel(const uint64_t *tbf, const uint64_t *bmin,
                                                             const uint64_t *bmax, uint64_t *tmin, uint64_t *tmax) {
   __shared__ uint64_t smn[256 / kWave], smx[256 / kWave];
@@ -757,17 +838,15 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
         }
       }
     }
-    // 3. keep / drop
-    uint64_t *head = pool.get<uint64_t>(n), *G = pool.get<uint64_t>(n + 1), *hp = pool.get<uint64_t>(n);
-    uint64_t *keep = pool.get<uint64_t>(n), *K = pool.get<uint64_t>(n + 1);
-    ck_head_kernel<<<grid(n), 256, 0, s>>>(A, n, kv, head);
-    CK(launch_scan(head, n, 0, G, ws2, s));
-    ck_headpos_kernel<<<grid(n), 256, 0, s>>>(head, G, n, hp);
-    // G[i] (exclusive) + head[i] - 1 = group id; for a non-head i the group id is G[i] - 1
-    ck_keep_kernel<<<grid(n), 256, 0, s>>>(A, head, G, hp, R.type, n, base_level, keep);
-    CK(launch_scan(keep, n, 0, K, ws2, s));
-    fetch(arena, pool, s, {K + n, reinterpret_cast<const uint64_t *>(bad), reinterpret_cast<const uint64_t *>(err_count),
-                     errs});
+    // 3. keep / drop: survivor counts and byte sums per tile, one scan
+    const uint64_t ftiles = (n + kFtTile - 1) / kFtTile;
+    uint8_t *keep = pool.get<uint8_t>(n);
+    uint64_t *tsum = pool.get<uint64_t>(3 * ftiles), *totals = pool.get<uint64_t>(3);
+    ck_keep_tile_kernel<<<static_cast<uint32_t>(ftiles), kFtThreads, 0, s>>>(A, n, kv, R.type, R.kl, R.vl, base_level,
+                                                                          keep, tsum);
+    ck_tile_scan_kernel<<<1, kFtThreads, 0, s>>>(tsum, ftiles, totals);
+    fetch(arena, pool, s, {totals, reinterpret_cast<const uint64_t *>(bad),
+                           reinterpret_cast<const uint64_t *>(err_count), errs});
     if (arena.host[2] != arena.host[3]) {
       err = "an input block failed to decode";
       return SSTC_E_INVALID_ARG;
@@ -780,16 +859,12 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     res[1] = m;
     Rec KR{pool.get<uint8_t>(m), pool.get<uint32_t>(m), pool.get<uint32_t>(m), pool.get<uint64_t>(m),
            pool.get<uint64_t>(m), pool.get<uint64_t>(m)};
-    uint64_t *dw = pool.get<uint64_t>(m), *ew = pool.get<uint64_t>(m);
-    ck_gather_kernel<<<grid(n), 256, 0, s>>>(A, keep, K, R, n, KR, dw, ew);
-    // 4. table split then block split (clamped at table ends); block weight =
-    // entry + offset entry, i.e. the prefix sums of the entry sizes + 16 i.
-    // Chain bounds: kept key+value bytes and entry+offset bytes are at most
-    // the input block bytes, and every table / block but the last of each
-    // clamp range reaches its threshold.
+    // 4. survivors gathered in merge order with their prefix sums; then the
+    // table split (key+value bytes, compact.cc:290) and the block split
+    // (entry + offset-entry bytes, table_builder.cc:57-59) clamped at table ends
     uint64_t *Pd = pool.get<uint64_t>(m + 1), *Pe = pool.get<uint64_t>(m + 1);
-    CK(launch_scan(dw, m, 0, Pd, ws2, s));
-    CK(launch_scan(ew, m, 0, Pe, ws2, s));
+    ck_compact_tile_kernel<<<static_cast<uint32_t>(ftiles), kFtThreads, 0, s>>>(A, n, keep, tsum, totals, R, KR, Pd,
+                                                                             Pe);
     uint64_t *tf = pool.get<uint64_t>(m + 1), *dn = pool.get<uint64_t>(2);
     segment(pool, Pd, 0, m, table_limit, nullptr, tf, dn, s, true);
     uint32_t *clamp = pool.get<uint32_t>(m + 1);
@@ -827,12 +902,13 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     EncArgs ea{d_src, d_src, sstc_records{KR.type, KR.kl, KR.vl, KR.tx, KR.ko, KR.vo}, bf, nb, Pe, bo, blen, d_dst, 1};
     ea.big = pool.get<uint32_t>(nb + 1);
     ea.nbig = ea.big + nb;
+    uint64_t *bmin = pool.get<uint64_t>(nb), *bmax = pool.get<uint64_t>(nb);
+    uint64_t *tmin = pool.get<uint64_t>(nt), *tmax = pool.get<uint64_t>(nt);
+    ea.bmin = bmin; // block min / max txn, reduced by the encode kernels
+    ea.bmax = bmax;
     CK(hipMemsetAsync(ea.nbig, 0, sizeof(uint32_t), s));
     CK(launch_enc_emit(ea, s));
     ck_meta_kernel<<<static_cast<uint32_t>((nb + 255) / 256), 256, 0, s>>>(bf, nb, btab, BL, MS, blen, tbf, d_table_off, tdata, KR, d_src, d_dst);
-    uint64_t *bmin = pool.get<uint64_t>(nb), *bmax = pool.get<uint64_t>(nb);
-    uint64_t *tmin = pool.get<uint64_t>(nt), *tmax = pool.get<uint64_t>(nt);
-    ck_blk_minmax_kernel<<<grid(nb * kWave), 256, 0, s>>>(bf, nb, KR, bmin, bmax);
     ck_tab_minmax_kernel<<<static_cast<uint32_t>(nt), 256, 0, s>>>(tbf, bmin, bmax, tmin, tmax);
     ck_footer_kernel<<<grid(nt), 256, 0, s>>>(nt, tbf, d_table_off, tdata, tmeta, tmin, tmax, d_dst);
     CK(hipGetLastError());

@@ -12,8 +12,10 @@
 //   decode_kernel       per-entry parse into a record table
 //                       (BlockReader accessors, sstable/block_reader.cc:59-114).
 //   enc_*_kernel        records -> blocks (BlockBuilder, block_builder.cc:12-109).
-//   seg_*_kernel        greedy block segmentation of TableBuilder::AddEntry
-//                       (table_builder.cc:57-59) by pointer doubling.
+//   seg_*_kernel        greedy block / table segmentation of TableBuilder::AddEntry
+//                       (table_builder.cc:57-59) and DoCompactJob (compact.cc:290):
+//                       per-tile chain walks + node-level pointer jumping, or
+//                       a wave hopping along few long segments.
 //   scan_*_kernel       device-wide exclusive scan (u64) used by the above.
 #include "sstc_device.h"
 #include "sstc_launch.h"
@@ -640,11 +642,45 @@ __device__ void enc_emit_block(const EncArgs &a, uint64_t b, uint8_t *slot) {
 }
 
 
+// min / max txn of block b by the whole workgroup (large blocks)
+__device__ void enc_blk_minmax(const EncArgs &a, uint64_t b) {
+  __shared__ uint64_t smn[kEncThreads / kWave], smx[kEncThreads / kWave];
+  const uint64_t f0 = a.blk_first[b], f1 = a.blk_first[b + 1];
+  uint64_t mn = ~0ull, mx = 0;
+  for (uint64_t r = f0 + threadIdx.x; r < f1; r += kEncThreads) {
+    const uint64_t x = a.in.txn[r];
+    mn = x < mn ? x : mn;
+    mx = x > mx ? x : mx;
+  }
+  for (uint32_t d = kWave / 2; d > 0; d >>= 1) {
+    const uint64_t x = __shfl_xor(mn, d, kWave), y = __shfl_xor(mx, d, kWave);
+    mn = x < mn ? x : mn;
+    mx = y > mx ? y : mx;
+  }
+  if (lane_id() == 0) {
+    smn[threadIdx.x / kWave] = mn;
+    smx[threadIdx.x / kWave] = mx;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (uint32_t w = 1; w < kEncThreads / kWave; w++) {
+      mn = smn[w] < mn ? smn[w] : mn;
+      mx = smx[w] > mx ? smx[w] : mx;
+    }
+    a.bmin[b] = mn;
+    a.bmax[b] = mx;
+  }
+  __syncthreads();
+}
+
 __global__ __launch_bounds__(kEncThreads) void enc_emit_kernel(EncArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t slot[kEncThreads * 16];
   if (a.big) {
     const uint32_t cnt = *a.nbig;
-    for (uint32_t i = blockIdx.x; i < cnt; i += gridDim.x) enc_emit_block(a, a.big[i], slot);
+    for (uint32_t i = blockIdx.x; i < cnt; i += gridDim.x) {
+      enc_emit_block(a, a.big[i], slot);
+      if (a.bmin) enc_blk_minmax(a, a.big[i]);
+    }
     return;
   }
   for (uint64_t b = blockIdx.x; b < a.nblocks; b += gridDim.x) enc_emit_block(a, b, slot);
@@ -715,9 +751,10 @@ __device__ __forceinline__ void emit_chunk(uint8_t *img, u32x4 v, uint32_t nxt, 
 // last 8; the compat reader may have changed it) and the offset entry.
 template <uint32_t kCopyQ>
 __device__ __forceinline__ void enc_copy_entries(const EncArgs &a, uint8_t *img, uint32_t pad, uint64_t f0,
-                                                 uint32_t n, uint64_t P0, uint32_t D) {
+                                                 uint32_t n, uint64_t P0, uint32_t D, uint64_t b) {
   const uint32_t lane = lane_id();
   const uint32_t g = lane & 15u, sub = lane >> 4;
+  uint64_t tmin = ~0ull, tmax = 0; // the block's min / max txn (table footer, table_builder.cc:47-49)
   for (uint32_t c0 = 0; c0 < n; c0 += kWave) {
     const uint32_t nc = n - c0 < kWave ? n - c0 : kWave;
     uint32_t my_o = 0, my_sz = 0, my_kl = 0, my_ty = 0;
@@ -779,6 +816,19 @@ __device__ __forceinline__ void enc_copy_entries(const EncArgs &a, uint8_t *img,
       for (int j = 0; j < 8; j++) e[my_sz - 8 + j] = static_cast<uint8_t>(my_tx >> (8 * j));
       lds_st_u64u(img, pad + D + 16 * (c0 + lane), my_o);
       lds_st_u64u(img, pad + D + 16 * (c0 + lane) + 8, my_sz);
+      tmin = my_tx < tmin ? my_tx : tmin;
+      tmax = my_tx > tmax ? my_tx : tmax;
+    }
+  }
+  if (a.bmin) {
+    for (uint32_t d = kWave / 2; d > 0; d >>= 1) {
+      const uint64_t x = __shfl_xor(tmin, d, kWave), y = __shfl_xor(tmax, d, kWave);
+      tmin = x < tmin ? x : tmin;
+      tmax = y > tmax ? y : tmax;
+    }
+    if (lane == 0) {
+      a.bmin[b] = tmin;
+      a.bmax[b] = tmax;
     }
   }
 }
@@ -807,7 +857,7 @@ __global__ __launch_bounds__(kEncWaves *kWave) void enc_lds_kernel(EncArgs a) {
   uint8_t *im = img + pad; // image byte 0 == block byte 0
 
   if constexpr (kMode == 1) {
-    enc_copy_entries<4>(a, img, pad, f0, n, P0, D);
+    enc_copy_entries<4>(a, img, pad, f0, n, P0, D, b);
   } else {
   for (uint32_t i = lane; i < n; i += kWave) {
     const uint64_t r = f0 + i;
@@ -871,12 +921,12 @@ struct SegW { // W(x) from an LDS window [base, base + n) or from HBM
   }
 };
 
-__device__ uint64_t seg_next_at(const SegW &W, uint64_t i, uint64_t nrec, uint64_t threshold,
-                                const uint32_t *clamp) {
-  const uint64_t lim = clamp ? clamp[i] : nrec;
+// the first e in [i, lim - 1] with W(e + 1) >= W(i) + threshold, plus one; lim
+// when the threshold is not reached before the clamp (the bisection then ends
+// at lim - 1 by itself: W is monotone)
+__device__ uint64_t seg_next_at(const SegW &W, uint64_t i, uint64_t lim, uint64_t threshold) {
   const uint64_t target = W(i) + threshold;
-  if (W(lim) < target) return lim;
-  uint64_t lo = i, hi = lim - 1; // smallest e in [i, lim - 1] with W(e + 1) >= target
+  uint64_t lo = i, hi = lim - 1;
   for (uint64_t span = 1;; span <<= 1) {
     const uint64_t e = i + span - 1;
     if (e >= lim - 1) break;
@@ -915,12 +965,23 @@ __global__ __launch_bounds__(kChThreads) void seg_walk_kernel(SegArgs a) {
   for (uint32_t x = tid; x < nl; x += kChThreads) lw[x] = a.Pw[c0 + x] + a.add * (c0 + x);
   __syncthreads();
   const SegW W{a.Pw, lw, a.add, c0, nl};
-  for (uint32_t p = tid; p < len; p += kChThreads) {
-    const uint32_t j = static_cast<uint32_t>(seg_next_at(W, c0 + p, a.m, a.threshold, a.clamp));
+  constexpr uint32_t kPer = kChTile / kChThreads;
+  uint64_t lim[kPer]; // clamps loaded up front: independent loads in flight together
+#pragma unroll
+  for (uint32_t r = 0; r < kPer; r++) {
+    const uint32_t p = tid + r * kChThreads;
+    lim[r] = p < len ? (a.clamp ? a.clamp[c0 + p] : a.m) : 0;
+  }
+#pragma unroll
+  for (uint32_t r = 0; r < kPer; r++) {
+    const uint32_t p = tid + r * kChThreads;
+    if (p >= len) break;
+    const uint32_t j = static_cast<uint32_t>(seg_next_at(W, c0 + p, lim[r], a.threshold));
     js[p] = j;
     a.J0[c0 + p] = j;
   }
-  if (tid == 0) s_wend = blockIdx.x ? seg_next_at(W, c0 - 1, a.m, a.threshold, a.clamp) : c0;
+  if (tid == 0)
+    s_wend = blockIdx.x ? seg_next_at(W, c0 - 1, a.clamp ? a.clamp[c0 - 1] : a.m, a.threshold) : c0;
   __syncthreads();
   const uint64_t wend = s_wend; // inclusive; >= c0
   const uint32_t nwin = static_cast<uint32_t>((wend < c1 - 1 ? wend : c1 - 1) - c0 + 1);

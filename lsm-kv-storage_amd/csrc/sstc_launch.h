@@ -62,6 +62,8 @@ struct EncArgs {
   // optional: blocks too large for an LDS slot are listed here by enc_lds_kernel
   // (*nbig zeroed by the caller) so enc_emit_kernel visits only them
   uint32_t *big = nullptr, *nbig = nullptr;
+  // optional (compaction, entries_in_src): per-block min / max txn
+  uint64_t *bmin = nullptr, *bmax = nullptr;
 };
 
 // point lookups (sstc_get.hip)
