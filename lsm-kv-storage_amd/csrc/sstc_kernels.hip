@@ -642,6 +642,123 @@ __device__ void enc_emit_block(const EncArgs &a, uint64_t b, uint8_t *slot) {
 }
 
 
+// Large block of a compaction (records decoded from blocks held in key_src):
+// every entry is already its own encoding in its input block, so the
+// workgroup copies whole entries.  An entry of at least kBigEntry bytes is
+// copied by all threads: each 16 B destination chunk (aligned) is funnel-
+// shifted from two aligned 16 B source chunks (the source / destination skew
+// is constant along the entry), kEmitUnroll chunks per thread in flight; the
+// partial chunks at its ends and the txn (the compat reader may have changed
+// it) go byte by byte.  Smaller entries are copied the same way by one wave
+// each.  Then the offset section and the extra.
+constexpr uint32_t kBigEntry = 2048, kEmitUnroll = 4, kBigList = 256;
+
+__device__ __forceinline__ u32x4 funnel16(const u32x4 &v0, const u32x4 &v1, uint32_t s) {
+  const uint32_t w[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+  const uint32_t q = s >> 2, r = s & 3u;
+  uint32_t o[5];
+#pragma unroll
+  for (uint32_t j = 0; j < 5; j++) { // o[j] = w[q + j] (q <= 3)
+    const uint32_t a0 = w[j], a1 = w[j + 1], a2 = w[j + 2], a3 = w[j + 3];
+    o[j] = q == 0 ? a0 : (q == 1 ? a1 : (q == 2 ? a2 : a3));
+  }
+  u32x4 out;
+  out.x = __builtin_amdgcn_alignbyte(o[1], o[0], r);
+  out.y = __builtin_amdgcn_alignbyte(o[2], o[1], r);
+  out.z = __builtin_amdgcn_alignbyte(o[3], o[2], r);
+  out.w = __builtin_amdgcn_alignbyte(o[4], o[3], r);
+  return out;
+}
+
+// copy len bytes sp -> dp (both unaligned) with threads t of nt: aligned 16 B
+// destination chunks funnel-shifted from aligned source chunks, kEmitUnroll
+// chunks per thread in flight, the partial chunks at both ends byte by byte.
+// The source may be read up to 31 B past sp + len (inside its block: the txn
+// and the offset section follow every entry).
+__device__ __forceinline__ void copy_span(uint8_t *dp, const uint8_t *sp, uint64_t len, uint32_t t, uint32_t nt) {
+  const uintptr_t d0 = reinterpret_cast<uintptr_t>(dp), d1 = d0 + len;
+  const uintptr_t cb = (d0 + 15) & ~static_cast<uintptr_t>(15), ce = d1 & ~static_cast<uintptr_t>(15);
+  if (cb >= ce) {
+    for (uint64_t x = t; x < len; x += nt) dp[x] = sp[x];
+    return;
+  }
+  const uint64_t nch = (ce - cb) >> 4;
+  const uint8_t *s0 = sp + (cb - d0); // source byte of the first full chunk
+  const uint32_t sh = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(s0) & 15u);
+  const u32x4 *sa = reinterpret_cast<const u32x4 *>(s0 - sh);
+  u32x4 *da = reinterpret_cast<u32x4 *>(cb);
+  for (uint64_t k0 = 0; k0 < nch; k0 += static_cast<uint64_t>(nt) * kEmitUnroll) {
+    u32x4 v0[kEmitUnroll], v1[kEmitUnroll];
+#pragma unroll
+    for (uint32_t u = 0; u < kEmitUnroll; u++) {
+      const uint64_t k = k0 + static_cast<uint64_t>(u) * nt + t;
+      if (k < nch) {
+        v0[u] = sa[k];
+        v1[u] = sh ? sa[k + 1] : v0[u];
+      }
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < kEmitUnroll; u++) {
+      const uint64_t k = k0 + static_cast<uint64_t>(u) * nt + t;
+      if (k < nch) __builtin_nontemporal_store(funnel16(v0[u], v1[u], sh), da + k);
+    }
+  }
+  for (uintptr_t x = d0 + t; x < cb; x += nt) dp[x - d0] = sp[x - d0];
+  for (uintptr_t x = ce + t; x < d1; x += nt) dp[x - d0] = sp[x - d0];
+}
+
+__device__ void enc_emit_block_entries(const EncArgs &a, uint64_t b) {
+  __shared__ uint32_t s_big[kBigList];
+  __shared__ uint32_t s_nbig;
+  const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid / kWave;
+  const uint64_t f0 = a.blk_first[b], f1 = a.blk_first[b + 1];
+  const uint64_t n = f1 - f0;
+  const uint64_t P0 = a.P[f0];
+  const uint64_t D = a.P[f1] - P0;
+  uint8_t *blk = a.dst + a.out_blk_off[b];
+  for (uint64_t r0 = 0; r0 < n; r0 += kBigList) { // entries in batches (a batch's big list fits LDS)
+    if (tid == 0) s_nbig = 0;
+    __syncthreads();
+    const uint64_t r1 = r0 + kBigList < n ? r0 + kBigList : n;
+    // entries below kBigEntry: a wave each (span copy + the txn)
+    for (uint64_t i = r0 + wave; i < r1; i += kEncThreads / kWave) {
+      const uint64_t r = f0 + i;
+      const uint64_t o = a.P[r] - P0, sz = a.P[r + 1] - a.P[r];
+      if (sz >= kBigEntry) {
+        if (lane == 0) s_big[atomicAdd(&s_nbig, 1u)] = static_cast<uint32_t>(i);
+        continue;
+      }
+      copy_span(blk + o, a.key_src + a.in.key_off[r] - 5, sz - 8, lane, kWave);
+      if (lane < 8) blk[o + sz - 8 + lane] = static_cast<uint8_t>(a.in.txn[r] >> (8 * lane));
+    }
+    __syncthreads();
+    const uint32_t nbig = s_nbig;
+    for (uint32_t e = 0; e < nbig; e++) { // large entries: the whole workgroup each
+      const uint64_t r = f0 + s_big[e];
+      const uint64_t o = a.P[r] - P0, sz = a.P[r + 1] - a.P[r];
+      copy_span(blk + o, a.key_src + a.in.key_off[r] - 5, sz - 8, tid, kEncThreads);
+      if (tid < 8) blk[o + sz - 8 + tid] = static_cast<uint8_t>(a.in.txn[r] >> (8 * tid));
+    }
+    __syncthreads();
+  }
+  // offset section (start, size per entry) and the extra (block_builder.cc:79-109)
+  for (uint64_t i = tid; i < n; i += kEncThreads) {
+    const uint64_t st = a.P[f0 + i] - P0, sz = a.P[f0 + i + 1] - a.P[f0 + i];
+    uint8_t *q = blk + D + 16 * i;
+    for (int j = 0; j < 8; j++) {
+      q[j] = static_cast<uint8_t>(st >> (8 * j));
+      q[8 + j] = static_cast<uint8_t>(sz >> (8 * j));
+    }
+  }
+  if (tid == 0) {
+    uint8_t *q = blk + D + 16 * n;
+    for (int j = 0; j < 8; j++) {
+      q[j] = static_cast<uint8_t>(n >> (8 * j));
+      q[8 + j] = static_cast<uint8_t>(D >> (8 * j));
+    }
+  }
+}
+
 // min / max txn of block b by the whole workgroup (large blocks)
 __device__ void enc_blk_minmax(const EncArgs &a, uint64_t b) {
   __shared__ uint64_t smn[kEncThreads / kWave], smx[kEncThreads / kWave];
@@ -678,7 +795,8 @@ __global__ __launch_bounds__(kEncThreads) void enc_emit_kernel(EncArgs a) {
   if (a.big) {
     const uint32_t cnt = *a.nbig;
     for (uint32_t i = blockIdx.x; i < cnt; i += gridDim.x) {
-      enc_emit_block(a, a.big[i], slot);
+      if (a.entries_in_src) enc_emit_block_entries(a, a.big[i]);
+      else enc_emit_block(a, a.big[i], slot);
       if (a.bmin) enc_blk_minmax(a, a.big[i]);
     }
     return;
