@@ -329,40 +329,59 @@ __global__ __launch_bounds__(kFtThreads) void ck_keep_tile_kernel(const SK *s, u
                                                                   const uint8_t *type, const uint32_t *kl,
                                                                   const uint32_t *vl, uint32_t base_level,
                                                                   uint8_t *keep, uint64_t *tsum) {
+  constexpr uint32_t kGroup = 4; // rows whose loads are in flight together
   const uint64_t t0 = static_cast<uint64_t>(blockIdx.x) * kFtTile;
   uint64_t v[3] = {0, 0, 0};
-  for (uint32_t j = 0; j < kFtItems; j++) { // row j: records t0 + 256 j + [0, 256), lane-consecutive
-    const uint64_t i = t0 + static_cast<uint64_t>(j) * kFtThreads + threadIdx.x;
-    if (i >= n) break;
-    const SK x = s[i];
-    uint32_t k;
-    if (i == 0) {
-      k = 1;
-    } else {
-      const SK prev = s[i - 1];
-      if (key_cmp(prev.p0, prev.p1, prev.kl, prev.id, x.p0, x.p1, x.kl, x.id, kv) != 0) {
-        k = type[x.id] == kTypePut ? 1u : (base_level ? 0u : 1u);
-      } else if (x.tx != prev.tx) {
-        k = 0;
-      } else {
-        k = 1;
-        for (uint64_t q = i - 1; q > 0; q--) {
-          const SK y = s[q - 1], z = s[q];
-          if (key_cmp(y.p0, y.p1, y.kl, y.id, z.p0, z.p1, z.kl, z.id, kv) != 0) break; // z is the head
-          if (y.tx != z.tx) {
-            k = 0;
-            break;
-          }
-        }
+  for (uint32_t j0 = 0; j0 < kFtItems; j0 += kGroup) {
+    SK x[kGroup], pv[kGroup];
+#pragma unroll
+    for (uint32_t g = 0; g < kGroup; g++) { // row j: records t0 + 256 j + [0, 256), lane-consecutive
+      const uint64_t i = t0 + static_cast<uint64_t>(j0 + g) * kFtThreads + threadIdx.x;
+      x[g] = SK{};
+      pv[g] = SK{};
+      if (i < n) {
+        x[g] = s[i];
+        if (i > 0) pv[g] = s[i - 1];
       }
     }
-    keep[i] = static_cast<uint8_t>(k);
-    if (k) {
-      const uint32_t a = kl[x.id], b = vl[x.id];
-      v[0] += 1;
-      v[1] += data_bytes(a, b);
-      v[2] += entry_size(a, b);
+    uint32_t kk[kGroup], a8[kGroup] = {}, b8[kGroup] = {};
+#pragma unroll
+    for (uint32_t g = 0; g < kGroup; g++) {
+      const uint64_t i = t0 + static_cast<uint64_t>(j0 + g) * kFtThreads + threadIdx.x;
+      uint32_t k = 0;
+      if (i < n) {
+        if (i == 0) {
+          k = 1;
+        } else if (key_cmp(pv[g].p0, pv[g].p1, pv[g].kl, pv[g].id, x[g].p0, x[g].p1, x[g].kl, x[g].id, kv) != 0) {
+          k = type[x[g].id] == kTypePut ? 1u : (base_level ? 0u : 1u);
+        } else if (x[g].tx == pv[g].tx) {
+          k = 1;
+          for (uint64_t q = i - 1; q > 0; q--) { // run of equal txns back to the group head
+            const SK y = s[q - 1], z = s[q];
+            if (key_cmp(y.p0, y.p1, y.kl, y.id, z.p0, z.p1, z.kl, z.id, kv) != 0) break; // z is the head
+            if (y.tx != z.tx) {
+              k = 0;
+              break;
+            }
+          }
+        }
+        keep[i] = static_cast<uint8_t>(k);
+      }
+      kk[g] = k;
     }
+#pragma unroll
+    for (uint32_t g = 0; g < kGroup; g++)
+      if (kk[g]) {
+        a8[g] = kl[x[g].id];
+        b8[g] = vl[x[g].id];
+      }
+#pragma unroll
+    for (uint32_t g = 0; g < kGroup; g++)
+      if (kk[g]) {
+        v[0] += 1;
+        v[1] += data_bytes(a8[g], b8[g]);
+        v[2] += entry_size(a8[g], b8[g]);
+      }
   }
   uint64_t tot[3];
   wg_scan3(v, tot);
@@ -398,38 +417,53 @@ __global__ __launch_bounds__(kFtThreads) void ck_tile_scan_kernel(uint64_t *tsum
 __global__ __launch_bounds__(kFtThreads) void ck_compact_tile_kernel(const SK *s, uint64_t n, const uint8_t *keep,
                                                                      const uint64_t *tsum, const uint64_t *totals,
                                                                      Rec R, Rec out, uint64_t *Pd, uint64_t *Pe) {
+  constexpr uint32_t kGroup = 4; // rows whose loads are in flight together
   const uint64_t t0 = static_cast<uint64_t>(blockIdx.x) * kFtTile;
   uint64_t base[3] = {tsum[3 * blockIdx.x], tsum[3 * blockIdx.x + 1], tsum[3 * blockIdx.x + 2]};
-  for (uint32_t j = 0; j < kFtItems; j++) { // row by row: survivors of a row are written lane-consecutively
-    const uint64_t r0 = t0 + static_cast<uint64_t>(j) * kFtThreads;
-    if (r0 >= n) break; // uniform over the workgroup
-    const uint64_t i = r0 + threadIdx.x;
-    const bool k = i < n && keep[i];
-    uint32_t id = 0, a = 0, b = 0;
-    uint64_t v[3] = {0, 0, 0};
-    if (k) {
-      id = s[i].id;
-      a = R.kl[id];
-      b = R.vl[id];
-      v[0] = 1;
-      v[1] = data_bytes(a, b);
-      v[2] = entry_size(a, b);
-    }
-    uint64_t tot[3];
-    wg_scan3(v, tot);
-    if (k) {
-      const uint64_t o = base[0] + v[0];
-      out.type[o] = R.type[id];
-      out.kl[o] = a;
-      out.vl[o] = b;
-      out.tx[o] = R.tx[id];
-      out.ko[o] = R.ko[id];
-      out.vo[o] = R.vo[id];
-      Pd[o] = base[1] + v[1];
-      Pe[o] = base[2] + v[2];
+  for (uint32_t j0 = 0; j0 < kFtItems; j0 += kGroup) {
+    if (t0 + static_cast<uint64_t>(j0) * kFtThreads >= n) break; // uniform over the workgroup
+    uint32_t km = 0, id[kGroup], kl[kGroup], vl[kGroup], ty[kGroup];
+    uint64_t tx[kGroup], ko[kGroup], vo[kGroup];
+#pragma unroll
+    for (uint32_t g = 0; g < kGroup; g++) {
+      const uint64_t i = t0 + static_cast<uint64_t>(j0 + g) * kFtThreads + threadIdx.x;
+      if (i < n && keep[i]) km |= 1u << g;
     }
 #pragma unroll
-    for (int c = 0; c < 3; c++) base[c] += tot[c];
+    for (uint32_t g = 0; g < kGroup; g++) {
+      const uint64_t i = t0 + static_cast<uint64_t>(j0 + g) * kFtThreads + threadIdx.x;
+      id[g] = (km >> g) & 1u ? s[i].id : 0u;
+    }
+#pragma unroll
+    for (uint32_t g = 0; g < kGroup; g++) {
+      const bool k = (km >> g) & 1u;
+      kl[g] = k ? R.kl[id[g]] : 0u;
+      vl[g] = k ? R.vl[id[g]] : 0u;
+      ty[g] = k ? R.type[id[g]] : 0u;
+      tx[g] = k ? R.tx[id[g]] : 0ull;
+      ko[g] = k ? R.ko[id[g]] : 0ull;
+      vo[g] = k ? R.vo[id[g]] : 0ull;
+    }
+#pragma unroll
+    for (uint32_t g = 0; g < kGroup; g++) { // row by row: survivors of a row are lane-consecutive
+      const bool k = (km >> g) & 1u;
+      uint64_t v[3] = {k ? 1ull : 0ull, k ? data_bytes(kl[g], vl[g]) : 0ull, k ? entry_size(kl[g], vl[g]) : 0ull};
+      uint64_t tot[3];
+      wg_scan3(v, tot);
+      if (k) {
+        const uint64_t q = base[0] + v[0];
+        out.type[q] = static_cast<uint8_t>(ty[g]);
+        out.kl[q] = kl[g];
+        out.vl[q] = vl[g];
+        out.tx[q] = tx[g];
+        out.ko[q] = ko[g];
+        out.vo[q] = vo[g];
+        Pd[q] = base[1] + v[1];
+        Pe[q] = base[2] + v[2];
+      }
+#pragma unroll
+      for (int c = 0; c < 3; c++) base[c] += tot[c];
+    }
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     Pd[totals[0]] = totals[1];

@@ -1031,22 +1031,27 @@ constexpr uint32_t kChTile = 2048, kChThreads = 256, kChMargin = 2048;
 constexpr uint32_t kSegRadix = 8;
 constexpr uint32_t kNoNode = 0xFFFFFFFFu;
 
+// LDS slot of W(base + x): one pad word per 8 so that threads walking 8
+// consecutive records each hit different banks
+__device__ __forceinline__ uint32_t lw_slot(uint64_t x) { return static_cast<uint32_t>(x + (x >> 3)); }
+
 struct SegW { // W(x) from an LDS window [base, base + n) or from HBM
   const uint64_t *Pw, *lw;
   uint64_t add, base, n;
   __device__ __forceinline__ uint64_t operator()(uint64_t x) const {
-    return x - base < n ? lw[x - base] : Pw[x] + add * x;
+    return x - base < n ? lw[lw_slot(x - base)] : Pw[x] + add * x;
   }
 };
 
 // the first e in [i, lim - 1] with W(e + 1) >= W(i) + threshold, plus one; lim
 // when the threshold is not reached before the clamp (the bisection then ends
-// at lim - 1 by itself: W is monotone)
-__device__ uint64_t seg_next_at(const SegW &W, uint64_t i, uint64_t lim, uint64_t threshold) {
+// at lim - 1 by itself: W is monotone).  Every e < from (>= i) is known to
+// fail: galloping starts there.
+__device__ uint64_t seg_next_at(const SegW &W, uint64_t i, uint64_t lim, uint64_t threshold, uint64_t from) {
   const uint64_t target = W(i) + threshold;
-  uint64_t lo = i, hi = lim - 1;
+  uint64_t lo = from, hi = lim - 1;
   for (uint64_t span = 1;; span <<= 1) {
-    const uint64_t e = i + span - 1;
+    const uint64_t e = from + span - 1;
     if (e >= lim - 1) break;
     if (W(e + 1) >= target) {
       hi = e;
@@ -1072,46 +1077,94 @@ struct SegArgs {
 };
 
 __global__ __launch_bounds__(kChThreads) void seg_walk_kernel(SegArgs a) {
-  __shared__ uint64_t lw[kChTile + kChMargin];
-  __shared__ uint32_t js[kChTile];
+  constexpr uint32_t kLw = kChTile + kChMargin;
+  __shared__ uint64_t lw[kLw + kLw / 8];
+  __shared__ uint32_t jn[kChTile], jc[kChTile];
   __shared__ uint64_t s_wend;
   const uint32_t tid = threadIdx.x;
   const uint64_t c0 = static_cast<uint64_t>(blockIdx.x) * kChTile;
   const uint64_t c1 = c0 + kChTile < a.m ? c0 + kChTile : a.m;
   const uint32_t len = static_cast<uint32_t>(c1 - c0);
-  const uint64_t nl = a.m + 1 - c0 < kChTile + kChMargin ? a.m + 1 - c0 : kChTile + kChMargin;
-  for (uint32_t x = tid; x < nl; x += kChThreads) lw[x] = a.Pw[c0 + x] + a.add * (c0 + x);
+  const uint64_t nl = a.m + 1 - c0 < kLw ? a.m + 1 - c0 : kLw;
+  { // all loads of the window in flight before the LDS stores
+    constexpr uint32_t kFill = kLw / kChThreads;
+    uint64_t v[kFill];
+#pragma unroll
+    for (uint32_t r = 0; r < kFill; r++) {
+      const uint32_t x = tid + r * kChThreads;
+      v[r] = x < nl ? a.Pw[c0 + x] : 0;
+    }
+#pragma unroll
+    for (uint32_t r = 0; r < kFill; r++) {
+      const uint32_t x = tid + r * kChThreads;
+      if (x < nl) lw[lw_slot(x)] = v[r] + a.add * (c0 + x);
+    }
+  }
   __syncthreads();
   const SegW W{a.Pw, lw, a.add, c0, nl};
+  if (tid == kChThreads - 1) { // entry window end: J0 of the record before the tile
+    const uint64_t i = c0 - 1;
+    s_wend = blockIdx.x ? seg_next_at(W, i, a.clamp ? a.clamp[i] : a.m, a.threshold, i) : c0;
+  }
+  // J0 of kPer consecutive records per thread: gallop for the first, then from
+  // the previous answer (J0 is monotone within an output table)
   constexpr uint32_t kPer = kChTile / kChThreads;
-  uint64_t lim[kPer]; // clamps loaded up front: independent loads in flight together
+  uint64_t lim[kPer];
 #pragma unroll
   for (uint32_t r = 0; r < kPer; r++) {
-    const uint32_t p = tid + r * kChThreads;
+    const uint32_t p = tid * kPer + r;
     lim[r] = p < len ? (a.clamp ? a.clamp[c0 + p] : a.m) : 0;
   }
+  uint64_t e_prev = 0;
 #pragma unroll
   for (uint32_t r = 0; r < kPer; r++) {
-    const uint32_t p = tid + r * kChThreads;
+    const uint32_t p = tid * kPer + r;
     if (p >= len) break;
-    const uint32_t j = static_cast<uint32_t>(seg_next_at(W, c0 + p, lim[r], a.threshold));
-    js[p] = j;
-    a.J0[c0 + p] = j;
+    const uint64_t i = c0 + p;
+    const uint64_t j = seg_next_at(W, i, lim[r], a.threshold, r && e_prev > i ? e_prev : i);
+    e_prev = j - 1;
+    jn[p] = static_cast<uint32_t>(j);
+    jc[p] = 1;
+    a.J0[i] = static_cast<uint32_t>(j);
   }
-  if (tid == 0)
-    s_wend = blockIdx.x ? seg_next_at(W, c0 - 1, a.clamp ? a.clamp[c0 - 1] : a.m, a.threshold) : c0;
   __syncthreads();
+  // pointer jumping inside the tile: jn[p] -> first chain position >= c1
+  // reached from p, jc[p] -> segments started on the way (p's included)
+  for (;;) {
+    uint32_t nx[kPer], nc[kPer];
+    int moved = 0;
+#pragma unroll
+    for (uint32_t r = 0; r < kPer; r++) {
+      const uint32_t p = tid + r * kChThreads;
+      nx[r] = 0;
+      nc[r] = 0;
+      if (p < len) {
+        nx[r] = jn[p];
+        nc[r] = jc[p];
+        if (nx[r] < c1) {
+          const uint32_t q = nx[r] - static_cast<uint32_t>(c0);
+          nc[r] += jc[q];
+          nx[r] = jn[q];
+          moved = 1;
+        }
+      }
+    }
+    if (!__syncthreads_or(moved)) break;
+#pragma unroll
+    for (uint32_t r = 0; r < kPer; r++) {
+      const uint32_t p = tid + r * kChThreads;
+      if (p < len) {
+        jn[p] = nx[r];
+        jc[p] = nc[r];
+      }
+    }
+    __syncthreads();
+  }
   const uint64_t wend = s_wend; // inclusive; >= c0
   const uint32_t nwin = static_cast<uint32_t>((wend < c1 - 1 ? wend : c1 - 1) - c0 + 1);
   for (uint32_t p = tid; p < nwin; p += kChThreads) {
-    uint64_t pos = c0 + p;
-    uint32_t cnt = 0;
-    while (pos < c1) {
-      pos = js[pos - c0];
-      cnt++;
-    }
-    a.Fx[c0 + p] = static_cast<uint32_t>(pos);
-    a.Fc[c0 + p] = cnt;
+    a.Fx[c0 + p] = jn[p];
+    a.Fc[c0 + p] = jc[p];
   }
   if (tid == 0) a.win[blockIdx.x] = nwin;
 }
@@ -1205,7 +1258,20 @@ __global__ __launch_bounds__(kChThreads) void seg_emit_kernel(const uint32_t *J0
   const uint32_t e = tentry[k];
   if (!e) return; // a segment spans the whole tile
   const uint64_t c0 = k * kChTile, c1 = c0 + kChTile < m ? c0 + kChTile : m;
-  for (uint32_t p = threadIdx.x; p < c1 - c0; p += kChThreads) js[p] = J0[c0 + p];
+  {
+    constexpr uint32_t kFill = kChTile / kChThreads;
+    uint32_t v[kFill];
+#pragma unroll
+    for (uint32_t r = 0; r < kFill; r++) {
+      const uint32_t p = threadIdx.x + r * kChThreads;
+      v[r] = p < c1 - c0 ? J0[c0 + p] : 0;
+    }
+#pragma unroll
+    for (uint32_t r = 0; r < kFill; r++) {
+      const uint32_t p = threadIdx.x + r * kChThreads;
+      if (p < c1 - c0) js[p] = v[r];
+    }
+  }
   __syncthreads();
   if (threadIdx.x == 0) {
     uint64_t pos = c0 + e - 1, b = tbefore[k];
