@@ -5,7 +5,7 @@
 cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 2
 export TMPDIR=/tmp
 tag=${1:-run}; shift
-args=${*:---steps 20 --no-cpu-baseline --no-e2e}
+args=${*:---steps 20 --no-cpu-baseline --no-e2e --no-hbm-variant}
 out=gpurun_out/prof_$tag
 mkdir -p $out
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/trace -o trace --output-format csv -- python3 bench.py $args > $out/trace.log 2>&1 || { echo "trace failed"; tail -20 $out/trace.log; exit 3; }
