@@ -110,3 +110,21 @@ def test_compact_no_records(codec, oracle):
         outs, res = codec.compact(tables, 4096, 1 << 20, 1)
         assert res.records_kept == kept == 0 and res.tables_out == 1
         assert len(outs) == len(want) == 1 and np.array_equal(outs[0], want[0])
+
+
+@pytest.mark.parametrize("k,n_per,space,dup", [(20, 12_000, 150_000, False), (9, 30_000, 60_000, True)])
+def test_compact_large_vs_oracle(codec, oracle, k, n_per, space, dup):
+    """Larger jobs: k > 8 inputs (two k-way merge passes), many merge windows,
+    filter and split tiles, overlapping keys (drops), duplicated (key, txn)
+    records across inputs (equal-txn runs) and many output tables."""
+    sets = W.compaction_inputs(k, n_per, space, seed=91 + k, vmax=160, p_delete=0.15, distinct=not dup)
+    if dup:  # the same records in two inputs: equal (key, txn) runs in the merge
+        sets[1] = {key: v.copy() for key, v in sets[0].items()}
+    ins = [oracle.table_build(r, 4096) for r in sets]
+    for base in (1, 0):
+        want, kept = oracle.compact(ins, 4096, 300_000, base)
+        outs, res = codec.compact(ins, 4096, 300_000, base)
+        assert res.records_kept == kept
+        assert len(outs) == len(want)
+        for o, w in zip(outs, want):
+            assert np.array_equal(o, w)
