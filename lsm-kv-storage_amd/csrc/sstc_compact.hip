@@ -66,11 +66,16 @@ __device__ __forceinline__ bool sk_less(const SK &a, const SK &b, const KeyView 
 }
 
 // Sortedness of every input run (TableBuilder requires sorted input,
-// table_builder.h:77): a record may not sort before its predecessor.
-__global__ void ck_check_sorted_kernel(const SK *s, const uint64_t *run_start, uint64_t nruns, uint64_t n,
-                                       KeyView kv, unsigned long long *bad) {
-  const uint64_t r = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (r == 0 || r >= n) return;
+// table_builder.h:77): decode_kernel checks each record against its
+// predecessor in the same block; this kernel checks the first record of every
+// non-empty block against the last record before it, unless it starts a run.
+__global__ void ck_check_blocks_kernel(const SK *s, const uint64_t *rec_base, uint64_t nblocks,
+                                       const uint64_t *run_start, uint64_t nruns, KeyView kv,
+                                       unsigned long long *bad) {
+  const uint64_t b = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (b >= nblocks) return;
+  const uint64_t r = rec_base[b];
+  if (r == 0 || rec_base[b + 1] == r) return;
   uint64_t lo = 0, hi = nruns; // run containing r: last run_start <= r
   while (lo + 1 < hi) {
     const uint64_t mid = (lo + hi) >> 1;
@@ -788,8 +793,10 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
           pool.get<uint64_t>(n), pool.get<uint64_t>(n)};
     uint32_t *status = pool.get<uint32_t>(nblocks);
     SK *A = pool.get<SK>(n ? n : 1), *B = pool.get<SK>(n ? n : 1);
+    unsigned long long *bad = reinterpret_cast<unsigned long long *>(pool.get<uint64_t>(1));
+    CK(hipMemsetAsync(bad, 0, 8, s));
     DecArgs da{d_src, d_blk_off, d_blk_len, nblocks, rb_all,
-               sstc_records{R.type, R.kl, R.vl, R.tx, R.ko, R.vo}, txn_mode, status, err_count, A};
+               sstc_records{R.type, R.kl, R.vl, R.tx, R.ko, R.vo}, txn_mode, status, err_count, A, bad};
     CK(launch_decode(da, s));
     if (n == 0) { // DoCompactJob still finishes its first (empty) output table
       fetch(arena, pool, s, {reinterpret_cast<const uint64_t *>(err_count), errs});
@@ -817,9 +824,7 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     uint64_t nruns = ntables;
     uint64_t *rb = pool.get<uint64_t>(nruns + 2);
     CK(hipMemcpyAsync(rb, run_start.data(), (nruns + 1) * 8, hipMemcpyHostToDevice, s));
-    unsigned long long *bad = reinterpret_cast<unsigned long long *>(pool.get<uint64_t>(1));
-    CK(hipMemsetAsync(bad, 0, 8, s));
-    ck_check_sorted_kernel<<<grid(n), 256, 0, s>>>(A, rb, nruns, n, kv, bad);
+    ck_check_blocks_kernel<<<grid(nblocks), 256, 0, s>>>(A, rb_all, nblocks, rb, nruns, kv, bad);
     // k-way merge passes; run boundaries of every pass are known on the host,
     // so all group descriptors go up in one upload (lives until the next sync)
     std::vector<KGroup> kg;

@@ -464,6 +464,9 @@ __device__ __forceinline__ uint32_t decode_block(const DecArgs &a, const R &rd, 
   uint32_t st = check_extra(len, n, doff);
   if (st == kBlkOk && n != uniform64(a.rec_base[b + 1]) - base) st = kBlkCountMismatch;
   if (st != kBlkOk) return st;
+  // previous record of the block (sortedness check): carried across chunks
+  uint64_t c0 = 0, c1 = 0, ctx = 0, cs = 0;
+  uint32_t ckl = 0;
   for (uint64_t i0 = 0; i0 < n; i0 += kWave) {
     const uint64_t i = i0 + lane;
     Entry e{};
@@ -474,6 +477,36 @@ __device__ __forceinline__ uint32_t decode_block(const DecArgs &a, const R &rd, 
     }
     const uint64_t bad = __ballot(e.code != kBlkOk);
     if (bad) return __shfl(e.code, __ffsll(static_cast<long long>(bad)) - 1, kWave);
+    if (a.unsorted) {
+      // TableBuilder requires sorted input (table_builder.h:77): a record may
+      // not sort before its predecessor (key asc, then txn desc)
+      const uint64_t k0 = i < n && e.klen ? key_prefix8(__builtin_bswap64(rd.u64(s + 5)), e.klen) : 0;
+      const uint64_t k1 = i < n && e.klen > 8 ? key_prefix8(__builtin_bswap64(rd.u64(s + 13)), e.klen - 8) : 0;
+      uint64_t q0 = __shfl_up(k0, 1u, kWave), q1 = __shfl_up(k1, 1u, kWave);
+      uint64_t qt = __shfl_up(e.txn, 1u, kWave), qs = __shfl_up(s, 1u, kWave);
+      uint32_t ql = __shfl_up(e.klen, 1u, kWave);
+      if (lane == 0) {
+        q0 = c0, q1 = c1, qt = ctx, qs = cs, ql = ckl;
+      }
+      bool viol = false;
+      if (i < n && i > 0) {
+        int c = k0 != q0 ? (k0 < q0 ? -1 : 1) : (k1 != q1 ? (k1 < q1 ? -1 : 1) : 0);
+        if (c == 0 && e.klen > 16 && ql > 16) {
+          const uint32_t m = e.klen < ql ? e.klen : ql;
+          for (uint32_t j = 16; j < m && c == 0; j++) {
+            const uint32_t x = rd.u8(s + 5 + j), y = rd.u8(qs + 5 + j);
+            if (x != y) c = x < y ? -1 : 1;
+          }
+        }
+        if (c == 0) c = e.klen < ql ? -1 : (e.klen > ql ? 1 : 0);
+        viol = c < 0 || (c == 0 && e.txn > qt);
+      }
+      const uint64_t v = __ballot(viol);
+      if (v && lane == 0) atomicAdd(a.unsorted, static_cast<unsigned long long>(__popcll(v)));
+      c0 = __shfl(k0, kWave - 1, kWave), c1 = __shfl(k1, kWave - 1, kWave);
+      ctx = __shfl(e.txn, kWave - 1, kWave), cs = __shfl(s, kWave - 1, kWave);
+      ckl = __shfl(e.klen, kWave - 1, kWave);
+    }
     if (i < n) {
       const uint64_t r = base + i;
       a.out.type[r] = static_cast<uint8_t>(e.type);

@@ -44,6 +44,8 @@ struct DecArgs {
   uint32_t *status; // may be null
   unsigned long long *err_count;
   SortKey *sk = nullptr; // optional merge keys (compaction)
+  // optional: count of records that sort before their predecessor in the block
+  unsigned long long *unsorted = nullptr;
   uint32_t xcd = 0;
 };
 
