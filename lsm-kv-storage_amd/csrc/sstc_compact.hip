@@ -41,6 +41,19 @@ struct KeyView {
 
 using SK = SortKey;
 
+// Device-side abort of the merge / filter kernels that run before the host
+// sees the decode and sortedness verdicts: a failed block leaves its records
+// (and their ids) unwritten, an unsorted run breaks the co-rank invariants the
+// merge windows rely on; either would send those kernels out of bounds.
+struct Abort {
+  const unsigned long long *err;  // context decode-error counter
+  const uint64_t *err0;           // its value before this job's decode
+  const unsigned long long *bad;  // unsorted records (null: not checked)
+  __device__ __forceinline__ bool operator()() const {
+    return *err != *err0 || (bad && *bad);
+  }
+};
+
 // three-way key compare: prefix, then (only when both are longer than 16 B and
 // the prefixes tie) the remaining bytes, then the length (std::string_view <)
 __device__ __forceinline__ int key_cmp(uint64_t a0, uint64_t a1, uint32_t al, uint32_t aid, uint64_t b0,
@@ -71,9 +84,9 @@ __device__ __forceinline__ bool sk_less(const SK &a, const SK &b, const KeyView 
 // non-empty block against the last record before it, unless it starts a run.
 __global__ void ck_check_blocks_kernel(const SK *s, const uint64_t *rec_base, uint64_t nblocks,
                                        const uint64_t *run_start, uint64_t nruns, KeyView kv,
-                                       unsigned long long *bad) {
+                                       unsigned long long *bad, Abort stop) {
   const uint64_t b = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (b >= nblocks) return;
+  if (b >= nblocks || stop()) return;
   const uint64_t r = rec_base[b];
   if (r == 0 || rec_base[b + 1] == r) return;
   uint64_t lo = 0, hi = nruns; // run containing r: last run_start <= r
@@ -130,10 +143,11 @@ __device__ __forceinline__ uint32_t find_group(const KGroup *g, uint32_t ng, uin
 }
 
 __global__ __launch_bounds__(256) void ck_kw_split_kernel(const SK *in, const KGroup *groups, uint32_t ngroups,
-                                                          uint32_t nids, KeyView kv, uint32_t *C, uint64_t *G) {
+                                                          uint32_t nids, KeyView kv, uint32_t *C, uint64_t *G,
+                                                          Abort stop) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t u = t >> 3, r = t & 7u;
-  if (u >= nids) return; // whole 8-lane groups leave together
+  if (u >= nids || stop()) return; // whole 8-lane groups leave together
   const KGroup &gr = groups[find_group(groups, ngroups, u, [](const KGroup &x) { return x.base; })];
   const uint32_t local = u - gr.base, nsamp = gr.sbase[gr.nruns], S = gr.stride;
   uint64_t c = 0;
@@ -189,9 +203,9 @@ __device__ __forceinline__ bool kw_before_lds(const SK *tile, uint32_t i, uint32
 // first splitter row of every merge window: window w starts at the first row
 // whose record rank G is >= w * kKWin (rows are sorted, G increasing)
 __global__ void ck_kw_bounds_kernel(const KGroup *groups, uint32_t ngroups, uint32_t nids, const uint64_t *G,
-                                    uint32_t *J) {
+                                    uint32_t *J, Abort stop) {
   const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
-  if (u >= nids) return;
+  if (u >= nids || stop()) return;
   const KGroup &gr = groups[find_group(groups, ngroups, u, [](const KGroup &x) { return x.base; })];
   const uint32_t j = u - gr.base, nsamp = gr.sbase[gr.nruns];
   const uint64_t N = gr.start[gr.nruns] - gr.start[0];
@@ -207,9 +221,11 @@ __global__ void ck_kw_bounds_kernel(const KGroup *groups, uint32_t ngroups, uint
 
 __global__ __launch_bounds__(kKThreads) void ck_kw_merge_kernel(const SK *in, SK *out, const KGroup *groups,
                                                                uint32_t ngroups, const uint32_t *C,
-                                                               const uint64_t *G, const uint32_t *J, KeyView kv) {
+                                                               const uint64_t *G, const uint32_t *J, KeyView kv,
+                                                               Abort stop) {
   __shared__ SK tile[kKRegion];
   __shared__ uint32_t s_j[2], s_off[kKWay + 1], s_lo[kKWay];
+  if (stop()) return; // uniform over the workgroup
   const KGroup &gr = groups[find_group(groups, ngroups, blockIdx.x, [](const KGroup &x) { return x.wg0; })];
   const uint32_t wl = blockIdx.x - gr.wg0, k = gr.nruns;
   const uint64_t *Gg = G + gr.base;
@@ -333,7 +349,8 @@ __device__ __forceinline__ uint64_t data_bytes(uint32_t kl, uint32_t vl) {
 __global__ __launch_bounds__(kFtThreads) void ck_keep_tile_kernel(const SK *s, uint64_t n, KeyView kv,
                                                                   const uint8_t *type, const uint32_t *kl,
                                                                   const uint32_t *vl, uint32_t base_level,
-                                                                  uint8_t *keep, uint64_t *tsum) {
+                                                                  uint8_t *keep, uint64_t *tsum, Abort stop) {
+  if (stop()) return; // uniform over the workgroup; the host rejects the job
   constexpr uint32_t kGroup = 4; // rows whose loads are in flight together
   const uint64_t t0 = static_cast<uint64_t>(blockIdx.x) * kFtTile;
   uint64_t v[3] = {0, 0, 0};
@@ -824,7 +841,8 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     uint64_t nruns = ntables;
     uint64_t *rb = pool.get<uint64_t>(nruns + 2);
     CK(hipMemcpyAsync(rb, run_start.data(), (nruns + 1) * 8, hipMemcpyHostToDevice, s));
-    ck_check_blocks_kernel<<<grid(nblocks), 256, 0, s>>>(A, rb_all, nblocks, rb, nruns, kv, bad);
+    const Abort dec_fail{err_count, errs, nullptr}, stop{err_count, errs, bad};
+    ck_check_blocks_kernel<<<grid(nblocks), 256, 0, s>>>(A, rb_all, nblocks, rb, nruns, kv, bad, dec_fail);
     // k-way merge passes; run boundaries of every pass are known on the host,
     // so all group descriptors go up in one upload (lives until the next sync)
     std::vector<KGroup> kg;
@@ -869,9 +887,9 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
         size_t at = 0;
         for (size_t p = 0; p < pass_groups.size(); p++) {
           const uint32_t ng = pass_groups[p];
-          ck_kw_split_kernel<<<grid(static_cast<uint64_t>(pass_ids[p]) * 8), 256, 0, s>>>(A, d_kg + at, ng, pass_ids[p], kv, Cm, Gm);
-          ck_kw_bounds_kernel<<<grid(pass_ids[p]), 256, 0, s>>>(d_kg + at, ng, pass_ids[p], Gm, Jm);
-          if (pass_wgs[p]) ck_kw_merge_kernel<<<pass_wgs[p], kKThreads, 0, s>>>(A, B, d_kg + at, ng, Cm, Gm, Jm, kv);
+          ck_kw_split_kernel<<<grid(static_cast<uint64_t>(pass_ids[p]) * 8), 256, 0, s>>>(A, d_kg + at, ng, pass_ids[p], kv, Cm, Gm, stop);
+          ck_kw_bounds_kernel<<<grid(pass_ids[p]), 256, 0, s>>>(d_kg + at, ng, pass_ids[p], Gm, Jm, stop);
+          if (pass_wgs[p]) ck_kw_merge_kernel<<<pass_wgs[p], kKThreads, 0, s>>>(A, B, d_kg + at, ng, Cm, Gm, Jm, kv, stop);
           std::swap(A, B);
           at += ng;
         }
@@ -882,7 +900,7 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     uint8_t *keep = pool.get<uint8_t>(n);
     uint64_t *tsum = pool.get<uint64_t>(3 * ftiles), *totals = pool.get<uint64_t>(3);
     ck_keep_tile_kernel<<<static_cast<uint32_t>(ftiles), kFtThreads, 0, s>>>(A, n, kv, R.type, R.kl, R.vl, base_level,
-                                                                          keep, tsum);
+                                                                          keep, tsum, stop);
     ck_tile_scan_kernel<<<1, kFtThreads, 0, s>>>(tsum, ftiles, totals);
     fetch(arena, pool, s, {totals, reinterpret_cast<const uint64_t *>(bad),
                            reinterpret_cast<const uint64_t *>(err_count), errs});

@@ -100,6 +100,36 @@ def test_compact_rejects_unsorted(codec, oracle):
         codec.compact([f], 4096, 1 << 20, 1)
 
 
+def test_compact_rejects_unsorted_multi_run(codec, oracle):
+    """An unsorted run among sorted ones, large enough for many merge windows:
+    the job is rejected (the merge kernels stand down on the device flag) and
+    the context stays usable."""
+    sets = W.compaction_inputs(3, 20_000, 50_000, seed=7, vmax=64, p_delete=0.1)
+    good = [oracle.table_build(r, 4096) for r in sets]
+    sets[1] = {key: v[::-1].copy() for key, v in sets[1].items()}  # keys descending
+    bad = [oracle.table_build(r, 4096) for r in sets]
+    with pytest.raises(Exception, match="not sorted"):
+        codec.compact(bad, 4096, 1 << 20, 1)
+    want, _ = oracle.compact(good, 4096, 1 << 20, 1)
+    outs, _ = codec.compact(good, 4096, 1 << 20, 1)
+    assert len(outs) == len(want) and all(np.array_equal(o, w) for o, w in zip(outs, want))
+
+
+def test_compact_rejects_corrupt_block(codec, oracle):
+    """A block whose extra is intact but whose entry lengths point outside it:
+    its records are never written, so everything after the decode must stand
+    down; the job reports the decode failure and the context stays usable."""
+    sets = W.compaction_inputs(4, 6000, 15_000, seed=8, vmax=64, p_delete=0.1)
+    ins = [oracle.table_build(r, 4096) for r in sets]
+    broken = ins[2].copy()
+    broken[1:5] = np.frombuffer(np.uint32(0xFFFF0000).tobytes(), np.uint8)  # entry 0 of block 0
+    with pytest.raises(Exception, match="decode"):
+        codec.compact([ins[0], ins[1], broken, ins[3]], 4096, 1 << 20, 1)
+    want, _ = oracle.compact(ins, 4096, 1 << 20, 1)
+    outs, _ = codec.compact(ins, 4096, 1 << 20, 1)
+    assert len(outs) == len(want) and all(np.array_equal(o, w) for o, w in zip(outs, want))
+
+
 def test_compact_no_records(codec, oracle):
     """No input records (no tables, or only empty 40 B SSTs): one empty output
     table, as DoCompactJob's first TableBuilder (compact.cc:234-243)."""
