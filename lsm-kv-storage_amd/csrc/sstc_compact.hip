@@ -36,7 +36,7 @@ namespace {
 // ------------------------------------------------------------------ kernels
 struct KeyView {
   const uint8_t *src;
-  const uint64_t *koff; // by record id
+  const RecX *rx; // by record id
 };
 
 using SK = SortKey;
@@ -61,8 +61,8 @@ __device__ __forceinline__ int key_cmp(uint64_t a0, uint64_t a1, uint32_t al, ui
   if (a0 != b0) return a0 < b0 ? -1 : 1;
   if (a1 != b1) return a1 < b1 ? -1 : 1;
   if (al > 16 && bl > 16) {
-    const uint8_t *pa = kv.src + kv.koff[aid];
-    const uint8_t *pb = kv.src + kv.koff[bid];
+    const uint8_t *pa = kv.src + kv.rx[aid].ko;
+    const uint8_t *pb = kv.src + kv.rx[bid].ko;
     const uint32_t m = al < bl ? al : bl;
     for (uint32_t j = 16; j < m; j++) {
       const uint32_t x = pa[j], y = pb[j];
@@ -347,9 +347,8 @@ __device__ __forceinline__ uint64_t data_bytes(uint32_t kl, uint32_t vl) {
 // its run of equal txns (records duplicated across inputs) to the head.
 // tsum[3 t + {0,1,2}] = kept records, their key+value bytes, their entry bytes.
 __global__ __launch_bounds__(kFtThreads) void ck_keep_tile_kernel(const SK *s, uint64_t n, KeyView kv,
-                                                                  const uint8_t *type, const uint32_t *kl,
-                                                                  const uint32_t *vl, uint32_t base_level,
-                                                                  uint8_t *keep, uint64_t *tsum, Abort stop) {
+                                                                  uint32_t base_level, uint8_t *keep,
+                                                                  uint64_t *tsum, Abort stop) {
   if (stop()) return; // uniform over the workgroup; the host rejects the job
   constexpr uint32_t kGroup = 4; // rows whose loads are in flight together
   const uint64_t t0 = static_cast<uint64_t>(blockIdx.x) * kFtTile;
@@ -366,7 +365,18 @@ __global__ __launch_bounds__(kFtThreads) void ck_keep_tile_kernel(const SK *s, u
         if (i > 0) pv[g] = s[i - 1];
       }
     }
-    uint32_t kk[kGroup], a8[kGroup] = {}, b8[kGroup] = {};
+    uint32_t kk[kGroup], vl[kGroup], ty[kGroup];
+#pragma unroll
+    for (uint32_t g = 0; g < kGroup; g++) { // the record's 16 B side fields, all rows in flight together
+      const uint64_t i = t0 + static_cast<uint64_t>(j0 + g) * kFtThreads + threadIdx.x;
+      vl[g] = 0;
+      ty[g] = 0;
+      if (i < n) {
+        const RecX r = kv.rx[x[g].id];
+        vl[g] = r.vl;
+        ty[g] = r.type;
+      }
+    }
 #pragma unroll
     for (uint32_t g = 0; g < kGroup; g++) {
       const uint64_t i = t0 + static_cast<uint64_t>(j0 + g) * kFtThreads + threadIdx.x;
@@ -375,7 +385,7 @@ __global__ __launch_bounds__(kFtThreads) void ck_keep_tile_kernel(const SK *s, u
         if (i == 0) {
           k = 1;
         } else if (key_cmp(pv[g].p0, pv[g].p1, pv[g].kl, pv[g].id, x[g].p0, x[g].p1, x[g].kl, x[g].id, kv) != 0) {
-          k = type[x[g].id] == kTypePut ? 1u : (base_level ? 0u : 1u);
+          k = ty[g] == kTypePut ? 1u : (base_level ? 0u : 1u);
         } else if (x[g].tx == pv[g].tx) {
           k = 1;
           for (uint64_t q = i - 1; q > 0; q--) { // run of equal txns back to the group head
@@ -394,15 +404,9 @@ __global__ __launch_bounds__(kFtThreads) void ck_keep_tile_kernel(const SK *s, u
 #pragma unroll
     for (uint32_t g = 0; g < kGroup; g++)
       if (kk[g]) {
-        a8[g] = kl[x[g].id];
-        b8[g] = vl[x[g].id];
-      }
-#pragma unroll
-    for (uint32_t g = 0; g < kGroup; g++)
-      if (kk[g]) {
         v[0] += 1;
-        v[1] += data_bytes(a8[g], b8[g]);
-        v[2] += entry_size(a8[g], b8[g]);
+        v[1] += data_bytes(x[g].kl, vl[g]);
+        v[2] += entry_size(x[g].kl, vl[g]);
       }
   }
   uint64_t tot[3];
@@ -438,14 +442,16 @@ __global__ __launch_bounds__(kFtThreads) void ck_tile_scan_kernel(uint64_t *tsum
 // bytes (table split), Pe = prefix sums of entry bytes (block split, encode)
 __global__ __launch_bounds__(kFtThreads) void ck_compact_tile_kernel(const SK *s, uint64_t n, const uint8_t *keep,
                                                                      const uint64_t *tsum, const uint64_t *totals,
-                                                                     Rec R, Rec out, uint64_t *Pd, uint64_t *Pe) {
+                                                                     const RecX *rx, Rec out, uint64_t *Pd,
+                                                                     uint64_t *Pe) {
   constexpr uint32_t kGroup = 4; // rows whose loads are in flight together
   const uint64_t t0 = static_cast<uint64_t>(blockIdx.x) * kFtTile;
   uint64_t base[3] = {tsum[3 * blockIdx.x], tsum[3 * blockIdx.x + 1], tsum[3 * blockIdx.x + 2]};
   for (uint32_t j0 = 0; j0 < kFtItems; j0 += kGroup) {
     if (t0 + static_cast<uint64_t>(j0) * kFtThreads >= n) break; // uniform over the workgroup
-    uint32_t km = 0, id[kGroup], kl[kGroup], vl[kGroup], ty[kGroup];
-    uint64_t tx[kGroup], ko[kGroup], vo[kGroup];
+    uint32_t km = 0, kl[kGroup], vl[kGroup], ty[kGroup];
+    uint64_t tx[kGroup], ko[kGroup];
+    SK x[kGroup];
 #pragma unroll
     for (uint32_t g = 0; g < kGroup; g++) {
       const uint64_t i = t0 + static_cast<uint64_t>(j0 + g) * kFtThreads + threadIdx.x;
@@ -454,17 +460,17 @@ __global__ __launch_bounds__(kFtThreads) void ck_compact_tile_kernel(const SK *s
 #pragma unroll
     for (uint32_t g = 0; g < kGroup; g++) {
       const uint64_t i = t0 + static_cast<uint64_t>(j0 + g) * kFtThreads + threadIdx.x;
-      id[g] = (km >> g) & 1u ? s[i].id : 0u;
+      x[g] = (km >> g) & 1u ? s[i] : SK{};
     }
 #pragma unroll
     for (uint32_t g = 0; g < kGroup; g++) {
       const bool k = (km >> g) & 1u;
-      kl[g] = k ? R.kl[id[g]] : 0u;
-      vl[g] = k ? R.vl[id[g]] : 0u;
-      ty[g] = k ? R.type[id[g]] : 0u;
-      tx[g] = k ? R.tx[id[g]] : 0ull;
-      ko[g] = k ? R.ko[id[g]] : 0ull;
-      vo[g] = k ? R.vo[id[g]] : 0ull;
+      const RecX r = k ? rx[x[g].id] : RecX{};
+      kl[g] = x[g].kl;
+      tx[g] = x[g].tx;
+      vl[g] = r.vl;
+      ty[g] = r.type;
+      ko[g] = r.ko;
     }
 #pragma unroll
     for (uint32_t g = 0; g < kGroup; g++) { // row by row: survivors of a row are lane-consecutive
@@ -479,7 +485,7 @@ __global__ __launch_bounds__(kFtThreads) void ck_compact_tile_kernel(const SK *s
         out.vl[q] = vl[g];
         out.tx[q] = tx[g];
         out.ko[q] = ko[g];
-        out.vo[q] = vo[g];
+        out.vo[q] = ty[g] != kTypeDeleted ? ko[g] + kl[g] + 4 : 0; // decode's val_off
         Pd[q] = base[1] + v[1];
         Pe[q] = base[2] + v[2];
       }
@@ -806,14 +812,14 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     }
     const uint64_t wsn = scan_workspace_elems(n + 1) + 64;
     uint64_t *ws2 = pool.get<uint64_t>(wsn);
-    Rec R{pool.get<uint8_t>(n), pool.get<uint32_t>(n), pool.get<uint32_t>(n), pool.get<uint64_t>(n),
-          pool.get<uint64_t>(n), pool.get<uint64_t>(n)};
+    RecX *RX = pool.get<RecX>(n);
     uint32_t *status = pool.get<uint32_t>(nblocks);
     SK *A = pool.get<SK>(n ? n : 1), *B = pool.get<SK>(n ? n : 1);
     unsigned long long *bad = reinterpret_cast<unsigned long long *>(pool.get<uint64_t>(1));
     CK(hipMemsetAsync(bad, 0, 8, s));
     DecArgs da{d_src, d_blk_off, d_blk_len, nblocks, rb_all,
-               sstc_records{R.type, R.kl, R.vl, R.tx, R.ko, R.vo}, txn_mode, status, err_count, A, bad};
+               sstc_records{}, txn_mode, status, err_count, A, bad};
+    da.rx = RX;
     CK(launch_decode(da, s));
     if (n == 0) { // DoCompactJob still finishes its first (empty) output table
       fetch(arena, pool, s, {reinterpret_cast<const uint64_t *>(err_count), errs});
@@ -837,7 +843,7 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
       return SSTC_OK;
     }
     // 2. sort keys + merge
-    const KeyView kv{d_src, R.ko};
+    const KeyView kv{d_src, RX};
     uint64_t nruns = ntables;
     uint64_t *rb = pool.get<uint64_t>(nruns + 2);
     CK(hipMemcpyAsync(rb, run_start.data(), (nruns + 1) * 8, hipMemcpyHostToDevice, s));
@@ -899,8 +905,8 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     const uint64_t ftiles = (n + kFtTile - 1) / kFtTile;
     uint8_t *keep = pool.get<uint8_t>(n);
     uint64_t *tsum = pool.get<uint64_t>(3 * ftiles), *totals = pool.get<uint64_t>(3);
-    ck_keep_tile_kernel<<<static_cast<uint32_t>(ftiles), kFtThreads, 0, s>>>(A, n, kv, R.type, R.kl, R.vl, base_level,
-                                                                          keep, tsum, stop);
+    ck_keep_tile_kernel<<<static_cast<uint32_t>(ftiles), kFtThreads, 0, s>>>(A, n, kv, base_level, keep, tsum,
+                                                                          stop);
     ck_tile_scan_kernel<<<1, kFtThreads, 0, s>>>(tsum, ftiles, totals);
     fetch(arena, pool, s, {totals, reinterpret_cast<const uint64_t *>(bad),
                            reinterpret_cast<const uint64_t *>(err_count), errs});
@@ -920,7 +926,7 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     // table split (key+value bytes, compact.cc:290) and the block split
     // (entry + offset-entry bytes, table_builder.cc:57-59) clamped at table ends
     uint64_t *Pd = pool.get<uint64_t>(m + 1), *Pe = pool.get<uint64_t>(m + 1);
-    ck_compact_tile_kernel<<<static_cast<uint32_t>(ftiles), kFtThreads, 0, s>>>(A, n, keep, tsum, totals, R, KR, Pd,
+    ck_compact_tile_kernel<<<static_cast<uint32_t>(ftiles), kFtThreads, 0, s>>>(A, n, keep, tsum, totals, RX, KR, Pd,
                                                                              Pe);
     uint64_t *tf = pool.get<uint64_t>(m + 1), *dn = pool.get<uint64_t>(2);
     segment(pool, Pd, 0, m, table_limit, nullptr, tf, dn, s, true);

@@ -509,12 +509,20 @@ __device__ __forceinline__ uint32_t decode_block(const DecArgs &a, const R &rd, 
     }
     if (i < n) {
       const uint64_t r = base + i;
-      a.out.type[r] = static_cast<uint8_t>(e.type);
-      a.out.key_len[r] = e.klen;
-      a.out.val_len[r] = e.vlen;
-      a.out.txn[r] = e.txn;
-      a.out.key_off[r] = off + s + 5;
-      a.out.val_off[r] = e.type != kTypeDeleted ? off + s + 9 + e.klen : 0;
+      if (a.rx) {
+        RecX x;
+        x.ko = off + s + 5;
+        x.vl = e.vlen;
+        x.type = e.type;
+        a.rx[r] = x;
+      } else {
+        a.out.type[r] = static_cast<uint8_t>(e.type);
+        a.out.key_len[r] = e.klen;
+        a.out.val_len[r] = e.vlen;
+        a.out.txn[r] = e.txn;
+        a.out.key_off[r] = off + s + 5;
+        a.out.val_off[r] = e.type != kTypeDeleted ? off + s + 9 + e.klen : 0;
+      }
       if (a.sk) {
         // 16 B big-endian key prefix (a key is followed by >= 40 B of block)
         SortKey k;

@@ -33,6 +33,14 @@ struct __attribute__((aligned(16))) SortKey {
   uint32_t kl, id;
 };
 
+// per-record fields of the compaction job beside its SortKey (key length and
+// txn live there): one 16 B gather per record instead of one per SoA column
+struct __attribute__((aligned(16))) RecX {
+  uint64_t ko;   // key offset in the source bytes (value offset = ko + kl + 4)
+  uint32_t vl;   // value length, kNoValue for a DELETE
+  uint32_t type; // ValueType
+};
+
 struct DecArgs {
   const uint8_t *src;
   const uint64_t *blk_off;
@@ -46,6 +54,7 @@ struct DecArgs {
   SortKey *sk = nullptr; // optional merge keys (compaction)
   // optional: count of records that sort before their predecessor in the block
   unsigned long long *unsorted = nullptr;
+  RecX *rx = nullptr; // compaction: written instead of the `out` columns
   uint32_t xcd = 0;
 };
 
