@@ -1335,11 +1335,21 @@ constexpr uint64_t kHopSpan = static_cast<uint64_t>(kWave) * kHopProbe;
 __device__ __forceinline__ uint64_t hop_below(const uint64_t *Pw, uint64_t add, uint64_t x0, uint64_t x1,
                                               uint64_t step, uint64_t target) {
   const uint32_t lane = lane_id();
+  // clamped, unconditional loads: all kHopProbe in flight together (a load
+  // under a branch is waited for before the branch joins)
+  uint64_t w[kHopProbe];
+#pragma unroll
+  for (uint32_t r = 0; r < kHopProbe; r++) {
+    const uint64_t x = x0 + (static_cast<uint64_t>(r) * kWave + lane) * step;
+    const uint64_t xc = x <= x1 ? x : x1;
+    w[r] = Pw[xc];
+  }
+  __builtin_amdgcn_sched_barrier(0); // keep the loads ahead of their uses
   bool b[kHopProbe];
 #pragma unroll
   for (uint32_t r = 0; r < kHopProbe; r++) {
     const uint64_t x = x0 + (static_cast<uint64_t>(r) * kWave + lane) * step;
-    b[r] = x <= x1 && Pw[x] + add * x < target;
+    b[r] = x <= x1 && w[r] + add * (x <= x1 ? x : x1) < target;
   }
   uint64_t nb = 0;
 #pragma unroll
@@ -1347,35 +1357,117 @@ __device__ __forceinline__ uint64_t hop_below(const uint64_t *Pw, uint64_t add, 
   return nb;
 }
 
+// exact hop from pos: the first x in [pos + 1, m] with W(x) >= target
+// (W(m) >= target), probing around pos + glen first when glen is known
+__device__ uint64_t hop_exact(const uint64_t *Pw, uint64_t add, uint64_t m, uint64_t pos, uint64_t glen,
+                              uint64_t target) {
+  uint64_t lo = pos + 1, hi = m;
+  if (glen) {
+    const uint64_t g0 = pos + glen > pos + 1 + kHopSpan / 2 ? pos + glen - kHopSpan / 2 : pos + 1;
+    const uint64_t g1 = g0 + kHopSpan - 1 < m ? g0 + kHopSpan - 1 : m;
+    const uint64_t nb = hop_below(Pw, add, g0, g1, 1, target);
+    if (nb == 0) hi = g0;
+    else if (g0 + nb <= g1) lo = hi = g0 + nb;
+    else lo = g1 + 1;
+  }
+  while (hi > lo) {
+    const uint64_t step = (hi - lo + kHopSpan) / kHopSpan; // ceil(span / kHopSpan)
+    const uint64_t nb = hop_below(Pw, add, lo, hi, step, target);
+    // probes below target form a prefix (W is monotone): answer in (lo + (nb - 1) step, lo + nb step]
+    const uint64_t h2 = lo + nb * step;
+    if (nb) lo = lo + (nb - 1) * step + 1;
+    hi = h2 < hi ? h2 : hi;
+  }
+  return lo;
+}
+
+// Speculation: once a segment length is known, one round loads kHopAhead
+// windows of kHopSpan records around pos + h * glen (h = 1..kHopAhead) in one
+// batch and resolves up to kHopAhead hops from registers; a hop whose answer
+// is not inside its window falls back to hop_exact and starts a new round.
+// Equal-sized tables: ~2 load round trips per kHopAhead tables instead of 2
+// per table.
+constexpr uint32_t kHopAhead = 8;
+
 __global__ __launch_bounds__(kWave) void seg_hops_kernel(const uint64_t *Pw, uint64_t add, uint64_t m,
                                                          uint64_t threshold, uint64_t *first, uint64_t *d_count) {
+  const uint32_t lane = lane_id();
   const uint64_t wm = Pw[m] + add * m;
-  uint64_t pos = 0, nseg = 0, glen = 0;
-  while (pos < m) {
-    if (lane_id() == 0) first[nseg] = pos;
-    nseg++;
-    const uint64_t target = Pw[pos] + add * pos + threshold;
-    if (wm < target) break; // the last segment runs to m
-    // answer: the first x in [pos + 1, m] with W(x) >= target (W(m) >= target)
-    uint64_t lo = pos + 1, hi = m;
-    if (glen) {
-      const uint64_t g0 = pos + glen > pos + 1 + kHopSpan / 2 ? pos + glen - kHopSpan / 2 : pos + 1;
-      const uint64_t g1 = g0 + kHopSpan - 1 < m ? g0 + kHopSpan - 1 : m;
-      const uint64_t nb = hop_below(Pw, add, g0, g1, 1, target);
-      if (nb == 0) hi = g0;
-      else if (g0 + nb <= g1) lo = hi = g0 + nb;
-      else lo = g1 + 1;
+  uint64_t pos = 0, nseg = 0, glen = 0, wpos = Pw[0];
+  bool done = false;
+  while (!done) {
+    if (glen == 0) { // no prediction yet: one exact hop
+      if (pos >= m) break;
+      if (lane == 0) first[nseg] = pos;
+      nseg++;
+      const uint64_t target = wpos + threshold;
+      if (wm < target) break; // the last segment runs to m
+      const uint64_t nx = hop_exact(Pw, add, m, pos, 0, target);
+      glen = nx - pos;
+      pos = nx;
+      if (pos >= m) break;
+      wpos = Pw[pos] + add * pos;
+      continue;
     }
-    while (hi > lo) {
-      const uint64_t step = (hi - lo + kHopSpan) / kHopSpan; // ceil(span / kHopSpan)
-      const uint64_t nb = hop_below(Pw, add, lo, hi, step, target);
-      // probes below target form a prefix (W is monotone): answer in (lo + (nb - 1) step, lo + nb step]
-      const uint64_t h2 = lo + nb * step;
-      if (nb) lo = lo + (nb - 1) * step + 1;
-      hi = h2 < hi ? h2 : hi;
+    uint64_t v[kHopAhead][kHopProbe], g0s[kHopAhead];
+#pragma unroll
+    for (uint32_t h = 0; h < kHopAhead; h++) {
+      const uint64_t e = pos + (h + 1) * glen;
+      g0s[h] = e > kHopSpan / 2 ? e - kHopSpan / 2 : 0;
+#pragma unroll
+      for (uint32_t r = 0; r < kHopProbe; r++) {
+        const uint64_t x = g0s[h] + static_cast<uint64_t>(r) * kWave + lane;
+        v[h][r] = Pw[x <= m ? x : m];
+      }
     }
-    glen = lo - pos;
-    pos = lo;
+    __builtin_amdgcn_sched_barrier(0); // all kHopAhead windows in flight together
+#pragma unroll
+    for (uint32_t h = 0; h < kHopAhead; h++) {
+#pragma unroll
+      for (uint32_t r = 0; r < kHopProbe; r++) {
+        const uint64_t x = g0s[h] + static_cast<uint64_t>(r) * kWave + lane;
+        // past m: >= any target (W(m) >= target)
+        v[h][r] = x <= m ? v[h][r] + add * x : ~0ull;
+      }
+    }
+#pragma unroll
+    for (uint32_t h = 0; h < kHopAhead; h++) {
+      if (lane == 0) first[nseg] = pos;
+      nseg++;
+      const uint64_t target = wpos + threshold;
+      if (wm < target) {
+        done = true;
+        break;
+      }
+      uint64_t nb = 0;
+#pragma unroll
+      for (uint32_t r = 0; r < kHopProbe; r++) nb += __popcll(__ballot(v[h][r] < target));
+      // records of the window at or before pos are below target too, so the
+      // answer is g0 + nb whenever it lies inside the window and nothing
+      // before the window can be the answer
+      const uint64_t g0 = g0s[h];
+      uint64_t nx, wnx;
+      const bool hit = nb < kHopSpan && (nb > 0 || g0 <= pos + 1);
+      if (hit) {
+        nx = g0 + nb;
+        uint64_t t = 0;
+#pragma unroll
+        for (uint32_t r = 0; r < kHopProbe; r++)
+          if (r == (nb >> 6)) t = v[h][r];
+        wnx = __shfl(t, static_cast<int>(nb & (kWave - 1)), kWave);
+      } else {
+        nx = hop_exact(Pw, add, m, pos, glen, target);
+        wnx = nx < m ? Pw[nx] + add * nx : wm;
+      }
+      glen = nx - pos;
+      pos = nx;
+      wpos = wnx;
+      if (pos >= m) {
+        done = true;
+        break;
+      }
+      if (!hit) break; // re-predict from the exact answer
+    }
   }
   if (lane_id() == 0) {
     first[nseg] = m;

@@ -13,5 +13,5 @@ for v in $vals; do
   export $var=$v
   timeout -k 10 300 rocprofv3 --kernel-trace -d gpurun_out/ab/t$v -o trace --output-format csv -- python3 tools/bench_compact.py $args > gpurun_out/ab/b$v.log 2>&1 || { echo "bench $v failed"; tail -20 gpurun_out/ab/b$v.log; exit 4; }
   echo "== $var=$v"; grep -o '"device_s_median": [0-9.e-]*' gpurun_out/ab/b$v.log; grep -o '"bit_exact[^,]*' gpurun_out/ab/b$v.log
-  python3 tools/trace_compact.py $(find gpurun_out/ab/t$v -name "*kernel_trace.csv" | head -1) | head -8
+  python3 tools/trace_compact.py $(find gpurun_out/ab/t$v -name "*kernel_trace.csv" | head -1) > gpurun_out/ab/k$v.txt; head -12 gpurun_out/ab/k$v.txt
 done
