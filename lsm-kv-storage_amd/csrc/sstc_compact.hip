@@ -358,25 +358,20 @@ __global__ __launch_bounds__(kFtThreads) void ck_keep_tile_kernel(const SK *s, u
 #pragma unroll
     for (uint32_t g = 0; g < kGroup; g++) { // row j: records t0 + 256 j + [0, 256), lane-consecutive
       const uint64_t i = t0 + static_cast<uint64_t>(j0 + g) * kFtThreads + threadIdx.x;
-      x[g] = SK{};
-      pv[g] = SK{};
-      if (i < n) {
-        x[g] = s[i];
-        if (i > 0) pv[g] = s[i - 1];
-      }
+      const uint64_t ic = i < n ? i : n - 1; // clamped, unconditional: the loads stay in flight together
+      x[g] = s[ic];
+      pv[g] = s[ic ? ic - 1 : 0];
     }
+    __builtin_amdgcn_sched_barrier(0);
     uint32_t kk[kGroup], vl[kGroup], ty[kGroup];
 #pragma unroll
     for (uint32_t g = 0; g < kGroup; g++) { // the record's 16 B side fields, all rows in flight together
       const uint64_t i = t0 + static_cast<uint64_t>(j0 + g) * kFtThreads + threadIdx.x;
-      vl[g] = 0;
-      ty[g] = 0;
-      if (i < n) {
-        const RecX r = kv.rx[x[g].id];
-        vl[g] = r.vl;
-        ty[g] = r.type;
-      }
+      const RecX r = kv.rx[x[g].id]; // unconditional (past n: the last record's)
+      vl[g] = i < n ? r.vl : 0u;
+      ty[g] = i < n ? r.type : 0u;
     }
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (uint32_t g = 0; g < kGroup; g++) {
       const uint64_t i = t0 + static_cast<uint64_t>(j0 + g) * kFtThreads + threadIdx.x;
@@ -452,20 +447,31 @@ __global__ __launch_bounds__(kFtThreads) void ck_compact_tile_kernel(const SK *s
     uint32_t km = 0, kl[kGroup], vl[kGroup], ty[kGroup];
     uint64_t tx[kGroup], ko[kGroup];
     SK x[kGroup];
+    // loads unconditional at clamped indices (a load under a branch is waited
+    // for before the branch joins): flags and keys of all rows, then the side
+    // records, each batch in flight together
+    uint32_t kb[kGroup];
 #pragma unroll
     for (uint32_t g = 0; g < kGroup; g++) {
       const uint64_t i = t0 + static_cast<uint64_t>(j0 + g) * kFtThreads + threadIdx.x;
-      if (i < n && keep[i]) km |= 1u << g;
+      const uint64_t ic = i < n ? i : n - 1;
+      kb[g] = keep[ic];
+      x[g] = s[ic];
     }
+    __builtin_amdgcn_sched_barrier(0);
+    RecX rr[kGroup];
+#pragma unroll
+    for (uint32_t g = 0; g < kGroup; g++) rr[g] = rx[x[g].id];
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (uint32_t g = 0; g < kGroup; g++) {
       const uint64_t i = t0 + static_cast<uint64_t>(j0 + g) * kFtThreads + threadIdx.x;
-      x[g] = (km >> g) & 1u ? s[i] : SK{};
+      if (i < n && kb[g]) km |= 1u << g;
     }
 #pragma unroll
     for (uint32_t g = 0; g < kGroup; g++) {
       const bool k = (km >> g) & 1u;
-      const RecX r = k ? rx[x[g].id] : RecX{};
+      const RecX r = k ? rr[g] : RecX{};
       kl[g] = x[g].kl;
       tx[g] = x[g].tx;
       vl[g] = r.vl;
