@@ -142,9 +142,24 @@ __device__ __forceinline__ uint32_t find_group(const KGroup *g, uint32_t ng, uin
   return lo;
 }
 
-__global__ __launch_bounds__(256) void ck_kw_split_kernel(const SK *in, const KGroup *groups, uint32_t ngroups,
-                                                          uint32_t nids, KeyView kv, uint32_t *C, uint64_t *G,
-                                                          Abort stop) {
+// the splitter records of a pass gathered by splitter id (run-major, sorted
+// within each run): the co-rank searches first run over this compact array
+// (a few MiB, cache resident) and only the last log2(S) probes touch the runs
+__global__ void ck_kw_sample_kernel(const SK *in, const KGroup *groups, uint32_t ngroups, uint32_t nids, SK *smp,
+                                    Abort stop) {
+  const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= nids || stop()) return;
+  const KGroup &gr = groups[find_group(groups, ngroups, u, [](const KGroup &x) { return x.base; })];
+  const uint32_t local = u - gr.base, nsamp = gr.sbase[gr.nruns];
+  if (local == nsamp) return; // sentinel row
+  uint32_t q = 0;
+  while (gr.sbase[q + 1] <= local) q++;
+  smp[u] = in[gr.start[q] + static_cast<uint64_t>(local - gr.sbase[q]) * gr.stride];
+}
+
+__global__ __launch_bounds__(256) void ck_kw_split_kernel(const SK *in, const SK *smp, const KGroup *groups,
+                                                          uint32_t ngroups, uint32_t nids, KeyView kv, uint32_t *C,
+                                                          uint64_t *G, Abort stop) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t u = t >> 3, r = t & 7u;
   if (u >= nids || stop()) return; // whole 8-lane groups leave together
@@ -162,8 +177,18 @@ __global__ __launch_bounds__(256) void ck_kw_split_kernel(const SK *in, const KG
       if (r == q) {
         c = p;
       } else {
-        const SK x = in[gr.start[q] + p];
-        uint64_t lo = 0, hi = len;
+        const SK x = smp[u];
+        // samples of run r (records j * S) that precede x: cs; then the
+        // co-rank lies in ((cs - 1) S, cs S]
+        const SK *rsmp = smp + gr.base + gr.sbase[r];
+        uint32_t slo = 0, shi = gr.sbase[r + 1] - gr.sbase[r];
+        while (slo < shi) {
+          const uint32_t mid = (slo + shi) >> 1;
+          if (kw_before(rsmp[mid], r, x, q, kv)) slo = mid + 1;
+          else shi = mid;
+        }
+        uint64_t lo = slo ? static_cast<uint64_t>(slo - 1) * S + 1 : 0;
+        uint64_t hi = static_cast<uint64_t>(slo) * S < len ? static_cast<uint64_t>(slo) * S : len;
         while (lo < hi) {
           const uint64_t mid = (lo + hi) >> 1;
           if (kw_before(in[rs + mid], r, x, q, kv)) lo = mid + 1;
@@ -896,10 +921,12 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
         uint32_t max_j = 0;
         for (size_t p = 0; p < pass_groups.size(); p++) max_j = std::max(max_j, pass_ids[p] + pass_wgs[p] + pass_groups[p]);
         uint32_t *Jm = pool.get<uint32_t>(max_j);
+        SK *Sm = pool.get<SK>(max_ids);
         size_t at = 0;
         for (size_t p = 0; p < pass_groups.size(); p++) {
           const uint32_t ng = pass_groups[p];
-          ck_kw_split_kernel<<<grid(static_cast<uint64_t>(pass_ids[p]) * 8), 256, 0, s>>>(A, d_kg + at, ng, pass_ids[p], kv, Cm, Gm, stop);
+          ck_kw_sample_kernel<<<grid(pass_ids[p]), 256, 0, s>>>(A, d_kg + at, ng, pass_ids[p], Sm, stop);
+          ck_kw_split_kernel<<<grid(static_cast<uint64_t>(pass_ids[p]) * 8), 256, 0, s>>>(A, Sm, d_kg + at, ng, pass_ids[p], kv, Cm, Gm, stop);
           ck_kw_bounds_kernel<<<grid(pass_ids[p]), 256, 0, s>>>(d_kg + at, ng, pass_ids[p], Gm, Jm, stop);
           if (pass_wgs[p]) ck_kw_merge_kernel<<<pass_wgs[p], kKThreads, 0, s>>>(A, B, d_kg + at, ng, Cm, Gm, Jm, kv, stop);
           std::swap(A, B);
