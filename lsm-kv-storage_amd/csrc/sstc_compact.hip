@@ -596,8 +596,9 @@ __global__ void ck_table_info_kernel(const uint64_t *tf, uint64_t nt, const uint
 }
 
 __global__ void ck_block_off_kernel(const uint32_t *btab, uint64_t nb, const uint64_t *BL, const uint64_t *tbf,
-                                    const uint64_t *toff, uint64_t *bo) {
+                                    const uint64_t *toff, uint64_t *bo, uint32_t *nbig) {
   const uint64_t b = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (b == 0) *nbig = 0; // the encode's large-block list starts empty
   if (b >= nb) return;
   const uint32_t t = btab[b];
   bo[b] = toff[t] + (BL[b] - BL[tbf[t]]);
@@ -776,32 +777,46 @@ __global__ void ck_pack_kernel(Words w, uint64_t *out) {
   if (threadIdx.x < w.n) out[threadIdx.x] = *w.p[threadIdx.x];
 }
 
-__global__ void ck_gather_words_kernel(const uint64_t *src, const uint64_t *idx, uint64_t n, uint64_t *out) {
+// run starts (record index of every input table's first block) to the device
+// and to the pinned host words; thread 0 also snapshots the context's decode
+// error counter and clears the unsorted count for this job
+__global__ void ck_run_starts_kernel(const uint64_t *rec_base, const uint64_t *tfb, uint64_t n, uint64_t *out,
+                                     uint64_t *host, const unsigned long long *err_count, uint64_t *errs,
+                                     unsigned long long *bad) {
   const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (i < n) out[i] = src[idx[i]];
+  if (i == 0) {
+    *errs = *err_count;
+    *bad = 0;
+  }
+  if (i < n) out[i] = host[i] = rec_base[tfb[i]];
 }
 
+// pinned, device-mapped, coherent host words: kernels store the job's few
+// host-bound values straight into them (no copy command per sync)
 void ensure_host(Arena &arena, uint64_t words) {
   if (arena.host && arena.host_cap >= words) return;
   if (arena.host) (void)hipHostFree(arena.host);
   arena.host = nullptr;
+  arena.host_dev = nullptr;
   arena.host_cap = 0;
   const uint64_t cap = words < 64 ? 64 : words;
-  if (hipHostMalloc(reinterpret_cast<void **>(&arena.host), cap * sizeof(uint64_t)) != hipSuccess) {
+  if (hipHostMalloc(reinterpret_cast<void **>(&arena.host), cap * sizeof(uint64_t),
+                    hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+      hipHostGetDevicePointer(reinterpret_cast<void **>(&arena.host_dev), arena.host, 0) != hipSuccess) {
+    if (arena.host) (void)hipHostFree(arena.host);
     arena.host = nullptr;
+    arena.host_dev = nullptr;
     throw std::runtime_error("pinned host words");
   }
   arena.host_cap = cap;
 }
 
-// device words -> pinned host words: one pack kernel, one copy, one sync
-void fetch(Arena &arena, Pool &pool, hipStream_t s, std::initializer_list<const uint64_t *> src) {
+// device words -> pinned host words: one pack kernel, one sync
+void fetch(Arena &arena, hipStream_t s, std::initializer_list<const uint64_t *> src) {
   ensure_host(arena, 64);
   Words w{};
   for (const uint64_t *p : src) w.p[w.n++] = p;
-  uint64_t *stage = pool.get<uint64_t>(8);
-  ck_pack_kernel<<<1, 64, 0, s>>>(w, stage);
-  CK(hipMemcpyAsync(arena.host, stage, w.n * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+  ck_pack_kernel<<<1, 64, 0, s>>>(w, arena.host_dev);
   CK(hipStreamSynchronize(s));
 }
 
@@ -827,12 +842,12 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     uint64_t *d_tfb = pool.get<uint64_t>(ntables + 1), *d_rs = pool.get<uint64_t>(ntables + 1);
     CK(launch_count(d_src, d_blk_off, d_blk_len, nblocks, rb_all, s));
     CK(launch_scan(rb_all, nblocks, 0, rb_all, ws, s));
-    CK(hipMemcpyAsync(errs, err_count, 8, hipMemcpyDeviceToDevice, s));
+    unsigned long long *bad = reinterpret_cast<unsigned long long *>(pool.get<uint64_t>(1));
     // record index of every input table's first record (its run start)
     CK(hipMemcpyAsync(d_tfb, h_tfb, (ntables + 1) * 8, hipMemcpyHostToDevice, s));
-    ck_gather_words_kernel<<<grid(ntables + 1), 256, 0, s>>>(rb_all, d_tfb, ntables + 1, d_rs);
     ensure_host(arena, ntables + 1);
-    CK(hipMemcpyAsync(arena.host, d_rs, (ntables + 1) * 8, hipMemcpyDeviceToHost, s));
+    ck_run_starts_kernel<<<grid(ntables + 1), 256, 0, s>>>(rb_all, d_tfb, ntables + 1, d_rs, arena.host_dev,
+                                                           err_count, errs, bad);
     CK(hipStreamSynchronize(s));
     std::vector<uint64_t> run_start(arena.host, arena.host + ntables + 1);
     const uint64_t n = run_start[ntables];
@@ -846,14 +861,12 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     RecX *RX = pool.get<RecX>(n);
     uint32_t *status = pool.get<uint32_t>(nblocks);
     SK *A = pool.get<SK>(n ? n : 1), *B = pool.get<SK>(n ? n : 1);
-    unsigned long long *bad = reinterpret_cast<unsigned long long *>(pool.get<uint64_t>(1));
-    CK(hipMemsetAsync(bad, 0, 8, s));
     DecArgs da{d_src, d_blk_off, d_blk_len, nblocks, rb_all,
                sstc_records{}, txn_mode, status, err_count, A, bad};
     da.rx = RX;
     CK(launch_decode(da, s));
     if (n == 0) { // DoCompactJob still finishes its first (empty) output table
-      fetch(arena, pool, s, {reinterpret_cast<const uint64_t *>(err_count), errs});
+      fetch(arena, s, {reinterpret_cast<const uint64_t *>(err_count), errs});
       if (arena.host[0] != arena.host[1]) {
         err = "an input block failed to decode";
         return SSTC_E_INVALID_ARG;
@@ -876,8 +889,7 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     // 2. sort keys + merge
     const KeyView kv{d_src, RX};
     uint64_t nruns = ntables;
-    uint64_t *rb = pool.get<uint64_t>(nruns + 2);
-    CK(hipMemcpyAsync(rb, run_start.data(), (nruns + 1) * 8, hipMemcpyHostToDevice, s));
+    const uint64_t *rb = d_rs; // run starts, nruns + 1
     const Abort dec_fail{err_count, errs, nullptr}, stop{err_count, errs, bad};
     ck_check_blocks_kernel<<<grid(nblocks), 256, 0, s>>>(A, rb_all, nblocks, rb, nruns, kv, bad, dec_fail);
     // k-way merge passes; run boundaries of every pass are known on the host,
@@ -941,7 +953,7 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     ck_keep_tile_kernel<<<static_cast<uint32_t>(ftiles), kFtThreads, 0, s>>>(A, n, kv, base_level, keep, tsum,
                                                                           stop);
     ck_tile_scan_kernel<<<1, kFtThreads, 0, s>>>(tsum, ftiles, totals);
-    fetch(arena, pool, s, {totals, reinterpret_cast<const uint64_t *>(bad),
+    fetch(arena, s, {totals, reinterpret_cast<const uint64_t *>(bad),
                            reinterpret_cast<const uint64_t *>(err_count), errs});
     if (arena.host[2] != arena.host[3]) {
       err = "an input block failed to decode";
@@ -967,7 +979,7 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     ck_table_end_kernel<<<grid(m + 1), 256, 0, s>>>(tf, dn, m, clamp);
     uint64_t *bf = pool.get<uint64_t>(m + 1);
     segment(pool, Pe, 16, m, block_threshold, clamp, bf, dn + 1, s, false);
-    fetch(arena, pool, s, {dn, dn + 1});
+    fetch(arena, s, {dn, dn + 1});
     const uint64_t nt = arena.host[0], nb = arena.host[1];
     if (nt > max_tables) {
       err = "more output tables than max_tables";
@@ -983,7 +995,7 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     uint64_t *tbf = pool.get<uint64_t>(nt + 1), *tdata = pool.get<uint64_t>(nt), *tmeta = pool.get<uint64_t>(nt);
     ck_table_info_kernel<<<grid(nt + 1), 256, 0, s>>>(tf, nt, bf, nb, BL, MS, tbf, tdata, tmeta, d_table_len);
     CK(launch_scan(d_table_len, nt, 0, d_table_off, ws2, s)); // d_table_off needs nt + 1 elements
-    fetch(arena, pool, s, {d_table_off + nt});
+    fetch(arena, s, {d_table_off + nt});
     const uint64_t total = arena.host[0];
     res[2] = nb;
     res[3] = nt;
@@ -993,16 +1005,16 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
       return SSTC_E_CAPACITY;
     }
     uint64_t *bo = pool.get<uint64_t>(nb);
-    ck_block_off_kernel<<<grid(nb), 256, 0, s>>>(btab, nb, BL, tbf, d_table_off, bo);
+    uint32_t *big = pool.get<uint32_t>(nb + 1);
+    ck_block_off_kernel<<<grid(nb), 256, 0, s>>>(btab, nb, BL, tbf, d_table_off, bo, big + nb);
     // 6. encode blocks, meta entries, footers
     EncArgs ea{d_src, d_src, sstc_records{KR.type, KR.kl, KR.vl, KR.tx, KR.ko, KR.vo}, bf, nb, Pe, bo, blen, d_dst, 1};
-    ea.big = pool.get<uint32_t>(nb + 1);
-    ea.nbig = ea.big + nb;
+    ea.big = big;
+    ea.nbig = big + nb;
     uint64_t *bmin = pool.get<uint64_t>(nb), *bmax = pool.get<uint64_t>(nb);
     uint64_t *tmin = pool.get<uint64_t>(nt), *tmax = pool.get<uint64_t>(nt);
     ea.bmin = bmin; // block min / max txn, reduced by the encode kernels
     ea.bmax = bmax;
-    CK(hipMemsetAsync(ea.nbig, 0, sizeof(uint32_t), s));
     CK(launch_enc_emit(ea, s));
     ck_meta_kernel<<<static_cast<uint32_t>((nb + 255) / 256), 256, 0, s>>>(bf, nb, btab, BL, MS, blen, tbf, d_table_off, tdata, KR, d_src, d_dst);
     ck_tab_minmax_kernel<<<static_cast<uint32_t>(nt), 256, 0, s>>>(tbf, bmin, bmax, tmin, tmax);

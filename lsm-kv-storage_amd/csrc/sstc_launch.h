@@ -121,7 +121,8 @@ hipError_t launch_segment(const uint64_t *Pw, uint64_t nrec, uint64_t threshold,
 struct Arena {
   void *base = nullptr;
   uint64_t cap = 0;
-  uint64_t *host = nullptr; // pinned host words: the job's few device -> host reads
+  uint64_t *host = nullptr;     // pinned host words: the job's few device -> host reads
+  uint64_t *host_dev = nullptr; // the same words as mapped into the device
   uint64_t host_cap = 0;
 };
 
