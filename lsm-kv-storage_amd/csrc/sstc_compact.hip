@@ -551,8 +551,9 @@ __global__ void ck_table_end_kernel(const uint64_t *tf, const uint64_t *d_nt, ui
 // block b: length, meta entry size, table index
 __global__ void ck_block_info_kernel(const uint64_t *bf, uint64_t nb, const uint64_t *Pe, const uint32_t *kl,
                                      const uint64_t *tf, uint64_t nt, uint64_t *blen, uint64_t *msz,
-                                     uint32_t *btab) {
+                                     uint32_t *btab, uint64_t *zws, uint64_t nz) {
   const uint64_t b = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (b < nz) zws[b] = 0; // look-back status words of the two block scans that follow
   if (b >= nb) return;
   const uint64_t f0 = bf[b], f1 = bf[b + 1];
   blen[b] = (Pe[f1] - Pe[f0]) + 16 * (f1 - f0) + 16;
@@ -840,8 +841,8 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     uint64_t *ws = pool.get<uint64_t>(nws);
     uint64_t *errs = pool.get<uint64_t>(2);
     uint64_t *d_tfb = pool.get<uint64_t>(ntables + 1), *d_rs = pool.get<uint64_t>(ntables + 1);
-    CK(launch_count(d_src, d_blk_off, d_blk_len, nblocks, rb_all, s));
-    CK(launch_scan(rb_all, nblocks, 0, rb_all, ws, s));
+    CK(launch_count(d_src, d_blk_off, d_blk_len, nblocks, rb_all, s, ws));
+    CK(launch_scan(rb_all, nblocks, 0, rb_all, ws, s, true));
     unsigned long long *bad = reinterpret_cast<unsigned long long *>(pool.get<uint64_t>(1));
     // record index of every input table's first record (its run start)
     CK(hipMemcpyAsync(d_tfb, h_tfb, (ntables + 1) * 8, hipMemcpyHostToDevice, s));
@@ -988,10 +989,12 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     // 5. layout
     uint64_t *blen = pool.get<uint64_t>(nb), *msz = pool.get<uint64_t>(nb);
     uint32_t *btab = pool.get<uint32_t>(nb);
-    ck_block_info_kernel<<<grid(nb), 256, 0, s>>>(bf, nb, Pe, KR.kl, tf, nt, blen, msz, btab);
+    const uint64_t nzb = scan_status_words(nb); // <= nb
+    uint64_t *ws3 = pool.get<uint64_t>(2 * nzb);
+    ck_block_info_kernel<<<grid(nb), 256, 0, s>>>(bf, nb, Pe, KR.kl, tf, nt, blen, msz, btab, ws3, 2 * nzb);
     uint64_t *BL = pool.get<uint64_t>(nb + 1), *MS = pool.get<uint64_t>(nb + 1);
-    CK(launch_scan(blen, nb, 0, BL, ws2, s));
-    CK(launch_scan(msz, nb, 0, MS, ws2, s));
+    CK(launch_scan(blen, nb, 0, BL, ws3, s, true));
+    CK(launch_scan(msz, nb, 0, MS, ws3 + nzb, s, true));
     uint64_t *tbf = pool.get<uint64_t>(nt + 1), *tdata = pool.get<uint64_t>(nt), *tmeta = pool.get<uint64_t>(nt);
     ck_table_info_kernel<<<grid(nt + 1), 256, 0, s>>>(tf, nt, bf, nb, BL, MS, tbf, tdata, tmeta, d_table_len);
     CK(launch_scan(d_table_len, nt, 0, d_table_off, ws2, s)); // d_table_off needs nt + 1 elements

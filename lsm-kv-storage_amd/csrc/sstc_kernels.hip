@@ -436,9 +436,17 @@ __global__ __launch_bounds__(kRtWaves *kWave, 8) void rt_kernel(RtArgs a) {
 // ---------------------------------------------------------------------------
 // Decode to the record table.
 // ---------------------------------------------------------------------------
+// grid-stride clear of nz words (a following scan's look-back status words),
+// folded into a kernel that runs anyway instead of a memset command
+__device__ __forceinline__ void zero_words(uint64_t *w, uint64_t nz) {
+  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+  for (uint64_t z = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; z < nz; z += stride) w[z] = 0;
+}
+
 __global__ void count_kernel(const uint8_t *src, const uint64_t *blk_off, const uint64_t *blk_len,
-                             uint64_t nblocks, uint64_t *counts) {
+                             uint64_t nblocks, uint64_t *counts, uint64_t *zws, uint64_t nz) {
   const uint64_t b = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  zero_words(zws, nz); // the look-back status words of the scan that follows
   if (b >= nblocks) return;
   const uint64_t len = blk_len[b];
   uint64_t c = 0;
@@ -1115,6 +1123,9 @@ struct SegArgs {
   uint32_t *J0, *Fx, *Fc; // by record
   uint64_t *win;          // per tile: entry-window size (scanned into node bases)
   uint64_t *first, *d_count;
+  uint64_t *zws;          // cleared here: the win scan's look-back status words
+  uint64_t nz;
+  uint32_t *tentry;       // cleared here: tiles + 1 entry counters
 };
 
 __global__ __launch_bounds__(kChThreads) void seg_walk_kernel(SegArgs a) {
@@ -1127,6 +1138,11 @@ __global__ __launch_bounds__(kChThreads) void seg_walk_kernel(SegArgs a) {
   const uint64_t c1 = c0 + kChTile < a.m ? c0 + kChTile : a.m;
   const uint32_t len = static_cast<uint32_t>(c1 - c0);
   const uint64_t nl = a.m + 1 - c0 < kLw ? a.m + 1 - c0 : kLw;
+  if (tid == 0) {
+    a.tentry[blockIdx.x] = 0;
+    if (blockIdx.x == 0) a.tentry[gridDim.x] = 0;
+    for (uint64_t z = blockIdx.x; z < a.nz; z += gridDim.x) a.zws[z] = 0;
+  }
   { // all loads of the window in flight before the LDS stores
     constexpr uint32_t kFill = kLw / kChThreads;
     uint64_t v[kFill];
@@ -1633,8 +1649,9 @@ hipError_t launch_roundtrip(const RtArgs &a, hipStream_t s) {
 }
 
 hipError_t launch_count(const uint8_t *src, const uint64_t *blk_off, const uint64_t *blk_len,
-                        uint64_t nblocks, uint64_t *counts, hipStream_t s) {
-  if (nblocks) count_kernel<<<grid_for(nblocks, 256), 256, 0, s>>>(src, blk_off, blk_len, nblocks, counts);
+                        uint64_t nblocks, uint64_t *counts, hipStream_t s, uint64_t *scan_ws) {
+  const uint64_t nz = scan_ws ? scan_status_words(nblocks) : 0;
+  if (nblocks) count_kernel<<<grid_for(nblocks, 256), 256, 0, s>>>(src, blk_off, blk_len, nblocks, counts, scan_ws, nz);
   return hipGetLastError();
 }
 
@@ -1647,15 +1664,19 @@ hipError_t launch_decode(const DecArgs &a, hipStream_t s) {
 
 uint64_t scan_workspace_elems(uint64_t n) { return (n + kLbTile - 1) / kLbTile + 2; }
 
+uint64_t scan_status_words(uint64_t n) { return n <= kScanTile ? 0 : (n + kLbTile - 1) / kLbTile + 1; }
+
 hipError_t launch_scan(const uint64_t *in, uint64_t n, uint64_t carry_in, uint64_t *out, uint64_t *ws,
-                       hipStream_t s) {
+                       hipStream_t s, bool ws_zeroed) {
   if (n <= kScanTile) {
     scan_apply_kernel<<<1, kScanThreads, 0, s>>>(in, n, nullptr, carry_in, out);
     return hipGetLastError();
   }
   const uint64_t tiles = (n + kLbTile - 1) / kLbTile;
-  hipError_t e = hipMemsetAsync(ws, 0, (tiles + 1) * sizeof(uint64_t), s);
-  if (e != hipSuccess) return e;
+  if (!ws_zeroed) {
+    hipError_t e = hipMemsetAsync(ws, 0, (tiles + 1) * sizeof(uint64_t), s);
+    if (e != hipSuccess) return e;
+  }
   scan_lookback_kernel<<<static_cast<uint32_t>(tiles), kScanThreads, 0, s>>>(in, n, carry_in, out, ws);
   return hipGetLastError();
 }
@@ -1727,16 +1748,15 @@ hipError_t launch_segment(const uint64_t *Pw, uint64_t nrec, uint64_t threshold,
   const SegLayout L(nrec);
   // u64 region 8-aligned relative to J (J itself is 256-aligned by the callers' allocators)
   uint64_t *U = reinterpret_cast<uint64_t *>(J + L.u64);
-  uint64_t *win = U + L.win, *base = U + L.base, *nn = U + L.nn, *visits = U + L.visits, *sws = U + L.sws;
+  uint64_t *win = U + L.win, *base = U + L.base, *visits = U + L.visits, *sws = U + L.sws;
   uint32_t *tentry = J + L.tentry, *tbefore = J + L.tbefore;
   const uint64_t stride = nrec + 1;
-  SegArgs a{Pw, add, nrec, threshold, clamp, J + L.J0, J + L.Fx, J + L.Fc, win, blk_first, d_nblocks};
+  SegArgs a{Pw, add, nrec, threshold, clamp, J + L.J0, J + L.Fx, J + L.Fc, win, blk_first, d_nblocks,
+            sws, scan_status_words(L.tiles), tentry};
   seg_walk_kernel<<<static_cast<uint32_t>(L.tiles), kChThreads, 0, s>>>(a);
-  hipError_t e = launch_scan(win, L.tiles, 0, base, sws, s); // base[tiles] = node count
+  hipError_t e = launch_scan(win, L.tiles, 0, base, sws, s, true); // base[tiles] = node count
   if (e != hipSuccess) return e;
-  e = hipMemcpyAsync(nn, base + L.tiles, sizeof(uint64_t), hipMemcpyDeviceToDevice, s);
-  if (e == hipSuccess) e = hipMemsetAsync(tentry, 0, (L.tiles + 1) * sizeof(uint32_t), s);
-  if (e != hipSuccess) return e;
+  const uint64_t *nn = base + L.tiles;
   NodeArgs na{J + L.Fx, J + L.Fc, base, nrec, L.tiles, J + L.Nx, J + L.Nc, J + L.Nt};
   seg_node_kernel<<<static_cast<uint32_t>(L.tiles), 256, 0, s>>>(na);
   const uint32_t pg = static_cast<uint32_t>(std::min<uint64_t>(grid_for(nrec + 1, 256), 2048));

@@ -101,11 +101,15 @@ hipError_t launch_get(const GetArgs &a, hipStream_t s);
 
 hipError_t launch_roundtrip(const RtArgs &a, hipStream_t s);
 hipError_t launch_count(const uint8_t *src, const uint64_t *blk_off, const uint64_t *blk_len,
-                        uint64_t nblocks, uint64_t *counts, hipStream_t s);
+                        uint64_t nblocks, uint64_t *counts, hipStream_t s, uint64_t *scan_ws = nullptr);
 hipError_t launch_decode(const DecArgs &a, hipStream_t s);
 uint64_t scan_workspace_elems(uint64_t n);
+// look-back status words a scan of n items needs cleared (0: single-workgroup scan)
+uint64_t scan_status_words(uint64_t n);
+// ws_zeroed: the caller cleared scan_status_words(n) words of ws in an earlier
+// kernel on the same stream (launch_count's scan_ws, ...), no memset here
 hipError_t launch_scan(const uint64_t *in, uint64_t n, uint64_t carry_in, uint64_t *out, uint64_t *ws,
-                       hipStream_t s);
+                       hipStream_t s, bool ws_zeroed = false);
 hipError_t launch_enc_sizes(const uint32_t *klen, const uint32_t *vlen, uint64_t nrec, uint64_t add,
                             uint64_t *sizes, hipStream_t s);
 hipError_t launch_enc_blk_len(const uint64_t *P, const uint64_t *blk_first, uint64_t nblocks,
