@@ -166,3 +166,18 @@ def test_live_reference(oracle, reflib, seed):
         fs = reflib.table_build(p, rec, 4096)
         assert np.array_equal(np.fromfile(p, np.uint8), oracle.table_build(rec, 4096))
         assert fs == os.path.getsize(p) + 1
+
+
+def test_oracle_fuzz_self_consistent(oracle):
+    """The corrupted-block set of tests/test_gpu_fuzz.py on the oracle alone:
+    its round trip and its decode agree on every block's status (except
+    NO_ROOM: a block that decodes but whose re-encoding outgrows its slot),
+    and the set mixes valid blocks with several distinct fault codes."""
+    from fuzz_blocks import fuzz_blocks
+    src, offs, lens, _ = fuzz_blocks(oracle, 0, nrec=3000)
+    _, _, st, _ = oracle.roundtrip(src, offs, lens, 0)
+    dec = np.array([oracle.decode_block(src[int(o):int(o + n)], 0, int(o))[0] for o, n in zip(offs, lens)])
+    no_room = st == 8  # ORC_BLK_NO_ROOM
+    assert (dec[no_room] == 0).all() and no_room.any()
+    assert np.array_equal(st[~no_room], dec[~no_room])
+    assert (st == 0).any() and len(set(st.tolist())) >= 5
