@@ -1308,34 +1308,90 @@ __global__ void seg_nentry_kernel(const uint32_t *Nx, const uint32_t *Nc, const 
   tbefore[t] = static_cast<uint32_t>(before);
 }
 
+// Block starts of a visited tile: the chain from its entry position, marked
+// by doubling inside the tile (every marked position marks its 2^r-th
+// successor, then the successor pointers double; a round that adds no mark
+// leaves the marked set closed, i.e. complete), then numbered by a prefix
+// count of the marks: O(log chain) barriers instead of a serial walk (a tile
+// of 64 KiB values is a 2048-step chain).  Chains estimated at <= 128 steps
+// (e.g. 4 KiB blocks of small records: ~73 per tile) are walked by one thread.
 __global__ __launch_bounds__(kChThreads) void seg_emit_kernel(const uint32_t *J0, uint64_t m, const uint32_t *tentry,
                                                               const uint32_t *tbefore, uint64_t *first) {
-  __shared__ uint32_t js[kChTile];
+  constexpr uint32_t kPer = kChTile / kChThreads;
+  constexpr uint16_t kOut = 0xFFFF; // successor outside the tile
+  constexpr uint32_t kSerialChain = 128;
+  __shared__ uint16_t nx[kChTile];
+  __shared__ uint8_t mk[kChTile];
+  __shared__ uint32_t s_wsum[kChThreads / kWave];
   const uint64_t k = blockIdx.x;
   const uint32_t e = tentry[k];
   if (!e) return; // a segment spans the whole tile
   const uint64_t c0 = k * kChTile, c1 = c0 + kChTile < m ? c0 + kChTile : m;
+  const uint32_t len = static_cast<uint32_t>(c1 - c0), tid = threadIdx.x;
   {
-    constexpr uint32_t kFill = kChTile / kChThreads;
-    uint32_t v[kFill];
+    uint32_t v[kPer];
 #pragma unroll
-    for (uint32_t r = 0; r < kFill; r++) {
-      const uint32_t p = threadIdx.x + r * kChThreads;
-      v[r] = p < c1 - c0 ? J0[c0 + p] : 0;
+    for (uint32_t r = 0; r < kPer; r++) {
+      const uint32_t p = tid + r * kChThreads;
+      v[r] = J0[c0 + (p < len ? p : len - 1)];
     }
 #pragma unroll
-    for (uint32_t r = 0; r < kFill; r++) {
-      const uint32_t p = threadIdx.x + r * kChThreads;
-      if (p < c1 - c0) js[p] = v[r];
+    for (uint32_t r = 0; r < kPer; r++) {
+      const uint32_t p = tid + r * kChThreads;
+      nx[p] = p < len && v[r] < c1 ? static_cast<uint16_t>(v[r] - c0) : kOut;
+      mk[p] = p == e - 1;
     }
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    uint64_t pos = c0 + e - 1, b = tbefore[k];
-    while (pos < c1) {
-      first[b++] = pos;
-      pos = js[pos - c0];
+  { // short chain (estimated from its first segment): one thread walks it
+    const uint32_t s0 = e - 1, q0 = nx[s0];
+    const uint32_t seg = q0 == kOut ? len - s0 : q0 - s0;
+    if ((len - s0) / seg <= kSerialChain) {
+      if (tid == 0) {
+        uint64_t b = tbefore[k];
+        for (uint32_t pos = s0; pos != kOut;) {
+          first[b++] = c0 + pos;
+          pos = nx[pos];
+        }
+      }
+      return;
     }
+  }
+  for (;;) {
+    uint16_t nn[kPer];
+    int added = 0;
+#pragma unroll
+    for (uint32_t r = 0; r < kPer; r++) {
+      const uint32_t p = tid * kPer + r;
+      const uint16_t q = nx[p];
+      nn[r] = kOut;
+      if (q != kOut) {
+        if (mk[p] && !mk[q]) {
+          mk[q] = 1;
+          added = 1;
+        }
+        nn[r] = nx[q];
+      }
+    }
+    if (!__syncthreads_or(added)) break;
+#pragma unroll
+    for (uint32_t r = 0; r < kPer; r++) nx[tid * kPer + r] = nn[r];
+    __syncthreads();
+  }
+  // number the marks: kPer contiguous positions per thread, workgroup scan
+  uint32_t cnt = 0;
+#pragma unroll
+  for (uint32_t r = 0; r < kPer; r++) cnt += mk[tid * kPer + r];
+  const uint32_t incl = wave_incl_scan_u32(cnt);
+  if (lane_id() == kWave - 1) s_wsum[tid / kWave] = incl;
+  __syncthreads();
+  uint32_t rank = incl - cnt;
+  for (uint32_t w = 0; w < tid / kWave; w++) rank += s_wsum[w];
+  const uint64_t b0 = tbefore[k];
+#pragma unroll
+  for (uint32_t r = 0; r < kPer; r++) {
+    const uint32_t p = tid * kPer + r;
+    if (mk[p]) first[b0 + rank++] = c0 + p;
   }
 }
 
