@@ -739,13 +739,13 @@ __device__ __forceinline__ void copy_span(uint8_t *dp, const uint8_t *sp, uint64
   for (uint64_t k0 = 0; k0 < nch; k0 += static_cast<uint64_t>(nt) * kEmitUnroll) {
     u32x4 v0[kEmitUnroll], v1[kEmitUnroll];
 #pragma unroll
-    for (uint32_t u = 0; u < kEmitUnroll; u++) {
+    for (uint32_t u = 0; u < kEmitUnroll; u++) { // clamped, unconditional: all loads in flight together
       const uint64_t k = k0 + static_cast<uint64_t>(u) * nt + t;
-      if (k < nch) {
-        v0[u] = sa[k];
-        v1[u] = sh ? sa[k + 1] : v0[u];
-      }
+      const uint64_t kc = k < nch ? k : nch - 1;
+      v0[u] = sa[kc];
+      v1[u] = sa[kc + 1]; // <= 16 B past the last full chunk (inside the allowance)
     }
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (uint32_t u = 0; u < kEmitUnroll; u++) {
       const uint64_t k = k0 + static_cast<uint64_t>(u) * nt + t;
