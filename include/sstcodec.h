@@ -232,6 +232,40 @@ int sstc_get_batch(sstc_ctx *ctx, const uint8_t *d_src, const sstc_block_index *
                    const uint64_t *d_q_key_off, const uint32_t *d_q_key_len, uint64_t nq, uint32_t *d_out_type,
                    uint64_t *d_out_val_off, uint32_t *d_out_val_len, uint64_t *d_out_block);
 
+/* ---- SST open on the device (replaces CreateAndSetupDataForTableReader's
+ *      DecodeExtraInfo + FetchBlockIndexInfo, sstable/table_reader.cc:52-156,
+ *      for many tables at once) --------------------------------------------- */
+
+#define SSTC_TAB_OK 0
+#define SSTC_TAB_BAD_FOOTER 1 /* image < 40 B, or the footer's meta section lies  */
+                              /* outside the image                               */
+#define SSTC_TAB_BAD_META 2   /* the meta section ends (or an entry runs past it)  */
+                              /* before num_blocks entries                       */
+#define SSTC_TAB_BAD_BLOCK 3  /* a block range lies outside the data section       */
+#define SSTC_TAB_TOO_LARGE 4  /* meta section >= 4 GiB                             */
+
+/* Table t is the SST image d_src[h_tab_off[t] .. + h_tab_bytes[t]) with
+ * h_tab_bytes[t] = TableBuilder::GetFileSize() - 1 (the reference reads the
+ * footer at file_size - 40 - 1).  The footers are read and the meta sections
+ * parsed on the device (the length-prefixed entry chain is recovered by
+ * pointer doubling over 32 KiB tiles, not walked): table t's blocks are
+ * [h_table_first_block[t], h_table_first_block[t+1]) of the outputs, with
+ * d_blk_off / d_first_key_off / d_last_key_off ABSOLUTE offsets into d_src,
+ * so (d_blk_off, d_blk_len, d_last_key_off, d_last_key_len, keys = d_src,
+ * d_table_first_block) is an sstc_block_index and (d_blk_off, d_blk_len,
+ * h_table_first_block) is sstc_compact's input.  Per-table status in
+ * h_table_status (SSTC_TAB_*): a table with a rejected footer gets no blocks;
+ * for BAD_META its block entries are undefined; for BAD_BLOCK the entries are
+ * the raw meta values.  h_footer (5 words per table: num_blocks, meta offset,
+ * meta length, min txn, max txn; NULL to skip), d_table_first_block (NULL to
+ * skip).  Returns SSTC_E_CAPACITY (with h_table_first_block filled) when
+ * more than max_blocks blocks are listed.  Synchronises the stream. */
+int sstc_open_tables(sstc_ctx *ctx, const uint8_t *d_src, uint64_t src_bytes, const uint64_t *h_tab_off,
+                     const uint64_t *h_tab_bytes, uint32_t ntables, uint64_t max_blocks, uint64_t *d_blk_off,
+                     uint64_t *d_blk_len, uint64_t *d_first_key_off, uint32_t *d_first_key_len,
+                     uint64_t *d_last_key_off, uint32_t *d_last_key_len, uint64_t *d_table_first_block,
+                     uint64_t *h_table_first_block, int32_t *h_table_status, uint64_t *h_footer);
+
 /* ---- file-to-file compaction (Compact::DoCompactJob end to end: the input
  *      SST files are read, compacted on the device and the output SSTs written
  *      and fsync'ed, db/compact.cc:232-322 with io/linux_file.cc:138-195) --- */

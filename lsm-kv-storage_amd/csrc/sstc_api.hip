@@ -284,6 +284,29 @@ int sstc_compact(sstc_ctx *c, const uint8_t *d_src, const uint64_t *d_blk_off, c
   return SSTC_OK;
 }
 
+int sstc_open_tables(sstc_ctx *c, const uint8_t *d_src, uint64_t src_bytes, const uint64_t *h_tab_off,
+                     const uint64_t *h_tab_bytes, uint32_t ntables, uint64_t max_blocks, uint64_t *d_blk_off,
+                     uint64_t *d_blk_len, uint64_t *d_first_key_off, uint32_t *d_first_key_len,
+                     uint64_t *d_last_key_off, uint32_t *d_last_key_len, uint64_t *d_table_first_block,
+                     uint64_t *h_table_first_block, int32_t *h_table_status, uint64_t *h_footer) {
+  if (!c || !h_table_first_block || (ntables && (!d_src || !h_tab_off || !h_tab_bytes || !h_table_status)))
+    return fail(SSTC_E_INVALID_ARG, "sstc_open_tables: NULL argument");
+  if (max_blocks && (!d_blk_off || !d_blk_len || !d_first_key_off || !d_first_key_len || !d_last_key_off ||
+                     !d_last_key_len))
+    return fail(SSTC_E_INVALID_ARG, "sstc_open_tables: NULL output array");
+  for (uint32_t t = 0; t < ntables; t++)
+    if (h_tab_off[t] > src_bytes || h_tab_bytes[t] > src_bytes - h_tab_off[t])
+      return fail(SSTC_E_INVALID_ARG, "sstc_open_tables: table image outside d_src");
+  if (int r = bind_device(c)) return r;
+  const sstc::OpenOut o{d_blk_off, d_blk_len, d_first_key_off, d_last_key_off, d_table_first_block,
+                        d_first_key_len, d_last_key_len};
+  std::string err;
+  const int rc = sstc::open_tables_impl(c->arena, c->stream, d_src, src_bytes, h_tab_off, h_tab_bytes, ntables,
+                                        max_blocks, o, h_table_first_block, h_table_status, h_footer, err);
+  if (rc != SSTC_OK) return fail(rc, ("sstc_open_tables: " + err).c_str());
+  return SSTC_OK;
+}
+
 int sstc_get_batch(sstc_ctx *c, const uint8_t *d_src, const sstc_block_index *index, const uint32_t *d_q_table,
                    const uint8_t *d_q_keys, uint64_t q_keys_bytes, const uint64_t *d_q_key_off,
                    const uint32_t *d_q_key_len, uint64_t nq, uint32_t *d_out_type, uint64_t *d_out_val_off,

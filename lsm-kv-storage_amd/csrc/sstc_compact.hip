@@ -1032,3 +1032,328 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
 }
 
 } // namespace sstc
+
+// ------------------------------------------------------------------ SST open
+// DecodeExtraInfo + FetchBlockIndexInfo (sstable/table_reader.cc:52-156) for
+// many SST images at once.  The meta section is a length-prefixed stream
+// (entry = u32 fkl | first key | u32 lkl | last key | u64 block offset | u64
+// block size, table_builder.cc:101-145) with no offset table, so the entry
+// starts are the chain 0 -> next(0) -> ... with next(p) = p + 24 + fkl + lkl.
+// It is recovered in parallel, 32 KiB tiles of the section at a time:
+//   ot_tile_kernel  next(p) for every byte position p of the tile; pointer
+//                   doubling in LDS gives, for every p, the entries the chain
+//                   from p holds inside the tile and the first chain position
+//                   past the tile (its exit)
+//   ot_hop_kernel   one lane per table follows the exits tile to tile
+//                   (section bytes / 32 KiB dependent loads) and records where
+//                   the chain enters each tile and with which entry index
+//   ot_emit_kernel  every entered tile marks its chain positions by doubling
+//                   from the entry point (after round r the first 2^(r+1)
+//                   positions are marked), ranks them with a workgroup scan
+//                   and writes the block index entries
+namespace sstc {
+namespace {
+
+constexpr uint32_t kOtTile = 32768, kOtThreads = 1024, kOtPer = kOtTile / kOtThreads;
+constexpr uint32_t kOtRounds = 11; // 2^11 > 32768 / 24 chain positions per tile
+constexpr uint16_t kOtOut = 0xFFFF;
+constexpr uint32_t kOtBad = 0xFFFFFFFFu;
+
+struct OtTable {
+  uint64_t meta;  // absolute offset of the meta section in d_src
+  uint64_t data;  // absolute offset of the table image (block offsets are relative to it)
+  uint64_t moff;  // data section length = meta section offset
+  uint64_t nb;    // footer num_blocks (0 for a table whose footer is rejected)
+  uint64_t fb;    // first output block
+  uint32_t mlen;  // meta section length (< 2^32 - 1)
+  uint32_t tile0; // first tile
+};
+
+__device__ __forceinline__ uint32_t ot_find(const OtTable *t, uint32_t nt, uint32_t g) {
+  uint32_t lo = 0, hi = nt; // last table with tile0 <= g
+  while (lo + 1 < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (t[mid].tile0 <= g) lo = mid;
+    else hi = mid;
+  }
+  return lo;
+}
+
+// next(p) for section position p, or kOtBad when the entry at p runs past the
+// section (the bounds FetchBlockIndexInfo leaves unchecked)
+__device__ __forceinline__ uint32_t ot_next(const uint8_t *m, uint32_t mlen, uint32_t p) {
+  if (static_cast<uint64_t>(p) + 4 > mlen) return kOtBad;
+  const uint64_t q = static_cast<uint64_t>(p) + 4 + g_u32u(m + p);
+  if (q + 4 > mlen) return kOtBad;
+  const uint64_t e = q + 20 + g_u32u(m + q);
+  return e > mlen ? kOtBad : static_cast<uint32_t>(e);
+}
+
+__global__ void ot_footer_kernel(const uint8_t *src, const uint64_t *foot_at, uint32_t nt, uint64_t *out) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nt || foot_at[t] == ~uint64_t(0)) return;
+  const uint8_t *f = src + foot_at[t];
+#pragma unroll
+  for (int k = 0; k < 5; k++) out[5 * static_cast<uint64_t>(t) + k] = g_u64u(f + 8 * k);
+}
+
+__global__ __launch_bounds__(kOtThreads) void ot_tile_kernel(const uint8_t *src, const OtTable *tabs, uint32_t nt,
+                                                             uint64_t *EC, uint32_t *tstart) {
+  __shared__ uint16_t sL[kOtTile]; // last in-tile position of the chain from p
+  __shared__ uint16_t sC[kOtTile]; // hops from p to it
+  const uint32_t g = blockIdx.x;
+  const OtTable T = tabs[ot_find(tabs, nt, g)];
+  const uint8_t *m = src + T.meta;
+  const uint32_t t0 = (g - T.tile0) * kOtTile;
+  const uint32_t n = min(kOtTile, T.mlen - t0);
+  if (threadIdx.x == 0) tstart[g] = kOtBad;
+  for (uint32_t k = 0; k < kOtPer; k++) {
+    const uint32_t p = threadIdx.x + k * kOtThreads;
+    if (p >= n) break;
+    const uint32_t e = ot_next(m, T.mlen, t0 + p);
+    const bool in = e != kOtBad && e < t0 + n;
+    sL[p] = static_cast<uint16_t>(in ? e - t0 : p);
+    sC[p] = in ? 1 : 0;
+  }
+  __syncthreads();
+  for (uint32_t r = 0; r < kOtRounds; r++) {
+    uint16_t l[kOtPer], c[kOtPer];
+#pragma unroll
+    for (uint32_t k = 0; k < kOtPer; k++) {
+      const uint32_t p = threadIdx.x + k * kOtThreads;
+      if (p < n) {
+        const uint32_t j = sL[p];
+        l[k] = sL[j];
+        c[k] = static_cast<uint16_t>(sC[p] + sC[j]);
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t k = 0; k < kOtPer; k++) {
+      const uint32_t p = threadIdx.x + k * kOtThreads;
+      if (p < n) {
+        sL[p] = l[k];
+        sC[p] = c[k];
+      }
+    }
+    __syncthreads();
+  }
+  uint64_t *ec = EC + static_cast<uint64_t>(g) * kOtTile;
+  for (uint32_t k = 0; k < kOtPer; k++) {
+    const uint32_t p = threadIdx.x + k * kOtThreads;
+    if (p >= n) break;
+    // the chain's last in-tile position: its entry is valid iff its next is
+    const uint32_t e = ot_next(m, T.mlen, t0 + sL[p]);
+    const uint64_t cnt = sC[p] + (e != kOtBad ? 1u : 0u);
+    ec[p] = e | (cnt << 32);
+  }
+}
+
+__global__ void ot_hop_kernel(const OtTable *tabs, uint32_t nt, const uint64_t *EC, uint32_t *tstart, uint64_t *tbase,
+                              int32_t *status) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nt) return;
+  const OtTable T = tabs[t];
+  if (T.nb == 0) return;
+  uint64_t x = 0, idx = 0;
+  for (;;) {
+    if (x >= T.mlen) { // the section ends before num_blocks entries
+      status[t] = SSTC_TAB_BAD_META;
+      return;
+    }
+    const uint32_t g = T.tile0 + static_cast<uint32_t>(x / kOtTile), o = static_cast<uint32_t>(x % kOtTile);
+    tstart[g] = o;
+    tbase[g] = idx;
+    const uint64_t v = EC[static_cast<uint64_t>(g) * kOtTile + o];
+    idx += v >> 32;
+    if (idx >= T.nb) return;
+    const uint32_t e = static_cast<uint32_t>(v);
+    if (e == kOtBad) {
+      status[t] = SSTC_TAB_BAD_META;
+      return;
+    }
+    x = e;
+  }
+}
+
+struct OtOut {
+  uint64_t *blk_off, *blk_len, *fk_off, *lk_off;
+  uint32_t *fk_len, *lk_len;
+};
+
+__global__ __launch_bounds__(kOtThreads) void ot_emit_kernel(const uint8_t *src, const OtTable *tabs, uint32_t nt,
+                                                             const uint32_t *tstart, const uint64_t *tbase, OtOut o,
+                                                             int32_t *status) {
+  __shared__ uint16_t sJ[kOtTile]; // f^(2^r)(p) inside the tile, kOtOut once it leaves
+  __shared__ uint8_t sM[kOtTile];  // p is a chain position
+  __shared__ uint32_t sW[kOtThreads / kWave];
+  const uint32_t g = blockIdx.x;
+  const uint32_t s = tstart[g];
+  if (s == kOtBad) return; // uniform: the chain skips this tile
+  const uint32_t ti = ot_find(tabs, nt, g);
+  const OtTable T = tabs[ti];
+  const uint8_t *m = src + T.meta;
+  const uint32_t t0 = (g - T.tile0) * kOtTile;
+  const uint32_t n = min(kOtTile, T.mlen - t0);
+  for (uint32_t k = 0; k < kOtPer; k++) {
+    const uint32_t p = threadIdx.x + k * kOtThreads;
+    if (p >= n) break;
+    const uint32_t e = ot_next(m, T.mlen, t0 + p);
+    sJ[p] = static_cast<uint16_t>(e != kOtBad && e < t0 + n ? e - t0 : kOtOut);
+    sM[p] = p == s;
+  }
+  __syncthreads();
+  for (uint32_t r = 0; r < kOtRounds; r++) {
+    // marks {f^i(s) : i < 2^r} -> {i < 2^(r+1)}; a mark set earlier in the same
+    // round only marks further chain positions, never others
+    for (uint32_t k = 0; k < kOtPer; k++) {
+      const uint32_t p = threadIdx.x + k * kOtThreads;
+      if (p >= n) break;
+      const uint32_t j = sJ[p];
+      if (sM[p] && j != kOtOut) sM[j] = 1;
+    }
+    __syncthreads();
+    if (r + 1 == kOtRounds) break;
+    uint16_t l[kOtPer];
+#pragma unroll
+    for (uint32_t k = 0; k < kOtPer; k++) {
+      const uint32_t p = threadIdx.x + k * kOtThreads;
+      if (p < n) {
+        const uint32_t j = sJ[p];
+        l[k] = j == kOtOut ? kOtOut : sJ[j];
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t k = 0; k < kOtPer; k++) {
+      const uint32_t p = threadIdx.x + k * kOtThreads;
+      if (p < n) sJ[p] = l[k];
+    }
+    __syncthreads();
+  }
+  // rank the marked positions: thread i owns [i * kOtPer, (i + 1) * kOtPer)
+  const uint32_t b0 = threadIdx.x * kOtPer;
+  uint32_t cnt = 0;
+  for (uint32_t k = 0; k < kOtPer; k++)
+    if (b0 + k < n) cnt += sM[b0 + k];
+  const uint32_t lane = lane_id(), w = threadIdx.x / kWave;
+  const uint32_t inc = wave_incl_scan_u32(cnt);
+  if (lane == kWave - 1) sW[w] = inc;
+  __syncthreads();
+  uint32_t rank = inc - cnt;
+  for (uint32_t v = 0; v < w; v++) rank += sW[v];
+  for (uint32_t k = 0; k < kOtPer; k++) {
+    const uint32_t p = b0 + k;
+    if (p >= n || !sM[p]) continue;
+    const uint64_t i = tbase[g] + rank++;
+    if (i >= T.nb) break;
+    const uint32_t pa = t0 + p;
+    if (ot_next(m, T.mlen, pa) == kOtBad) break; // past the valid entries (status is BAD_META)
+    const uint32_t fkl = g_u32u(m + pa), lkl = g_u32u(m + pa + 4 + fkl);
+    const uint64_t bo = g_u64u(m + pa + 8 + fkl + lkl), bl = g_u64u(m + pa + 16 + fkl + lkl);
+    const uint64_t b = T.fb + i;
+    o.blk_off[b] = T.data + bo;
+    o.blk_len[b] = bl;
+    o.fk_off[b] = T.meta + pa + 4;
+    o.fk_len[b] = fkl;
+    o.lk_off[b] = T.meta + pa + 8 + fkl;
+    o.lk_len[b] = lkl;
+    if (bo > T.moff || bl > T.moff - bo) atomicCAS(&status[ti], SSTC_TAB_OK, SSTC_TAB_BAD_BLOCK);
+  }
+}
+
+} // namespace
+
+int open_tables_impl(Arena &arena, hipStream_t s, const uint8_t *d_src, uint64_t src_bytes, const uint64_t *h_off,
+                     const uint64_t *h_bytes, uint32_t nt, uint64_t max_blocks, const OpenOut &out, uint64_t *h_tfb,
+                     int32_t *h_status, uint64_t *h_footer, std::string &err) {
+  try {
+    // pinned words: [0, nt) footer addresses, [nt, 6 nt) footers, then the
+    // table descriptors, the first-block prefix and the statuses
+    const uint64_t w_tab = 6 * static_cast<uint64_t>(nt), w_tfb = w_tab + 6 * static_cast<uint64_t>(nt);
+    const uint64_t w_st = w_tfb + nt + 1, words = w_st + nt / 2 + 2;
+    ensure_host(arena, words);
+    uint64_t *H = arena.host;
+    std::vector<int32_t> st(nt, SSTC_TAB_OK);
+    for (uint32_t t = 0; t < nt; t++) {
+      H[t] = h_bytes[t] >= 40 ? h_off[t] + h_bytes[t] - 40 : ~uint64_t(0);
+      if (h_bytes[t] < 40) st[t] = SSTC_TAB_BAD_FOOTER;
+    }
+    if (nt) {
+      ot_footer_kernel<<<grid(nt), 256, 0, s>>>(d_src, arena.host_dev, nt, arena.host_dev + nt);
+      CK(hipGetLastError());
+      CK(hipStreamSynchronize(s));
+    }
+    std::vector<OtTable> tabs(nt);
+    uint64_t total = 0, tiles = 0;
+    h_tfb[0] = 0;
+    for (uint32_t t = 0; t < nt; t++) {
+      const uint64_t *f = H + nt + 5 * static_cast<uint64_t>(t);
+      uint64_t nb = 0, moff = 0, mlen = 0;
+      if (st[t] == SSTC_TAB_OK) {
+        nb = f[0];
+        moff = f[1];
+        mlen = f[2];
+        if (moff > h_bytes[t] - 40 || mlen > h_bytes[t] - 40 - moff) st[t] = SSTC_TAB_BAD_FOOTER;
+        else if (mlen >= kOtBad) st[t] = SSTC_TAB_TOO_LARGE;
+        else if (nb > mlen / 24) st[t] = SSTC_TAB_BAD_META; // every entry takes >= 24 B
+      }
+      if (h_footer) {
+        for (int k = 0; k < 5; k++) h_footer[5 * static_cast<uint64_t>(t) + k] = st[t] == SSTC_TAB_BAD_FOOTER ? 0 : f[k];
+      }
+      OtTable &T = tabs[t];
+      T.data = h_off[t];
+      T.meta = h_off[t] + moff;
+      T.moff = moff;
+      T.nb = st[t] == SSTC_TAB_OK ? nb : 0;
+      T.fb = total;
+      T.mlen = st[t] == SSTC_TAB_OK ? static_cast<uint32_t>(mlen) : 0;
+      T.tile0 = static_cast<uint32_t>(tiles);
+      total += T.nb;
+      if (T.nb) tiles += (mlen + kOtTile - 1) / kOtTile;
+      else T.mlen = 0; // no tiles: nothing to parse
+      h_tfb[t + 1] = total;
+    }
+    for (uint32_t t = 0; t < nt; t++) h_status[t] = st[t];
+    if (total > max_blocks) {
+      err = "block index capacity too small (" + std::to_string(total) + " blocks)";
+      return SSTC_E_CAPACITY;
+    }
+    if (tiles >= (uint64_t(1) << 31)) {
+      err = "meta sections too large";
+      return SSTC_E_INVALID_ARG;
+    }
+    (void)src_bytes;
+    std::memcpy(H + w_tab, tabs.data(), nt * sizeof(OtTable));
+    std::memcpy(H + w_tfb, h_tfb, (nt + 1) * sizeof(uint64_t));
+    std::memcpy(H + w_st, st.data(), nt * sizeof(int32_t));
+    Pool pool(arena);
+    OtTable *d_tabs = pool.get<OtTable>(nt);
+    int32_t *d_st = pool.get<int32_t>(nt);
+    if (nt) {
+      CK(hipMemcpyAsync(d_tabs, H + w_tab, nt * sizeof(OtTable), hipMemcpyHostToDevice, s));
+      CK(hipMemcpyAsync(d_st, H + w_st, nt * sizeof(int32_t), hipMemcpyHostToDevice, s));
+    }
+    if (out.table_first_block)
+      CK(hipMemcpyAsync(out.table_first_block, H + w_tfb, (nt + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, s));
+    if (tiles) {
+      uint64_t *EC = pool.get<uint64_t>(tiles * kOtTile);
+      uint32_t *tstart = pool.get<uint32_t>(tiles);
+      uint64_t *tbase = pool.get<uint64_t>(tiles);
+      ot_tile_kernel<<<static_cast<uint32_t>(tiles), kOtThreads, 0, s>>>(d_src, d_tabs, nt, EC, tstart);
+      ot_hop_kernel<<<grid(nt, 64), 64, 0, s>>>(d_tabs, nt, EC, tstart, tbase, d_st);
+      OtOut o{out.blk_off, out.blk_len, out.first_key_off, out.last_key_off, out.first_key_len, out.last_key_len};
+      ot_emit_kernel<<<static_cast<uint32_t>(tiles), kOtThreads, 0, s>>>(d_src, d_tabs, nt, tstart, tbase, o, d_st);
+      CK(hipGetLastError());
+    }
+    if (nt) CK(hipMemcpyAsync(H + w_st, d_st, nt * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    CK(hipStreamSynchronize(s));
+    std::memcpy(h_status, H + w_st, nt * sizeof(int32_t));
+    return SSTC_OK;
+  } catch (const std::exception &e) {
+    err = e.what();
+    return SSTC_E_HIP;
+  }
+}
+
+} // namespace sstc

@@ -137,4 +137,14 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
                  uint8_t *d_dst, uint64_t dst_cap, uint64_t *d_table_off, uint64_t *d_table_len, uint64_t max_tables,
                  uint64_t *res, std::string &err);
 
+// SST open on the device (sstc_open_tables): block index outputs
+struct OpenOut {
+  uint64_t *blk_off, *blk_len, *first_key_off, *last_key_off, *table_first_block;
+  uint32_t *first_key_len, *last_key_len;
+};
+
+int open_tables_impl(Arena &arena, hipStream_t s, const uint8_t *d_src, uint64_t src_bytes, const uint64_t *h_off,
+                     const uint64_t *h_bytes, uint32_t nt, uint64_t max_blocks, const OpenOut &out, uint64_t *h_tfb,
+                     int32_t *h_status, uint64_t *h_footer, std::string &err);
+
 } // namespace sstc

@@ -62,6 +62,9 @@ class FilesTiming(ctypes.Structure):
                 ("store_s", ctypes.c_double), ("total_s", ctypes.c_double)]
 
 
+SSTC_TAB_OK, SSTC_TAB_BAD_FOOTER, SSTC_TAB_BAD_META, SSTC_TAB_BAD_BLOCK, SSTC_TAB_TOO_LARGE = 0, 1, 2, 3, 4
+
+
 class SstcError(RuntimeError):
     pass
 
@@ -98,6 +101,8 @@ def load():
                                         c_vp, c_vp, c_u64, P(CompactResult)]),
         "sstc_get_batch": (ctypes.c_int, [c_vp, c_vp, P(BlockIndex), c_vp, c_vp, c_u64, c_vp, c_vp, c_u64, c_vp, c_vp,
                                           c_vp, c_vp]),
+        "sstc_open_tables": (ctypes.c_int, [c_vp, c_vp, c_u64, c_vp, c_vp, c_u32, c_u64, c_vp, c_vp, c_vp, c_vp,
+                                            c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
         "sstc_pipe_create": (ctypes.c_int, [c_vp, c_u32, P(c_vp)]),
         "sstc_pipe_destroy": (ctypes.c_int, [c_vp]),
         "sstc_compact_files": (ctypes.c_int, [c_vp, c_vp, c_vp, c_u32, ctypes.c_char_p, c_u64, P(CompactParams),

@@ -166,6 +166,55 @@ class Codec:
               "sstc_encode_blocks")
         return dst, out_off, out_len[:nb]
 
+    # ---- SST open ------------------------------------------------------------
+    def open_tables(self, src, tab_bytes, tab_off=None, max_blocks=None, strict=False):
+        """sstc_open_tables: footers + meta sections of the SST images in the
+        device u8 tensor `src` (table t = src[tab_off[t] .. + tab_bytes[t]),
+        tab_bytes = GetFileSize() - 1; back to back when tab_off is None)
+        parsed on the device.  Returns a dict of device tensors (blk_off,
+        blk_len, first_key_off, first_key_len, last_key_off, last_key_len,
+        table_first_block_dev; key / block offsets absolute into src) and numpy
+        table_first_block, status (SSTC_TAB_*), footer (ntables x 5).
+        strict: raise unless every table is SSTC_TAB_OK."""
+        import numpy as np
+        nt = len(tab_bytes)
+        tb = np.ascontiguousarray(tab_bytes, np.uint64)
+        if tab_off is None:
+            to = np.zeros(nt, np.uint64)
+            if nt > 1:
+                to[1:] = np.cumsum(tb[:-1])
+        else:
+            to = np.ascontiguousarray(tab_off, np.uint64)
+        if max_blocks is None:  # every block takes >= 24 B of meta + >= 16 B of data
+            max_blocks = int(tb.sum()) // 40 + 1
+        dev = self.device
+        cap = max(int(max_blocks), 1)
+        o = {k: torch.empty(cap, dtype=torch.int64, device=dev)
+             for k in ("blk_off", "blk_len", "first_key_off", "last_key_off")}
+        o["first_key_len"] = torch.empty(cap, dtype=torch.int32, device=dev)
+        o["last_key_len"] = torch.empty(cap, dtype=torch.int32, device=dev)
+        o["table_first_block_dev"] = torch.empty(nt + 1, dtype=torch.int64, device=dev)
+        tfb = np.zeros(nt + 1, np.uint64)
+        status = np.zeros(max(nt, 1), np.int32)
+        footer = np.zeros((max(nt, 1), 5), np.uint64)
+        vp = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+        self._stream()
+        check(self.lib.sstc_open_tables(self.h, _p(src), int(src.numel()), vp(to), vp(tb), nt, int(max_blocks),
+                                        _p(o["blk_off"]), _p(o["blk_len"]), _p(o["first_key_off"]),
+                                        _p(o["first_key_len"]), _p(o["last_key_off"]), _p(o["last_key_len"]),
+                                        _p(o["table_first_block_dev"]), vp(tfb), vp(status), vp(footer)),
+              "sstc_open_tables")
+        nb = int(tfb[nt])
+        for k in ("blk_off", "blk_len", "first_key_off", "last_key_off", "first_key_len", "last_key_len"):
+            o[k] = o[k][:nb]
+        o["table_first_block"] = tfb
+        o["status"] = status[:nt]
+        o["footer"] = footer[:nt]
+        if strict and nt and (status[:nt] != _lib.SSTC_TAB_OK).any():
+            bad = int(np.flatnonzero(status[:nt])[0])
+            raise _lib.SstcError(f"sstc_open_tables: table {bad} rejected (status {int(status[bad])})")
+        return o
+
     # ---- compaction ----------------------------------------------------------
     def compact(self, tables, block_threshold=4096, table_limit=32 << 20, base_level=1,
                 txn_mode=_lib.SSTC_TXN_COMPAT):
@@ -177,22 +226,10 @@ class Codec:
             files = [np.ascontiguousarray(t, np.uint8) for t in tables]
         else:
             files = list(tables)
-        # block index of every table (host parse of footer + meta section)
-        offs, lens, tfb, bases = [], [], [0], []
-        base = 0
-        for f in files:
-            idx = _table_index(f)
-            offs.append(idx[0] + base)
-            lens.append(idx[1])
-            tfb.append(tfb[-1] + len(idx[0]))
-            bases.append(base)
-            base += f.size
+        # block index of every table: footers + meta sections parsed on the device
         src = torch.from_numpy(np.concatenate(files) if files else np.zeros(1, np.uint8)).to(self.device)
-        blk_off = torch.from_numpy(np.concatenate(offs).astype(np.uint64).view(np.int64) if offs else
-                                   np.zeros(0, np.int64)).to(self.device)
-        blk_len = torch.from_numpy(np.concatenate(lens).astype(np.uint64).view(np.int64) if lens else
-                                   np.zeros(0, np.int64)).to(self.device)
-        h_tfb = np.asarray(tfb, np.uint64)
+        idx = self.open_tables(src, [f.size for f in files], strict=True)
+        blk_off, blk_len, h_tfb = idx["blk_off"], idx["blk_len"], idx["table_first_block"]
         cap = int(src.numel()) * 2 + 4096
         dst = torch.zeros(cap, dtype=torch.uint8, device=self.device)
         max_t = cap // 40 + 1
@@ -228,22 +265,13 @@ class Lookup:
         import numpy as np
         self.codec = codec
         dev = codec.device
-        offs, lens, lko, lkl, tfb, base = [], [], [], [], [0], 0
-        for f in tables:
-            o, ln, ko, kl = _table_index(f, keys=True)
-            offs.append(o + np.uint64(base))
-            lens.append(ln)
-            lko.append(ko + np.uint64(base))
-            lkl.append(kl)
-            tfb.append(tfb[-1] + len(o))
-            base += f.size
-        cat = lambda xs, dt: np.concatenate(xs).astype(dt) if xs and sum(len(x) for x in xs) else np.zeros(1, dt)  # noqa: E731
         self.src = torch.from_numpy(np.concatenate(tables) if tables else np.zeros(1, np.uint8)).to(dev)
-        self.blk_off = torch.from_numpy(cat(offs, np.uint64).view(np.int64)).to(dev)
-        self.blk_len = torch.from_numpy(cat(lens, np.uint64).view(np.int64)).to(dev)
-        self.lk_off = torch.from_numpy(cat(lko, np.uint64).view(np.int64)).to(dev)
-        self.lk_len = torch.from_numpy(cat(lkl, np.uint32).view(np.int32)).to(dev)
-        self.tfb = torch.from_numpy(np.asarray(tfb, np.uint64).view(np.int64)).to(dev)
+        # block indexes parsed on the device (footer + meta section per table)
+        idx = codec.open_tables(self.src, [f.size for f in tables], strict=True)
+        one = lambda t: t if t.numel() else torch.zeros(1, dtype=t.dtype, device=dev)  # noqa: E731
+        self.blk_off, self.blk_len = one(idx["blk_off"]), one(idx["blk_len"])
+        self.lk_off, self.lk_len = one(idx["last_key_off"]), one(idx["last_key_len"])
+        self.tfb = idx["table_first_block_dev"]
         self.ntables = len(tables)
         self.base = [0]
         for f in tables:
