@@ -128,17 +128,28 @@ def run_bench(args, rank, world, dev, codec, td):
         files.append(np.fromfile(p, np.uint8))
         paths.append((p, fs))
     gen_s = time.perf_counter() - t0
-    offs, lens, tfb, base = [], [], [0], 0
+    # block index: footers + meta sections parsed on the device (sstc_open_tables),
+    # checked against the host walk (Python restatement of table_reader.cc:86-156)
+    src = torch.from_numpy(np.concatenate(files)).to(dev)
+    sizes = [f.size for f in files]
+    idx = codec.open_tables(src, sizes, strict=True)
+    open_ms = []
+    for _ in range(5):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        idx = codec.open_tables(src, sizes, strict=True)
+        open_ms.append((time.perf_counter() - t0) * 1e3)
+    t0 = time.perf_counter()
+    offs, lens, base = [], [], 0
     for f in files:
         o, ln = _table_index(f)
         offs.append(o + np.uint64(base))
         lens.append(ln)
-        tfb.append(tfb[-1] + len(o))
         base += f.size
-    src = torch.from_numpy(np.concatenate(files)).to(dev)
-    bo = torch.from_numpy(np.concatenate(offs).view(np.int64)).to(dev)
-    bl = torch.from_numpy(np.concatenate(lens).view(np.int64)).to(dev)
-    h_tfb = np.asarray(tfb, np.uint64)
+    host_index_ms = (time.perf_counter() - t0) * 1e3
+    bo, bl, h_tfb = idx["blk_off"], idx["blk_len"], idx["table_first_block"]
+    assert np.array_equal(bo.cpu().numpy().view(np.uint64), np.concatenate(offs))
+    assert np.array_equal(bl.cpu().numpy().view(np.uint64), np.concatenate(lens))
     cap = int(src.numel()) + (1 << 20)
     dst = torch.empty(cap, dtype=torch.uint8, device=dev)
     max_t = 1 << 16
@@ -172,7 +183,8 @@ def run_bench(args, rank, world, dev, codec, td):
     all_in = SH.sum_over_ranks(in_bytes, dev)
     med = float(np.median(times))
     name = {3: "config3" + ("-overlap" if args.overlap else ""), 4: "config4", 5: "config5"}[args.config]
-    out = {"workload": name, "ranks": world, "ssts_per_rank": args.ssts, "keys_per_sst": args.keys,
+    out = {"open_tables_ms": round(float(np.median(open_ms)), 3), "host_index_py_ms": round(host_index_ms, 1),
+           "workload": name, "ranks": world, "ssts_per_rank": args.ssts, "keys_per_sst": args.keys,
            "input_bytes_per_rank": in_bytes, "records_in": res.records_in, "records_kept": res.records_kept,
            "tables_out": nt, "blocks_out": res.blocks_out, "bytes_out": res.bytes_out,
            "device_s_median": med, "device_GiBps_in_all_ranks": all_in / med / 2 ** 30,
