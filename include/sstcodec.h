@@ -160,6 +160,12 @@ int sstc_roundtrip_blocks(sstc_ctx *ctx, const uint8_t *d_src, uint8_t *d_dst,
                           uint64_t nblocks, uint32_t txn_mode, uint64_t *d_out_blk_len,
                           uint32_t *d_block_status);
 
+/* Diagnostic: the copy ceiling the codec kernels are compared to — a plain
+ * device copy of nbytes (multiple of 16, both pointers 16 B aligned), one
+ * 16 B non-temporal load + store per lane.  Asynchronous on the context's
+ * stream.  Not part of the reference interface. */
+int sstc_copy_probe(sstc_ctx *ctx, const uint8_t *d_src, uint8_t *d_dst, uint64_t nbytes);
+
 /* ---- compaction job (replaces Compact::DoCompactJob, db/compact.cc:232-363,
  *      with its MergeIterator, db/merge_iterator.cc) ------------------------ */
 

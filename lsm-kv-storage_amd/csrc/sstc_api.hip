@@ -284,6 +284,15 @@ int sstc_compact(sstc_ctx *c, const uint8_t *d_src, const uint64_t *d_blk_off, c
   return SSTC_OK;
 }
 
+int sstc_copy_probe(sstc_ctx *c, const uint8_t *d_src, uint8_t *d_dst, uint64_t nbytes) {
+  if (!c || (nbytes && (!d_src || !d_dst))) return fail(SSTC_E_INVALID_ARG, "sstc_copy_probe: NULL argument");
+  if ((nbytes | reinterpret_cast<uintptr_t>(d_src) | reinterpret_cast<uintptr_t>(d_dst)) & 15u)
+    return fail(SSTC_E_INVALID_ARG, "sstc_copy_probe: size and pointers must be 16 B aligned");
+  if (int r = bind_device(c)) return r;
+  SSTC_HIP(sstc::launch_copy_probe(d_src, d_dst, nbytes / 16, c->stream), "sstc_copy_probe launch");
+  return SSTC_OK;
+}
+
 int sstc_open_tables(sstc_ctx *c, const uint8_t *d_src, uint64_t src_bytes, const uint64_t *h_tab_off,
                      const uint64_t *h_tab_bytes, uint32_t ntables, uint64_t max_blocks, uint64_t *d_blk_off,
                      uint64_t *d_blk_len, uint64_t *d_first_key_off, uint32_t *d_first_key_len,

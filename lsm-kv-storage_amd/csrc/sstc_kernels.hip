@@ -1697,6 +1697,22 @@ static inline uint32_t grid_for(uint64_t n, uint32_t per) { return static_cast<u
 
 
 
+// copy ceiling probe (sstc_copy_probe): the best plain copy of the same bytes
+// (one 16 B non-temporal load + store per lane, profiles/r01_ab_variants.md)
+typedef uint32_t probe_u32x4 __attribute__((ext_vector_type(4)));
+__global__ __launch_bounds__(256) void copy_probe_kernel(const probe_u32x4 *__restrict__ s,
+                                                         probe_u32x4 *__restrict__ d, uint64_t n) {
+  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (i < n) __builtin_nontemporal_store(__builtin_nontemporal_load(s + i), d + i);
+}
+
+hipError_t launch_copy_probe(const uint8_t *src, uint8_t *dst, uint64_t n16, hipStream_t s) {
+  if (n16)
+    copy_probe_kernel<<<static_cast<uint32_t>((n16 + 255) / 256), 256, 0, s>>>(
+        reinterpret_cast<const probe_u32x4 *>(src), reinterpret_cast<probe_u32x4 *>(dst), n16);
+  return hipGetLastError();
+}
+
 hipError_t launch_roundtrip(const RtArgs &a, hipStream_t s) {
   // blocks in dispatch order: the XCD-grouped order measured +3 % at config 2
   // (256 MiB, Infinity-Cache resident) but -2.5 % on 1 GiB (profiles/r01_ab_xcd.log)

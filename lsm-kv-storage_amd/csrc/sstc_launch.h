@@ -100,6 +100,7 @@ struct GetArgs {
 hipError_t launch_get(const GetArgs &a, hipStream_t s);
 
 hipError_t launch_roundtrip(const RtArgs &a, hipStream_t s);
+hipError_t launch_copy_probe(const uint8_t *src, uint8_t *dst, uint64_t n16, hipStream_t s);
 hipError_t launch_count(const uint8_t *src, const uint64_t *blk_off, const uint64_t *blk_len,
                         uint64_t nblocks, uint64_t *counts, hipStream_t s, uint64_t *scan_ws = nullptr);
 hipError_t launch_decode(const DecArgs &a, hipStream_t s);
