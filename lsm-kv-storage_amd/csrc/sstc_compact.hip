@@ -1089,6 +1089,31 @@ __device__ __forceinline__ uint32_t ot_next(const uint8_t *m, uint32_t mlen, uin
   return e > mlen ? kOtBad : static_cast<uint32_t>(e);
 }
 
+// ot_next for kOtPer positions of a thread (each < mlen) with all first-length
+// loads in flight together, then all second-length loads: the per-position
+// form serializes 2 dependent global loads per position.  A load at p < mlen
+// stays inside the image (the 40 B footer follows the section); the second
+// load's address is clamped and its result dropped when invalid.
+// (groups of kOtBatch positions: the whole thread's set at once spills)
+constexpr uint32_t kOtBatch = 8;
+__device__ __forceinline__ void ot_next_group(const uint8_t *m, uint32_t mlen, const uint32_t *pos, uint32_t *e) {
+  uint32_t k1[kOtBatch], q[kOtBatch];
+#pragma unroll
+  for (uint32_t k = 0; k < kOtBatch; k++) k1[k] = g_u32u(m + pos[k]);
+#pragma unroll
+  for (uint32_t k = 0; k < kOtBatch; k++) {
+    const uint64_t qq = static_cast<uint64_t>(pos[k]) + 4 + k1[k];
+    const bool ok = static_cast<uint64_t>(pos[k]) + 4 <= mlen && qq + 4 <= mlen;
+    q[k] = ok ? static_cast<uint32_t>(qq) : kOtBad;
+  }
+#pragma unroll
+  for (uint32_t k = 0; k < kOtBatch; k++) {
+    const uint32_t k2 = g_u32u(m + (q[k] == kOtBad ? 0u : q[k]));
+    const uint64_t ee = static_cast<uint64_t>(q[k]) + 20 + k2;
+    e[k] = q[k] != kOtBad && ee <= mlen ? static_cast<uint32_t>(ee) : kOtBad;
+  }
+}
+
 __global__ void ot_footer_kernel(const uint8_t *src, const uint64_t *foot_at, uint32_t nt, uint64_t *out) {
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= nt || foot_at[t] == ~uint64_t(0)) return;
@@ -1107,13 +1132,24 @@ __global__ __launch_bounds__(kOtThreads) void ot_tile_kernel(const uint8_t *src,
   const uint32_t t0 = (g - T.tile0) * kOtTile;
   const uint32_t n = min(kOtTile, T.mlen - t0);
   if (threadIdx.x == 0) tstart[g] = kOtBad;
-  for (uint32_t k = 0; k < kOtPer; k++) {
-    const uint32_t p = threadIdx.x + k * kOtThreads;
-    if (p >= n) break;
-    const uint32_t e = ot_next(m, T.mlen, t0 + p);
-    const bool in = e != kOtBad && e < t0 + n;
-    sL[p] = static_cast<uint16_t>(in ? e - t0 : p);
-    sC[p] = in ? 1 : 0;
+#pragma unroll 1
+  for (uint32_t g0 = 0; g0 < kOtPer; g0 += kOtBatch) {
+    uint32_t pos[kOtBatch], nx[kOtBatch];
+#pragma unroll
+    for (uint32_t j = 0; j < kOtBatch; j++) {
+      const uint32_t p = threadIdx.x + (g0 + j) * kOtThreads;
+      pos[j] = t0 + (p < n ? p : 0u);
+    }
+    ot_next_group(m, T.mlen, pos, nx);
+#pragma unroll
+    for (uint32_t j = 0; j < kOtBatch; j++) {
+      const uint32_t p = threadIdx.x + (g0 + j) * kOtThreads;
+      if (p < n) {
+        const bool in = nx[j] != kOtBad && nx[j] < t0 + n;
+        sL[p] = static_cast<uint16_t>(in ? nx[j] - t0 : p);
+        sC[p] = in ? 1 : 0;
+      }
+    }
   }
   __syncthreads();
   for (uint32_t r = 0; r < kOtRounds; r++) {
@@ -1139,13 +1175,24 @@ __global__ __launch_bounds__(kOtThreads) void ot_tile_kernel(const uint8_t *src,
     __syncthreads();
   }
   uint64_t *ec = EC + static_cast<uint64_t>(g) * kOtTile;
-  for (uint32_t k = 0; k < kOtPer; k++) {
-    const uint32_t p = threadIdx.x + k * kOtThreads;
-    if (p >= n) break;
-    // the chain's last in-tile position: its entry is valid iff its next is
-    const uint32_t e = ot_next(m, T.mlen, t0 + sL[p]);
-    const uint64_t cnt = sC[p] + (e != kOtBad ? 1u : 0u);
-    ec[p] = e | (cnt << 32);
+  // the chain's last in-tile position: its entry is valid iff its next is
+#pragma unroll 1
+  for (uint32_t g0 = 0; g0 < kOtPer; g0 += kOtBatch) {
+    uint32_t pos[kOtBatch], nx[kOtBatch];
+#pragma unroll
+    for (uint32_t j = 0; j < kOtBatch; j++) {
+      const uint32_t p = threadIdx.x + (g0 + j) * kOtThreads;
+      pos[j] = t0 + (p < n ? sL[p] : 0u);
+    }
+    ot_next_group(m, T.mlen, pos, nx);
+#pragma unroll
+    for (uint32_t j = 0; j < kOtBatch; j++) {
+      const uint32_t p = threadIdx.x + (g0 + j) * kOtThreads;
+      if (p < n) {
+        const uint64_t cnt = sC[p] + (nx[j] != kOtBad ? 1u : 0u);
+        ec[p] = nx[j] | (cnt << 32);
+      }
+    }
   }
 }
 
@@ -1195,12 +1242,23 @@ __global__ __launch_bounds__(kOtThreads) void ot_emit_kernel(const uint8_t *src,
   const uint8_t *m = src + T.meta;
   const uint32_t t0 = (g - T.tile0) * kOtTile;
   const uint32_t n = min(kOtTile, T.mlen - t0);
-  for (uint32_t k = 0; k < kOtPer; k++) {
-    const uint32_t p = threadIdx.x + k * kOtThreads;
-    if (p >= n) break;
-    const uint32_t e = ot_next(m, T.mlen, t0 + p);
-    sJ[p] = static_cast<uint16_t>(e != kOtBad && e < t0 + n ? e - t0 : kOtOut);
-    sM[p] = p == s;
+#pragma unroll
+  for (uint32_t g0 = 0; g0 < kOtPer; g0 += kOtBatch) {
+    uint32_t pos[kOtBatch], nx[kOtBatch];
+#pragma unroll
+    for (uint32_t j = 0; j < kOtBatch; j++) {
+      const uint32_t p = threadIdx.x + (g0 + j) * kOtThreads;
+      pos[j] = t0 + (p < n ? p : 0u);
+    }
+    ot_next_group(m, T.mlen, pos, nx);
+#pragma unroll
+    for (uint32_t j = 0; j < kOtBatch; j++) {
+      const uint32_t p = threadIdx.x + (g0 + j) * kOtThreads;
+      if (p < n) {
+        sJ[p] = static_cast<uint16_t>(nx[j] != kOtBad && nx[j] < t0 + n ? nx[j] - t0 : kOtOut);
+        sM[p] = p == s;
+      }
+    }
   }
   __syncthreads();
   for (uint32_t r = 0; r < kOtRounds; r++) {
