@@ -254,7 +254,7 @@ int sstc_get_batch(sstc_ctx *ctx, const uint8_t *d_src, const sstc_block_index *
  * h_tab_bytes[t] = TableBuilder::GetFileSize() - 1 (the reference reads the
  * footer at file_size - 40 - 1).  The footers are read and the meta sections
  * parsed on the device (the length-prefixed entry chain is recovered by
- * pointer doubling over 32 KiB tiles, not walked): table t's blocks are
+ * pointer doubling over 16 KiB tiles, not walked): table t's blocks are
  * [h_table_first_block[t], h_table_first_block[t+1]) of the outputs, with
  * d_blk_off / d_first_key_off / d_last_key_off ABSOLUTE offsets into d_src,
  * so (d_blk_off, d_blk_len, d_last_key_off, d_last_key_len, keys = d_src,

@@ -1039,13 +1039,13 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
 // (entry = u32 fkl | first key | u32 lkl | last key | u64 block offset | u64
 // block size, table_builder.cc:101-145) with no offset table, so the entry
 // starts are the chain 0 -> next(0) -> ... with next(p) = p + 24 + fkl + lkl.
-// It is recovered in parallel, 32 KiB tiles of the section at a time:
+// It is recovered in parallel, 16 KiB tiles of the section at a time:
 //   ot_tile_kernel  next(p) for every byte position p of the tile; pointer
 //                   doubling in LDS gives, for every p, the entries the chain
 //                   from p holds inside the tile and the first chain position
 //                   past the tile (its exit)
 //   ot_hop_kernel   one lane per table follows the exits tile to tile
-//                   (section bytes / 32 KiB dependent loads) and records where
+//                   (section bytes / 16 KiB dependent loads) and records where
 //                   the chain enters each tile and with which entry index
 //   ot_emit_kernel  every entered tile marks its chain positions by doubling
 //                   from the entry point (after round r the first 2^(r+1)
@@ -1054,8 +1054,9 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
 namespace sstc {
 namespace {
 
-constexpr uint32_t kOtTile = 32768, kOtThreads = 1024, kOtPer = kOtTile / kOtThreads;
-constexpr uint32_t kOtRounds = 11; // 2^11 > 32768 / 24 chain positions per tile
+constexpr uint32_t kOtTile = 16384, kOtThreads = 1024, kOtPer = kOtTile / kOtThreads;
+constexpr uint32_t kOtRounds = 10; // 2^10 > 16384 / 24 chain positions per tile
+static_assert((1u << kOtRounds) > kOtTile / 24 && kOtPer % 8 == 0, "doubling rounds must cover a tile's chain");
 constexpr uint16_t kOtOut = 0xFFFF;
 constexpr uint32_t kOtBad = 0xFFFFFFFFu;
 
