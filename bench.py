@@ -162,65 +162,28 @@ def cpu_baseline_threads(sample_src, sample_off, sample_len, threads=16, seconds
                       f"on one thread)"}
 
 
-def e2e_rate(codec, src, off, ln, dev, chunk_blocks=4096, reps=3, nbuf=3):
-    """Host-memory -> host-memory rate: pinned H2D, fused kernel, D2H.  One
-    stream per engine (uploads, kernels, downloads), so each DMA direction
-    streams back to back; a ring of `nbuf` device buffer pairs, reuse ordered
-    by events.  Returns GiB/s of input bytes.  PCIe-bound by construction."""
-    nb = off.numel()
+def e2e_rate(codec, src, off, ln, chunk_bytes=16 << 20, reps=5):
+    """Host-memory -> host-memory rate through the library's own pipeline
+    (sstc_roundtrip_host: pinned H2D on an upload stream, rt_kernel on the
+    context's stream, D2H on a download stream, 3 device buffer pairs ordered
+    by events).  Returns GiB/s of input bytes.  PCIe-bound by construction
+    (profiles/r01_pcie_probe.log: 49 GB/s each way when both directions run)."""
     nbytes = src.numel()
     h_src = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
     h_dst = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
     h_src.copy_(src.cpu())
-    up, work, down = (torch.cuda.Stream(dev) for _ in range(3))
-    nchunks = (nb + chunk_blocks - 1) // chunk_blocks
-    cb = chunk_blocks * BLOCK_BYTES
-    d_in = [torch.empty(cb, dtype=torch.uint8, device=dev) for _ in range(nbuf)]
-    d_out = [torch.empty(cb, dtype=torch.uint8, device=dev) for _ in range(nbuf)]
-    local_off = (torch.arange(chunk_blocks, device=dev, dtype=torch.int64) * BLOCK_BYTES)
-    local_len = torch.full((chunk_blocks,), BLOCK_BYTES, dtype=torch.int64, device=dev)
-    out_len = torch.empty(chunk_blocks, dtype=torch.int64, device=dev)
-    status = torch.empty(chunk_blocks, dtype=torch.int32, device=dev)
-    ev = lambda: torch.cuda.Event()  # noqa: E731
-
-    def one_pass():
-        uploaded, computed, downloaded = {}, {}, {}
-        for c in range(nchunks):
-            k = c % nbuf
-            b0, b1 = c * chunk_blocks, min(nb, (c + 1) * chunk_blocks)
-            n = (b1 - b0) * BLOCK_BYTES
-            h0 = b0 * BLOCK_BYTES
-            with torch.cuda.stream(up):
-                if c >= nbuf:
-                    up.wait_event(computed[c - nbuf])  # d_in[k] consumed
-                d_in[k][:n].copy_(h_src[h0:h0 + n], non_blocking=True)
-                uploaded[c] = ev()
-                uploaded[c].record(up)
-            with torch.cuda.stream(work):
-                work.wait_event(uploaded[c])
-                if c >= nbuf:
-                    work.wait_event(downloaded[c - nbuf])  # d_out[k] drained
-                codec.roundtrip(d_in[k], local_off[: b1 - b0], local_len[: b1 - b0], dst=d_out[k],
-                                out_len=out_len, status=status)
-                computed[c] = ev()
-                computed[c].record(work)
-            with torch.cuda.stream(down):
-                down.wait_event(computed[c])
-                h_dst[h0:h0 + n].copy_(d_out[k][:n], non_blocking=True)
-                downloaded[c] = ev()
-                downloaded[c].record(down)
-        torch.cuda.synchronize()
-
-    one_pass()
-    ok = torch.equal(h_dst, h_src)
+    o = off.cpu().numpy().view(np.uint64)
+    n = ln.cpu().numpy().view(np.uint64)
+    _, st = codec.roundtrip_host(h_src, h_dst, o, n, chunk_bytes=chunk_bytes)
+    ok = bool(torch.equal(h_dst, h_src)) and bool((st == 0).all())
     t0 = time.perf_counter()
     for _ in range(reps):
-        one_pass()
+        codec.roundtrip_host(h_src, h_dst, o, n, chunk_bytes=chunk_bytes)
     el = (time.perf_counter() - t0) / reps
-    return {"value": round(nbytes / el / 2 ** 30, 2), "unit": "GiB/s", "verified": bool(ok),
-            "how": f"pinned host -> H2D -> rt_kernel -> D2H -> pinned host, {nchunks} chunks of "
-                   f"{chunk_blocks} blocks, one stream per engine (upload / kernel / download), "
-                   f"{nbuf} device buffer pairs, {nbytes} B input"}
+    return {"value": round(nbytes / el / 2 ** 30, 2), "unit": "GiB/s", "verified": ok,
+            "how": f"sstc_roundtrip_host: pinned host -> H2D -> rt_kernel -> D2H -> pinned host, "
+                   f"{chunk_bytes >> 20} MiB chunks, upload / kernel / download streams, 3 device buffer pairs, "
+                   f"{nbytes} B input"}
 
 
 def hbm_variant(codec, dev, nblocks, steps=10):
@@ -373,7 +336,7 @@ def main():
             if not args.no_hbm_variant:
                 out["roofline"]["hbm_1gib"] = hbm_variant(codec, dev, 4 * nb)
             if not args.no_e2e:
-                out["e2e_pcie"] = e2e_rate(codec, src, off, ln, dev)
+                out["e2e_pcie"] = e2e_rate(codec, src, off, ln)
             if not args.no_cpu_baseline:
                 k = min(nb, 16384)
                 s = src[: k * BLOCK_BYTES].cpu().numpy()

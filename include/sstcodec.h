@@ -160,6 +160,20 @@ int sstc_roundtrip_blocks(sstc_ctx *ctx, const uint8_t *d_src, uint8_t *d_dst,
                           uint64_t nblocks, uint32_t txn_mode, uint64_t *d_out_blk_len,
                           uint32_t *d_block_status);
 
+/* Host-resident round trip (the path starts and ends in host memory, as
+ * compaction's SST files do): the blocks of h_src (ascending, disjoint,
+ * inside nbytes; pinned memory for full PCIe rate) are streamed through the
+ * device in chunks of <= chunk_bytes (>= 4096; a larger block travels alone):
+ * H2D on an upload stream, sstc_roundtrip_blocks on the context's stream,
+ * D2H on a download stream, a ring of 3 device buffer pairs ordered by
+ * events, so both copy directions and the kernels overlap.  Results as
+ * sstc_roundtrip_blocks, written to h_dst at the blocks' offsets; a rejected
+ * block keeps its source bytes, bytes between blocks are unspecified.
+ * h_out_blk_len / h_block_status may be NULL.  Synchronises. */
+int sstc_roundtrip_host(sstc_ctx *ctx, const uint8_t *h_src, uint8_t *h_dst, uint64_t nbytes,
+                        const uint64_t *h_blk_off, const uint64_t *h_blk_len, uint64_t nblocks, uint32_t txn_mode,
+                        uint64_t chunk_bytes, uint64_t *h_out_blk_len, uint32_t *h_block_status);
+
 /* Diagnostic: the copy ceiling the codec kernels are compared to — a plain
  * device copy of nbytes (multiple of 16, both pointers 16 B aligned), one
  * 16 B non-temporal load + store per lane.  Asynchronous on the context's

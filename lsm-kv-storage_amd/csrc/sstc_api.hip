@@ -8,6 +8,8 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <vector>
+#include <algorithm>
 
 #include "../../include/sstcodec.h"
 #include "sstc_launch.h"
@@ -24,6 +26,22 @@ struct sstc_ctx {
   uint64_t *P = nullptr;                    // cap_records + 1
   uint32_t *jump = nullptr;                 // cap_jump
   sstc::Arena arena;                        // compaction workspace
+  struct HostPipe *pipe = nullptr;          // sstc_roundtrip_host staging (lazy)
+};
+
+// sstc_roundtrip_host: one stream per copy engine beside the context's stream,
+// a ring of device buffer pairs ordered by events, pinned staging for the
+// per-block arrays
+constexpr int kPipeBuf = 3;
+struct HostPipe {
+  hipStream_t up = nullptr, down = nullptr;
+  hipEvent_t ev_up[kPipeBuf] = {}, ev_comp[kPipeBuf] = {}, ev_down[kPipeBuf] = {};
+  uint8_t *d_buf = nullptr; // kPipeBuf x (in, out) spans
+  uint64_t cap_span = 0;
+  uint64_t *d_blk = nullptr; // rel offset, length, out length (3 x nblocks) + status words
+  uint64_t cap_blocks = 0;
+  uint64_t *h_stage = nullptr; // pinned: rel offsets + lengths, then the results
+  uint64_t cap_stage = 0;
 };
 
 namespace {
@@ -138,6 +156,20 @@ int sstc_ctx_destroy(sstc_ctx *c) {
   bind_device(c);
   (void)hipStreamSynchronize(c->stream);
   if (c->arena.host) (void)hipHostFree(c->arena.host);
+  if (HostPipe *hp = c->pipe) {
+    for (hipStream_t st : {hp->up, hp->down})
+      if (st) {
+        (void)hipStreamSynchronize(st);
+        (void)hipStreamDestroy(st);
+      }
+    for (int k = 0; k < kPipeBuf; k++)
+      for (hipEvent_t e : {hp->ev_up[k], hp->ev_comp[k], hp->ev_down[k]})
+        if (e) (void)hipEventDestroy(e);
+    if (hp->d_buf) (void)hipFree(hp->d_buf);
+    if (hp->d_blk) (void)hipFree(hp->d_blk);
+    if (hp->h_stage) (void)hipHostFree(hp->h_stage);
+    delete hp;
+  }
   for (void *p : {c->counters, c->arena.base,
                   static_cast<void *>(c->scan_ws), static_cast<void *>(c->sizes),
                   static_cast<void *>(c->P), static_cast<void *>(c->jump)})
@@ -251,6 +283,107 @@ int sstc_roundtrip_blocks(sstc_ctx *c, const uint8_t *d_src, uint8_t *d_dst,
   sstc::RtArgs a{d_src, d_dst, d_blk_off, d_blk_len, nblocks, txn_mode, d_out_blk_len, d_block_status,
                  c->err_count, c->num_cus};
   SSTC_HIP(sstc::launch_roundtrip(a, c->stream), "roundtrip kernels");
+  return SSTC_OK;
+}
+
+int sstc_roundtrip_host(sstc_ctx *c, const uint8_t *h_src, uint8_t *h_dst, uint64_t nbytes,
+                        const uint64_t *h_blk_off, const uint64_t *h_blk_len, uint64_t nblocks, uint32_t txn_mode,
+                        uint64_t chunk_bytes, uint64_t *h_out_blk_len, uint32_t *h_block_status) {
+  if (!c || (nblocks && (!h_src || !h_dst || !h_blk_off || !h_blk_len)))
+    return fail(SSTC_E_INVALID_ARG, "sstc_roundtrip_host: NULL argument");
+  if (h_src == h_dst && nblocks) return fail(SSTC_E_INVALID_ARG, "h_dst must not alias h_src");
+  if (txn_mode > SSTC_TXN_CORRECT) return fail(SSTC_E_INVALID_ARG, "bad txn_mode");
+  if (chunk_bytes < 4096) return fail(SSTC_E_INVALID_ARG, "chunk_bytes must be >= 4096");
+  if (nblocks >= 0xFFFFFFFFull) return fail(SSTC_E_INVALID_ARG, "too many blocks for one call");
+  uint64_t prev_end = 0;
+  for (uint64_t b = 0; b < nblocks; b++) {
+    if (h_blk_off[b] < prev_end || h_blk_off[b] > nbytes || h_blk_len[b] > nbytes - h_blk_off[b])
+      return fail(SSTC_E_INVALID_ARG, "sstc_roundtrip_host: blocks must be ascending, disjoint and inside h_src");
+    prev_end = h_blk_off[b] + h_blk_len[b];
+  }
+  if (!nblocks) return SSTC_OK;
+  if (int r = bind_device(c)) return r;
+  // chunks: runs of consecutive blocks whose byte span (from the first block's
+  // offset rounded down to 16) fits chunk_bytes; a larger block is a chunk alone
+  struct Chunk {
+    uint64_t b0, b1, lo, hi;
+  };
+  std::vector<Chunk> ch;
+  uint64_t span = 0;
+  for (uint64_t b = 0; b < nblocks;) {
+    Chunk k{b, b + 1, h_blk_off[b] & ~uint64_t(15), h_blk_off[b] + h_blk_len[b]};
+    while (k.b1 < nblocks && h_blk_off[k.b1] + h_blk_len[k.b1] - k.lo <= chunk_bytes) {
+      k.hi = h_blk_off[k.b1] + h_blk_len[k.b1];
+      k.b1++;
+    }
+    span = std::max(span, k.hi - k.lo);
+    ch.push_back(k);
+    b = k.b1;
+  }
+  if (!c->pipe) c->pipe = new HostPipe();
+  HostPipe &hp = *c->pipe;
+  if (!hp.up) {
+    SSTC_HIP(hipStreamCreateWithFlags(&hp.up, hipStreamNonBlocking), "upload stream");
+    SSTC_HIP(hipStreamCreateWithFlags(&hp.down, hipStreamNonBlocking), "download stream");
+    for (int k = 0; k < kPipeBuf; k++) {
+      SSTC_HIP(hipEventCreateWithFlags(&hp.ev_up[k], hipEventDisableTiming), "pipeline events");
+      SSTC_HIP(hipEventCreateWithFlags(&hp.ev_comp[k], hipEventDisableTiming), "pipeline events");
+      SSTC_HIP(hipEventCreateWithFlags(&hp.ev_down[k], hipEventDisableTiming), "pipeline events");
+    }
+  }
+  SSTC_HIP(hipStreamSynchronize(hp.up), "hipStreamSynchronize");
+  SSTC_HIP(hipStreamSynchronize(hp.down), "hipStreamSynchronize");
+  const uint64_t slot = (span + 16 + 255) & ~uint64_t(255);
+  if (int r = grow(c, hp.d_buf, hp.cap_span, 2 * kPipeBuf * slot, "pipeline buffers")) return r;
+  if (int r = grow(c, hp.d_blk, hp.cap_blocks, 4 * nblocks, "pipeline block arrays")) return r;
+  if (hp.cap_stage < 4 * nblocks) {
+    if (hp.h_stage) (void)hipHostFree(hp.h_stage);
+    hp.h_stage = nullptr;
+    hp.cap_stage = 0;
+    SSTC_HIP(hipHostMalloc(reinterpret_cast<void **>(&hp.h_stage), 4 * nblocks * sizeof(uint64_t)),
+             "pipeline pinned staging");
+    hp.cap_stage = 4 * nblocks;
+  }
+  uint64_t *rel = hp.h_stage, *len = hp.h_stage + nblocks;
+  for (const Chunk &k : ch)
+    for (uint64_t b = k.b0; b < k.b1; b++) {
+      rel[b] = h_blk_off[b] - k.lo;
+      len[b] = h_blk_len[b];
+    }
+  uint64_t *d_rel = hp.d_blk, *d_len = hp.d_blk + nblocks, *d_olen = hp.d_blk + 2 * nblocks;
+  uint32_t *d_st = reinterpret_cast<uint32_t *>(hp.d_blk + 3 * nblocks);
+  hipStream_t work = c->stream;
+  SSTC_HIP(hipMemcpyAsync(d_rel, rel, 2 * nblocks * sizeof(uint64_t), hipMemcpyHostToDevice, hp.up),
+           "block arrays upload");
+  for (size_t i = 0; i < ch.size(); i++) {
+    const Chunk &k = ch[i];
+    const int s = static_cast<int>(i % kPipeBuf);
+    uint8_t *d_in = hp.d_buf + 2 * s * slot, *d_out = d_in + slot;
+    const uint64_t n = k.hi - k.lo;
+    if (i >= kPipeBuf) SSTC_HIP(hipStreamWaitEvent(hp.up, hp.ev_comp[s], 0), "wait");
+    SSTC_HIP(hipMemcpyAsync(d_in, h_src + k.lo, n, hipMemcpyHostToDevice, hp.up), "chunk upload");
+    SSTC_HIP(hipEventRecord(hp.ev_up[s], hp.up), "event");
+    SSTC_HIP(hipStreamWaitEvent(work, hp.ev_up[s], 0), "wait");
+    if (i >= kPipeBuf) SSTC_HIP(hipStreamWaitEvent(work, hp.ev_down[s], 0), "wait");
+    // rejected blocks and gaps keep the source bytes
+    SSTC_HIP(hipMemcpyAsync(d_out, d_in, n, hipMemcpyDeviceToDevice, work), "chunk copy");
+    sstc::RtArgs a{d_in, d_out, d_rel + k.b0, d_len + k.b0, k.b1 - k.b0, txn_mode, d_olen + k.b0, d_st + k.b0,
+                   c->err_count, c->num_cus};
+    SSTC_HIP(sstc::launch_roundtrip(a, work), "roundtrip kernels");
+    SSTC_HIP(hipEventRecord(hp.ev_comp[s], work), "event");
+    SSTC_HIP(hipStreamWaitEvent(hp.down, hp.ev_comp[s], 0), "wait");
+    const uint64_t first = h_blk_off[k.b0];
+    SSTC_HIP(hipMemcpyAsync(h_dst + first, d_out + (first - k.lo), k.hi - first, hipMemcpyDeviceToHost, hp.down),
+             "chunk download");
+    SSTC_HIP(hipEventRecord(hp.ev_down[s], hp.down), "event");
+  }
+  SSTC_HIP(hipMemcpyAsync(hp.h_stage + 2 * nblocks, d_olen, nblocks * (sizeof(uint64_t) + sizeof(uint32_t)),
+                          hipMemcpyDeviceToHost, work),
+           "results download");
+  SSTC_HIP(hipStreamSynchronize(work), "hipStreamSynchronize");
+  SSTC_HIP(hipStreamSynchronize(hp.down), "hipStreamSynchronize");
+  if (h_out_blk_len) std::memcpy(h_out_blk_len, hp.h_stage + 2 * nblocks, nblocks * sizeof(uint64_t));
+  if (h_block_status) std::memcpy(h_block_status, hp.h_stage + 3 * nblocks, nblocks * sizeof(uint32_t));
   return SSTC_OK;
 }
 

@@ -101,6 +101,8 @@ def load():
                                         c_vp, c_vp, c_u64, P(CompactResult)]),
         "sstc_get_batch": (ctypes.c_int, [c_vp, c_vp, P(BlockIndex), c_vp, c_vp, c_u64, c_vp, c_vp, c_u64, c_vp, c_vp,
                                           c_vp, c_vp]),
+        "sstc_roundtrip_host": (ctypes.c_int, [c_vp, c_vp, c_vp, c_u64, c_vp, c_vp, c_u64, c_u32, c_u64, c_vp,
+                                               c_vp]),
         "sstc_copy_probe": (ctypes.c_int, [c_vp, c_vp, c_vp, c_u64]),
         "sstc_open_tables": (ctypes.c_int, [c_vp, c_vp, c_u64, c_vp, c_vp, c_u32, c_u64, c_vp, c_vp, c_vp, c_vp,
                                             c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),

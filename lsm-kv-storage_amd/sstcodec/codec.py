@@ -110,6 +110,24 @@ class Codec:
                                              txn_mode, _p(out_len), _p(status)), "sstc_roundtrip_blocks")
         return dst, out_len, status
 
+    def roundtrip_host(self, h_src, h_dst, blk_off, blk_len, txn_mode=_lib.SSTC_TXN_COMPAT, chunk_bytes=16 << 20):
+        """sstc_roundtrip_host: blocks in host memory (u8 CPU tensors, pinned
+        for full rate; numpy offsets / lengths) streamed through the device.
+        Returns numpy (out_len, status)."""
+        import numpy as np
+        off = np.ascontiguousarray(blk_off, np.uint64)
+        ln = np.ascontiguousarray(blk_len, np.uint64)
+        nb = off.size
+        out_len = np.zeros(max(nb, 1), np.uint64)
+        status = np.zeros(max(nb, 1), np.uint32)
+        vp = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+        self._stream()
+        check(self.lib.sstc_roundtrip_host(self.h, ctypes.c_void_p(h_src.data_ptr()),
+                                           ctypes.c_void_p(h_dst.data_ptr()), h_src.numel(), vp(off), vp(ln), nb,
+                                           txn_mode, int(chunk_bytes), vp(out_len), vp(status)),
+              "sstc_roundtrip_host")
+        return out_len[:nb], status[:nb]
+
     def roundtrip_raw(self, src, dst, blk_off, blk_len, nb, txn_mode=_lib.SSTC_TXN_COMPAT,
                       out_len=None, status=None):
         """Minimal-overhead launch for timing loops (pointers pre-resolved by caller)."""
