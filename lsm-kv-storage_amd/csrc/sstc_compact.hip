@@ -1047,17 +1047,16 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
 //   ot_hop_kernel   one lane per table follows the exits tile to tile
 //                   (section bytes / 16 KiB dependent loads) and records where
 //                   the chain enters each tile and with which entry index
-//   ot_emit_kernel  every entered tile marks its chain positions by doubling
-//                   from the entry point (after round r the first 2^(r+1)
-//                   positions are marked), ranks them with a workgroup scan
-//                   and writes the block index entries
+//   ot_emit_kernel  every entered tile is staged in LDS, one lane walks the
+//                   chain from the entry point (the tile kernel already proved
+//                   where it starts), and the workgroup writes the block index
+//                   entries in parallel
 namespace sstc {
 namespace {
 
 constexpr uint32_t kOtTile = 16384, kOtThreads = 1024, kOtPer = kOtTile / kOtThreads;
 constexpr uint32_t kOtRounds = 10; // 2^10 > 16384 / 24 chain positions per tile
 static_assert((1u << kOtRounds) > kOtTile / 24 && kOtPer % 8 == 0, "doubling rounds must cover a tile's chain");
-constexpr uint16_t kOtOut = 0xFFFF;
 constexpr uint32_t kOtBad = 0xFFFFFFFFu;
 
 struct OtTable {
@@ -1080,22 +1079,14 @@ __device__ __forceinline__ uint32_t ot_find(const OtTable *t, uint32_t nt, uint3
   return lo;
 }
 
-// next(p) for section position p, or kOtBad when the entry at p runs past the
-// section (the bounds FetchBlockIndexInfo leaves unchecked)
-__device__ __forceinline__ uint32_t ot_next(const uint8_t *m, uint32_t mlen, uint32_t p) {
-  if (static_cast<uint64_t>(p) + 4 > mlen) return kOtBad;
-  const uint64_t q = static_cast<uint64_t>(p) + 4 + g_u32u(m + p);
-  if (q + 4 > mlen) return kOtBad;
-  const uint64_t e = q + 20 + g_u32u(m + q);
-  return e > mlen ? kOtBad : static_cast<uint32_t>(e);
-}
-
-// ot_next for kOtPer positions of a thread (each < mlen) with all first-length
-// loads in flight together, then all second-length loads: the per-position
-// form serializes 2 dependent global loads per position.  A load at p < mlen
-// stays inside the image (the 40 B footer follows the section); the second
-// load's address is clamped and its result dropped when invalid.
-// (groups of kOtBatch positions: the whole thread's set at once spills)
+// next(p) = p + 24 + fkl + lkl, or kOtBad when the entry at p runs past the
+// section (the bounds FetchBlockIndexInfo leaves unchecked), for kOtBatch
+// positions (each < mlen) of a thread: all first-length loads in flight
+// together, then all second-length loads (one position at a time serializes
+// 2 dependent global loads per position; the whole thread's set at once
+// spills).  A load at p < mlen stays inside the image (the 40 B footer
+// follows the section); the second load's address is clamped and its result
+// dropped when invalid.
 constexpr uint32_t kOtBatch = 8;
 __device__ __forceinline__ void ot_next_group(const uint8_t *m, uint32_t mlen, const uint32_t *pos, uint32_t *e) {
   uint32_t k1[kOtBatch], q[kOtBatch];
@@ -1229,12 +1220,18 @@ struct OtOut {
   uint32_t *fk_len, *lk_len;
 };
 
-__global__ __launch_bounds__(kOtThreads) void ot_emit_kernel(const uint8_t *src, const OtTable *tabs, uint32_t nt,
-                                                             const uint32_t *tstart, const uint64_t *tbase, OtOut o,
-                                                             int32_t *status) {
-  __shared__ uint16_t sJ[kOtTile]; // f^(2^r)(p) inside the tile, kOtOut once it leaves
-  __shared__ uint8_t sM[kOtTile];  // p is a chain position
-  __shared__ uint32_t sW[kOtThreads / kWave];
+// the chain from the tile's entry point is walked by one lane over the tile
+// staged in LDS (two dependent LDS reads per entry, <= 683 entries), then the
+// workgroup parses the listed entries in parallel.  It replaced a marking pass
+// by pointer doubling from the entry point (10 rounds of barriers over every
+// byte position): config 3 162 -> 85 us.
+constexpr uint32_t kOtEmitThreads = 256, kOtMaxEntries = kOtTile / 24 + 1;
+__global__ __launch_bounds__(kOtEmitThreads) void ot_emit_kernel(const uint8_t *src, const OtTable *tabs, uint32_t nt,
+                                                                 const uint32_t *tstart, const uint64_t *tbase,
+                                                                 OtOut o, int32_t *status) {
+  __shared__ uint32_t sImg[kOtTile / 4 + 4];
+  __shared__ uint16_t sPos[kOtMaxEntries];
+  __shared__ uint32_t sCnt;
   const uint32_t g = blockIdx.x;
   const uint32_t s = tstart[g];
   if (s == kOtBad) return; // uniform: the chain skips this tile
@@ -1243,79 +1240,51 @@ __global__ __launch_bounds__(kOtThreads) void ot_emit_kernel(const uint8_t *src,
   const uint8_t *m = src + T.meta;
   const uint32_t t0 = (g - T.tile0) * kOtTile;
   const uint32_t n = min(kOtTile, T.mlen - t0);
-#pragma unroll
-  for (uint32_t g0 = 0; g0 < kOtPer; g0 += kOtBatch) {
-    uint32_t pos[kOtBatch], nx[kOtBatch];
-#pragma unroll
-    for (uint32_t j = 0; j < kOtBatch; j++) {
-      const uint32_t p = threadIdx.x + (g0 + j) * kOtThreads;
-      pos[j] = t0 + (p < n ? p : 0u);
+  // words covering tile bytes [0, n + 8); the reads past the section stay in
+  // the image (the 40 B footer follows it)
+  const uint32_t W = (n + 8 + 3) / 4;
+  for (uint32_t i = threadIdx.x; i < W; i += kOtEmitThreads) sImg[i] = g_u32u(m + t0 + 4 * i);
+  __syncthreads();
+  const uint8_t *img = reinterpret_cast<const uint8_t *>(sImg);
+  const uint64_t base = tbase[g];
+  const uint64_t want = base < T.nb ? T.nb - base : 0;
+  const uint64_t lim = T.mlen - t0; // section end, tile-relative
+  if (threadIdx.x == 0) {
+    uint64_t p = s;
+    uint32_t j = 0;
+    while (p < n && j < want && p + 4 <= lim) {
+      const uint64_t q = p + 4 + lds_u32u(img, static_cast<uint32_t>(p));
+      if (q + 4 > lim) break;
+      const uint32_t k2 = q <= n ? lds_u32u(img, static_cast<uint32_t>(q)) : g_u32u(m + t0 + q);
+      const uint64_t e = q + 20 + k2;
+      if (e > lim) break;
+      sPos[j++] = static_cast<uint16_t>(p);
+      p = e;
     }
-    ot_next_group(m, T.mlen, pos, nx);
-#pragma unroll
-    for (uint32_t j = 0; j < kOtBatch; j++) {
-      const uint32_t p = threadIdx.x + (g0 + j) * kOtThreads;
-      if (p < n) {
-        sJ[p] = static_cast<uint16_t>(nx[j] != kOtBad && nx[j] < t0 + n ? nx[j] - t0 : kOtOut);
-        sM[p] = p == s;
-      }
-    }
+    sCnt = j;
   }
   __syncthreads();
-  for (uint32_t r = 0; r < kOtRounds; r++) {
-    // marks {f^i(s) : i < 2^r} -> {i < 2^(r+1)}; a mark set earlier in the same
-    // round only marks further chain positions, never others
-    for (uint32_t k = 0; k < kOtPer; k++) {
-      const uint32_t p = threadIdx.x + k * kOtThreads;
-      if (p >= n) break;
-      const uint32_t j = sJ[p];
-      if (sM[p] && j != kOtOut) sM[j] = 1;
+  const uint32_t cnt = sCnt;
+  for (uint32_t j = threadIdx.x; j < cnt; j += kOtEmitThreads) {
+    const uint32_t p = sPos[j];
+    const uint32_t fkl = lds_u32u(img, p);
+    const uint64_t q = p + 4ull + fkl;
+    const uint32_t lkl = q <= n ? lds_u32u(img, static_cast<uint32_t>(q)) : g_u32u(m + t0 + q);
+    const uint64_t r = q + 4 + lkl;
+    uint64_t bo, bl;
+    if (r + 16 <= n) {
+      bo = lds_u64u(img, static_cast<uint32_t>(r));
+      bl = lds_u64u(img, static_cast<uint32_t>(r + 8));
+    } else {
+      bo = g_u64u(m + t0 + r);
+      bl = g_u64u(m + t0 + r + 8);
     }
-    __syncthreads();
-    if (r + 1 == kOtRounds) break;
-    uint16_t l[kOtPer];
-#pragma unroll
-    for (uint32_t k = 0; k < kOtPer; k++) {
-      const uint32_t p = threadIdx.x + k * kOtThreads;
-      if (p < n) {
-        const uint32_t j = sJ[p];
-        l[k] = j == kOtOut ? kOtOut : sJ[j];
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (uint32_t k = 0; k < kOtPer; k++) {
-      const uint32_t p = threadIdx.x + k * kOtThreads;
-      if (p < n) sJ[p] = l[k];
-    }
-    __syncthreads();
-  }
-  // rank the marked positions: thread i owns [i * kOtPer, (i + 1) * kOtPer)
-  const uint32_t b0 = threadIdx.x * kOtPer;
-  uint32_t cnt = 0;
-  for (uint32_t k = 0; k < kOtPer; k++)
-    if (b0 + k < n) cnt += sM[b0 + k];
-  const uint32_t lane = lane_id(), w = threadIdx.x / kWave;
-  const uint32_t inc = wave_incl_scan_u32(cnt);
-  if (lane == kWave - 1) sW[w] = inc;
-  __syncthreads();
-  uint32_t rank = inc - cnt;
-  for (uint32_t v = 0; v < w; v++) rank += sW[v];
-  for (uint32_t k = 0; k < kOtPer; k++) {
-    const uint32_t p = b0 + k;
-    if (p >= n || !sM[p]) continue;
-    const uint64_t i = tbase[g] + rank++;
-    if (i >= T.nb) break;
-    const uint32_t pa = t0 + p;
-    if (ot_next(m, T.mlen, pa) == kOtBad) break; // past the valid entries (status is BAD_META)
-    const uint32_t fkl = g_u32u(m + pa), lkl = g_u32u(m + pa + 4 + fkl);
-    const uint64_t bo = g_u64u(m + pa + 8 + fkl + lkl), bl = g_u64u(m + pa + 16 + fkl + lkl);
-    const uint64_t b = T.fb + i;
+    const uint64_t b = T.fb + base + j;
     o.blk_off[b] = T.data + bo;
     o.blk_len[b] = bl;
-    o.fk_off[b] = T.meta + pa + 4;
+    o.fk_off[b] = T.meta + t0 + p + 4;
     o.fk_len[b] = fkl;
-    o.lk_off[b] = T.meta + pa + 8 + fkl;
+    o.lk_off[b] = T.meta + t0 + q + 4;
     o.lk_len[b] = lkl;
     if (bo > T.moff || bl > T.moff - bo) atomicCAS(&status[ti], SSTC_TAB_OK, SSTC_TAB_BAD_BLOCK);
   }
@@ -1402,7 +1371,7 @@ int open_tables_impl(Arena &arena, hipStream_t s, const uint8_t *d_src, uint64_t
       ot_tile_kernel<<<static_cast<uint32_t>(tiles), kOtThreads, 0, s>>>(d_src, d_tabs, nt, EC, tstart);
       ot_hop_kernel<<<grid(nt, 64), 64, 0, s>>>(d_tabs, nt, EC, tstart, tbase, d_st);
       OtOut o{out.blk_off, out.blk_len, out.first_key_off, out.last_key_off, out.first_key_len, out.last_key_len};
-      ot_emit_kernel<<<static_cast<uint32_t>(tiles), kOtThreads, 0, s>>>(d_src, d_tabs, nt, tstart, tbase, o, d_st);
+      ot_emit_kernel<<<static_cast<uint32_t>(tiles), kOtEmitThreads, 0, s>>>(d_src, d_tabs, nt, tstart, tbase, o, d_st);
       CK(hipGetLastError());
     }
     if (nt) CK(hipMemcpyAsync(H + w_st, d_st, nt * sizeof(int32_t), hipMemcpyDeviceToHost, s));
