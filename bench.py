@@ -14,10 +14,10 @@ generated on the host (synthetic, deterministic); a warm-up round trip is
 checked for identity before timing.
 
 roofline: the dominant (only) kernel of a step is rt_kernel.  Algorithmic bytes per launch
-= B x (4188 read + 4188 written); duration = HIP events on
-the codec's stream around each sstc_roundtrip_blocks call (includes the
-launch gap between back-to-back calls, so the
-fraction is slightly conservative); peak = 8 TB/s (MI355X_MICROARCH.md).
+= B x (4188 read + 4188 written); duration = span of HIP
+events on the codec's stream at the two ends of the K timed calls / K
+(includes the launch gaps between back-to-back calls, so the fraction is
+slightly conservative against the rocprofv3 kernel average); peak = 8 TB/s (MI355X_MICROARCH.md).
 traffic = HBM bytes per launch from rocprofv3 PMC passes (FETCH_SIZE x 2 for
 gfx950 + WRITE_SIZE, KB units), read from profiles/pmc_traffic.json when it was
 collected for this workload, else null.
@@ -80,20 +80,23 @@ def time_roundtrip(codec, src, dst, off, ln, steps, warmup, stream, dist_on):
     for _ in range(warmup):
         rc = codec.roundtrip_raw(*args)
         assert rc == 0
-    evs = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
+    # HIP events at the two ends of the timed region only: an event recorded
+    # between launches adds ~2.5 us per step (tools/ab_launch.py,
+    # profiles/r01_ab_launch.log); the per-launch average is their span / K
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if dist_on:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    evs[0].record(stream)
-    for i in range(steps):
+    e0.record(stream)
+    for _ in range(steps):
         codec.roundtrip_raw(*args)
-        evs[i + 1].record(stream)
+    e1.record(stream)
     torch.cuda.synchronize()
     if dist_on:
         dist.barrier()
     wall = time.perf_counter() - t0
-    per_launch = [evs[i].elapsed_time(evs[i + 1]) for i in range(steps)]
+    per_launch = [e0.elapsed_time(e1) / steps] * steps
     return wall, per_launch, out_len, status
 
 
@@ -188,8 +191,8 @@ def e2e_rate(codec, src, off, ln, chunk_bytes=16 << 20, reps=5):
 
 def hbm_variant(codec, dev, nblocks, steps=10):
     """The same fused round trip over nblocks (default 4 x config 2, ~1.1 GB in
-    + 1.1 GB out: beyond the 256 MiB Infinity Cache, so HBM-bound).  Mean HIP-
-    event time per launch over `steps` back-to-back launches; identity checked."""
+    + 1.1 GB out: beyond the 256 MiB Infinity Cache, so HBM-bound).  HIP-event
+    span of `steps` back-to-back launches / steps; identity checked."""
     import ctypes
     src, off, ln = make_blocks(codec, dev, nblocks, 0)
     dst = torch.empty_like(src)
@@ -201,15 +204,15 @@ def hbm_variant(codec, dev, nblocks, steps=10):
     stream = torch.cuda.current_stream(dev)
     for _ in range(2):
         assert codec.roundtrip_raw(*args) == 0
-    evs = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
-    evs[0].record(stream)
-    for i in range(steps):
+    e0.record(stream)
+    for _ in range(steps):
         codec.roundtrip_raw(*args)
-        evs[i + 1].record(stream)
+    e1.record(stream)
     torch.cuda.synchronize()
     ok = bool(torch.equal(dst, src)) and bool((status == 0).all())
-    ms = float(np.mean([evs[i].elapsed_time(evs[i + 1]) for i in range(steps)]))
+    ms = e0.elapsed_time(e1) / steps
     alg = 2 * nblocks * BLOCK_BYTES
     achieved = alg / (ms * 1e-3) / 1e9
     del src, dst, off, ln, out_len, status
