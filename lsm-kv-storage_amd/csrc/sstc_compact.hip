@@ -1044,7 +1044,7 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
 //                   doubling in LDS gives, for every p, the entries the chain
 //                   from p holds inside the tile and the first chain position
 //                   past the tile (its exit)
-//   ot_hop_kernel   one lane per table follows the exits tile to tile
+//   ot_hop_kernel   one wave per table follows the exits tile to tile
 //                   (section bytes / 16 KiB dependent loads) and records where
 //                   the chain enters each tile and with which entry index
 //   ot_emit_kernel  every entered tile is staged in LDS, one lane walks the
@@ -1188,31 +1188,65 @@ __global__ __launch_bounds__(kOtThreads) void ot_tile_kernel(const uint8_t *src,
   }
 }
 
-__global__ void ot_hop_kernel(const OtTable *tabs, uint32_t nt, const uint64_t *EC, uint32_t *tstart, uint64_t *tbase,
-                              int32_t *status) {
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= nt) return;
+// One wave per table.  The chain enters a tile near its start (within one
+// entry of the previous exit: 56 B at 16 B keys), so the exit words of the
+// first kOtWinPos positions of kOtWinTiles tiles are fetched into LDS in one
+// batch of coalesced loads and the hops inside that window resolve from LDS;
+// an entry point further into a tile reads its word from HBM.
+constexpr uint32_t kOtWinTiles = 64, kOtWinPos = kWave, kOtWinBatch = 16;
+__global__ __launch_bounds__(kWave) void ot_hop_kernel(const OtTable *tabs, uint32_t nt, const uint64_t *EC,
+                                                       uint32_t *tstart, uint64_t *tbase, int32_t *status) {
+  __shared__ uint64_t sW[kOtWinTiles][kOtWinPos];
+  const uint32_t t = blockIdx.x;
   const OtTable T = tabs[t];
-  if (T.nb == 0) return;
+  if (T.nb == 0) return; // uniform
+  const uint32_t lane = threadIdx.x;
+  const uint32_t ntiles = (T.mlen + kOtTile - 1) / kOtTile;
   uint64_t x = 0, idx = 0;
+  uint32_t wb = ~0u; // first (table-relative) tile of the LDS window
+  int32_t st = SSTC_TAB_OK;
   for (;;) {
     if (x >= T.mlen) { // the section ends before num_blocks entries
-      status[t] = SSTC_TAB_BAD_META;
-      return;
+      st = SSTC_TAB_BAD_META;
+      break;
     }
-    const uint32_t g = T.tile0 + static_cast<uint32_t>(x / kOtTile), o = static_cast<uint32_t>(x % kOtTile);
-    tstart[g] = o;
-    tbase[g] = idx;
-    const uint64_t v = EC[static_cast<uint64_t>(g) * kOtTile + o];
+    const uint32_t gl = static_cast<uint32_t>(x / kOtTile), o = static_cast<uint32_t>(x % kOtTile);
+    uint64_t v;
+    if (o < kOtWinPos) {
+      if (wb == ~0u || gl < wb || gl >= wb + kOtWinTiles) {
+        wb = gl;
+        const uint32_t rows = min(kOtWinTiles, ntiles - gl);
+        for (uint32_t i0 = 0; i0 < rows; i0 += kOtWinBatch) {
+          uint64_t w[kOtWinBatch];
+#pragma unroll
+          for (uint32_t j = 0; j < kOtWinBatch; j++) {
+            const uint32_t row = min(i0 + j, rows - 1); // clamped: loads issue unconditionally
+            w[j] = EC[static_cast<uint64_t>(T.tile0 + wb + row) * kOtTile + lane];
+          }
+#pragma unroll
+          for (uint32_t j = 0; j < kOtWinBatch; j++)
+            if (i0 + j < rows) sW[i0 + j][lane] = w[j];
+        }
+        __syncthreads();
+      }
+      v = sW[gl - wb][o];
+    } else {
+      v = EC[static_cast<uint64_t>(T.tile0 + gl) * kOtTile + o];
+    }
+    if (lane == 0) {
+      tstart[T.tile0 + gl] = o;
+      tbase[T.tile0 + gl] = idx;
+    }
     idx += v >> 32;
-    if (idx >= T.nb) return;
+    if (idx >= T.nb) break;
     const uint32_t e = static_cast<uint32_t>(v);
     if (e == kOtBad) {
-      status[t] = SSTC_TAB_BAD_META;
-      return;
+      st = SSTC_TAB_BAD_META;
+      break;
     }
     x = e;
   }
+  if (lane == 0 && st != SSTC_TAB_OK) status[t] = st;
 }
 
 struct OtOut {
@@ -1369,7 +1403,7 @@ int open_tables_impl(Arena &arena, hipStream_t s, const uint8_t *d_src, uint64_t
       uint32_t *tstart = pool.get<uint32_t>(tiles);
       uint64_t *tbase = pool.get<uint64_t>(tiles);
       ot_tile_kernel<<<static_cast<uint32_t>(tiles), kOtThreads, 0, s>>>(d_src, d_tabs, nt, EC, tstart);
-      ot_hop_kernel<<<grid(nt, 64), 64, 0, s>>>(d_tabs, nt, EC, tstart, tbase, d_st);
+      ot_hop_kernel<<<nt, kWave, 0, s>>>(d_tabs, nt, EC, tstart, tbase, d_st);
       OtOut o{out.blk_off, out.blk_len, out.first_key_off, out.last_key_off, out.first_key_len, out.last_key_len};
       ot_emit_kernel<<<static_cast<uint32_t>(tiles), kOtEmitThreads, 0, s>>>(d_src, d_tabs, nt, tstart, tbase, o, d_st);
       CK(hipGetLastError());
