@@ -60,7 +60,7 @@ for name, fn in (("h2d", h2d), ("d2h", d2h), ("both", both)):
 # native pipeline (sstc_roundtrip_host): per-chunk enqueue cost is C++, not Python
 o = off.cpu().numpy().view("u8")
 n = ln.cpu().numpy().view("u8")
-for chunk_mb in (2, 4, 8, 17, 34):
+for chunk_mb in (2, 4, 8, 16, 32):
     cb = chunk_mb << 20
     codec.roundtrip_host(h_src, h_dst, o, n, chunk_bytes=cb)
     torch.cuda.synchronize()
