@@ -4,10 +4,13 @@
 
 One "step" = one fused decode -> re-encode pass (sstc_roundtrip_blocks) over
 B blocks resident in HBM (default B = 65 536 uniform 4188 B blocks, 16 B keys /
-100 B values = BASELINE config 2).  With N > 1 (torchrun, one rank per GPU)
-every rank owns its own disjoint shard of B blocks (weak scaling, no data-path
-collective); the barrier and the max-over-ranks timing are the only
-communication.  value = input bytes of all ranks / max-over-ranks time, GiB/s.
+100 B values = BASELINE config 2).  With --gpus N > 1 the script launches N
+ranks itself (torch.distributed.run as a child process, before any GPU call;
+under an external torchrun it joins as one rank), rank r on GPU r; every rank
+owns its own disjoint shard of B blocks (weak scaling, no data-path
+collective); the barrier and the per-rank timings (gathered over RCCL) are the
+only communication.  value = input bytes of all ranks / max-over-ranks time,
+GiB/s; per_rank lists each GPU's GiB/s and roofline fraction.
 
 Input blocks are produced on the GPU by the codec's own encoder from records
 generated on the host (synthetic, deterministic); a warm-up round trip is
@@ -24,9 +27,13 @@ collected for this workload, else null.
 
 cpu_baseline: the reference's own code (oracle/_ref/libsstref.so: BlockReader +
 BlockReaderIterator -> BlockBuilder), one thread, on a bounded sample of the
-same blocks; falls back to the clean-room oracle ("port") if the reference
-build is absent.  cpu_baseline_16_threads: the same on 16 host threads (the
-box's CPU share per GPU; generous, the reference compacts on one thread).
+same blocks, pinned to one CPU; falls back to the clean-room oracle ("port")
+if the reference build is absent.  cpu_baseline_all: the same on nproc host
+threads (the job's CPU share), each pinned to its own CPU; generous, the
+reference compacts on one thread.
+
+legs (N=1): decode alone and encode alone over the same blocks, each with its
+own roofline sub-object.
 """
 import argparse
 import json
@@ -36,12 +43,12 @@ import time
 
 import numpy as np
 import torch
-import torch.distributed as dist
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "lsm-kv-storage_amd"))
 
 import sstcodec  # noqa: E402
+from sstcodec import launch  # noqa: E402
 from sstcodec import shard  # noqa: E402
 from sstcodec import workload as W  # noqa: E402
 from sstcodec.codec import RecordTable  # noqa: E402
@@ -69,7 +76,7 @@ def make_blocks(codec, dev, nblocks, rank):
     return src, off[:-1].contiguous(), ln.contiguous()
 
 
-def time_roundtrip(codec, src, dst, off, ln, steps, warmup, stream, dist_on):
+def time_roundtrip(codec, src, dst, off, ln, steps, warmup, stream, ranks):
     import ctypes
     nb = off.numel()
     out_len = torch.empty(nb, dtype=torch.int64, device=src.device)
@@ -84,8 +91,7 @@ def time_roundtrip(codec, src, dst, off, ln, steps, warmup, stream, dist_on):
     # between launches adds ~2.5 us per step (tools/ab_launch.py,
     # profiles/r01_ab_launch.log); the per-launch average is their span / K
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    if dist_on:
-        dist.barrier()
+    ranks.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     e0.record(stream)
@@ -93,8 +99,7 @@ def time_roundtrip(codec, src, dst, off, ln, steps, warmup, stream, dist_on):
         codec.roundtrip_raw(*args)
     e1.record(stream)
     torch.cuda.synchronize()
-    if dist_on:
-        dist.barrier()
+    ranks.barrier()
     wall = time.perf_counter() - t0
     per_launch = [e0.elapsed_time(e1) / steps] * steps
     return wall, per_launch, out_len, status
@@ -112,6 +117,9 @@ def cpu_baseline(sample_src, sample_off, sample_len, seconds=10.0):
         lib = O.Oracle()
         run = lambda: lib.roundtrip(sample_src, sample_off, sample_len, 0)  # noqa: E731
     dst = np.zeros_like(sample_src)
+    old = os.sched_getaffinity(0)
+    cpu = current_cpu()
+    os.sched_setaffinity(0, {cpu})
     run()  # warm
     passes = 0
     t0 = time.perf_counter()
@@ -121,18 +129,20 @@ def cpu_baseline(sample_src, sample_off, sample_len, seconds=10.0):
         el = time.perf_counter() - t0
         if el >= seconds:
             break
+    os.sched_setaffinity(0, old)
     nbytes = passes * int(sample_len.sum())
-    return {"value": nbytes / el / 2 ** 30, "unit": "GiB/s", "cores": 1, "kind": kind,
+    return {"value": nbytes / el / 2 ** 30, "unit": "GiB/s", "cores": 1, "kind": kind, "pinned_cpu": cpu,
             "sample": f"{sample_len.size} blocks x {int(sample_len[0])} B (same uniform workload), "
                       f"{passes} passes in {el:.1f} s, 1 thread, decode (BlockReader/Iterator) + "
                       f"re-encode (BlockBuilder) in host memory"}
 
 
-def cpu_baseline_threads(sample_src, sample_off, sample_len, threads=16, seconds=5.0):
-    """The same reference round trip on `threads` host threads (blocks split
-    into contiguous ranges, one per thread; ctypes releases the GIL).  A
-    generous baseline: the reference runs one compaction at a time on one
-    thread (db/db_impl.cc:548).  16 = the GPU box's CPU share per GPU."""
+def cpu_baseline_threads(sample_src, sample_off, sample_len, threads, seconds=5.0):
+    """The same reference round trip on `threads` host threads (= nproc, the CPU
+    share this job is given), blocks split into contiguous ranges, thread k
+    pinned to the k-th CPU of the affinity mask (ctypes releases the GIL).  A
+    GENEROUS baseline: the reference runs one compaction at a time on one
+    thread (db/db_impl.cc:548)."""
     import threading
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
@@ -140,6 +150,11 @@ def cpu_baseline_threads(sample_src, sample_off, sample_len, threads=16, seconds
         lib = O.RefLib()
     except (FileNotFoundError, OSError):
         return None
+    cpus = sorted(os.sched_getaffinity(0))
+    n_aff = len(cpus)
+    threads = max(1, min(threads, n_aff))
+    c0 = cpus.index(current_cpu()) if current_cpu() in cpus else 0
+    cpus = (cpus[c0:] + cpus[:c0])[:threads]
     nb = sample_off.size
     parts = np.array_split(np.arange(nb), threads)
     dsts = [np.zeros_like(sample_src) for _ in range(threads)]
@@ -147,6 +162,7 @@ def cpu_baseline_threads(sample_src, sample_off, sample_len, threads=16, seconds
     stop = time.perf_counter() + seconds
 
     def work(k):
+        os.sched_setaffinity(0, {cpus[k]})  # pid 0 = this thread (Linux)
         idx = parts[k]
         o, ln = sample_off[idx], sample_len[idx]
         while time.perf_counter() < stop:
@@ -161,8 +177,11 @@ def cpu_baseline_threads(sample_src, sample_off, sample_len, threads=16, seconds
         t.join()
     el = time.perf_counter() - t0
     return {"value": sum(done) / el / 2 ** 30, "unit": "GiB/s", "cores": threads, "kind": "reference",
-            "sample": f"{nb} blocks split over {threads} threads, {el:.1f} s (generous: the reference compacts "
-                      f"on one thread)"}
+            "nproc": nproc(), "os_cpu_count": os.cpu_count(), "affinity_cpus": n_aff,
+            "pinning": f"thread k -> CPU {cpus[0]}+k of the affinity mask (sched_setaffinity; start = the CPU "
+                                 f"the bench ran on)",
+            "label": "generous: the reference compacts on one thread",
+            "sample": f"{nb} blocks split over {threads} threads, {el:.1f} s"}
 
 
 def e2e_rate(codec, src, off, ln, chunk_bytes=16 << 20, reps=5):
@@ -260,9 +279,92 @@ def copy_peak(codec, dev, nbytes, reps=10):
     return 2 * nbytes / (ms * 1e-3) / 1e9
 
 
+def nproc():
+    """GNU nproc (honours the affinity mask and OMP_NUM_THREADS, i.e. the
+    CPU share a job is given on the GPU box) with os.cpu_count() beside it."""
+    import shutil
+    import subprocess
+    try:
+        return int(subprocess.run([shutil.which("nproc") or "nproc"], capture_output=True, text=True,
+                                  check=True).stdout.strip())
+    except (OSError, ValueError, subprocess.CalledProcessError):
+        return len(os.sched_getaffinity(0))
+
+
+def current_cpu():
+    """CPU this thread runs on now (/proc/self/stat field 39): the pinned
+    baselines start there rather than at CPU 0, which on a shared host is the
+    likeliest to be busy."""
+    try:
+        with open("/proc/thread-self/stat") as f:
+            return int(f.read().rsplit(")", 1)[1].split()[36])
+    except (OSError, ValueError, IndexError):
+        return min(os.sched_getaffinity(0))
+
+
+def time_leg(codec, stream, call, steps, warmup=3):
+    """HIP-event span of `steps` back-to-back calls on the codec's stream / steps (ms)."""
+    for _ in range(warmup):
+        rc = call()
+        assert rc == 0, rc
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record(stream)
+    for _ in range(steps):
+        call()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / steps
+
+
+def codec_legs(codec, dev, stream, src, off, ln, steps):
+    """Decode alone (sstc_decode_blocks: blocks -> SoA record table) and encode
+    alone (sstc_encode_blocks: SoA + key/value arenas -> blocks) over the same
+    config-2 blocks, each with its own roofline (a decode
+    counts B_in + SoA bytes out; an encode counts block bytes out + key/value
+    bytes read + SoA bytes read).  Both outputs are verified."""
+    import ctypes
+    nb = off.numel()
+    P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    rec_base = codec.count(src, off, ln)
+    table, _, status = codec.decode(src, off, ln, rec_base=rec_base)
+    nrec = table.n
+    c = table.c()
+    dec = lambda: codec.lib.sstc_decode_blocks(codec.h, P(src), P(off), P(ln), nb, P(rec_base), c,  # noqa: E731
+                                               sstcodec.SSTC_TXN_COMPAT, P(status))
+    codec._stream()
+    dms = time_leg(codec, stream, dec, steps)
+    ok_dec = bool((status == 0).all()) and nrec == nb * PER_BLOCK
+    soa = 33 * nrec
+    d_alg = nb * BLOCK_BYTES + soa
+    # encode from the decoded table: keys / values are read in place from the
+    # input blocks (key_off / val_off point into src), first = every 28 records
+    first = torch.arange(0, nrec + 1, PER_BLOCK, dtype=torch.int64, device=dev)
+    dst = torch.zeros_like(src)
+    out_off = torch.empty(nb + 1, dtype=torch.int64, device=dev)
+    out_len = torch.empty(nb, dtype=torch.int64, device=dev)
+    enc = lambda: codec.lib.sstc_encode_blocks(codec.h, P(src), P(src), c, nrec, P(first), nb, 0,  # noqa: E731
+                                               P(dst), P(out_off), P(out_len))
+    ems = time_leg(codec, stream, enc, steps)
+    ok_enc = bool(torch.equal(dst, src))
+    kv = nrec * (16 + 100)
+    e_alg = nb * BLOCK_BYTES + kv + soa
+    leg = lambda ms, alg, kern, how, ok: {  # noqa: E731
+        "ms": round(ms, 5), "GiBps_blocks": round(nb * BLOCK_BYTES / (ms * 1e-3) / 2 ** 30, 1),
+        "roofline": {"bound": "hbm", "achieved": round(alg / (ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBPS,
+                     "unit": "GB/s", "frac": round(alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+                     "alg_bytes_per_launch": alg, "kernel": kern, "bytes": how},
+        "verified": ok}
+    return {"decode": leg(dms, d_alg, "decode_kernel", f"{nb} x {BLOCK_BYTES} B blocks read + {nrec} x 33 B SoA "
+                          "records written", ok_dec),
+            "encode": leg(ems, e_alg, "enc_sizes + scan + enc_lds_kernel<0>",
+                          f"{nb} x {BLOCK_BYTES} B blocks written + {nrec} x 116 B key/value read + "
+                          f"{nrec} x 33 B SoA read", ok_enc)}
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1, help="ranks (one per GPU); >1 launches them itself")
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--blocks", type=int, default=65536, help="blocks per GPU (config 2: 65536)")
@@ -270,19 +372,23 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host->device->host rate")
     ap.add_argument("--no-hbm-variant", action="store_true", help="skip the 4x (1 GiB, HBM-bound) measurement")
+    ap.add_argument("--no-legs", action="store_true", help="skip the decode-only / encode-only legs")
+    ap.add_argument("--plumbing", action="store_true",
+                    help="CPU-only launcher check (gloo, host copy as the step): NOT a measurement")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist_on = world > 1
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if dist_on:
-        dist.init_process_group("nccl", device_id=dev)
+    # N ranks: launch them (child processes, before anything touches the GPU)
+    rc = launch.relaunch(args.gpus, os.path.abspath(__file__), sys.argv[1:])
+    if rc is not None:
+        sys.exit(rc)
+    ranks = launch.init_ranks(args.gpus, "gloo" if args.plumbing else "nccl")
+    if args.plumbing:
+        return plumbing(args, ranks)
+    dev = ranks.device
+    rank, world = ranks.rank, ranks.world
     stream = torch.cuda.current_stream(dev)
 
-    codec = sstcodec.Codec(local)
+    codec = sstcodec.Codec(ranks.local)
     nb = args.blocks
     codec.reserve(nb, nb * PER_BLOCK)
     src, off, ln = make_blocks(codec, dev, nb, rank)
@@ -291,21 +397,21 @@ def main():
     dst = torch.empty_like(src)
 
     wall, per_launch, out_len, status = time_roundtrip(codec, src, dst, off, ln, args.steps, args.warmup,
-                                                       stream, dist_on)
+                                                       stream, ranks)
     # correctness of what was timed: identity round trip, no block errors
     ok = bool(torch.equal(dst, src)) and bool((status == 0).all()) and bool((out_len == BLOCK_BYTES).all())
     if not ok:
         raise SystemExit("round trip output differs from input: timing invalid")
 
-    wall_max = shard.max_over_ranks(wall, dev)
     in_bytes = nb * BLOCK_BYTES
-    total_in = in_bytes * world * args.steps
-    value = total_in / wall_max / 2 ** 30
-    ms_step = wall_max / args.steps * 1e3
-
     launch_ms = float(np.mean(per_launch))
     alg = 2 * in_bytes  # read + written per launch
     achieved = alg / (launch_ms * 1e-3) / 1e9
+    per_rank = ranks.gather([wall, launch_ms])
+    wall_max = max(w for w, _ in per_rank)
+    total_in = in_bytes * world * args.steps
+    value = total_in / wall_max / 2 ** 30
+    ms_step = wall_max / args.steps * 1e3
     traffic = read_traffic(nb)
 
     if rank == 0:
@@ -332,10 +438,17 @@ def main():
                          "kernel": "rt_kernel", "alg_bytes_per_launch": alg,
                          "launch_ms_events": round(launch_ms, 5)},
         }
+        if world > 1:
+            out["per_rank"] = [{"rank": r, "GiBps": round(in_bytes * args.steps / w / 2 ** 30, 2),
+                                "launch_ms_events": round(lm, 5),
+                                "roofline_frac": round(alg / (lm * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)}
+                               for r, (w, lm) in enumerate(per_rank)]
         if world == 1:
             cp = copy_peak(codec, dev, (alg // 2 + 15) // 16 * 16)
             out["roofline"]["copy_peak_GBps"] = round(cp, 1)
             out["roofline"]["frac_of_copy_peak"] = round(achieved / cp, 4)
+            if not args.no_legs:
+                out["legs"] = codec_legs(codec, dev, stream, src, off, ln, max(10, args.steps // 2))
             if not args.no_hbm_variant:
                 out["roofline"]["hbm_1gib"] = hbm_variant(codec, dev, 4 * nb)
             if not args.no_e2e:
@@ -346,13 +459,36 @@ def main():
                 o = off[:k].cpu().numpy().view(np.uint64)
                 l_ = ln[:k].cpu().numpy().view(np.uint64)
                 out["cpu_baseline"] = cpu_baseline(s, o, l_, args.cpu_seconds)
-                all_cores = cpu_baseline_threads(s, o, l_, 16, min(5.0, args.cpu_seconds))
+                all_cores = cpu_baseline_threads(s, o, l_, nproc(), min(5.0, args.cpu_seconds))
                 if all_cores:
-                    out["cpu_baseline_16_threads"] = all_cores
+                    out["cpu_baseline_all"] = all_cores
         print(json.dumps(out), flush=True)
-    if dist_on:
-        dist.barrier()
-        dist.destroy_process_group()
+    ranks.close()
+
+
+def plumbing(args, ranks):
+    """The launcher / rank / timing / aggregation path of the bench without a
+    GPU: each rank copies its shard's bytes on the host as its "step".  For
+    the CPU test of `--gpus N` (tests/test_bench_launch.py); not a measurement."""
+    nb = min(args.blocks, 256)
+    a = np.full(nb * BLOCK_BYTES, ranks.rank, np.uint8)
+    b = np.empty_like(a)
+    ranks.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        np.copyto(b, a)
+    ranks.barrier()
+    wall = time.perf_counter() - t0
+    per_rank = ranks.gather([wall, float(b[0])])
+    wall_max = max(w for w, _ in per_rank)
+    if ranks.rank == 0:
+        print(json.dumps({"metric": METRIC, "value": round(nb * BLOCK_BYTES * ranks.world * args.steps / wall_max
+                                                          / 2 ** 30, 3),
+                          "unit": "GiB/s", "n_gpus": ranks.world, "steps": args.steps, "warmup": args.warmup,
+                          "scaling": "weak", "data": "plumbing check (host copy, gloo): not a measurement",
+                          "per_rank": [{"rank": r, "shard_tag": int(t)} for r, (_, t) in enumerate(per_rank)]}),
+              flush=True)
+    ranks.close()
 
 
 if __name__ == "__main__":

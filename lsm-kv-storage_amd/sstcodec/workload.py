@@ -124,6 +124,54 @@ def uniform_block_layout(nblocks, per_block=28, key_len=16, val_len=100):
     return off, np.full(nblocks, blen, np.uint64)
 
 
+CONFIG_DEFAULTS = {3: (8, 1_000_000), 4: (128, 100_000), 5: (8, 5000)}
+
+
+def config_inputs(config, rank=0, ssts=None, keys=None, overlap=False, ranges=False, key_space=20000):
+    """Input record sets (one per input SST, iterator order) of BASELINE.json
+    configs 3-5, exactly as tests/golden/make_golden_configs.py fed them to the
+    reference:
+
+    config 3  `ssts` x `keys` uniform records; SST s holds k%015d of i*ssts+s
+              (disjoint interleave), 100 B values (splitmix64 seed s+1), txns
+              ascending and unique; overlap=True: the same key set i in every
+              SST with distinct txns (the drop path); ranges=True: SST s holds
+              one contiguous key range.
+    config 4  rank r's shard of 1024 SSTs: keys [r*K, (r+1)*K), K = ssts*keys,
+              SST s holds base + i*ssts + s; seeds / txns by global SST id.
+    config 5  W.compaction_inputs: keys from a shared space of `key_space`,
+              Zipf(1.1) values clamped to [8 B, 64 KiB], 10 % DELETE (seed 55+rank).
+    """
+    d_ssts, d_keys = CONFIG_DEFAULTS[config]
+    ssts = ssts or d_ssts
+    keys = keys or d_keys
+    if config == 3:
+        out = []
+        for s in range(ssts):
+            i = np.arange(keys, dtype=np.uint64)
+            if overlap:
+                k = i
+            elif ranges:
+                k = i + np.uint64(s * keys)
+            else:
+                k = i * np.uint64(ssts) + np.uint64(s)
+            out.append(uniform_records(keys, key_index=k, seed=s + 1, txn_start=1 + s * keys))
+        return out
+    if config == 4:
+        K = ssts * keys
+        base = np.uint64(rank * K)
+        out = []
+        for s in range(ssts):
+            i = np.arange(keys, dtype=np.uint64)
+            g = rank * ssts + s
+            out.append(uniform_records(keys, key_index=base + i * np.uint64(ssts) + np.uint64(s), seed=g + 1,
+                                       txn_start=1 + g * keys))
+        return out
+    if config == 5:
+        return compaction_inputs(ssts, keys, key_space, seed=55 + rank, vmin=8, vmax=65536, zipf=1.1, p_delete=0.1)
+    raise ValueError(f"no input generator for config {config}")
+
+
 def compaction_inputs(k, n_per, key_space, seed=5, p_delete=0.1, vmin=8, vmax=200, key_width=16,
                       distinct=True, zipf=None):
     """k record sets (one per input SST, iterator order), each sorted by key,

@@ -1,0 +1,95 @@
+"""Full-size compaction fixtures of BASELINE.json configs 3-5 from the REFERENCE.
+
+    make -C oracle && python tests/golden/make_golden_configs.py [case ...]
+
+SURVEY.md §8(c) item 6: for each case, the generator parameters (seeds are
+fixed inside sstcodec.workload.config_inputs), the SHA-256 and GetFileSize()
+of every input SST written by the reference's own TableBuilder
+(oracle/_ref/libsstref.so, /root/reference/sstable/table_builder.cc) and of
+every output SST of the reference's MergeIterator + TableReaderIterator +
+TableBuilder driven by oracle/_ref/ref_compact (the DoCompactJob loop of
+/root/reference/db/compact.cc:232-322) with the 4096 B block threshold and the
+32 MiB output split (compact.cc:290, config.cc defaults).
+
+The GPU tests (tests/test_gpu_configs.py) regenerate the same inputs on the
+box from these parameters, check the input hashes (so the inputs are the
+reference's), compact them with sstc_compact / sstc_compact_files and compare
+the output hashes.  Output: tests/golden/compaction_configs.json (data only).
+"""
+import hashlib
+import json
+import os
+import sys
+import tempfile
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+sys.path.insert(0, os.path.join(ROOT, "lsm-kv-storage_amd"))
+
+from oracle import RefLib, ref_compact  # noqa: E402
+from sstcodec import workload as W  # noqa: E402
+
+OUT = os.path.join(HERE, "compaction_configs.json")
+
+# name -> config_inputs arguments (+ base levels to record)
+CASES = {
+    "config3": {"config": 3},
+    "config3_overlap": {"config": 3, "overlap": True},
+    "config4_rank0": {"config": 4, "rank": 0},
+    "config5": {"config": 5},
+}
+
+
+def sha_file(p):
+    h = hashlib.sha256()
+    with open(p, "rb") as f:
+        for chunk in iter(lambda: f.read(1 << 24), b""):
+            h.update(chunk)
+    return h.hexdigest()
+
+
+def make_case(ref, name, gen, td):
+    t0 = time.time()
+    sets = W.config_inputs(**gen)
+    ins = []
+    for i, rec in enumerate(sets):
+        p = os.path.join(td, f"in{i}.sst")
+        ins.append((p, ref.table_build(p, rec, 4096)))
+    del sets
+    case = {"gen": gen, "block_threshold": 4096, "table_limit": 32 << 20,
+            "inputs": [{"sha256": sha_file(p), "file_size": fs} for p, fs in ins]}
+    for base in (1,):
+        od = os.path.join(td, f"out{base}")
+        os.makedirs(od)
+        t1 = time.time()
+        outs = ref_compact(ins, od, 4096, 32 << 20, base)
+        case["ref_compact_s"] = round(time.time() - t1, 2)
+        case[f"outputs_base{base}"] = [{"sha256": sha_file(p), "file_size": fs} for p, fs in outs]
+        for p, _ in outs:
+            os.remove(p)
+    for p, _ in ins:
+        os.remove(p)
+    print(f"{name}: {len(ins)} inputs -> {len(case['outputs_base1'])} outputs ({time.time() - t0:.1f} s)",
+          flush=True)
+    return case
+
+
+def main():
+    ref = RefLib()
+    names = sys.argv[1:] or list(CASES)
+    manifest = {}
+    if os.path.exists(OUT):
+        with open(OUT) as f:
+            manifest = json.load(f)
+    for name in names:
+        with tempfile.TemporaryDirectory() as td:
+            manifest[name] = make_case(ref, name, CASES[name], td)
+        with open(OUT, "w") as f:
+            json.dump(manifest, f, indent=1)
+    print("compaction_configs.json written")
+
+
+if __name__ == "__main__":
+    main()

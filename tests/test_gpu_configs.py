@@ -1,0 +1,91 @@
+"""BASELINE configs 3, 3-overlap, 4 (rank-0 shard) and 5 at their full size on the
+GPU, against the reference's own outputs (tests/golden/compaction_configs.json,
+made by tests/golden/make_golden_configs.py from oracle/_ref: the reference's
+TableBuilder for the inputs, its MergeIterator + TableReaderIterator +
+TableBuilder under the DoCompactJob loop of /root/reference/db/compact.cc:232-322
+for the outputs).
+
+Per case, on the box:
+  1. the input record sets are regenerated from the recorded parameters
+     (sstcodec.workload.config_inputs) and written by this framework's own
+     flush-path sstc::TableBuilder (GPU encode): every input file must hash to
+     the reference TableBuilder's bytes (table_builder.cc:35-211 at scale);
+  2. sstc_compact (device job) over the resident images: every output SST must
+     hash to the reference's output and have its GetFileSize();
+  3. sstc_compact_files (file -> file pipeline) over the input files: the same.
+Config 3 crosses the 32 MiB output split (compact.cc:290) 27 times.
+"""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+from conftest import GOLDEN
+from sstcodec import workload as W
+
+pytestmark = pytest.mark.gpu
+CASES = json.load(open(os.path.join(GOLDEN, "compaction_configs.json")))
+
+
+@pytest.fixture(scope="module")
+def codec():
+    import sstcodec
+    return sstcodec.Codec(0)
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a, np.uint8).tobytes()).hexdigest()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("name", ["config5", "config3_overlap", "config3", "config4_rank0"])
+def test_config_full_size_vs_reference(codec, tmp_path, name):
+    import torch
+    import sstcodec
+    from sstcodec.table import build_table
+
+    case = CASES[name]
+    want = case["outputs_base1"]
+    # 1. inputs through the flush-path TableBuilder, equal to the reference's files
+    paths, sizes, imgs = [], [], []
+    for i, rec in enumerate(W.config_inputs(**case["gen"])):
+        p = str(tmp_path / f"in{i}.sst")
+        fs, _ = build_table(codec, p, rec, case["block_threshold"])
+        img = np.fromfile(p, np.uint8)
+        w = case["inputs"][i]
+        assert fs == w["file_size"] == img.size + 1, f"input {i}: GetFileSize"
+        assert sha(img) == w["sha256"], f"input {i} differs from the reference TableBuilder's file"
+        paths.append(p)
+        sizes.append(fs)
+        imgs.append(img)
+    print(f"{name}: {len(imgs)} inputs equal to the reference's", flush=True)
+
+    # 2. device-resident compaction job
+    outs, res = codec.compact(imgs, case["block_threshold"], case["table_limit"], 1)
+    del imgs
+    assert res.tables_out == len(outs) == len(want)
+    for t, (o, w) in enumerate(zip(outs, want)):
+        assert o.size + 1 == w["file_size"], f"output {t}: GetFileSize"
+        assert sha(o) == w["sha256"], f"output {t} differs from the reference's"
+    del outs
+    torch.cuda.empty_cache()
+    print(f"{name}: device job -> {len(want)} outputs equal to the reference's", flush=True)
+
+    # 3. file -> file pipeline
+    pipe = sstcodec.FilePipe(codec, io_threads=8)
+    try:
+        od = tmp_path / "out"
+        od.mkdir()
+        fouts, _ = pipe.compact_files(paths, sizes, str(od) + "/", 1, case["block_threshold"],
+                                      case["table_limit"], 1, fsync=False)
+    finally:
+        pipe.close()
+    assert len(fouts) == len(want)
+    for (sid, fsize, _, _), w in zip(fouts, want):
+        p = str(od / f"{sid}.sst")
+        img = np.fromfile(p, np.uint8)
+        assert fsize == w["file_size"] == img.size + 1
+        assert sha(img) == w["sha256"], f"file output {sid} differs from the reference's"
+        os.remove(p)
+    print(f"{name}: file pipeline -> {len(want)} outputs equal to the reference's", flush=True)

@@ -74,3 +74,22 @@ def test_live_ref_compact(oracle):
         assert len(outs) == len(mine) > 2
         for (p, fs), m in zip(outs, mine):
             assert np.array_equal(np.fromfile(p, np.uint8), m) and fs == m.size + 1
+
+
+CONFIGS = json.load(open(os.path.join(GOLDEN, "compaction_configs.json")))
+
+
+@pytest.mark.parametrize("name", sorted(CONFIGS))
+def test_config_full_size_matches_reference(oracle, name):
+    """BASELINE configs 3 / 3-overlap / 4 (rank-0 shard) / 5 at full size: the
+    oracle's inputs equal the reference TableBuilder's files and its compaction
+    equals the reference's outputs (tests/golden/make_golden_configs.py)."""
+    case = CONFIGS[name]
+    files = [oracle.table_build(r, case["block_threshold"]) for r in W.config_inputs(**case["gen"])]
+    for f, want in zip(files, case["inputs"]):
+        assert f.size + 1 == want["file_size"] and sha(f) == want["sha256"]
+    outs, _ = oracle.compact(files, case["block_threshold"], case["table_limit"], 1)
+    want = case["outputs_base1"]
+    assert len(outs) == len(want)
+    for o, w in zip(outs, want):
+        assert o.size + 1 == w["file_size"] and sha(o) == w["sha256"]
