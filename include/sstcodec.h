@@ -95,7 +95,11 @@ uint32_t sstc_version(void);
 const char *sstc_last_error_string(void);
 
 /* Context: device, stream and workspace.  stream is a hipStream_t (NULL = the
- * null stream); it may be changed between calls with sstc_ctx_set_stream. */
+ * null stream); it may be changed between calls with sstc_ctx_set_stream,
+ * which orders the new stream after all work already queued on the old one
+ * (an event recorded on the old stream, waited on by the new one), because
+ * every call of a context shares its workspace.  A context is not
+ * thread-safe: one host thread at a time (SURVEY.md §8(b) threading). */
 int sstc_ctx_create(int device, void *stream, sstc_ctx **out);
 int sstc_ctx_destroy(sstc_ctx *ctx);
 int sstc_ctx_set_stream(sstc_ctx *ctx, void *stream);

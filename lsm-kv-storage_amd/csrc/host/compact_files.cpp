@@ -34,6 +34,8 @@
 #include "sstcodec.h"
 
 extern "C" int sstc__fail(int code, const char *what); // sstc_api.hip: sets sstc_last_error_string
+extern "C" int sstc__ctx_device(const sstc_ctx *ctx);   // sstc_api.hip: the device a context is bound to
+extern "C" int sstc__ctx_sync(sstc_ctx *ctx);           // sstc_api.hip: synchronize the context's stream
 
 struct sstc_pipe {
   sstc_ctx *ctx = nullptr;
@@ -182,8 +184,10 @@ extern "C" {
 int sstc_pipe_create(sstc_ctx *ctx, uint32_t io_threads, sstc_pipe **out) {
   if (!ctx || !out) return sstc__fail(SSTC_E_INVALID_ARG, "sstc_pipe_create: NULL argument");
   *out = nullptr;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return sstc__fail(SSTC_E_NO_DEVICE, "no HIP device");
+  // the pipe's stream and buffers live on the context's device, whatever the
+  // calling thread's current device is
+  const int dev = sstc__ctx_device(ctx);
+  if (dev < 0 || hipSetDevice(dev) != hipSuccess) return sstc__fail(SSTC_E_NO_DEVICE, "no HIP device");
   sstc_pipe *p = new sstc_pipe();
   p->ctx = ctx;
   p->device = dev;
@@ -222,6 +226,14 @@ int sstc_compact_files(sstc_pipe *pipe, const char *const *in_paths, const uint6
   if (hipSetDevice(pipe->device) != hipSuccess) return sstc__fail(SSTC_E_HIP, "hipSetDevice");
   const auto t0 = clk::now();
   hipStream_t s = pipe->stream;
+  // error exits once copies may be in flight: drain the pipe's stream (and the
+  // context's, after the device job) so the next call never frees or refills
+  // pinned / device staging that a pending copy or kernel still reads
+  auto bail = [&](int code, const char *what) {
+    (void)hipStreamSynchronize(s);
+    (void)sstc__ctx_sync(pipe->ctx);
+    return sstc__fail(code, what);
+  };
 
   // ---- index: footers + meta sections, one thread per file
   std::vector<InFile> files(n_in);
@@ -296,7 +308,7 @@ int sstc_compact_files(sstc_pipe *pipe, const char *const *in_paths, const uint6
     if (herr == hipSuccess) herr = hipMemcpyAsync(pipe->d_src + at, pipe->h_in + at, k.len, hipMemcpyHostToDevice, s);
   }
   for (auto &t : readers) t.join();
-  if (!read_ok) return sstc__fail(SSTC_E_INVALID_ARG, "sstc_compact_files: input read failed");
+  if (!read_ok) return bail(SSTC_E_INVALID_ARG, "sstc_compact_files: input read failed");
   // block index (absolute offsets into the staged data sections)
   uint64_t *h_off = reinterpret_cast<uint64_t *>(pipe->h_in + idx_at), *h_len = h_off + nblocks;
   for (uint32_t i = 0, b = 0; i < n_in; i++)
@@ -306,12 +318,12 @@ int sstc_compact_files(sstc_pipe *pipe, const char *const *in_paths, const uint6
     }
   const uint64_t max_tables = std::min(total / params->table_limit + 2, total / 13 + 2);
   if (grow_dev(pipe->d_idx, pipe->cap_d_idx, 2 * nblocks + 2 * max_tables + 2))
-    return sstc__fail(SSTC_E_NOMEM, "sstc_compact_files: index staging");
+    return bail(SSTC_E_NOMEM, "sstc_compact_files: index staging");
   uint64_t *d_off = pipe->d_idx, *d_len = d_off + nblocks, *d_toff = d_len + nblocks, *d_tlen = d_toff + max_tables + 1;
   if (herr == hipSuccess && nblocks)
     herr = hipMemcpyAsync(d_off, h_off, 16 * nblocks, hipMemcpyHostToDevice, s);
   if (herr == hipSuccess) herr = hipStreamSynchronize(s);
-  if (herr != hipSuccess) return sstc__fail(SSTC_E_HIP, "sstc_compact_files: H2D");
+  if (herr != hipSuccess) return bail(SSTC_E_HIP, "sstc_compact_files: H2D");
   const auto t2 = clk::now();
 
   // ---- compact on the device
@@ -319,12 +331,15 @@ int sstc_compact_files(sstc_pipe *pipe, const char *const *in_paths, const uint6
   uint64_t cap = total + total / 2 + (1u << 20);
   int rc = SSTC_E_CAPACITY;
   for (int attempt = 0; attempt < 2 && rc == SSTC_E_CAPACITY; attempt++) {
-    if (grow_dev(pipe->d_dst, pipe->cap_d_dst, cap)) return sstc__fail(SSTC_E_NOMEM, "sstc_compact_files: output");
+    if (grow_dev(pipe->d_dst, pipe->cap_d_dst, cap)) return bail(SSTC_E_NOMEM, "sstc_compact_files: output");
     rc = sstc_compact(pipe->ctx, pipe->d_src, d_off, d_len, nblocks, tfb.data(), n_in, params, pipe->d_dst,
                       pipe->cap_d_dst, d_toff, d_tlen, max_tables, &res);
     cap = res.bytes_out; // exact size known after a capacity miss
   }
-  if (rc != SSTC_OK) return rc; // sstc_compact set the error string
+  if (rc != SSTC_OK) { // sstc_compact set the error string
+    (void)sstc__ctx_sync(pipe->ctx);
+    return rc;
+  }
   const auto t3 = clk::now();
 
   // ---- store: per-table D2H with an event, writer threads pwrite + fsync

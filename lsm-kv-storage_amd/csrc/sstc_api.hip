@@ -18,11 +18,14 @@ struct sstc_ctx {
   int device = 0;
   uint32_t num_cus = 256;
   hipStream_t stream = nullptr;
+  hipEvent_t switch_ev = nullptr;           // orders a new stream after the old one
   uint64_t cap_records = 0, cap_scan = 0, cap_jump = 0;
+  uint32_t scan_epoch = 0;                  // tag of the last scan on scan_ws (0: ws all zero)
   void *counters = nullptr;                 // 64 B: error counter
   unsigned long long *err_count = nullptr;  // 1
   uint64_t *scan_ws = nullptr;              // cap_scan
-  uint64_t *sizes = nullptr;                // cap_records + 1
+  uint32_t *blist = nullptr;                // cap_blist: encode's large-block list (count, then ids)
+  uint64_t cap_blist = 0;
   uint64_t *P = nullptr;                    // cap_records + 1
   uint32_t *jump = nullptr;                 // cap_jump
   sstc::Arena arena;                        // compaction workspace
@@ -86,20 +89,33 @@ template <class T> int grow(sstc_ctx *c, T *&p, uint64_t &cap, uint64_t need, co
   return SSTC_OK;
 }
 
+// scan_ws is zeroed when (re)allocated; every scan on it then takes a fresh
+// epoch (sstc::launch_scan), so no memset precedes a scan.  When the 14-bit
+// epoch would wrap, the words are cleared once and the count restarts.
 int ensure_scan(sstc_ctx *c, uint64_t n) {
-  return grow(c, c->scan_ws, c->cap_scan, sstc::scan_workspace_elems(n), "scan workspace");
+  const uint64_t old = c->cap_scan;
+  const uint64_t *before = c->scan_ws;
+  if (int r = grow(c, c->scan_ws, c->cap_scan, sstc::scan_workspace_elems(n), "scan workspace")) return r;
+  if (c->scan_ws != before || c->cap_scan != old) {
+    SSTC_HIP(hipMemsetAsync(c->scan_ws, 0, c->cap_scan * sizeof(uint64_t), c->stream), "scan workspace clear");
+    c->scan_epoch = 0;
+  }
+  return SSTC_OK;
+}
+
+int next_epoch(sstc_ctx *c, uint32_t &epoch) {
+  if (c->scan_epoch + 1 >= sstc::kScanEpochs) {
+    SSTC_HIP(hipMemsetAsync(c->scan_ws, 0, c->cap_scan * sizeof(uint64_t), c->stream), "scan workspace clear");
+    c->scan_epoch = 0;
+  }
+  epoch = ++c->scan_epoch;
+  return SSTC_OK;
 }
 
 int ensure_blocks(sstc_ctx *c, uint64_t nb) { return ensure_scan(c, nb + 1); }
 
 int ensure_records(sstc_ctx *c, uint64_t nr) {
-  uint64_t cap = c->cap_records;
-  int r = grow(c, c->sizes, cap, nr + 1, "record workspace");
-  if (r) return r;
-  uint64_t cap2 = c->cap_records;
-  r = grow(c, c->P, cap2, nr + 1, "record workspace");
-  if (r) return r;
-  c->cap_records = cap < cap2 ? cap : cap2;
+  if (int r = grow(c, c->P, c->cap_records, nr + 1, "record workspace")) return r;
   return ensure_scan(c, nr + 1);
 }
 
@@ -117,6 +133,11 @@ uint32_t sstc_version(void) { return SSTC_ABI_VERSION; }
 // internal: lets the host-only translation units (host/*.cpp) report errors
 // through sstc_last_error_string
 int sstc__fail(int code, const char *what) { return fail(code, what); }
+int sstc__ctx_device(const sstc_ctx *c) { return c ? c->device : -1; }
+int sstc__ctx_sync(sstc_ctx *c) {
+  if (!c || bind_device(c)) return SSTC_E_NO_DEVICE;
+  return hipStreamSynchronize(c->stream) == hipSuccess ? SSTC_OK : SSTC_E_HIP;
+}
 
 const char *sstc_last_error_string(void) { return g_last_error.c_str(); }
 
@@ -170,17 +191,28 @@ int sstc_ctx_destroy(sstc_ctx *c) {
     if (hp->h_stage) (void)hipHostFree(hp->h_stage);
     delete hp;
   }
+  if (c->switch_ev) (void)hipEventDestroy(c->switch_ev);
   for (void *p : {c->counters, c->arena.base,
-                  static_cast<void *>(c->scan_ws), static_cast<void *>(c->sizes),
+                  static_cast<void *>(c->scan_ws), static_cast<void *>(c->blist),
                   static_cast<void *>(c->P), static_cast<void *>(c->jump)})
     if (p) (void)hipFree(p);
   delete c;
   return SSTC_OK;
 }
 
+// A context's workspace (scan scratch, record arrays, compaction arena, mapped
+// host words, error counter) is shared by every call, so a stream switch must
+// not let work on the new stream overtake work still queued on the old one:
+// the new stream waits on an event recorded on the old stream.
 int sstc_ctx_set_stream(sstc_ctx *c, void *stream) {
   if (!c) return fail(SSTC_E_INVALID_ARG, "ctx is NULL");
-  c->stream = static_cast<hipStream_t>(stream);
+  hipStream_t ns = static_cast<hipStream_t>(stream);
+  if (ns == c->stream) return SSTC_OK;
+  if (int r = bind_device(c)) return r;
+  if (!c->switch_ev) SSTC_HIP(hipEventCreateWithFlags(&c->switch_ev, hipEventDisableTiming), "stream switch event");
+  SSTC_HIP(hipEventRecord(c->switch_ev, c->stream), "stream switch: record on the old stream");
+  SSTC_HIP(hipStreamWaitEvent(ns, c->switch_ev, 0), "stream switch: new stream waits");
+  c->stream = ns;
   return SSTC_OK;
 }
 
@@ -217,8 +249,10 @@ int sstc_count_records(sstc_ctx *c, const uint8_t *d_src, const uint64_t *d_blk_
     return fail(SSTC_E_INVALID_ARG, "sstc_count_records: NULL argument");
   if (int r = bind_device(c)) return r;
   if (int r = ensure_scan(c, nblocks + 1)) return r;
+  uint32_t ep = 0;
+  if (int r = next_epoch(c, ep)) return r;
   SSTC_HIP(sstc::launch_count(d_src, d_blk_off, d_blk_len, nblocks, d_rec_base, c->stream), "count kernel");
-  SSTC_HIP(sstc::launch_scan(d_rec_base, nblocks, 0, d_rec_base, c->scan_ws, c->stream), "scan");
+  SSTC_HIP(sstc::launch_scan(d_rec_base, nblocks, 0, d_rec_base, c->scan_ws, c->stream, false, ep), "scan");
   return SSTC_OK;
 }
 
@@ -245,8 +279,9 @@ int sstc_segment_records(sstc_ctx *c, const uint32_t *d_key_len, const uint32_t 
   if (int r = ensure_records(c, nrec)) return r;
   if (int r = grow(c, c->jump, c->cap_jump, sstc::segment_workspace_u32(nrec), "segmentation workspace")) return r;
   // weights = entry_size + 16 (block_builder.cc:33), Pw = exclusive scan
-  SSTC_HIP(sstc::launch_enc_sizes(d_key_len, d_val_len, nrec, 16, c->sizes, c->stream), "weights");
-  SSTC_HIP(sstc::launch_scan(c->sizes, nrec, 0, c->P, c->scan_ws, c->stream), "scan");
+  uint32_t ep = 0;
+  if (int r = next_epoch(c, ep)) return r;
+  SSTC_HIP(sstc::launch_scan_entry_sizes(d_key_len, d_val_len, nrec, 16, c->P, c->scan_ws, c->stream, ep), "scan");
   SSTC_HIP(sstc::launch_segment(c->P, nrec, block_threshold, c->jump, d_nblocks, d_blk_first, c->stream),
            "segment kernels");
   return SSTC_OK;
@@ -260,13 +295,19 @@ int sstc_encode_blocks(sstc_ctx *c, const uint8_t *d_key_src, const uint8_t *d_v
       (nrec && (!d_key_src || !d_val_src || bad_records(in))))
     return fail(SSTC_E_INVALID_ARG, "sstc_encode_blocks: NULL argument");
   if (int r = bind_device(c)) return r;
+  if (nblocks >= 0xFFFFFFFFull) return fail(SSTC_E_INVALID_ARG, "too many blocks for one call");
   if (int r = ensure_records(c, nrec)) return r;
-  if (int r = ensure_scan(c, nblocks + 1)) return r;
-  SSTC_HIP(sstc::launch_enc_sizes(in.key_len, in.val_len, nrec, 0, c->sizes, c->stream), "sizes");
-  SSTC_HIP(sstc::launch_scan(c->sizes, nrec, 0, c->P, c->scan_ws, c->stream), "scan");
-  SSTC_HIP(sstc::launch_enc_blk_len(c->P, d_blk_first, nblocks, d_out_blk_len, c->stream), "block sizes");
-  SSTC_HIP(sstc::launch_scan(d_out_blk_len, nblocks, out_base, d_out_blk_off, c->scan_ws, c->stream), "scan");
+  if (int r = grow(c, c->blist, c->cap_blist, nblocks + 2, "block list")) return r;
+  // P = exclusive scan of the entry sizes (computed inside the scan), block
+  // offsets / sizes in closed form from P, then the block images
+  uint32_t ep = 0;
+  if (int r = next_epoch(c, ep)) return r;
+  SSTC_HIP(sstc::launch_scan_entry_sizes(in.key_len, in.val_len, nrec, 0, c->P, c->scan_ws, c->stream, ep), "scan");
+  SSTC_HIP(sstc::launch_enc_blocks(c->P, d_blk_first, nblocks, out_base, d_out_blk_off, d_out_blk_len, c->blist,
+                                   c->stream), "block sizes");
   sstc::EncArgs a{d_key_src, d_val_src, in, d_blk_first, nblocks, c->P, d_out_blk_off, d_out_blk_len, d_dst};
+  a.nbig = c->blist;
+  a.big = c->blist + 1;
   SSTC_HIP(sstc::launch_enc_emit(a, c->stream), "emit kernel");
   return SSTC_OK;
 }

@@ -578,18 +578,27 @@ __global__ __launch_bounds__(kDecWaves *kWave) void decode_kernel(DecArgs a) {
 // ---------------------------------------------------------------------------
 // Encode: records -> blocks.
 // ---------------------------------------------------------------------------
-__global__ void enc_sizes_kernel(const uint32_t *klen, const uint32_t *vlen, uint64_t nrec,
-                                 uint64_t add, uint64_t *sizes) {
-  const uint64_t r = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (r < nrec) sizes[r] = entry_size(klen[r], vlen[r]) + add;
-}
-
-__global__ void enc_blk_len_kernel(const uint64_t *P, const uint64_t *blk_first, uint64_t nblocks,
-                                   uint64_t *blk_len) {
+// Block sizes and offsets of an encode in closed form: block b holds records
+// [f_b, f_b+1), its bytes are the entries (P = exclusive scan of the entry
+// sizes) + 16 per offset entry + the 16 B extra (block_builder.cc:79-109), so
+// off[b] = out_base + P[f_b] - P[f_0] + 16 (f_b - f_0) + 16 b -- no second scan.
+// off[nblocks] = end of the last block.  Also clears the large-block list.
+__global__ void enc_blocks_kernel(const uint64_t *P, const uint64_t *blk_first, uint64_t nblocks, uint64_t out_base,
+                                  uint64_t *blk_off, uint64_t *blk_len, uint32_t *nbig) {
   const uint64_t b = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (b >= nblocks) return;
-  const uint64_t f0 = blk_first[b], f1 = blk_first[b + 1];
-  blk_len[b] = (P[f1] - P[f0]) + 16 * (f1 - f0) + 16;
+  if (b == 0 && nbig) *nbig = 0;
+  if (b > nblocks) return;
+  if (nblocks == 0) { // blk_first may be NULL
+    blk_off[0] = out_base;
+    return;
+  }
+  const uint64_t f0 = blk_first[0], fb = blk_first[b];
+  const uint64_t p0 = P[f0], pb = P[fb];
+  blk_off[b] = out_base + (pb - p0) + 16 * (fb - f0) + 16 * b;
+  if (b < nblocks) {
+    const uint64_t f1 = blk_first[b + 1];
+    blk_len[b] = (P[f1] - pb) + 16 * (f1 - fb) + 16;
+  }
 }
 
 // One workgroup per block; each thread assembles 16-byte output chunks aligned
@@ -1000,6 +1009,131 @@ __device__ __forceinline__ void enc_copy_entries(const EncArgs &a, uint8_t *img,
   }
 }
 
+// One LDS dword of an image, clipped to the image bytes [lo, hi): a dword
+// wholly inside is one ds_write_b32, a straddling one is written byte by byte
+// (the neighbouring bytes belong to other fields, written by other lanes).
+__device__ __forceinline__ void lds_put_clip(uint8_t *img, int32_t yy, uint32_t v, int32_t lo, int32_t hi) {
+  if (yy >= lo && yy + 4 <= hi) {
+    *reinterpret_cast<uint32_t *>(img + yy) = v;
+    return;
+  }
+#pragma unroll
+  for (int32_t k = 0; k < 4; k++)
+    if (yy + k >= lo && yy + k < hi) img[yy + k] = static_cast<uint8_t>(v >> (8 * k));
+}
+
+// Chunk c of a span (16 aligned source bytes v + the first dword of chunk c+1)
+// into the image: dwords j = 0..3 at y + 16 c + 4 j, plus for chunk 0 the dword
+// before (its top bytes are the span's first bytes when the skew r0 moves them
+// there).  Together the chunks cover [lo, hi) exactly.
+__device__ __forceinline__ void emit_chunk_clip(uint8_t *img, u32x4 v, uint32_t nxt, uint32_t r0, int32_t y,
+                                                int32_t lo, int32_t hi, bool first) {
+  if (first) lds_put_clip(img, y - 4, __builtin_amdgcn_alignbyte(v.x, 0u, r0), lo, hi);
+  lds_put_clip(img, y, __builtin_amdgcn_alignbyte(v.y, v.x, r0), lo, hi);
+  lds_put_clip(img, y + 4, __builtin_amdgcn_alignbyte(v.z, v.y, r0), lo, hi);
+  lds_put_clip(img, y + 8, __builtin_amdgcn_alignbyte(v.w, v.z, r0), lo, hi);
+  lds_put_clip(img, y + 12, __builtin_amdgcn_alignbyte(nxt, v.w, r0), lo, hi);
+}
+
+// Records -> block image (sstc_encode_blocks: keys and values in two arenas).
+// Every record is two spans, its key (image offset o + 5) and its value (o + 9
+// + klen); a round takes 32 records = 64 spans, one per owner lane.  Spans are
+// copied by groups of G lanes, 64 / G spans per wave instruction: lane g of a
+// group loads the ALIGNED 16 B source chunk g (chunks g + G, g + 2G, ... in
+// further rounds), funnel-shifts it with the first dword of chunk g + 1 (from
+// its right neighbour; the group's last lane loads it) into dword-aligned LDS
+// stores, and clips the dwords at the span's ends to byte stores, so the
+// loads are 16 B per lane and coalesced per span instead of a lane walking a
+// record's bytes.  kQ span groups are loaded before any is stored (kQ wide
+// loads in flight per lane).  Then a lane per record writes the header
+// fields, the txn and the offset entry (block_builder.cc:36-93), whose bytes
+// are disjoint from the spans'.
+template <uint32_t G, uint32_t kQ>
+__device__ __forceinline__ void enc_copy_fields(const EncArgs &a, uint8_t *img, uint32_t pad, uint64_t f0,
+                                                uint32_t n, uint64_t P0, uint32_t D) {
+  constexpr uint32_t kS = kWave / G; // spans per wave instruction
+  const uint32_t lane = lane_id();
+  const uint32_t g = lane % G, sub = lane / G;
+  for (uint32_t c0 = 0; c0 < n; c0 += kWave / 2) {
+    const uint32_t nc = n - c0 < kWave / 2 ? n - c0 : kWave / 2;
+    const uint32_t ns = 2 * nc;
+    uint64_t my_src = 0;
+    uint32_t my_len = 0, my_ds = 0;
+    if (lane < ns) { // span owner: lane 2i = key of record c0 + i, lane 2i + 1 = its value
+      const uint64_t r = f0 + c0 + (lane >> 1);
+      const uint32_t o = static_cast<uint32_t>(a.P[r] - P0);
+      const uint32_t kl = a.in.key_len[r];
+      if ((lane & 1u) == 0) {
+        my_src = reinterpret_cast<uint64_t>(a.key_src + a.in.key_off[r]);
+        my_len = kl;
+        my_ds = pad + o + 5;
+      } else {
+        const uint32_t vl = a.in.val_len[r];
+        my_len = vl != kNoValue ? vl : 0u;
+        my_src = my_len ? reinterpret_cast<uint64_t>(a.val_src + a.in.val_off[r]) : 0ull;
+        my_ds = pad + o + 9 + kl;
+      }
+    }
+    for (uint32_t p0 = 0; p0 < ns; p0 += kS * kQ) {
+      u32x4 v[kQ];
+      uint32_t r0_[kQ], nch_[kQ];
+      int32_t y_[kQ], lo_[kQ], hi_[kQ];
+      const uint8_t *A_[kQ];
+#pragma unroll
+      for (uint32_t q = 0; q < kQ; q++) {
+        const uint32_t i = p0 + q * kS + sub;
+        const int sl = static_cast<int>(i & 63u);
+        const uint32_t slo = __shfl(static_cast<uint32_t>(my_src), sl, kWave);
+        const uint32_t shi = __shfl(static_cast<uint32_t>(my_src >> 32), sl, kWave);
+        const uint32_t len = __shfl(my_len, sl, kWave), ds = __shfl(my_ds, sl, kWave);
+        const uint8_t *sp = reinterpret_cast<const uint8_t *>((static_cast<uint64_t>(shi) << 32) | slo);
+        const uint32_t mis = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(sp) & 15u);
+        const uint8_t *A = sp - mis;
+        const uint32_t nch = i < ns && len ? (mis + len + 15u) >> 4 : 0u;
+        v[q] = g < nch ? *reinterpret_cast<const u32x4 *>(A + 16 * g) : u32x4{0u, 0u, 0u, 0u};
+        r0_[q] = (mis - ds) & 3u;
+        y_[q] = static_cast<int32_t>(ds) - static_cast<int32_t>(mis) + static_cast<int32_t>(r0_[q]);
+        lo_[q] = static_cast<int32_t>(ds);
+        hi_[q] = static_cast<int32_t>(ds + len);
+        nch_[q] = nch;
+        A_[q] = A;
+      }
+#pragma unroll
+      for (uint32_t q = 0; q < kQ; q++) {
+        for (uint32_t c = g, k = 0; c - g < nch_[q]; c += G, k++) {
+          const u32x4 w = k == 0 ? v[q]
+                                 : (c < nch_[q] ? *reinterpret_cast<const u32x4 *>(A_[q] + 16 * c)
+                                                : u32x4{0u, 0u, 0u, 0u});
+          uint32_t nx = __shfl_down(w.x, 1u, G);
+          if (g == G - 1) nx = c + 1 < nch_[q] ? *reinterpret_cast<const uint32_t *>(A_[q] + 16 * (c + 1)) : 0u;
+          if (c < nch_[q])
+            emit_chunk_clip(img, w, nx, r0_[q], y_[q] + 16 * static_cast<int32_t>(c), lo_[q], hi_[q], c == 0);
+        }
+      }
+    }
+  }
+  // header fields, txn, offset entry: lane per record (coalesced SoA loads)
+  uint8_t *im = img + pad;
+  for (uint32_t i = lane; i < n; i += kWave) {
+    const uint64_t r = f0 + i;
+    const uint64_t pr = a.P[r];
+    const uint32_t o = static_cast<uint32_t>(pr - P0);
+    const uint32_t sz = static_cast<uint32_t>(a.P[r + 1] - pr);
+    const uint32_t kl = a.in.key_len[r], vl = a.in.val_len[r];
+    const uint64_t tx = a.in.txn[r];
+    im[o] = a.in.type[r];
+#pragma unroll
+    for (int j = 0; j < 4; j++) im[o + 1 + j] = static_cast<uint8_t>(kl >> (8 * j));
+    if (vl != kNoValue) {
+#pragma unroll
+      for (int j = 0; j < 4; j++) im[o + 5 + kl + j] = static_cast<uint8_t>(vl >> (8 * j));
+    }
+    lds_st_u64u(im, o + sz - 8, tx);
+    lds_st_u64u(im, D + 16 * i, o);
+    lds_st_u64u(im, D + 16 * i + 8, sz);
+  }
+}
+
 template <uint32_t kMode> // 0: lane per record, 1: whole-entry copy (compaction)
 __global__ __launch_bounds__(kEncWaves *kWave) void enc_lds_kernel(EncArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kEncSlotWaves * kEncSlot];
@@ -1026,26 +1160,7 @@ __global__ __launch_bounds__(kEncWaves *kWave) void enc_lds_kernel(EncArgs a) {
   if constexpr (kMode == 1) {
     enc_copy_entries<4>(a, img, pad, f0, n, P0, D, b);
   } else {
-  for (uint32_t i = lane; i < n; i += kWave) {
-    const uint64_t r = f0 + i;
-    const uint32_t o = static_cast<uint32_t>(a.P[r] - P0);
-    const uint32_t sz = static_cast<uint32_t>(a.P[r + 1] - a.P[r]);
-    const uint32_t kl = a.in.key_len[r], vl = a.in.val_len[r];
-    const uint64_t tx = a.in.txn[r];
-    const uint32_t t = sz - 8; // txn position in the entry
-    {
-      im[o] = a.in.type[r];
-      for (int j = 0; j < 4; j++) im[o + 1 + j] = static_cast<uint8_t>(kl >> (8 * j));
-      lane_copy(im + o + 5, a.key_src + a.in.key_off[r], kl);
-      if (vl != kNoValue) {
-        for (int j = 0; j < 4; j++) im[o + 5 + kl + j] = static_cast<uint8_t>(vl >> (8 * j));
-        lane_copy(im + o + 9 + kl, a.val_src + a.in.val_off[r], vl);
-      }
-    }
-    for (int j = 0; j < 8; j++) im[o + t + j] = static_cast<uint8_t>(tx >> (8 * j));
-    lds_st_u64u(im, D + 16 * i, o);
-    lds_st_u64u(im, D + 16 * i + 8, sz);
-  }
+    enc_copy_fields<8, 2>(a, img, pad, f0, n, P0, D);
   }
   if (lane == 0) {
     lds_st_u64u(im, D + 16 * n, n);
@@ -1573,16 +1688,28 @@ __device__ __forceinline__ uint64_t wg_excl_scan_u64(uint64_t v, uint64_t &total
   return base + incl - v;
 }
 
+// Scan inputs: a u64 array, or the entry sizes of a record table computed on
+// the fly (the encode's offsets, block_builder.cc:19-21, without a sizes array).
+struct ArrIn {
+  const uint64_t *p;
+  __device__ __forceinline__ uint64_t operator()(uint64_t i) const { return p[i]; }
+};
+struct EntryIn {
+  const uint32_t *kl, *vl;
+  uint64_t add;
+  __device__ __forceinline__ uint64_t operator()(uint64_t i) const { return entry_size(kl[i], vl[i]) + add; }
+};
+
 // out[i] = carry_in + sum(in[0..i)), out[n] = carry_in + total.  in may alias out.
-__global__ __launch_bounds__(kScanThreads) void scan_apply_kernel(const uint64_t *in, uint64_t n,
-                                                                  const uint64_t *tile_base,
+template <class In>
+__global__ __launch_bounds__(kScanThreads) void scan_apply_kernel(In in, uint64_t n, const uint64_t *tile_base,
                                                                   uint64_t carry_in, uint64_t *out) {
   const uint64_t t0 = static_cast<uint64_t>(blockIdx.x) * kScanTile + threadIdx.x * kScanItems;
   uint64_t v[kScanItems];
   uint64_t s = 0;
 #pragma unroll
   for (uint32_t j = 0; j < kScanItems; j++) {
-    v[j] = t0 + j < n ? in[t0 + j] : 0;
+    v[j] = t0 + j < n ? in(t0 + j) : 0;
     s += v[j];
   }
   uint64_t tot;
@@ -1599,34 +1726,44 @@ __global__ __launch_bounds__(kScanThreads) void scan_apply_kernel(const uint64_t
   }
 }
 
-// Tile status word: 2 flag bits + 62 value bits in ONE u64, published and
-// polled with agent-scope atomics (per-XCD L2s are not coherent; an sc1 store
-// / sc1 load pair on a single word needs no separate fence).  Totals must stay
-// below 2^62.  Tiles are numbered by a ticket counter so every tile a
-// workgroup waits on is already resident.  ws = [ticket, status[tiles]],
-// zeroed by the launcher.
+// Tile status word: 2 flag bits | 14-bit epoch | 48 value bits in ONE u64,
+// published and polled with agent-scope atomics (per-XCD L2s are not
+// coherent; an sc1 store / sc1 load pair on a single word needs no separate
+// fence).  Totals must stay below 2^48.  A word counts only when its epoch is
+// the launch's: a context tags every scan on its own workspace with a new
+// epoch, so stale words of earlier calls are ignored and no memset precedes
+// the scan (epoch 0 = the caller cleared the words in an earlier kernel).
+// Tiles are numbered by a ticket counter so every tile a workgroup waits on is
+// already resident; the tile that draws the last ticket resets the counter
+// for the next launch.  ws = [ticket, status[tiles]].
 constexpr uint32_t kLbItems = 16, kLbTile = kScanThreads * kLbItems;
-constexpr uint64_t kLbAgg = 1ull << 62, kLbInc = 2ull << 62, kLbVal = kLbAgg - 1;
+constexpr uint64_t kLbAgg = 1ull << 62, kLbInc = 2ull << 62, kLbVal = (1ull << 48) - 1;
+constexpr uint32_t kLbEpochShift = 48;
 constexpr uint64_t kLbSpinLimit = 1ull << 24; // never reached unless a tile died
 
 __device__ __forceinline__ uint32_t lb_idx(uint32_t i) { return i + (i >> 4); } // 1 pad per 16
 
-__global__ __launch_bounds__(kScanThreads) void scan_lookback_kernel(const uint64_t *in, uint64_t n,
-                                                                     uint64_t carry_in, uint64_t *out,
-                                                                     uint64_t *ws) {
+template <class In>
+__global__ __launch_bounds__(kScanThreads) void scan_lookback_kernel(In in, uint64_t n, uint64_t carry_in,
+                                                                     uint64_t *out, uint64_t *ws, uint32_t epoch) {
   __shared__ uint64_t sm[kLbTile + kLbTile / 16];
   __shared__ uint64_t s_wsum[kScanThreads / kWave];
   __shared__ uint64_t s_tile, s_prefix;
   const uint32_t tid = threadIdx.x, lane = lane_id(), w = tid / kWave;
-  if (tid == 0) s_tile = __hip_atomic_fetch_add(ws, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (tid == 0) {
+    const uint64_t t = __hip_atomic_fetch_add(ws, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (t + 1 == gridDim.x) __hip_atomic_store(ws, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_tile = t;
+  }
   __syncthreads();
   const uint64_t tile = s_tile;
   const uint64_t base = tile * kLbTile;
+  const uint64_t tag = static_cast<uint64_t>(epoch) << kLbEpochShift;
   uint64_t *status = ws + 1;
 #pragma unroll
   for (uint32_t j = 0; j < kLbItems; j++) {
     const uint32_t i = j * kScanThreads + tid;
-    sm[lb_idx(i)] = base + i < n ? in[base + i] : 0;
+    sm[lb_idx(i)] = base + i < n ? in(base + i) : 0;
   }
   __syncthreads();
   uint64_t v[kLbItems], sum = 0;
@@ -1648,15 +1785,16 @@ __global__ __launch_bounds__(kScanThreads) void scan_lookback_kernel(const uint6
   if (w == 0) {
     uint64_t prefix = 0;
     if (tile == 0) {
-      if (lane == 0) __hip_atomic_store(&status[0], kLbInc | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (lane == 0) __hip_atomic_store(&status[0], kLbInc | tag | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     } else {
-      if (lane == 0) __hip_atomic_store(&status[tile], kLbAgg | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (lane == 0) __hip_atomic_store(&status[tile], kLbAgg | tag | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       int64_t p = static_cast<int64_t>(tile) - 1; // window [p - 63, p]
       uint64_t spins = 0;
       for (;;) {
         const int64_t q = p - static_cast<int64_t>(lane);
-        const uint64_t st = q >= 0 ? __hip_atomic_load(&status[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                   : kLbInc;
+        uint64_t st = q >= 0 ? __hip_atomic_load(&status[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                             : kLbInc | tag;
+        if (((st >> kLbEpochShift) & 0x3FFFu) != epoch) st = 0; // a stale word: not published yet
         const uint64_t inc = __ballot((st >> 62) == 2);
         const uint32_t need = inc ? static_cast<uint32_t>(__ffsll(static_cast<long long>(inc))) : kWave;
         const uint64_t zero = __ballot((st >> 62) == 0 && lane < need);
@@ -1670,7 +1808,8 @@ __global__ __launch_bounds__(kScanThreads) void scan_lookback_kernel(const uint6
         p -= kWave;
       }
       if (lane == 0)
-        __hip_atomic_store(&status[tile], kLbInc | (prefix + total), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&status[tile], kLbInc | tag | (prefix + total), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
     }
     if (lane == 0) s_prefix = prefix;
   }
@@ -1738,30 +1877,38 @@ uint64_t scan_workspace_elems(uint64_t n) { return (n + kLbTile - 1) / kLbTile +
 
 uint64_t scan_status_words(uint64_t n) { return n <= kScanTile ? 0 : (n + kLbTile - 1) / kLbTile + 1; }
 
-hipError_t launch_scan(const uint64_t *in, uint64_t n, uint64_t carry_in, uint64_t *out, uint64_t *ws,
-                       hipStream_t s, bool ws_zeroed) {
+template <class In>
+static hipError_t scan_any(In in, uint64_t n, uint64_t carry_in, uint64_t *out, uint64_t *ws, hipStream_t s,
+                           bool ws_zeroed, uint32_t epoch) {
   if (n <= kScanTile) {
-    scan_apply_kernel<<<1, kScanThreads, 0, s>>>(in, n, nullptr, carry_in, out);
+    scan_apply_kernel<In><<<1, kScanThreads, 0, s>>>(in, n, nullptr, carry_in, out);
     return hipGetLastError();
   }
   const uint64_t tiles = (n + kLbTile - 1) / kLbTile;
-  if (!ws_zeroed) {
+  if (ws_zeroed) {
+    epoch = 0;
+  } else if (epoch == 0) {
     hipError_t e = hipMemsetAsync(ws, 0, (tiles + 1) * sizeof(uint64_t), s);
     if (e != hipSuccess) return e;
   }
-  scan_lookback_kernel<<<static_cast<uint32_t>(tiles), kScanThreads, 0, s>>>(in, n, carry_in, out, ws);
+  scan_lookback_kernel<In><<<static_cast<uint32_t>(tiles), kScanThreads, 0, s>>>(in, n, carry_in, out, ws, epoch);
   return hipGetLastError();
 }
 
-hipError_t launch_enc_sizes(const uint32_t *klen, const uint32_t *vlen, uint64_t nrec, uint64_t add,
-                            uint64_t *sizes, hipStream_t s) {
-  if (nrec) enc_sizes_kernel<<<grid_for(nrec, 256), 256, 0, s>>>(klen, vlen, nrec, add, sizes);
-  return hipGetLastError();
+hipError_t launch_scan(const uint64_t *in, uint64_t n, uint64_t carry_in, uint64_t *out, uint64_t *ws,
+                       hipStream_t s, bool ws_zeroed, uint32_t epoch) {
+  return scan_any(ArrIn{in}, n, carry_in, out, ws, s, ws_zeroed, epoch);
 }
 
-hipError_t launch_enc_blk_len(const uint64_t *P, const uint64_t *blk_first, uint64_t nblocks,
-                              uint64_t *blk_len, hipStream_t s) {
-  if (nblocks) enc_blk_len_kernel<<<grid_for(nblocks, 256), 256, 0, s>>>(P, blk_first, nblocks, blk_len);
+hipError_t launch_scan_entry_sizes(const uint32_t *klen, const uint32_t *vlen, uint64_t nrec, uint64_t add,
+                                   uint64_t *out, uint64_t *ws, hipStream_t s, uint32_t epoch) {
+  return scan_any(EntryIn{klen, vlen, add}, nrec, 0, out, ws, s, false, epoch);
+}
+
+hipError_t launch_enc_blocks(const uint64_t *P, const uint64_t *blk_first, uint64_t nblocks, uint64_t out_base,
+                             uint64_t *blk_off, uint64_t *blk_len, uint32_t *nbig, hipStream_t s) {
+  enc_blocks_kernel<<<grid_for(nblocks + 1, 256), 256, 0, s>>>(P, blk_first, nblocks, out_base, blk_off, blk_len,
+                                                              nbig);
   return hipGetLastError();
 }
 
@@ -1770,7 +1917,9 @@ hipError_t launch_enc_emit(const EncArgs &a, hipStream_t s) {
   const uint32_t g = grid_for(a.nblocks, kEncWaves);
   if (!a.entries_in_src) enc_lds_kernel<0><<<g, kEncWaves * kWave, 0, s>>>(a);
   else enc_lds_kernel<1><<<g, kEncWaves * kWave, 0, s>>>(a);
-  enc_emit_kernel<<<static_cast<uint32_t>(a.nblocks < 2048 ? a.nblocks : 2048), kEncThreads, 0, s>>>(a);
+  // blocks past an LDS slot: those listed by enc_lds_kernel when a list is given
+  const uint64_t cap = a.big ? 512 : 2048;
+  enc_emit_kernel<<<static_cast<uint32_t>(a.nblocks < cap ? a.nblocks : cap), kEncThreads, 0, s>>>(a);
   return hipGetLastError();
 }
 

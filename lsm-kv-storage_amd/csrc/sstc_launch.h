@@ -108,13 +108,19 @@ uint64_t scan_workspace_elems(uint64_t n);
 // look-back status words a scan of n items needs cleared (0: single-workgroup scan)
 uint64_t scan_status_words(uint64_t n);
 // ws_zeroed: the caller cleared scan_status_words(n) words of ws in an earlier
-// kernel on the same stream (launch_count's scan_ws, ...), no memset here
+// kernel on the same stream (launch_count's scan_ws, ...), no memset here.
+// epoch (1..kScanEpochs-1): ws holds status words of earlier scans tagged with
+// other epochs (a context's own workspace, see sstc_api.hip next_epoch): no
+// memset either.  Neither: the status words are cleared with a memset.
+constexpr uint32_t kScanEpochs = 1u << 14;
 hipError_t launch_scan(const uint64_t *in, uint64_t n, uint64_t carry_in, uint64_t *out, uint64_t *ws,
-                       hipStream_t s, bool ws_zeroed = false);
-hipError_t launch_enc_sizes(const uint32_t *klen, const uint32_t *vlen, uint64_t nrec, uint64_t add,
-                            uint64_t *sizes, hipStream_t s);
-hipError_t launch_enc_blk_len(const uint64_t *P, const uint64_t *blk_first, uint64_t nblocks,
-                              uint64_t *blk_len, hipStream_t s);
+                       hipStream_t s, bool ws_zeroed = false, uint32_t epoch = 0);
+// out = exclusive scan of the entry sizes (+ add) of records (klen, vlen)
+hipError_t launch_scan_entry_sizes(const uint32_t *klen, const uint32_t *vlen, uint64_t nrec, uint64_t add,
+                                   uint64_t *out, uint64_t *ws, hipStream_t s, uint32_t epoch);
+// block offsets (nblocks + 1) and sizes of an encode from P (closed form); clears *nbig
+hipError_t launch_enc_blocks(const uint64_t *P, const uint64_t *blk_first, uint64_t nblocks, uint64_t out_base,
+                             uint64_t *blk_off, uint64_t *blk_len, uint32_t *nbig, hipStream_t s);
 hipError_t launch_enc_emit(const EncArgs &a, hipStream_t s);
 // greedy segmentation; J = segment_workspace_u32(nrec) u32 of device workspace
 uint64_t segment_workspace_u32(uint64_t nrec);

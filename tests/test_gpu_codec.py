@@ -391,3 +391,48 @@ def test_segment_tiles_vs_oracle(codec, oracle, case):
         want = oracle.segment(rec, T)
         got = cpu_u64(codec.segment(records_table(rec), T))
         assert np.array_equal(got, want), (case, T)
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_encode_span_alignments_vs_oracle(codec, oracle, seed):
+    """Keys / values at every source alignment (arena offsets shuffled, so
+    spans start at any byte of a 16 B chunk), lengths 0..40 around the chunk
+    and dword edges, DELETEs (no value fields), values spanning several chunk
+    rounds, blocks of > 64 tiny records and blocks past an LDS slot."""
+    rng = np.random.default_rng(300 + seed)
+    n = 6000
+    klen = rng.integers(0, 41, n).astype(np.uint32)
+    vlen = rng.integers(0, 41, n).astype(np.uint32)
+    big = rng.random(n) < 0.03
+    vlen[big] = rng.integers(100, 6000, int(big.sum()))
+    typ = (rng.random(n) < 0.15).astype(np.uint8)
+    vlen[typ == 1] = W.NO_VALUE
+    # arenas with gaps: every key / value at a random byte offset
+    kgap = rng.integers(0, 16, n).astype(np.uint64)
+    key_off = np.cumsum(klen.astype(np.uint64) + kgap) - klen.astype(np.uint64)
+    vb = np.where(vlen == W.NO_VALUE, 0, vlen).astype(np.uint64)
+    vgap = rng.integers(0, 16, n).astype(np.uint64)
+    val_off = np.cumsum(vb + vgap) - vb
+    rec = {"type": typ, "key_len": klen, "val_len": vlen, "txn": rng.integers(0, 2 ** 63, n, dtype=np.uint64),
+           "key_off": key_off, "val_off": np.where(typ == 1, 0, val_off).astype(np.uint64),
+           "key_src": rng.integers(0, 256, int(key_off[-1] + klen[-1]) + 1, dtype=np.uint8),
+           "val_src": rng.integers(0, 256, int(val_off[-1] + vb[-1]) + 1, dtype=np.uint8)}
+    T = [4096, 1024, 16384][seed]
+    first = oracle.segment(rec, T)
+    want, woff, wlen = oracle.encode_blocks(rec, first, base=seed * 5)
+    dst, off, ln = codec.encode(records_table(rec), t8(rec["key_src"]), t8(rec["val_src"]), t64(first),
+                                out_base=seed * 5)
+    torch.cuda.synchronize()
+    assert np.array_equal(cpu_u64(off)[:-1], woff) and np.array_equal(cpu_u64(ln), wlen)
+    assert np.array_equal(dst.cpu().numpy()[seed * 5:seed * 5 + want.size], want)
+
+
+def test_encode_empty(codec):
+    """No blocks: out_blk_off[0] = out_base, nothing written."""
+    rec = W.uniform_records(0)
+    first = torch.zeros(1, dtype=torch.int64, device=DEV)
+    dst = torch.zeros(16, dtype=torch.uint8, device=DEV)
+    d, off, ln = codec.encode(records_table(rec), t8(np.zeros(8, np.uint8)), t8(np.zeros(8, np.uint8)), first,
+                              out_base=7, dst=dst)
+    torch.cuda.synchronize()
+    assert int(off[0]) == 7 and int(dst.abs().sum()) == 0
