@@ -1,3 +1,4 @@
+#include <cstdlib>
 // sstc_kernels.hip — CDNA4 (gfx950) kernels of the SST block codec.
 //
 // Kernels (each cites the reference function whose byte work it replaces):
@@ -1009,30 +1010,27 @@ __device__ __forceinline__ void enc_copy_entries(const EncArgs &a, uint8_t *img,
   }
 }
 
-// One LDS dword of an image, clipped to the image bytes [lo, hi): a dword
-// wholly inside is one ds_write_b32, a straddling one is written byte by byte
-// (the neighbouring bytes belong to other fields, written by other lanes).
-__device__ __forceinline__ void lds_put_clip(uint8_t *img, int32_t yy, uint32_t v, int32_t lo, int32_t hi) {
-  if (yy >= lo && yy + 4 <= hi) {
-    *reinterpret_cast<uint32_t *>(img + yy) = v;
-    return;
-  }
-#pragma unroll
-  for (int32_t k = 0; k < 4; k++)
-    if (yy + k >= lo && yy + k < hi) img[yy + k] = static_cast<uint8_t>(v >> (8 * k));
-}
-
 // Chunk c of a span (16 aligned source bytes v + the first dword of chunk c+1)
 // into the image: dwords j = 0..3 at y + 16 c + 4 j, plus for chunk 0 the dword
 // before (its top bytes are the span's first bytes when the skew r0 moves them
-// there).  Together the chunks cover [lo, hi) exactly.
-__device__ __forceinline__ void emit_chunk_clip(uint8_t *img, u32x4 v, uint32_t nxt, uint32_t r0, int32_t y,
-                                                int32_t lo, int32_t hi, bool first) {
-  if (first) lds_put_clip(img, y - 4, __builtin_amdgcn_alignbyte(v.x, 0u, r0), lo, hi);
-  lds_put_clip(img, y, __builtin_amdgcn_alignbyte(v.y, v.x, r0), lo, hi);
-  lds_put_clip(img, y + 4, __builtin_amdgcn_alignbyte(v.z, v.y, r0), lo, hi);
-  lds_put_clip(img, y + 8, __builtin_amdgcn_alignbyte(v.w, v.z, r0), lo, hi);
-  lds_put_clip(img, y + 12, __builtin_amdgcn_alignbyte(nxt, v.w, r0), lo, hi);
+// there).  Every dword that meets [lo, hi) is stored whole, the others go to a
+// per-lane dummy word (no branches): a dword at an end of the span also
+// overwrites up to 3 bytes beyond it, which always belong to the entry's own
+// header fields (klen before a key, vlen after it or before a value, txn after
+// the last field: block_builder.cc:36-77) -- the record pass that follows
+// rewrites every header byte, so it must run after the spans.
+__device__ __forceinline__ void put_dw(uint8_t *img, uint32_t *dummy, int32_t yy, uint32_t v, int32_t lo, int32_t hi) {
+  uint32_t *p = (yy + 4 > lo && yy < hi) ? reinterpret_cast<uint32_t *>(img + yy) : dummy;
+  *p = v;
+}
+
+__device__ __forceinline__ void emit_chunk_clip(uint8_t *img, uint32_t *dummy, u32x4 v, uint32_t nxt, uint32_t r0,
+                                                int32_t y, int32_t lo, int32_t hi, bool first) {
+  put_dw(img, dummy, first ? y - 4 : -64, __builtin_amdgcn_alignbyte(v.x, 0u, r0), lo, hi);
+  put_dw(img, dummy, y, __builtin_amdgcn_alignbyte(v.y, v.x, r0), lo, hi);
+  put_dw(img, dummy, y + 4, __builtin_amdgcn_alignbyte(v.z, v.y, r0), lo, hi);
+  put_dw(img, dummy, y + 8, __builtin_amdgcn_alignbyte(v.w, v.z, r0), lo, hi);
+  put_dw(img, dummy, y + 12, __builtin_amdgcn_alignbyte(nxt, v.w, r0), lo, hi);
 }
 
 // Records -> block image (sstc_encode_blocks: keys and values in two arenas).
@@ -1044,99 +1042,104 @@ __device__ __forceinline__ void emit_chunk_clip(uint8_t *img, u32x4 v, uint32_t 
 // its right neighbour; the group's last lane loads it) into dword-aligned LDS
 // stores, and clips the dwords at the span's ends to byte stores, so the
 // loads are 16 B per lane and coalesced per span instead of a lane walking a
-// record's bytes.  kQ span groups are loaded before any is stored (kQ wide
-// loads in flight per lane).  Then a lane per record writes the header
-// fields, the txn and the offset entry (block_builder.cc:36-93), whose bytes
-// are disjoint from the spans'.
+// record's bytes.  Every load of a round is issued before its first store:
+// the record fields (lane per span owner and lane per record), then kQ span
+// groups at a time (kQ wide loads in flight per lane).  The lane per record
+// writes the header fields, the txn and the offset entry
+// (block_builder.cc:36-93), whose bytes are disjoint from the spans'.
 template <uint32_t G, uint32_t kQ>
-__device__ __forceinline__ void enc_copy_fields(const EncArgs &a, uint8_t *img, uint32_t pad, uint64_t f0,
-                                                uint32_t n, uint64_t P0, uint32_t D) {
+__device__ __forceinline__ void enc_copy_fields(const EncArgs &a, uint8_t *img, uint32_t *dummy, uint32_t pad,
+                                                uint64_t f0, uint32_t n, uint64_t P0, uint32_t D) {
   constexpr uint32_t kS = kWave / G; // spans per wave instruction
   const uint32_t lane = lane_id();
   const uint32_t g = lane % G, sub = lane / G;
+  uint8_t *im = img + pad;
   for (uint32_t c0 = 0; c0 < n; c0 += kWave / 2) {
     const uint32_t nc = n - c0 < kWave / 2 ? n - c0 : kWave / 2;
     const uint32_t ns = 2 * nc;
-    uint64_t my_src = 0;
-    uint32_t my_len = 0, my_ds = 0;
-    if (lane < ns) { // span owner: lane 2i = key of record c0 + i, lane 2i + 1 = its value
-      const uint64_t r = f0 + c0 + (lane >> 1);
-      const uint32_t o = static_cast<uint32_t>(a.P[r] - P0);
-      const uint32_t kl = a.in.key_len[r];
-      if ((lane & 1u) == 0) {
-        my_src = reinterpret_cast<uint64_t>(a.key_src + a.in.key_off[r]);
-        my_len = kl;
-        my_ds = pad + o + 5;
-      } else {
-        const uint32_t vl = a.in.val_len[r];
-        my_len = vl != kNoValue ? vl : 0u;
-        my_src = my_len ? reinterpret_cast<uint64_t>(a.val_src + a.in.val_off[r]) : 0ull;
-        my_ds = pad + o + 9 + kl;
-      }
-    }
+    // span owner: lane 2i = key of record c0 + i, lane 2i + 1 = its value;
+    // record lane: lane i < nc holds record c0 + i's header fields
+    const uint32_t ri = lane < ns ? lane >> 1 : 0u, hi_ = lane < nc ? lane : 0u;
+    const uint64_t rs = f0 + c0 + ri, rh = f0 + c0 + hi_;
+    const uint64_t ps = a.P[rs], ph = a.P[rh], ph1 = a.P[rh + 1];
+    const uint32_t kls = a.in.key_len[rs], vls = a.in.val_len[rs];
+    const uint64_t kos = a.in.key_off[rs], vos = a.in.val_off[rs];
+    const uint32_t klh = a.in.key_len[rh], vlh = a.in.val_len[rh], tyh = a.in.type[rh];
+    const uint64_t txh = a.in.txn[rh];
+    // span of this owner lane (selects, no branches; lanes >= ns own empty spans)
+    const bool is_key = (lane & 1u) == 0;
+    const uint32_t o_s = static_cast<uint32_t>(ps - P0);
+    const uint32_t vlen_s = vls != kNoValue ? vls : 0u;
+    const uint32_t my_len = lane < ns ? (is_key ? kls : vlen_s) : 0u;
+    const uint64_t my_src = is_key ? reinterpret_cast<uint64_t>(a.key_src + kos)
+                                   : (vlen_s ? reinterpret_cast<uint64_t>(a.val_src + vos) : 0ull);
+    const uint32_t my_ds = pad + o_s + (is_key ? 5u : 9u + kls);
+    const uint32_t my_nch = my_len ? ((static_cast<uint32_t>(my_src & 15u) + my_len + 15u) >> 4) : 0u;
+    const bool longs = __any(my_nch > G); // wave-uniform: some span needs more than one round of chunks
+    const u32x4 *safe = reinterpret_cast<const u32x4 *>(a.P); // a valid address for masked-off loads
     for (uint32_t p0 = 0; p0 < ns; p0 += kS * kQ) {
       u32x4 v[kQ];
-      uint32_t r0_[kQ], nch_[kQ];
-      int32_t y_[kQ], lo_[kQ], hi_[kQ];
-      const uint8_t *A_[kQ];
+      const uint8_t *sp_[kQ];
+      uint32_t len_[kQ], ds_[kQ];
 #pragma unroll
       for (uint32_t q = 0; q < kQ; q++) {
         const uint32_t i = p0 + q * kS + sub;
         const int sl = static_cast<int>(i & 63u);
         const uint32_t slo = __shfl(static_cast<uint32_t>(my_src), sl, kWave);
         const uint32_t shi = __shfl(static_cast<uint32_t>(my_src >> 32), sl, kWave);
-        const uint32_t len = __shfl(my_len, sl, kWave), ds = __shfl(my_ds, sl, kWave);
-        const uint8_t *sp = reinterpret_cast<const uint8_t *>((static_cast<uint64_t>(shi) << 32) | slo);
-        const uint32_t mis = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(sp) & 15u);
-        const uint8_t *A = sp - mis;
-        const uint32_t nch = i < ns && len ? (mis + len + 15u) >> 4 : 0u;
-        v[q] = g < nch ? *reinterpret_cast<const u32x4 *>(A + 16 * g) : u32x4{0u, 0u, 0u, 0u};
-        r0_[q] = (mis - ds) & 3u;
-        y_[q] = static_cast<int32_t>(ds) - static_cast<int32_t>(mis) + static_cast<int32_t>(r0_[q]);
-        lo_[q] = static_cast<int32_t>(ds);
-        hi_[q] = static_cast<int32_t>(ds + len);
-        nch_[q] = nch;
-        A_[q] = A;
+        const uint32_t len = __shfl(my_len, sl, kWave); // 0 for i >= ns (owner lane >= ns)
+        ds_[q] = __shfl(my_ds, sl, kWave);
+        sp_[q] = reinterpret_cast<const uint8_t *>((static_cast<uint64_t>(shi) << 32) | slo);
+        len_[q] = len;
+        const uint32_t mis = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(sp_[q]) & 15u);
+        const uint32_t nch = len ? (mis + len + 15u) >> 4 : 0u;
+        v[q] = *(g < nch ? reinterpret_cast<const u32x4 *>(sp_[q] - mis + 16 * g) : safe);
       }
 #pragma unroll
       for (uint32_t q = 0; q < kQ; q++) {
-        for (uint32_t c = g, k = 0; c - g < nch_[q]; c += G, k++) {
-          const u32x4 w = k == 0 ? v[q]
-                                 : (c < nch_[q] ? *reinterpret_cast<const u32x4 *>(A_[q] + 16 * c)
-                                                : u32x4{0u, 0u, 0u, 0u});
-          uint32_t nx = __shfl_down(w.x, 1u, G);
-          if (g == G - 1) nx = c + 1 < nch_[q] ? *reinterpret_cast<const uint32_t *>(A_[q] + 16 * (c + 1)) : 0u;
-          if (c < nch_[q])
-            emit_chunk_clip(img, w, nx, r0_[q], y_[q] + 16 * static_cast<int32_t>(c), lo_[q], hi_[q], c == 0);
+        const uint32_t mis = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(sp_[q]) & 15u);
+        const uint32_t len = len_[q], ds = ds_[q];
+        const uint32_t nch = len ? (mis + len + 15u) >> 4 : 0u;
+        const uint8_t *A = sp_[q] - mis;
+        const uint32_t r0 = (mis - ds) & 3u;
+        const int32_t y = static_cast<int32_t>(ds) - static_cast<int32_t>(mis) + static_cast<int32_t>(r0);
+        const int32_t lo = static_cast<int32_t>(ds), hi = static_cast<int32_t>(ds + len);
+        // round 0, branch-free: chunk g; lanes past the span's chunks store to the sink
+        uint32_t nx = __shfl_down(v[q].x, 1u, G);
+        if (longs && g == G - 1) nx = G < nch ? *reinterpret_cast<const uint32_t *>(A + 16 * G) : 0u;
+        const int32_t no = -(1 << 30); // empty interval: every store of the lane goes to the sink
+        emit_chunk_clip(img, dummy, v[q], nx, r0, y + 16 * static_cast<int32_t>(g), g < nch ? lo : no,
+                        g < nch ? hi : no, g == 0);
+        if (longs) { // further rounds (spans longer than G chunks)
+          for (uint32_t c = g + G; c - g < nch; c += G) {
+            const u32x4 w = c < nch ? *reinterpret_cast<const u32x4 *>(A + 16 * c) : u32x4{0u, 0u, 0u, 0u};
+            uint32_t nx2 = __shfl_down(w.x, 1u, G);
+            if (g == G - 1) nx2 = c + 1 < nch ? *reinterpret_cast<const uint32_t *>(A + 16 * (c + 1)) : 0u;
+            if (c < nch) emit_chunk_clip(img, dummy, w, nx2, r0, y + 16 * static_cast<int32_t>(c), lo, hi, false);
+          }
         }
       }
     }
-  }
-  // header fields, txn, offset entry: lane per record (coalesced SoA loads)
-  uint8_t *im = img + pad;
-  for (uint32_t i = lane; i < n; i += kWave) {
-    const uint64_t r = f0 + i;
-    const uint64_t pr = a.P[r];
-    const uint32_t o = static_cast<uint32_t>(pr - P0);
-    const uint32_t sz = static_cast<uint32_t>(a.P[r + 1] - pr);
-    const uint32_t kl = a.in.key_len[r], vl = a.in.val_len[r];
-    const uint64_t tx = a.in.txn[r];
-    im[o] = a.in.type[r];
+    if (lane < nc) { // header fields, txn, offset entry of record c0 + lane (after the spans)
+      const uint32_t o = static_cast<uint32_t>(ph - P0), sz = static_cast<uint32_t>(ph1 - ph);
+      im[o] = static_cast<uint8_t>(tyh);
 #pragma unroll
-    for (int j = 0; j < 4; j++) im[o + 1 + j] = static_cast<uint8_t>(kl >> (8 * j));
-    if (vl != kNoValue) {
+      for (int j = 0; j < 4; j++) im[o + 1 + j] = static_cast<uint8_t>(klh >> (8 * j));
+      uint8_t *vp = vlh != kNoValue ? im + o + 5 + klh : reinterpret_cast<uint8_t *>(dummy);
 #pragma unroll
-      for (int j = 0; j < 4; j++) im[o + 5 + kl + j] = static_cast<uint8_t>(vl >> (8 * j));
+      for (int j = 0; j < 4; j++) vp[j] = static_cast<uint8_t>(vlh >> (8 * j));
+#pragma unroll
+      for (int j = 0; j < 8; j++) im[o + sz - 8 + j] = static_cast<uint8_t>(txh >> (8 * j));
+      lds_st_u64u(im, D + 16 * (c0 + lane), o); // D & 3 is wave-uniform
+      lds_st_u64u(im, D + 16 * (c0 + lane) + 8, sz);
     }
-    lds_st_u64u(im, o + sz - 8, tx);
-    lds_st_u64u(im, D + 16 * i, o);
-    lds_st_u64u(im, D + 16 * i + 8, sz);
   }
 }
 
-template <uint32_t kMode> // 0: lane per record, 1: whole-entry copy (compaction)
+template <uint32_t kMode, uint32_t G = 8, uint32_t kQ = 2> // 0: two arenas (key / value spans), 1: whole-entry copy (compaction)
 __global__ __launch_bounds__(kEncWaves *kWave) void enc_lds_kernel(EncArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kEncSlotWaves * kEncSlot];
+  __shared__ uint32_t s_dummy[kMode == 0 ? kEncWaves * kWave : 1]; // per-lane sink of clipped stores
   const uint32_t wave = uniform(threadIdx.x / kWave);
   const uint32_t lane = lane_id();
   const uint32_t wg = a.xcd ? xcd_logical_block(blockIdx.x, gridDim.x) : blockIdx.x;
@@ -1160,7 +1163,7 @@ __global__ __launch_bounds__(kEncWaves *kWave) void enc_lds_kernel(EncArgs a) {
   if constexpr (kMode == 1) {
     enc_copy_entries<4>(a, img, pad, f0, n, P0, D, b);
   } else {
-    enc_copy_fields<8, 2>(a, img, pad, f0, n, P0, D);
+    enc_copy_fields<G, kQ>(a, img, s_dummy + threadIdx.x, pad, f0, n, P0, D);
   }
   if (lane == 0) {
     lds_st_u64u(im, D + 16 * n, n);
@@ -1915,7 +1918,14 @@ hipError_t launch_enc_blocks(const uint64_t *P, const uint64_t *blk_first, uint6
 hipError_t launch_enc_emit(const EncArgs &a, hipStream_t s) {
   if (!a.nblocks) return hipSuccess;
   const uint32_t g = grid_for(a.nblocks, kEncWaves);
-  if (!a.entries_in_src) enc_lds_kernel<0><<<g, kEncWaves * kWave, 0, s>>>(a);
+  static const int var = getenv("SSTC_ENC_VARIANT") ? atoi(getenv("SSTC_ENC_VARIANT")) : 0; // A/B (temporary)
+  if (!a.entries_in_src) {
+    if (var == 1) enc_lds_kernel<0, 8, 4><<<g, kEncWaves * kWave, 0, s>>>(a);
+    else if (var == 2) enc_lds_kernel<0, 16, 2><<<g, kEncWaves * kWave, 0, s>>>(a);
+    else if (var == 3) enc_lds_kernel<0, 4, 4><<<g, kEncWaves * kWave, 0, s>>>(a);
+    else if (var == 4) enc_lds_kernel<0, 8, 8><<<g, kEncWaves * kWave, 0, s>>>(a);
+    else enc_lds_kernel<0><<<g, kEncWaves * kWave, 0, s>>>(a);
+  }
   else enc_lds_kernel<1><<<g, kEncWaves * kWave, 0, s>>>(a);
   // blocks past an LDS slot: those listed by enc_lds_kernel when a list is given
   const uint64_t cap = a.big ? 512 : 2048;
