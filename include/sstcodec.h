@@ -193,7 +193,17 @@ typedef struct sstc_compact_params {
                             /* output SST is finished once its key+value bytes */
                             /* reach it (compact.cc:290)                       */
   uint32_t base_level;      /* 1: IsBaseLevelForKey() holds for every key, so a */
-                            /* tombstone that starts a key group is dropped    */
+                            /* tombstone that starts a key group is dropped.   */
+                            /* This is the only state the reference reaches    */
+                            /* (only L0->L1 compactions exist, so levels >= 2  */
+                            /* stay empty, compact.cc:365-380) and the only    */
+                            /* mode that claims reference parity.  0: every    */
+                            /* such tombstone is kept (the branch compact.cc:  */
+                            /* 347-349 takes for a key equal to the smallest   */
+                            /* key of a level->=2 SST) -- framework-defined    */
+                            /* semantics for engines with deeper levels,       */
+                            /* pinned by the restated driver oracle/           */
+                            /* ref_compact.cc, not by a reachable reference run */
   uint32_t txn_mode;        /* SSTC_TXN_COMPAT = the reference iterator's txn   */
 } sstc_compact_params;
 
@@ -207,7 +217,10 @@ typedef struct sstc_compact_result {
  * h_table_first_block[t+1]) (HOST array, ntables+1 elements).  Every input
  * table must be sorted (key ascending, equal keys txn descending), as
  * TableBuilder requires.  Records merge in MergeIterator order (key asc, txn
- * desc; equal (key, txn): lower input table first), ShouldKeepEntry filters
+ * desc; equal (key, txn): lower input table first -- the reference's
+ * std::priority_queue orders such ties by heap history, so inputs holding the
+ * same (key, txn) with different contents may differ in order; identical
+ * copies, the only kind the engine writes, give the same bytes), ShouldKeepEntry filters
  * them, and the survivors are written as complete SST images (blocks, meta
  * section, 40 B footer) back to back into d_dst: table t at d_table_off[t]
  * with d_table_len[t] bytes (TableBuilder::GetFileSize() = d_table_len[t] + 1).

@@ -211,3 +211,44 @@ def compaction_inputs(k, n_per, key_space, seed=5, p_delete=0.1, vmin=8, vmax=20
                     "val_off": np.where(typ == TYPE_DELETED, 0, val_off).astype(np.uint64),
                     "key_src": key_src, "val_src": val_src})
     return out
+
+
+def cross_duplicate_inputs(k, n_per, key_space, seed=5, p_shared=0.5, p_delete=0.2, same_content=True,
+                           vmax=40, key_width=16):
+    """k sorted record sets in which the same (key, txn) appears in several
+    tables -- the case where the merge order among equal (key, txn) records
+    decides the output bytes (ShouldKeepEntry keeps them all,
+    compact.cc:357-362).  Every key has one shared version (txn, type, value);
+    a table that holds the key takes the shared version with probability
+    p_shared, else a table-unique txn.  same_content=False: the shared txn
+    comes with the table's own type / value (not reachable through the
+    engine, whose txn ids are unique per write)."""
+    rng = np.random.default_rng(seed)
+    shared_txn = (rng.permutation(key_space).astype(np.uint64) + np.uint64(1)) * np.uint64(1000)
+    shared_typ = (rng.random(key_space) < p_delete).astype(np.uint8)
+    shared_vl = rng.integers(0, vmax + 1, key_space).astype(np.uint32)
+    shared_seed = rng.integers(0, 1 << 30, key_space)
+    out = []
+    for t in range(k):
+        idx = np.sort(rng.choice(key_space, size=min(n_per, key_space), replace=False))
+        n = idx.size
+        share = rng.random(n) < p_shared
+        typ = np.where(share & same_content, shared_typ[idx], (rng.random(n) < p_delete).astype(np.uint8))
+        vl = np.where(share & same_content, shared_vl[idx], rng.integers(0, vmax + 1, n)).astype(np.uint32)
+        txn = np.where(share, shared_txn[idx], shared_txn[idx] + np.uint64(1 + t)).astype(np.uint64)
+        vals = []
+        for j in range(n):
+            if typ[j] == TYPE_DELETED:
+                continue
+            s = int(shared_seed[idx[j]]) if (share[j] and same_content) else int(rng.integers(0, 1 << 30))
+            vals.append(random_bytes(s, int(vl[j])))
+        vl = np.where(typ == TYPE_DELETED, np.uint32(NO_VALUE), vl).astype(np.uint32)
+        vb = np.where(vl == NO_VALUE, 0, vl).astype(np.uint64)
+        val_off = np.zeros(n, np.uint64)
+        val_off[1:] = np.cumsum(vb[:-1])
+        val_src = np.concatenate(vals + [np.zeros(8, np.uint8)])
+        out.append({"type": typ.astype(np.uint8), "key_len": np.full(n, key_width, np.uint32), "val_len": vl,
+                    "txn": txn, "key_off": np.arange(n, dtype=np.uint64) * np.uint64(key_width),
+                    "val_off": np.where(typ == TYPE_DELETED, 0, val_off).astype(np.uint64),
+                    "key_src": fixed_keys(idx.astype(np.uint64), key_width), "val_src": val_src})
+    return out

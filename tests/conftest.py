@@ -41,3 +41,61 @@ def reflib():
 
 
 BLOCK_SETS = ["kat_basic.npz", "kat_edge.npz", "block_uniform.npz", "blocks_mixed.npz", "blocks_edge.npz"]
+
+
+def sst_records(oracle, img):
+    """Records of an SST image in file order: (key, txn, type, value or None),
+    parsed with the oracle (table_reader.cc:52-156, block_reader.cc:59-114)."""
+    idx = oracle.table_index(img)
+    out = []
+    for o, ln in zip(idx["blk_off"], idx["blk_len"]):
+        st, d = oracle.decode_block(img[int(o):int(o + ln)], 1, int(o))  # correct txn mode
+        assert st == 0
+        for t, kl, vl, tx, ko, vo in zip(d["type"], d["key_len"], d["val_len"], d["txn"], d["key_off"], d["val_off"]):
+            key = bytes(img[int(ko):int(ko) + int(kl)])
+            val = None if vl == 0xFFFFFFFF else bytes(img[int(vo):int(vo) + int(vl)])
+            out.append((key, int(tx), int(t), val))
+    return out
+
+
+def tie_case(g, name, base):
+    ins = [g[f"{name}_in{i}"] for i in range(4)]
+    outs = sorted((k for k in g if k.startswith(f"{name}_base{base}_out")), key=lambda x: int(x.rsplit("out", 1)[1]))
+    return ins, [g[k] for k in outs]
+
+
+def _runs(recs):
+    out = []
+    for r in recs:
+        if out and out[-1][0] == r[:2]:
+            out[-1][1].append(r)
+        else:
+            out.append((r[:2], [r]))
+    return out
+
+
+def same_up_to_tie_order(a, b, inputs):
+    """Two compaction outputs (record streams) of the same inputs that may
+    differ only in how runs of equal (key, txn) coming from several inputs
+    were ordered: the same (key, txn) sequence, identical runs for pairs that
+    occur in one input only, and for tied pairs only records of the inputs
+    (which of them survive ShouldKeepEntry depends on the order, compact.cc:
+    324-363)."""
+    from collections import Counter
+    seen = Counter()
+    pool = {}
+    for recs in inputs:
+        for p in {r[:2] for r in recs}:
+            seen[p] += 1
+        for r in recs:
+            pool.setdefault(r[:2], []).append(r)
+    ra, rb = _runs(a), _runs(b)
+    if [p for p, _ in ra] != [p for p, _ in rb]:
+        return False
+    for (p, x), (_, y) in zip(ra, rb):
+        if seen[p] <= 1:
+            if x != y:
+                return False
+        elif not all(r in pool[p] for r in x + y):
+            return False
+    return True

@@ -106,6 +106,8 @@ def block_set(ref, name, rec, first, extra=None):
 
 def main():
     ref = RefLib()
+    if sys.argv[1:] == ["ties"]:
+        return tie_fixtures(ref)
 
     # 1. tests/test_block.cc:57-138 (BasicEncode) and :140-187 (EdgeCasesEncode)
     basic = records_from_list([(0, b"apple", b"value1", 12345), (0, b"apply", b"success", 9876),
@@ -161,6 +163,9 @@ def main():
     # 7. point lookups (TableReader::GetValue -> BlockReader::GetValue)
     lookup_fixtures(ref)
 
+    # 8. equal (key, txn) records across inputs (merge tie order)
+    tie_fixtures(ref)
+
 
 COMPACTION_CASES = [
     # name, k, n_per, key_space, vmax, table_limit, distinct, extra generator args
@@ -206,6 +211,35 @@ def compaction_fixtures(ref):
     with open(os.path.join(HERE, "compaction.json"), "w") as f:
         json.dump(manifest, f, indent=1)
     print("compaction.json written")
+
+
+TIE_CASES = [("same", True), ("diff", False)]
+
+
+def tie_fixtures(ref):
+    """The same (key, txn) in several inputs (sstcodec.workload.cross_duplicate_inputs),
+    compacted by the reference driver (base level 1 and 0).  'same': the copies
+    are identical (what the engine can produce: one write, one txn) -- the
+    build must match these bytes.  'diff': same txn, different type / value:
+    the reference's std::priority_queue (merge_iterator.h:91-95) orders such
+    ties by its heap history; the outputs are stored whole so the tests can
+    pin everything but that order (divergences)."""
+    arrays = {}
+    for name, same in TIE_CASES:
+        sets = W.cross_duplicate_inputs(4, 300, 400, seed=17, same_content=same)
+        with tempfile.TemporaryDirectory() as td:
+            ins = []
+            for i, rec in enumerate(sets):
+                p = os.path.join(td, f"in{i}.sst")
+                ins.append((p, ref.table_build(p, rec, 4096)))
+                arrays[f"{name}_in{i}"] = np.fromfile(p, np.uint8)
+            for base in (1, 0):
+                od = os.path.join(td, f"out{base}")
+                os.makedirs(od)
+                outs = ref_compact(ins, od, 4096, 6000, base)
+                for j, (p, _) in enumerate(outs):
+                    arrays[f"{name}_base{base}_out{j}"] = np.fromfile(p, np.uint8)
+    save("compact_ties.npz", **arrays)
 
 
 def sorted_ragged(n, seed):
