@@ -16,8 +16,25 @@
  *                       CreateAndSetupDataForBlockReader (:212-241) by one
  *                       batched GPU decode of every block.
  *
+ *   sstc::BlockReader / TableReader::CreateAndSetupDataForBlockReader(s)
+ *                       the decoded records of one data block
+ *                       (block_reader.h:24-45,104-119, table_reader.h:99-101);
+ *                       the batched form decodes many blocks in one GPU call.
+ *   sstc::TableReaderIterator
+ *                       the record stream of table_reader_iterator.cc:46-149
+ *                       (SeekToFirst / Next / Prev / Seek / accessors) over the
+ *                       whole table decoded in one GPU call.
+ *
+ * Drop-in surface: TableBuilder(std::string&&, const Config*) takes any config
+ * type with GetSSTBlockSize() (db/config.h) and uses the calling thread's
+ * context (ThreadContext()), and AddEntry accepts the engine's own
+ * db::ValueType (any enum with PUT = 0 / DELETED = 1), so db/compact.cc and
+ * db/db_impl.cc compile unchanged against `namespace kvs::sstable { using
+ * TableBuilder = ::sstc::TableBuilder; }`.
+ *
  * Error behaviour follows the reference: Open() returns false, Finish() throws
- * std::runtime_error; the C shim returns SSTC_* codes instead.
+ * std::runtime_error, CreateAndSetupDataForBlockReader returns nullptr on a
+ * read failure; the C shim returns SSTC_* codes instead.
  */
 #ifndef SSTC_TABLE_H
 #define SSTC_TABLE_H
@@ -26,11 +43,25 @@
 
 #ifdef __cplusplus
 #include <cstdint>
+#include <memory>
 #include <string>
 #include <string_view>
+#include <type_traits>
+#include <utility>
 #include <vector>
 
 namespace sstc {
+
+/* db/status.h:11-19, common/macros.h */
+enum class ValueType : uint8_t { PUT = 0, DELETED = 1, NOT_FOUND = 2, kTooManyOpenFiles = 3 };
+using TxnId = uint64_t;
+using BlockOffset = uint64_t;
+using BlockSize = uint64_t;
+
+/* The calling host thread's context on the current HIP device, created on
+ * first use and destroyed at thread exit (the reference builds / reads SSTs
+ * from pool threads, one TableBuilder per thread: db/db_impl.cc:354-362). */
+sstc_ctx *ThreadContext();
 
 /* One meta entry (reference sstable/block_index.h:22-57). */
 struct BlockIndex {
@@ -44,6 +75,10 @@ class TableBuilder {
 public:
   /* block_threshold = Config::GetSSTBlockSize() (config/config.toml:11). */
   TableBuilder(std::string filename, uint64_t block_threshold, sstc_ctx *ctx);
+  /* table_builder.h:65: TableBuilder(std::string &&, const db::Config *) */
+  template <class Config, class = decltype(std::declval<const Config *>()->GetSSTBlockSize())>
+  TableBuilder(std::string &&filename, const Config *config)
+      : TableBuilder(std::move(filename), static_cast<uint64_t>(config->GetSSTBlockSize()), ThreadContext()) {}
   ~TableBuilder();
   TableBuilder(const TableBuilder &) = delete;
   TableBuilder &operator=(const TableBuilder &) = delete;
@@ -51,6 +86,11 @@ public:
   bool Open();
   /* value.data() == nullptr -> no value fields (a DELETE), like the reference. */
   void AddEntry(std::string_view key, std::string_view value, uint64_t txn_id, uint8_t value_type);
+  /* table_builder.h:81: AddEntry(string_view, string_view, TxnId, db::ValueType) */
+  template <class VT, class = std::enable_if_t<std::is_enum_v<VT>>>
+  void AddEntry(std::string_view key, std::string_view value, TxnId txn_id, VT value_type) {
+    AddEntry(key, value, txn_id, static_cast<uint8_t>(value_type));
+  }
   void FlushBlock();
   void Finish();
 
@@ -79,11 +119,55 @@ private:
   uint64_t current_offset_ = 0;
 };
 
+/* The records of one data block, decoded on the GPU (BlockReaderData +
+ * BlockReader accessors, block_reader.h:24-45,104-119, block_reader.cc:59-114).
+ * Views point into the block bytes the reader owns.  GetValue of a DELETE is
+ * a null view (value.data() == nullptr), of a PUT a non-null view even when
+ * empty, so AddEntry(GetKey(i), GetValue(i), ...) re-encodes exactly. */
+class BlockReader {
+public:
+  uint64_t NumEntries() const { return type_.size(); }
+  ValueType GetType(uint64_t i) const { return static_cast<ValueType>(type_[i]); }
+  std::string_view GetKey(uint64_t i) const {
+    return {reinterpret_cast<const char *>(buf_.data()) + key_off_[i], key_len_[i]};
+  }
+  std::string_view GetValue(uint64_t i) const {
+    if (val_len_[i] == SSTC_NO_VALUE) return {};
+    return {reinterpret_cast<const char *>(buf_.data()) + val_off_[i], val_len_[i]};
+  }
+  TxnId GetTransactionId(uint64_t i) const { return txn_[i]; }
+  int Status() const { return status_; } /* SSTC_BLK_* of this block */
+
+private:
+  friend class TableReader;
+  std::vector<uint8_t> buf_; /* the block's bytes */
+  std::vector<uint8_t> type_;
+  std::vector<uint32_t> key_len_, val_len_;
+  std::vector<uint64_t> txn_, key_off_, val_off_;
+  int status_ = SSTC_BLK_OK;
+};
+
 class TableReader {
 public:
   /* file_size as recorded by TableBuilder::GetFileSize() (bytes + 1). */
   static TableReader *Open(const std::string &filename, uint64_t file_size, sstc_ctx *ctx);
+  /* CreateAndSetupDataForTableReader(std::string&&, SSTId, uint64_t) on the
+   * calling thread's context (table_reader.h:134-136); nullptr on failure. */
+  static std::unique_ptr<TableReader> Create(std::string &&filename, uint64_t table_id, uint64_t file_size) {
+    (void)table_id;
+    return std::unique_ptr<TableReader>(Open(filename, file_size, ThreadContext()));
+  }
   ~TableReader();
+
+  /* table_reader.h:99-101: pread one block and decode it (one GPU call). */
+  std::unique_ptr<BlockReader> CreateAndSetupDataForBlockReader(BlockOffset offset, uint64_t block_size,
+                                                               uint32_t txn_mode = SSTC_TXN_COMPAT) const;
+  /* The same for many blocks with ONE decode call (what compaction and scans
+   * want: every block of a table at once).  Entries are nullptr for blocks
+   * that could not be read. */
+  std::vector<std::unique_ptr<BlockReader>> CreateAndSetupDataForBlockReaders(
+      const std::vector<std::pair<BlockOffset, uint64_t>> &blocks, uint32_t txn_mode = SSTC_TXN_COMPAT) const;
+  uint64_t GetFileSize() const { return bytes_ + 1; }
 
   const std::vector<BlockIndex> &GetBlockIndex() const { return index_; }
   uint64_t GetMinTxn() const { return min_txn_; }
@@ -102,6 +186,51 @@ private:
   uint64_t bytes_ = 0, meta_off_ = 0;
   uint64_t min_txn_ = 0, max_txn_ = 0;
   std::vector<BlockIndex> index_;
+};
+
+/* table_reader_iterator.cc:46-149 over a table decoded whole on the GPU at the
+ * first Seek (one sstc_count_records + sstc_decode_blocks call instead of a
+ * pread and a BlockReader per block). */
+class TableReaderIterator {
+public:
+  explicit TableReaderIterator(TableReader *table, uint32_t txn_mode = SSTC_TXN_COMPAT)
+      : table_(table), txn_mode_(txn_mode) {}
+  bool IsValid() const { return pos_ < n_; }
+  void SeekToFirst() {
+    Load();
+    pos_ = 0;
+  }
+  void SeekToLast() {
+    Load();
+    pos_ = n_ ? n_ - 1 : n_;
+  }
+  /* first entry whose key is >= key (block_reader_iterator.cc:84-119) */
+  void Seek(std::string_view key);
+  void Next() {
+    if (pos_ < n_) pos_++;
+  }
+  void Prev() { pos_ = pos_ == 0 || pos_ >= n_ ? n_ : pos_ - 1; }
+  std::string_view GetKey() const {
+    return {reinterpret_cast<const char *>(data_.data()) + key_off_[pos_], key_len_[pos_]};
+  }
+  std::string_view GetValue() const {
+    if (val_len_[pos_] == SSTC_NO_VALUE) return {};
+    return {reinterpret_cast<const char *>(data_.data()) + val_off_[pos_], val_len_[pos_]};
+  }
+  ValueType GetType() const { return static_cast<ValueType>(type_[pos_]); }
+  TxnId GetTransactionId() const { return txn_[pos_]; }
+  int Status() const { return status_; } /* first failing block's SSTC_BLK_* code */
+
+private:
+  void Load();
+  TableReader *table_;
+  uint32_t txn_mode_;
+  bool loaded_ = false;
+  int status_ = SSTC_BLK_OK;
+  uint64_t pos_ = 0, n_ = 0;
+  std::vector<uint8_t> data_, type_;
+  std::vector<uint32_t> key_len_, val_len_;
+  std::vector<uint64_t> txn_, key_off_, val_off_;
 };
 
 } // namespace sstc

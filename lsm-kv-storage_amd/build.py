@@ -70,6 +70,16 @@ def build(verbose=False):
         if verbose:
             print(" ".join(cmd))
         subprocess.run(cmd, check=True)
+    # a C++ caller compiled against include/sstc_table.h (the drop-in surface):
+    # the DoCompactJob loop over sstc::TableBuilder / TableReaderIterator
+    tu = os.path.join(ROOT, "tests", "cpp", "compact_loop.cc")
+    exe = os.path.join(LIB, "sstc_compact_loop")
+    if os.path.exists(tu) and _newer(exe, [tu, so, os.path.join(ROOT, "include", "sstc_table.h")]):
+        cmd = [os.environ.get("CXX", "g++"), "-O2", "-std=c++17", "-Wall", "-I" + os.path.join(ROOT, "include"), tu,
+               "-o", exe, "-L" + LIB, "-lsstcodec", "-Wl,-rpath,$ORIGIN"]
+        if verbose:
+            print(" ".join(cmd))
+        subprocess.run(cmd, check=True)
     return so
 
 

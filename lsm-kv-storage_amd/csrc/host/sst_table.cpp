@@ -240,6 +240,71 @@ TableReader::~TableReader() {
   if (fd_ >= 0) ::close(fd_);
 }
 
+namespace {
+// Batched GPU decode of blocks (off[b], len[b]) inside the host bytes `data`:
+// per-block record counts and status, record fields with offsets into data.
+struct HostRecords {
+  std::vector<uint8_t> type;
+  std::vector<uint32_t> kl, vl, status;
+  std::vector<uint64_t> txn, ko, vo, base;
+};
+
+int decode_host(sstc_ctx *ctx, std::vector<uint8_t> &data, const std::vector<uint64_t> &off,
+                const std::vector<uint64_t> &len, uint32_t txn_mode, HostRecords &out) {
+  const uint64_t nb = off.size();
+  if (data.empty()) data.push_back(0);
+  DevBuf d_src = upload(data), d_off = upload(off), d_len = upload(len), d_base((nb + 1) * 8),
+         d_status(nb * 4 + 4);
+  check(sstc_count_records(ctx, d_src.as<uint8_t>(), d_off.as<uint64_t>(), d_len.as<uint64_t>(), nb,
+                           d_base.as<uint64_t>()),
+        "sstc_count_records");
+  uint64_t errs = 0;
+  check(sstc_ctx_error_count(ctx, &errs), "sync");
+  out.base.resize(nb + 1);
+  if (hipMemcpy(out.base.data(), d_base.p, (nb + 1) * 8, hipMemcpyDeviceToHost) != hipSuccess) return SSTC_E_HIP;
+  const uint64_t n = out.base[nb];
+  DevBuf d_type(n + 1), d_kl(4 * n + 4), d_vl(4 * n + 4), d_txn(8 * n + 8), d_ko(8 * n + 8), d_vo(8 * n + 8);
+  sstc_records rec{d_type.as<uint8_t>(), d_kl.as<uint32_t>(), d_vl.as<uint32_t>(),
+                   d_txn.as<uint64_t>(), d_ko.as<uint64_t>(), d_vo.as<uint64_t>()};
+  check(sstc_decode_blocks(ctx, d_src.as<uint8_t>(), d_off.as<uint64_t>(), d_len.as<uint64_t>(), nb,
+                           d_base.as<uint64_t>(), rec, txn_mode, d_status.as<uint32_t>()),
+        "sstc_decode_blocks");
+  check(sstc_ctx_error_count(ctx, &errs), "sync");
+  out.status.resize(nb);
+  out.type.resize(n);
+  out.kl.resize(n);
+  out.vl.resize(n);
+  out.txn.resize(n);
+  out.ko.resize(n);
+  out.vo.resize(n);
+  bool ok = hipMemcpy(out.status.data(), d_status.p, nb * 4, hipMemcpyDeviceToHost) == hipSuccess;
+  ok = ok && hipMemcpy(out.type.data(), d_type.p, n, hipMemcpyDeviceToHost) == hipSuccess;
+  ok = ok && hipMemcpy(out.kl.data(), d_kl.p, 4 * n, hipMemcpyDeviceToHost) == hipSuccess;
+  ok = ok && hipMemcpy(out.vl.data(), d_vl.p, 4 * n, hipMemcpyDeviceToHost) == hipSuccess;
+  ok = ok && hipMemcpy(out.txn.data(), d_txn.p, 8 * n, hipMemcpyDeviceToHost) == hipSuccess;
+  ok = ok && hipMemcpy(out.ko.data(), d_ko.p, 8 * n, hipMemcpyDeviceToHost) == hipSuccess;
+  ok = ok && hipMemcpy(out.vo.data(), d_vo.p, 8 * n, hipMemcpyDeviceToHost) == hipSuccess;
+  return ok ? SSTC_OK : SSTC_E_HIP;
+}
+
+struct CtxHolder { // one context per host thread, destroyed at thread exit
+  sstc_ctx *ctx = nullptr;
+  ~CtxHolder() {
+    if (ctx) sstc_ctx_destroy(ctx);
+  }
+};
+} // namespace
+
+sstc_ctx *ThreadContext() {
+  thread_local CtxHolder h;
+  if (!h.ctx) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    check(sstc_ctx_create(dev, nullptr, &h.ctx), "sstc_ctx_create");
+  }
+  return h.ctx;
+}
+
 int TableReader::DecodeAll(uint32_t txn_mode, std::vector<uint8_t> &data, std::vector<uint8_t> &type,
                            std::vector<uint32_t> &key_len, std::vector<uint32_t> &val_len,
                            std::vector<uint64_t> &txn, std::vector<uint64_t> &key_off,
@@ -253,42 +318,83 @@ int TableReader::DecodeAll(uint32_t txn_mode, std::vector<uint8_t> &data, std::v
     len[b] = index_[b].size;
     if (off[b] > meta_off_ || len[b] > meta_off_ - off[b]) return SSTC_E_INVALID_ARG;
   }
-  if (data.empty()) data.push_back(0);
-  DevBuf d_src = upload(data), d_off = upload(off), d_len = upload(len), d_base((nb + 1) * 8),
-         d_status(nb * 4 + 4);
-  check(sstc_count_records(ctx_, d_src.as<uint8_t>(), d_off.as<uint64_t>(), d_len.as<uint64_t>(), nb,
-                           d_base.as<uint64_t>()),
-        "sstc_count_records");
-  uint64_t errs = 0;
-  check(sstc_ctx_error_count(ctx_, &errs), "sync");
-  std::vector<uint64_t> base(nb + 1);
-  if (hipMemcpy(base.data(), d_base.p, (nb + 1) * 8, hipMemcpyDeviceToHost) != hipSuccess) return SSTC_E_HIP;
-  const uint64_t n = base[nb];
-  DevBuf d_type(n + 1), d_kl(4 * n + 4), d_vl(4 * n + 4), d_txn(8 * n + 8), d_ko(8 * n + 8), d_vo(8 * n + 8);
-  sstc_records rec{d_type.as<uint8_t>(), d_kl.as<uint32_t>(), d_vl.as<uint32_t>(),
-                   d_txn.as<uint64_t>(), d_ko.as<uint64_t>(), d_vo.as<uint64_t>()};
-  check(sstc_decode_blocks(ctx_, d_src.as<uint8_t>(), d_off.as<uint64_t>(), d_len.as<uint64_t>(), nb,
-                           d_base.as<uint64_t>(), rec, txn_mode, d_status.as<uint32_t>()),
-        "sstc_decode_blocks");
-  check(sstc_ctx_error_count(ctx_, &errs), "sync");
-  std::vector<uint32_t> status(nb);
-  type.resize(n);
-  key_len.resize(n);
-  val_len.resize(n);
-  txn.resize(n);
-  key_off.resize(n);
-  val_off.resize(n);
-  bool ok = hipMemcpy(status.data(), d_status.p, nb * 4, hipMemcpyDeviceToHost) == hipSuccess;
-  ok = ok && hipMemcpy(type.data(), d_type.p, n, hipMemcpyDeviceToHost) == hipSuccess;
-  ok = ok && hipMemcpy(key_len.data(), d_kl.p, 4 * n, hipMemcpyDeviceToHost) == hipSuccess;
-  ok = ok && hipMemcpy(val_len.data(), d_vl.p, 4 * n, hipMemcpyDeviceToHost) == hipSuccess;
-  ok = ok && hipMemcpy(txn.data(), d_txn.p, 8 * n, hipMemcpyDeviceToHost) == hipSuccess;
-  ok = ok && hipMemcpy(key_off.data(), d_ko.p, 8 * n, hipMemcpyDeviceToHost) == hipSuccess;
-  ok = ok && hipMemcpy(val_off.data(), d_vo.p, 8 * n, hipMemcpyDeviceToHost) == hipSuccess;
-  if (!ok) return SSTC_E_HIP;
+  HostRecords r;
+  if (int rc = decode_host(ctx_, data, off, len, txn_mode, r)) return rc;
+  type = std::move(r.type);
+  key_len = std::move(r.kl);
+  val_len = std::move(r.vl);
+  txn = std::move(r.txn);
+  key_off = std::move(r.ko);
+  val_off = std::move(r.vo);
   for (uint64_t b = 0; b < nb; b++)
-    if (status[b] != SSTC_BLK_OK) return static_cast<int>(status[b]);
+    if (r.status[b] != SSTC_BLK_OK) return static_cast<int>(r.status[b]);
   return SSTC_BLK_OK;
+}
+
+std::vector<std::unique_ptr<BlockReader>> TableReader::CreateAndSetupDataForBlockReaders(
+    const std::vector<std::pair<BlockOffset, uint64_t>> &blocks, uint32_t txn_mode) const {
+  // table_reader.cc:212-241 for every block: pread, then ONE batched decode
+  const uint64_t nb = blocks.size();
+  std::vector<std::unique_ptr<BlockReader>> out(nb);
+  std::vector<uint64_t> off, len, which;
+  std::vector<uint8_t> data;
+  for (uint64_t b = 0; b < nb; b++) {
+    const auto [o, l] = blocks[b];
+    if (o > bytes_ || l > bytes_ - o) continue; // read failure -> nullptr (table_reader.cc:218-224)
+    const uint64_t at = data.size();
+    data.resize(at + l);
+    if (l && !pread_all(fd_, data.data() + at, l, o)) {
+      data.resize(at);
+      continue;
+    }
+    off.push_back(at);
+    len.push_back(l);
+    which.push_back(b);
+  }
+  if (which.empty()) return out;
+  HostRecords r;
+  check(decode_host(ctx_, data, off, len, txn_mode, r), "block decode");
+  for (uint64_t k = 0; k < which.size(); k++) {
+    auto br = std::unique_ptr<BlockReader>(new BlockReader());
+    br->buf_.assign(data.begin() + off[k], data.begin() + off[k] + len[k]);
+    br->status_ = static_cast<int>(r.status[k]);
+    for (uint64_t i = r.base[k]; i < r.base[k + 1]; i++) {
+      br->type_.push_back(r.type[i]);
+      br->key_len_.push_back(r.kl[i]);
+      br->val_len_.push_back(r.vl[i]);
+      br->txn_.push_back(r.txn[i]);
+      br->key_off_.push_back(r.ko[i] - off[k]);
+      br->val_off_.push_back(r.vl[i] == SSTC_NO_VALUE ? 0 : r.vo[i] - off[k]);
+    }
+    out[which[k]] = std::move(br);
+  }
+  return out;
+}
+
+std::unique_ptr<BlockReader> TableReader::CreateAndSetupDataForBlockReader(BlockOffset offset, uint64_t block_size,
+                                                                           uint32_t txn_mode) const {
+  auto v = CreateAndSetupDataForBlockReaders({{offset, block_size}}, txn_mode);
+  return std::move(v[0]);
+}
+
+// ---------------------------------------------------------- TableReaderIterator
+void TableReaderIterator::Load() {
+  if (loaded_) return;
+  loaded_ = true;
+  status_ = table_->DecodeAll(txn_mode_, data_, type_, key_len_, val_len_, txn_, key_off_, val_off_);
+  n_ = status_ == SSTC_BLK_OK ? type_.size() : 0;
+}
+
+void TableReaderIterator::Seek(std::string_view key) {
+  Load();
+  uint64_t lo = 0, hi = n_; // first entry with key >= `key` (entries are key-ascending)
+  while (lo < hi) {
+    const uint64_t mid = (lo + hi) / 2;
+    pos_ = mid;
+    if (GetKey() < key) lo = mid + 1;
+    else hi = mid;
+  }
+  pos_ = lo;
 }
 
 } // namespace sstc

@@ -1,0 +1,83 @@
+"""A C++ caller compiled against include/sstc_table.h (tests/cpp/compact_loop.cc,
+built by lsm-kv-storage_amd/build.py): the DoCompactJob loop of
+/root/reference/db/compact.cc:232-322 written with the reference's own
+spellings over the drop-in types (kvs::sstable::TableBuilder = sstc::TableBuilder
+constructed from (std::string&&, const db::Config*), AddEntry with
+db::ValueType, inputs through sstc::TableReaderIterator, the reference
+MergeIterator's std::priority_queue).  Its output files must be the
+reference's bytes -- including the equal-(key, txn) tie order, which the host
+heap reproduces."""
+import hashlib
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+from conftest import GOLDEN, ROOT, load_golden, tie_case
+from sstcodec import workload as W
+
+pytestmark = pytest.mark.gpu
+EXE = os.path.join(ROOT, "lsm-kv-storage_amd", "lib", "sstc_compact_loop")
+CASES = json.load(open(os.path.join(GOLDEN, "compaction.json")))
+
+
+def write(tmp_path, files):
+    args = []
+    for i, f in enumerate(files):
+        p = str(tmp_path / f"in{i}.sst")
+        f.tofile(p)
+        args += [p, str(f.size + 1)]
+    return args
+
+
+def run_loop(tmp_path, files, limit, base):
+    od = tmp_path / f"out{base}"
+    od.mkdir(exist_ok=True)
+    r = subprocess.run([EXE, str(od), "4096", str(limit), str(base)] + write(tmp_path, files), capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    outs = [ln.rsplit(" ", 1) for ln in r.stdout.strip().splitlines()]
+    return [(np.fromfile(p, np.uint8), int(s)) for p, s in outs]
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+@pytest.mark.parametrize("base", [1, 0])
+def test_cpp_compact_loop_matches_reference(oracle, tmp_path, name, base):
+    case = CASES[name]
+    sets = W.compaction_inputs(case["k"], case["n_per"], case["key_space"], vmax=case["vmax"],
+                               distinct=case["distinct"], **case.get("gen", {}))
+    files = [oracle.table_build(r, case["block_threshold"]) for r in sets]
+    outs = run_loop(tmp_path, files, case["table_limit"], base)
+    want = case[f"outputs_base{base}"]
+    assert len(outs) == len(want)
+    for (img, fs), w in zip(outs, want):
+        assert fs == w["file_size"] == img.size + 1
+        assert hashlib.sha256(img.tobytes()).hexdigest() == w["sha256"]
+
+
+@pytest.mark.parametrize("name", ["same", "diff"])
+@pytest.mark.parametrize("base", [1, 0])
+def test_cpp_compact_loop_ties_match_reference(tmp_path, name, base):
+    """Equal (key, txn) across inputs, identical AND differing copies: the host
+    std::priority_queue pops ties in the reference's order, so even the
+    'diff' case is the reference's bytes on this path."""
+    ins, want = tie_case(load_golden("compact_ties.npz"), name, base)
+    outs = run_loop(tmp_path, ins, 6000, base)
+    assert len(outs) == len(want)
+    for (img, fs), w in zip(outs, want):
+        assert np.array_equal(img, w) and fs == w.size + 1
+
+
+def test_cpp_block_readers_and_iterator(oracle, tmp_path):
+    """CreateAndSetupDataForBlockReader (one block per call) and the batched
+    form against the TableReaderIterator stream, record by record (DELETE ->
+    null value view, empty PUT value -> non-null view), plus Seek."""
+    rec = W.mixed_records(3000, seed=5)
+    order = np.lexsort((np.arange(3000), [bytes(rec["key_src"][int(o):int(o) + int(k)])
+                                          for o, k in zip(rec["key_off"], rec["key_len"])]))
+    rec = {k: (v[order] if v.size == 3000 else v) for k, v in rec.items()}
+    files = [oracle.table_build(rec, 4096), oracle.table_build(rec, 32768)]
+    r = subprocess.run([EXE, "--readers"] + write(tmp_path, files), capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, (r.returncode, r.stderr)
+    assert r.stdout.strip() == f"readers ok {2 * 3000}"
