@@ -183,3 +183,17 @@ def test_ties_vs_reference(codec, oracle, base):
     a = [r for o in outs for r in sst_records(oracle, o)]
     b = [r for w in want for r in sst_records(oracle, w)]
     assert same_up_to_tie_order(a, b, [sst_records(oracle, i) for i in ins])
+
+
+@pytest.mark.parametrize("base", [1, 0])
+def test_compact_many_entries_per_block(codec, oracle, base):
+    """Tiny entries (8-byte values, half DELETEs: ~85 entries per 4 KiB block),
+    so the encode copies blocks in several 64-entry rounds and the dwords at
+    round boundaries overlap the neighbouring entries' bytes."""
+    sets = W.compaction_inputs(5, 6000, 12000, seed=23, vmin=0, vmax=8, p_delete=0.5)
+    ins = [oracle.table_build(r, 4096) for r in sets]
+    want, kept = oracle.compact(ins, 4096, 90_000, base)
+    outs, res = codec.compact(ins, 4096, 90_000, base)
+    assert res.records_kept == kept and len(outs) == len(want)
+    for o, w in zip(outs, want):
+        assert np.array_equal(o, w)
