@@ -1859,6 +1859,8 @@ hipError_t launch_copy_probe(const uint8_t *src, uint8_t *dst, uint64_t n16, hip
 hipError_t launch_roundtrip(const RtArgs &a, hipStream_t s) {
   // blocks in dispatch order: the XCD-grouped order measured +3 % at config 2
   // (256 MiB, Infinity-Cache resident) but -2.5 % on 1 GiB (profiles/r01_ab_xcd.log)
+  // (persistent waves looping over blocks in one slot, and storing the staged
+  // block before the parse, were both slower: profiles/r02_ab/rt_ab.md)
   if (a.nblocks) rt_kernel<<<grid_for(a.nblocks, kRtWaves), kRtWaves * kWave, 0, s>>>(a);
   return hipGetLastError();
 }
