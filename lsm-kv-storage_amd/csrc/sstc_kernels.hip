@@ -1,4 +1,3 @@
-#include <cstdlib>
 // sstc_kernels.hip — CDNA4 (gfx950) kernels of the SST block codec.
 //
 // Kernels (each cites the reference function whose byte work it replaces):
@@ -1925,14 +1924,9 @@ hipError_t launch_enc_blocks(const uint64_t *P, const uint64_t *blk_first, uint6
 hipError_t launch_enc_emit(const EncArgs &a, hipStream_t s) {
   if (!a.nblocks) return hipSuccess;
   const uint32_t g = grid_for(a.nblocks, kEncWaves);
-  static const int var = getenv("SSTC_ENC_VARIANT") ? atoi(getenv("SSTC_ENC_VARIANT")) : 0; // A/B (temporary)
-  if (!a.entries_in_src) {
-    if (var == 1) enc_lds_kernel<0, 8, 4><<<g, kEncWaves * kWave, 0, s>>>(a);
-    else if (var == 2) enc_lds_kernel<0, 16, 2><<<g, kEncWaves * kWave, 0, s>>>(a);
-    else if (var == 3) enc_lds_kernel<0, 4, 4><<<g, kEncWaves * kWave, 0, s>>>(a);
-    else if (var == 4) enc_lds_kernel<0, 8, 8><<<g, kEncWaves * kWave, 0, s>>>(a);
-    else enc_lds_kernel<0><<<g, kEncWaves * kWave, 0, s>>>(a);
-  }
+  // G = 8 lanes per span, 2 span groups in flight: G = 16 and kQ = 4 / 8 were
+  // slower (profiles/r02_ab/encode_ab.md)
+  if (!a.entries_in_src) enc_lds_kernel<0><<<g, kEncWaves * kWave, 0, s>>>(a);
   else enc_lds_kernel<1><<<g, kEncWaves * kWave, 0, s>>>(a);
   // blocks past an LDS slot: those listed by enc_lds_kernel when a list is given
   const uint64_t cap = a.big ? 512 : 2048;
