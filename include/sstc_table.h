@@ -93,9 +93,19 @@ public:
   }
   void FlushBlock();
   void Finish();
+  /* n records from SoA arrays (val_len[i] == SSTC_NO_VALUE: no value fields),
+   * the same as n AddEntry calls */
+  void AddEntries(uint64_t n, const uint8_t *type, const uint32_t *key_len, const uint32_t *val_len,
+                  const uint64_t *txn, const uint8_t *key_src, const uint64_t *key_off, const uint8_t *val_src,
+                  const uint64_t *val_off);
 
   std::string_view GetSmallestKey() const { return table_smallest_key_; }
-  std::string_view GetLargestKey() const { return table_largest_key_; }
+  /* the last key added (a view into the builder's key arena; no string copy
+   * per AddEntry, the reference's #1 host hotspot, table_builder.cc:37-53) */
+  std::string_view GetLargestKey() const {
+    if (type_.empty()) return {};
+    return {reinterpret_cast<const char *>(keys_.data()) + key_off_.back(), key_len_.back()};
+  }
   std::string_view GetFilename() const { return filename_; }
   uint64_t GetFileSize() const { return current_offset_ + 1; } /* table_builder.cc:228 */
   uint64_t GetDataSize() const { return data_size_; }
@@ -113,7 +123,7 @@ private:
   std::vector<uint8_t> keys_, vals_;
   std::vector<uint64_t> blk_first_{0};
   uint64_t block_size_ = 0; /* sum(entry_size + 16) of the open block */
-  std::string table_smallest_key_, table_largest_key_;
+  std::string table_smallest_key_;
   uint64_t min_txn_ = UINT64_MAX, max_txn_ = 0;
   uint64_t data_size_ = 0;
   uint64_t current_offset_ = 0;

@@ -25,14 +25,6 @@ uint64_t entry_size(uint32_t klen, uint32_t vlen) {
   return 13ull + klen + (vlen != SSTC_NO_VALUE ? 4ull + vlen : 0ull); // block_builder.cc:19-21
 }
 
-void put32(std::vector<uint8_t> &b, uint32_t v) {
-  const uint8_t *p = reinterpret_cast<const uint8_t *>(&v);
-  b.insert(b.end(), p, p + 4);
-}
-void put64(std::vector<uint8_t> &b, uint64_t v) {
-  const uint8_t *p = reinterpret_cast<const uint8_t *>(&v);
-  b.insert(b.end(), p, p + 8);
-}
 uint32_t get32(const uint8_t *p) {
   uint32_t v;
   std::memcpy(&v, p, 4);
@@ -135,10 +127,50 @@ void TableBuilder::AddEntry(std::string_view key, std::string_view value, uint64
   txn_.push_back(txn_id);
   if (txn_id < min_txn_) min_txn_ = txn_id;
   if (txn_id > max_txn_) max_txn_ = txn_id;
-  table_largest_key_ = std::string(key);
   data_size_ += key.size() + (value.data() ? value.size() : 0);
   block_size_ += entry_size(key_len_.back(), val_len_.back()) + 16; // block_builder.cc:33
   if (block_size_ >= threshold_) FlushBlock();
+}
+
+void TableBuilder::AddEntries(uint64_t n, const uint8_t *type, const uint32_t *key_len, const uint32_t *val_len,
+                              const uint64_t *txn, const uint8_t *key_src, const uint64_t *key_off,
+                              const uint8_t *val_src, const uint64_t *val_off) {
+  // AddEntry's bookkeeping (table_builder.cc:35-60) in one loop: SoA appends
+  // and the running block size; keys / values appended per record
+  type_.reserve(type_.size() + n);
+  key_len_.reserve(key_len_.size() + n);
+  val_len_.reserve(val_len_.size() + n);
+  txn_.reserve(txn_.size() + n);
+  key_off_.reserve(key_off_.size() + n);
+  val_off_.reserve(val_off_.size() + n);
+  uint64_t kb = 0, vb = 0;
+  for (uint64_t i = 0; i < n; i++) {
+    kb += key_len[i];
+    vb += val_len[i] != SSTC_NO_VALUE ? val_len[i] : 0;
+  }
+  keys_.reserve(keys_.size() + kb);
+  vals_.reserve(vals_.size() + vb);
+  for (uint64_t i = 0; i < n; i++) {
+    const uint32_t kl = key_len[i], vl = val_len[i];
+    if (table_smallest_key_.empty()) table_smallest_key_.assign(reinterpret_cast<const char *>(key_src + key_off[i]), kl);
+    type_.push_back(type[i]);
+    key_len_.push_back(kl);
+    key_off_.push_back(keys_.size());
+    keys_.insert(keys_.end(), key_src + key_off[i], key_src + key_off[i] + kl);
+    if (vl != SSTC_NO_VALUE) {
+      val_off_.push_back(vals_.size());
+      vals_.insert(vals_.end(), val_src + val_off[i], val_src + val_off[i] + vl);
+    } else {
+      val_off_.push_back(0);
+    }
+    val_len_.push_back(vl);
+    txn_.push_back(txn[i]);
+    if (txn[i] < min_txn_) min_txn_ = txn[i];
+    if (txn[i] > max_txn_) max_txn_ = txn[i];
+    data_size_ += kl + (vl != SSTC_NO_VALUE ? vl : 0);
+    block_size_ += entry_size(kl, vl) + 16; // block_builder.cc:33
+    if (block_size_ >= threshold_) FlushBlock();
+  }
 }
 
 void TableBuilder::FlushBlock() {
@@ -147,6 +179,47 @@ void TableBuilder::FlushBlock() {
   block_size_ = 0;
 }
 
+namespace {
+// per-host-thread staging reused across Finish() calls (flush / compaction
+// threads each build many SSTs): one pinned host buffer and one device buffer,
+// grown when needed, so a Finish makes no allocation in steady state and its
+// copies run from / into pinned memory
+struct Staging {
+  uint8_t *host = nullptr, *dev = nullptr;
+  uint64_t host_cap = 0, dev_cap = 0;
+  ~Staging() {
+    if (host) (void)hipHostFree(host);
+    if (dev) (void)hipFree(dev);
+  }
+  uint8_t *Host(uint64_t n) {
+    if (n > host_cap) {
+      if (host) (void)hipHostFree(host);
+      host = nullptr;
+      host_cap = 0;
+      const uint64_t c = n + n / 4;
+      if (hipHostMalloc(reinterpret_cast<void **>(&host), c, hipHostMallocDefault) != hipSuccess)
+        throw std::runtime_error("hipHostMalloc failed");
+      host_cap = c;
+    }
+    return host;
+  }
+  uint8_t *Dev(uint64_t n) {
+    if (n > dev_cap) {
+      if (dev) (void)hipFree(dev);
+      dev = nullptr;
+      dev_cap = 0;
+      const uint64_t c = n + n / 4;
+      if (hipMalloc(reinterpret_cast<void **>(&dev), c) != hipSuccess) throw std::runtime_error("hipMalloc failed");
+      dev_cap = c;
+    }
+    return dev;
+  }
+};
+thread_local Staging g_stage;
+
+uint64_t align256(uint64_t x) { return (x + 255) & ~uint64_t(255); }
+} // namespace
+
 void TableBuilder::Finish() {
   if (fd_ < 0) throw std::runtime_error("TableBuilder::Finish: file not open");
   FlushBlock();
@@ -154,49 +227,66 @@ void TableBuilder::Finish() {
   const uint64_t nb = blk_first_.size() - 1;
   uint64_t data_bytes = 16 * nb + 16 * n;
   for (uint64_t i = 0; i < n; i++) data_bytes += entry_size(key_len_[i], val_len_[i]);
-
-  std::vector<uint8_t> file(data_bytes);
+  uint64_t meta_bytes = 0;
+  for (uint64_t b = 0; b < nb; b++) meta_bytes += 24 + key_len_[blk_first_[b]] + key_len_[blk_first_[b + 1] - 1];
+  const uint64_t file_bytes = data_bytes + meta_bytes + 40;
+  if (keys_.empty()) keys_.push_back(0);
+  if (vals_.empty()) vals_.push_back(0);
+  // input image (SoA + arenas + block starts) packed at 256 B boundaries
+  const uint64_t o_type = 0, o_kl = align256(o_type + n), o_vl = align256(o_kl + 4 * n),
+                 o_txn = align256(o_vl + 4 * n), o_ko = align256(o_txn + 8 * n), o_vo = align256(o_ko + 8 * n),
+                 o_first = align256(o_vo + 8 * n), o_keys = align256(o_first + 8 * (nb + 1)),
+                 o_vals = align256(o_keys + keys_.size()), in_bytes = align256(o_vals + vals_.size());
+  const uint64_t o_dst = in_bytes, o_off = align256(o_dst + data_bytes), o_len = align256(o_off + 8 * (nb + 1)),
+                 dev_bytes = align256(o_len + 8 * nb + 8);
+  uint8_t *h = g_stage.Host(std::max(in_bytes, file_bytes) + 16 * nb + 16);
   std::vector<uint64_t> blk_off(nb + 1), blk_len(nb);
   if (nb) {
-    if (keys_.empty()) keys_.push_back(0);
-    if (vals_.empty()) vals_.push_back(0);
-    DevBuf d_type = upload(type_), d_kl = upload(key_len_), d_vl = upload(val_len_), d_txn = upload(txn_),
-           d_ko = upload(key_off_), d_vo = upload(val_off_), d_keys = upload(keys_), d_vals = upload(vals_),
-           d_first = upload(blk_first_);
-    DevBuf d_dst(data_bytes), d_off((nb + 1) * 8), d_len(nb * 8);
-    sstc_records rec{d_type.as<uint8_t>(), d_kl.as<uint32_t>(), d_vl.as<uint32_t>(),
-                     d_txn.as<uint64_t>(), d_ko.as<uint64_t>(), d_vo.as<uint64_t>()};
-    check(sstc_encode_blocks(ctx_, d_keys.as<uint8_t>(), d_vals.as<uint8_t>(), rec, n, d_first.as<uint64_t>(), nb,
-                             0, d_dst.as<uint8_t>(), d_off.as<uint64_t>(), d_len.as<uint64_t>()),
+    std::memcpy(h + o_type, type_.data(), n);
+    std::memcpy(h + o_kl, key_len_.data(), 4 * n);
+    std::memcpy(h + o_vl, val_len_.data(), 4 * n);
+    std::memcpy(h + o_txn, txn_.data(), 8 * n);
+    std::memcpy(h + o_ko, key_off_.data(), 8 * n);
+    std::memcpy(h + o_vo, val_off_.data(), 8 * n);
+    std::memcpy(h + o_first, blk_first_.data(), 8 * (nb + 1));
+    std::memcpy(h + o_keys, keys_.data(), keys_.size());
+    std::memcpy(h + o_vals, vals_.data(), vals_.size());
+    uint8_t *d = g_stage.Dev(dev_bytes);
+    if (hipMemcpy(d, h, in_bytes, hipMemcpyHostToDevice) != hipSuccess) throw std::runtime_error("hipMemcpy H2D failed");
+    sstc_records rec{d + o_type, reinterpret_cast<uint32_t *>(d + o_kl), reinterpret_cast<uint32_t *>(d + o_vl),
+                     reinterpret_cast<uint64_t *>(d + o_txn), reinterpret_cast<uint64_t *>(d + o_ko),
+                     reinterpret_cast<uint64_t *>(d + o_vo)};
+    check(sstc_encode_blocks(ctx_, d + o_keys, d + o_vals, rec, n, reinterpret_cast<uint64_t *>(d + o_first), nb, 0,
+                             d + o_dst, reinterpret_cast<uint64_t *>(d + o_off), reinterpret_cast<uint64_t *>(d + o_len)),
           "sstc_encode_blocks");
     uint64_t errs = 0;
     check(sstc_ctx_error_count(ctx_, &errs), "sstc_ctx_error_count"); // synchronises the stream
-    if (hipMemcpy(file.data(), d_dst.p, data_bytes, hipMemcpyDeviceToHost) != hipSuccess ||
-        hipMemcpy(blk_off.data(), d_off.p, (nb + 1) * 8, hipMemcpyDeviceToHost) != hipSuccess ||
-        hipMemcpy(blk_len.data(), d_len.p, nb * 8, hipMemcpyDeviceToHost) != hipSuccess)
+    // blocks straight into the file image, the block index beside it
+    if (hipMemcpy(h, d + o_dst, data_bytes, hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(blk_off.data(), d + o_off, (nb + 1) * 8, hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(blk_len.data(), d + o_len, nb * 8, hipMemcpyDeviceToHost) != hipSuccess)
       throw std::runtime_error("hipMemcpy D2H failed");
   }
-  // meta section: one entry per block (table_builder.cc:101-145)
-  const uint64_t meta_off = data_bytes;
+  // meta section: one entry per block (table_builder.cc:101-145), then the
+  // footer (table_builder.cc:179-211), appended to the file image in place
+  uint8_t *w = h + data_bytes;
+  auto put = [&w](const void *p, uint64_t len) {
+    std::memcpy(w, p, len);
+    w += len;
+  };
   for (uint64_t b = 0; b < nb; b++) {
     const uint64_t f = blk_first_[b], l = blk_first_[b + 1] - 1;
-    put32(file, key_len_[f]);
-    file.insert(file.end(), keys_.begin() + key_off_[f], keys_.begin() + key_off_[f] + key_len_[f]);
-    put32(file, key_len_[l]);
-    file.insert(file.end(), keys_.begin() + key_off_[l], keys_.begin() + key_off_[l] + key_len_[l]);
-    put64(file, blk_off[b]);
-    put64(file, blk_len[b]);
+    put(&key_len_[f], 4);
+    put(keys_.data() + key_off_[f], key_len_[f]);
+    put(&key_len_[l], 4);
+    put(keys_.data() + key_off_[l], key_len_[l]);
+    put(&blk_off[b], 8);
+    put(&blk_len[b], 8);
   }
-  const uint64_t meta_len = file.size() - meta_off;
-  // footer (table_builder.cc:179-211)
-  put64(file, nb);
-  put64(file, meta_off);
-  put64(file, meta_len);
-  put64(file, min_txn_);
-  put64(file, max_txn_);
-  if (!pwrite_all(fd_, file.data(), file.size(), 0))
-    throw std::runtime_error("Error when flushing sstable"); // table_builder.cc:155-170
-  current_offset_ = file.size();
+  const uint64_t meta_off = data_bytes, foot[5] = {nb, meta_off, meta_bytes, min_txn_, max_txn_};
+  put(foot, 40);
+  if (!pwrite_all(fd_, h, file_bytes, 0)) throw std::runtime_error("Error when flushing sstable"); // table_builder.cc:155-170
+  current_offset_ = file_bytes;
   if (::fsync(fd_) < 0) throw std::runtime_error("fsync failed");
 }
 
@@ -438,15 +528,8 @@ int sstc_tb_add(sstc_table_builder *tb, const uint8_t *key, uint32_t key_len, co
 int sstc_tb_add_batch(sstc_table_builder *tb, uint64_t n, const uint8_t *type, const uint32_t *key_len,
                       const uint32_t *val_len, const uint64_t *txn, const uint8_t *key_src,
                       const uint64_t *key_off, const uint8_t *val_src, const uint64_t *val_off) {
-  if (!tb) return SSTC_E_INVALID_ARG;
-  static const char kEmpty[1] = {0};
-  for (uint64_t i = 0; i < n; i++) {
-    std::string_view k(key_len[i] ? reinterpret_cast<const char *>(key_src + key_off[i]) : kEmpty, key_len[i]);
-    std::string_view v;
-    if (val_len[i] != SSTC_NO_VALUE)
-      v = std::string_view(val_len[i] ? reinterpret_cast<const char *>(val_src + val_off[i]) : kEmpty, val_len[i]);
-    tb->tb.AddEntry(k, v, txn[i], type[i]);
-  }
+  if (!tb || (n && (!type || !key_len || !val_len || !txn || !key_off || !val_off))) return SSTC_E_INVALID_ARG;
+  tb->tb.AddEntries(n, type, key_len, val_len, txn, key_src, key_off, val_src, val_off);
   return SSTC_OK;
 }
 
