@@ -4,7 +4,15 @@
 
 Outputs go to lsm-kv-storage_amd/lib/ (git-ignored, shipped to the GPU box with
 the repo snapshot).  hipcc cross-compiles for gfx950 without a GPU.
+
+Rebuilds are decided by CONTENT, not mtime: every output records the SHA-256
+of the sources and headers it was built from in lib/build_info.json, and an
+output whose recorded inputs differ from the tree's is rebuilt.  The same
+file is the provenance record (`tests/test_abi.py` checks it matches the tree,
+so a stale prebuilt library cannot pass silently).
 """
+import hashlib
+import json
 import os
 import shutil
 import subprocess
@@ -27,15 +35,64 @@ def _hipcc():
     raise RuntimeError("hipcc not found: the codec has no CPU build")
 
 
+INFO = os.path.join(LIB, "build_info.json")
+
+
+def _sha(path):
+    with open(path, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
+
+
+def _load_info():
+    try:
+        with open(INFO) as f:
+            return json.load(f)
+    except (OSError, ValueError):
+        return {}
+
+
+_info = {}
+_state = {"changed": False}
+
+
 def _newer(target, deps):
-    if not os.path.exists(target):
-        return True
-    t = os.path.getmtime(target)
-    return any(os.path.getmtime(d) > t for d in deps)
+    """True when `target` is missing or was built from other contents of `deps`
+    (recorded in build_info.json); records the new input hashes."""
+    key = os.path.relpath(target, ROOT)
+    want = {os.path.relpath(d, ROOT): _sha(d) for d in deps if os.path.exists(d)}
+    stale = not os.path.exists(target) or _info.get(key, {}).get("inputs") != want
+    if stale:
+        _info[key] = {"inputs": want}
+        _state["changed"] = True
+    return stale
+
+
+def tree_matches_build():
+    """(ok, mismatches): every recorded output exists and its recorded inputs
+    equal the tree's current contents."""
+    info = _load_info()
+    bad = []
+    for out, rec in info.items():
+        if out == "toolchain" or "/obj/" in out:  # objects do not travel to the GPU box
+            continue
+        if not os.path.exists(os.path.join(ROOT, out)):
+            bad.append(out)
+            continue
+        deps = rec.get("sources", rec.get("inputs", {}))
+        for src, h in deps.items():
+            if "/obj/" in src:
+                continue
+            p = os.path.join(ROOT, src)
+            if not os.path.exists(p) or _sha(p) != h:
+                bad.append(f"{out} <- {src}")
+    return (bool(info) and not bad), bad
 
 
 def build(verbose=False):
     os.makedirs(os.path.join(LIB, "obj"), exist_ok=True)
+    _info.clear()
+    _info.update(_load_info())
+    _state["changed"] = False
     hipcc = _hipcc()
     headers = [os.path.join(CSRC, h) for h in ("sstc_device.h", "sstc_launch.h")]
     headers.append(os.path.join(ROOT, "include", "sstcodec.h"))
@@ -65,6 +122,8 @@ def build(verbose=False):
             subprocess.run(cmd, check=True)
         objs.append(o)
     so = os.path.join(LIB, "libsstcodec.so")
+    srcs = [os.path.join(CSRC, x) for x in HIP_SOURCES + HOST_SOURCES] + headers + \
+        [h for h in host_headers if os.path.exists(h)]
     if _newer(so, objs):
         cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", so] + objs
         if verbose:
@@ -80,6 +139,13 @@ def build(verbose=False):
         if verbose:
             print(" ".join(cmd))
         subprocess.run(cmd, check=True)
+    # provenance of what ships (lib/obj stays behind): the sources behind the library
+    _info[os.path.relpath(so, ROOT)]["sources"] = {os.path.relpath(x, ROOT): _sha(x) for x in srcs if os.path.exists(x)}
+    if _state["changed"] or "toolchain" not in _info:
+        ver = subprocess.run([hipcc, "--version"], capture_output=True, text=True).stdout.strip().splitlines()
+        _info["toolchain"] = {"hipcc": ver[0] if ver else "", "arch": ARCH}
+    with open(INFO, "w") as f:
+        json.dump(_info, f, indent=1, sort_keys=True)
     return so
 
 
