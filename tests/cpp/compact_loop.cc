@@ -13,7 +13,7 @@
 //
 //   sstc_compact_loop out_dir block_size table_limit base_level [file size]...
 //
-// prints "path GetFileSize()" per output, like oracle/_ref/ref_compact.
+// prints "path smallest_key_hex largest_key_hex GetFileSize()" per output.
 //
 //   sstc_compact_loop --readers [file size]...
 //
@@ -157,8 +157,18 @@ int main(int argc, char **argv) {
 
     uint64_t next_id = 0;
     auto new_name = [&] { return out_dir + "/" + std::to_string(next_id++) + ".sst"; };
-    auto report = [](sstable::TableBuilder &t) {
-      std::printf("%s %llu\n", std::string(t.GetFilename()).c_str(), static_cast<unsigned long long>(t.GetFileSize()));
+    auto hex = [](std::string_view k) {
+      std::string h;
+      for (unsigned char c : k) {
+        char b[3];
+        std::snprintf(b, sizeof b, "%02x", c);
+        h += b;
+      }
+      return h.empty() ? std::string("-") : h;
+    };
+    auto report = [&](sstable::TableBuilder &t) { // what VersionEdit::AddNewFiles records (compact.cc:292-297)
+      std::printf("%s %s %s %llu\n", std::string(t.GetFilename()).c_str(), hex(t.GetSmallestKey()).c_str(),
+                  hex(t.GetLargestKey()).c_str(), static_cast<unsigned long long>(t.GetFileSize()));
     };
     // ---- db/compact.cc:232-322, the loop body as the reference writes it
     std::string filename = new_name();

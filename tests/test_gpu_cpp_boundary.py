@@ -15,6 +15,7 @@ import subprocess
 import numpy as np
 import pytest
 from conftest import GOLDEN, ROOT, load_golden, tie_case
+from test_gpu_files import first_last_key
 from sstcodec import workload as W
 
 pytestmark = pytest.mark.gpu
@@ -37,8 +38,16 @@ def run_loop(tmp_path, files, limit, base):
     r = subprocess.run([EXE, str(od), "4096", str(limit), str(base)] + write(tmp_path, files), capture_output=True,
                        text=True, timeout=120)
     assert r.returncode == 0, r.stderr
-    outs = [ln.rsplit(" ", 1) for ln in r.stdout.strip().splitlines()]
-    return [(np.fromfile(p, np.uint8), int(s)) for p, s in outs]
+    outs = []
+    for ln in r.stdout.strip().splitlines():
+        p, lo, hi, s = ln.split(" ")
+        img = np.fromfile(p, np.uint8)
+        # GetSmallestKey / GetLargestKey (what AddNewFiles records) = first / last key of the file
+        want_lo, want_hi = first_last_key(img)
+        assert (bytes.fromhex(lo) if lo != "-" else b"") == want_lo
+        assert (bytes.fromhex(hi) if hi != "-" else b"") == want_hi
+        outs.append((img, int(s)))
+    return outs
 
 
 @pytest.mark.parametrize("name", sorted(CASES))
