@@ -1032,110 +1032,108 @@ __device__ __forceinline__ void emit_chunk_clip(uint8_t *img, uint32_t *dummy, u
   put_dw(img, dummy, y + 12, __builtin_amdgcn_alignbyte(nxt, v.w, r0), lo, hi);
 }
 
-// Records -> block image (sstc_encode_blocks: keys and values in two arenas).
-// Every record is two spans, its key (image offset o + 5) and its value (o + 9
-// + klen); a round takes 32 records = 64 spans, one per owner lane.  Spans are
-// copied by groups of G lanes, 64 / G spans per wave instruction: lane g of a
-// group loads the ALIGNED 16 B source chunk g (chunks g + G, g + 2G, ... in
-// further rounds), funnel-shifts it with the first dword of chunk g + 1 (from
-// its right neighbour; the group's last lane loads it) into dword-aligned LDS
-// stores, and clips the dwords at the span's ends to byte stores, so the
-// loads are 16 B per lane and coalesced per span instead of a lane walking a
-// record's bytes.  Every load of a round is issued before its first store:
-// the record fields (lane per span owner and lane per record), then kQ span
-// groups at a time (kQ wide loads in flight per lane).  The lane per record
-// writes the header fields, the txn and the offset entry
-// (block_builder.cc:36-93), whose bytes are disjoint from the spans'.
+// One pass of span copies into a block image (enc_copy_split).  Owner lane
+// i < nspan holds span i = (offset into `base`, length, image position).
+// Spans are copied by groups of G lanes, 64 / G spans per wave instruction:
+// lane g of a group loads the ALIGNED 16 B source chunk g (chunks g + G,
+// g + 2G, ... in further rounds, only when some span needs them), funnel-
+// shifts it with the first dword of chunk g + 1 (its right neighbour's, by a
+// width-64 shuffle; the group's last lane loads it) into dword-aligned LDS
+// stores (emit_chunk_clip), so the loads are 16 B per lane and coalesced per
+// span.  kQ span groups are loaded before any is stored.
 template <uint32_t G, uint32_t kQ>
-__device__ __forceinline__ void enc_copy_fields(const EncArgs &a, uint8_t *img, uint32_t *dummy, uint32_t pad,
-                                                uint64_t f0, uint32_t n, uint64_t P0, uint32_t D) {
-  constexpr uint32_t kS = kWave / G; // spans per wave instruction
+__device__ __forceinline__ void copy_spans(const uint8_t *base, uint8_t *img, uint32_t *dummy, uint32_t nspan,
+                                           uint64_t my_off, uint32_t my_len, uint32_t my_ds, const u32x4 *safe) {
+  constexpr uint32_t kS = kWave / G;
   const uint32_t lane = lane_id();
   const uint32_t g = lane % G, sub = lane / G;
-  uint8_t *im = img + pad;
-  for (uint32_t c0 = 0; c0 < n; c0 += kWave / 2) {
-    const uint32_t nc = n - c0 < kWave / 2 ? n - c0 : kWave / 2;
-    const uint32_t ns = 2 * nc;
-    // span owner: lane 2i = key of record c0 + i, lane 2i + 1 = its value;
-    // record lane: lane i < nc holds record c0 + i's header fields
-    const uint32_t ri = lane < ns ? lane >> 1 : 0u, hi_ = lane < nc ? lane : 0u;
-    const uint64_t rs = f0 + c0 + ri, rh = f0 + c0 + hi_;
-    const uint64_t ps = a.P[rs], ph = a.P[rh], ph1 = a.P[rh + 1];
-    const uint32_t kls = a.in.key_len[rs], vls = a.in.val_len[rs];
-    const uint64_t kos = a.in.key_off[rs], vos = a.in.val_off[rs];
-    const uint32_t klh = a.in.key_len[rh], vlh = a.in.val_len[rh], tyh = a.in.type[rh];
-    const uint64_t txh = a.in.txn[rh];
-    // span of this owner lane (selects, no branches; lanes >= ns own empty spans)
-    const bool is_key = (lane & 1u) == 0;
-    const uint32_t o_s = static_cast<uint32_t>(ps - P0);
-    const uint32_t vlen_s = vls != kNoValue ? vls : 0u;
-    const uint32_t my_len = lane < ns ? (is_key ? kls : vlen_s) : 0u;
-    const uint64_t my_src = is_key ? reinterpret_cast<uint64_t>(a.key_src + kos)
-                                   : (vlen_s ? reinterpret_cast<uint64_t>(a.val_src + vos) : 0ull);
-    const uint32_t my_ds = pad + o_s + (is_key ? 5u : 9u + kls);
-    const uint32_t my_nch = my_len ? ((static_cast<uint32_t>(my_src & 15u) + my_len + 15u) >> 4) : 0u;
-    const bool longs = __any(my_nch > G); // wave-uniform: some span needs more than one round of chunks
-    const u32x4 *safe = reinterpret_cast<const u32x4 *>(a.P); // a valid address for masked-off loads
-    for (uint32_t p0 = 0; p0 < ns; p0 += kS * kQ) {
-      u32x4 v[kQ];
-      const uint8_t *sp_[kQ];
-      uint32_t len_[kQ], ds_[kQ];
+  const uintptr_t my_addr = reinterpret_cast<uintptr_t>(base + my_off);
+  const uint32_t my_nch = my_len ? ((static_cast<uint32_t>(my_addr & 15u) + my_len + 15u) >> 4) : 0u;
+  const bool longs = __any(my_nch > G); // wave-uniform
+  const int32_t no = -(1 << 30);
+  for (uint32_t p0 = 0; p0 < nspan; p0 += kS * kQ) {
+    u32x4 v[kQ];
+    const uint8_t *sp_[kQ];
+    uint32_t len_[kQ], ds_[kQ];
 #pragma unroll
-      for (uint32_t q = 0; q < kQ; q++) {
-        const uint32_t i = p0 + q * kS + sub;
-        const int sl = static_cast<int>(i & 63u);
-        const uint32_t slo = __shfl(static_cast<uint32_t>(my_src), sl, kWave);
-        const uint32_t shi = __shfl(static_cast<uint32_t>(my_src >> 32), sl, kWave);
-        const uint32_t len = __shfl(my_len, sl, kWave); // 0 for i >= ns (owner lane >= ns)
-        ds_[q] = __shfl(my_ds, sl, kWave);
-        sp_[q] = reinterpret_cast<const uint8_t *>((static_cast<uint64_t>(shi) << 32) | slo);
-        len_[q] = len;
-        const uint32_t mis = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(sp_[q]) & 15u);
-        const uint32_t nch = len ? (mis + len + 15u) >> 4 : 0u;
-        v[q] = *(g < nch ? reinterpret_cast<const u32x4 *>(sp_[q] - mis + 16 * g) : safe);
-      }
+    for (uint32_t q = 0; q < kQ; q++) {
+      const uint32_t i = p0 + q * kS + sub;
+      const int sl = static_cast<int>(i & 63u);
+      const uint32_t olo = __shfl(static_cast<uint32_t>(my_off), sl, kWave);
+      const uint32_t ohi = __shfl(static_cast<uint32_t>(my_off >> 32), sl, kWave);
+      len_[q] = __shfl(my_len, sl, kWave); // 0 for owners >= nspan
+      ds_[q] = __shfl(my_ds, sl, kWave);
+      sp_[q] = base + ((static_cast<uint64_t>(ohi) << 32) | olo);
+      const uint32_t mis = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(sp_[q]) & 15u);
+      const uint32_t nch = len_[q] ? (mis + len_[q] + 15u) >> 4 : 0u;
+      v[q] = *(g < nch ? reinterpret_cast<const u32x4 *>(sp_[q] - mis + 16 * g) : safe);
+    }
 #pragma unroll
-      for (uint32_t q = 0; q < kQ; q++) {
-        const uint32_t mis = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(sp_[q]) & 15u);
-        const uint32_t len = len_[q], ds = ds_[q];
-        const uint32_t nch = len ? (mis + len + 15u) >> 4 : 0u;
-        const uint8_t *A = sp_[q] - mis;
-        const uint32_t r0 = (mis - ds) & 3u;
-        const int32_t y = static_cast<int32_t>(ds) - static_cast<int32_t>(mis) + static_cast<int32_t>(r0);
-        const int32_t lo = static_cast<int32_t>(ds), hi = static_cast<int32_t>(ds + len);
-        // round 0, branch-free: chunk g; lanes past the span's chunks store to the sink
-        uint32_t nx = __shfl_down(v[q].x, 1u, G);
-        if (longs && g == G - 1) nx = G < nch ? *reinterpret_cast<const uint32_t *>(A + 16 * G) : 0u;
-        const int32_t no = -(1 << 30); // empty interval: every store of the lane goes to the sink
-        emit_chunk_clip(img, dummy, v[q], nx, r0, y + 16 * static_cast<int32_t>(g), g < nch ? lo : no,
-                        g < nch ? hi : no, g == 0);
-        if (longs) { // further rounds (spans longer than G chunks)
-          for (uint32_t c = g + G; c - g < nch; c += G) {
-            const u32x4 w = c < nch ? *reinterpret_cast<const u32x4 *>(A + 16 * c) : u32x4{0u, 0u, 0u, 0u};
-            uint32_t nx2 = __shfl_down(w.x, 1u, G);
-            if (g == G - 1) nx2 = c + 1 < nch ? *reinterpret_cast<const uint32_t *>(A + 16 * (c + 1)) : 0u;
-            if (c < nch) emit_chunk_clip(img, dummy, w, nx2, r0, y + 16 * static_cast<int32_t>(c), lo, hi, false);
-          }
+    for (uint32_t q = 0; q < kQ; q++) {
+      const uint32_t mis = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(sp_[q]) & 15u);
+      const uint32_t len = len_[q], ds = ds_[q];
+      const uint32_t nch = len ? (mis + len + 15u) >> 4 : 0u;
+      const uint8_t *A = sp_[q] - mis;
+      const uint32_t r0 = (mis - ds) & 3u;
+      const int32_t y = static_cast<int32_t>(ds) - static_cast<int32_t>(mis) + static_cast<int32_t>(r0);
+      const int32_t lo = static_cast<int32_t>(ds), hi = static_cast<int32_t>(ds + len);
+      uint32_t nx = __shfl_down(v[q].x, 1u, kWave);
+      if (g == G - 1) nx = 0u;
+      if (longs && g == G - 1) nx = G < nch ? *reinterpret_cast<const uint32_t *>(A + 16 * G) : 0u;
+      emit_chunk_clip(img, dummy, v[q], nx, r0, y + 16 * static_cast<int32_t>(g), g < nch ? lo : no,
+                      g < nch ? hi : no, g == 0);
+      if (longs) {
+        for (uint32_t c = g + G; c - g < nch; c += G) {
+          const u32x4 w = c < nch ? *reinterpret_cast<const u32x4 *>(A + 16 * c) : u32x4{0u, 0u, 0u, 0u};
+          uint32_t nx2 = __shfl_down(w.x, 1u, kWave);
+          if (g == G - 1) nx2 = c + 1 < nch ? *reinterpret_cast<const uint32_t *>(A + 16 * (c + 1)) : 0u;
+          if (c < nch) emit_chunk_clip(img, dummy, w, nx2, r0, y + 16 * static_cast<int32_t>(c), lo, hi, false);
         }
       }
     }
-    if (lane < nc) { // header fields, txn, offset entry of record c0 + lane (after the spans)
-      const uint32_t o = static_cast<uint32_t>(ph - P0), sz = static_cast<uint32_t>(ph1 - ph);
-      im[o] = static_cast<uint8_t>(tyh);
+  }
+}
+
+// Records -> block image with the keys and the values in two passes of span
+// copies, each with its own group size: GK lanes per key (2: a 16 B key is one
+// or two chunks, 32 keys per wave instruction), GV per value (8: a 100 B value
+// is 7-8 chunks).  A round takes 64 records; the lane per record then writes
+// the header fields, txn and offset entry (block_builder.cc:36-93).
+template <uint32_t GK, uint32_t GV, uint32_t kQ>
+__device__ __forceinline__ void enc_copy_split(const EncArgs &a, uint8_t *img, uint32_t *dummy, uint32_t pad,
+                                               uint64_t f0, uint32_t n, uint64_t P0, uint32_t D) {
+  const uint32_t lane = lane_id();
+  uint8_t *im = img + pad;
+  const u32x4 *safe = reinterpret_cast<const u32x4 *>(a.P); // a valid address for masked-off loads
+  for (uint32_t c0 = 0; c0 < n; c0 += kWave) {
+    const uint32_t nc = n - c0 < kWave ? n - c0 : kWave;
+    const uint64_t r = f0 + c0 + (lane < nc ? lane : 0u);
+    const uint64_t pr = a.P[r], pr1 = a.P[r + 1];
+    const uint32_t kl = a.in.key_len[r], vl = a.in.val_len[r], ty = a.in.type[r];
+    const uint64_t ko = a.in.key_off[r], vo = a.in.val_off[r], tx = a.in.txn[r];
+    const uint32_t o = static_cast<uint32_t>(pr - P0), sz = static_cast<uint32_t>(pr1 - pr);
+    const bool on = lane < nc;
+    copy_spans<GK, kQ>(a.key_src, img, dummy, nc, ko, on ? kl : 0u, pad + o + 5, safe);
+    const uint32_t vlen = on && vl != kNoValue ? vl : 0u;
+    copy_spans<GV, kQ>(a.val_src, img, dummy, nc, vlen ? vo : 0ull, vlen, pad + o + 9 + kl, safe);
+    if (on) { // header fields, txn, offset entry (after both span passes)
+      im[o] = static_cast<uint8_t>(ty);
 #pragma unroll
-      for (int j = 0; j < 4; j++) im[o + 1 + j] = static_cast<uint8_t>(klh >> (8 * j));
-      uint8_t *vp = vlh != kNoValue ? im + o + 5 + klh : reinterpret_cast<uint8_t *>(dummy);
+      for (int j = 0; j < 4; j++) im[o + 1 + j] = static_cast<uint8_t>(kl >> (8 * j));
+      uint8_t *vp = vl != kNoValue ? im + o + 5 + kl : reinterpret_cast<uint8_t *>(dummy);
 #pragma unroll
-      for (int j = 0; j < 4; j++) vp[j] = static_cast<uint8_t>(vlh >> (8 * j));
+      for (int j = 0; j < 4; j++) vp[j] = static_cast<uint8_t>(vl >> (8 * j));
 #pragma unroll
-      for (int j = 0; j < 8; j++) im[o + sz - 8 + j] = static_cast<uint8_t>(txh >> (8 * j));
+      for (int j = 0; j < 8; j++) im[o + sz - 8 + j] = static_cast<uint8_t>(tx >> (8 * j));
       lds_st_u64u(im, D + 16 * (c0 + lane), o); // D & 3 is wave-uniform
       lds_st_u64u(im, D + 16 * (c0 + lane) + 8, sz);
     }
   }
 }
 
-template <uint32_t kMode, uint32_t G = 8, uint32_t kQ = 2> // 0: two arenas (key / value spans), 1: whole-entry copy (compaction)
+// kMode 0: two arenas (key spans in groups of GK lanes, then value spans in
+// groups of GV, kQ span groups in flight); 1: whole-entry copy (compaction)
+template <uint32_t kMode, uint32_t GK = 2, uint32_t GV = 8, uint32_t kQ = 2>
 __global__ __launch_bounds__(kEncWaves *kWave) void enc_lds_kernel(EncArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kEncSlotWaves * kEncSlot];
   __shared__ uint32_t s_dummy[kMode == 0 ? kEncWaves * kWave : 1]; // per-lane sink of clipped stores
@@ -1162,7 +1160,7 @@ __global__ __launch_bounds__(kEncWaves *kWave) void enc_lds_kernel(EncArgs a) {
   if constexpr (kMode == 1) {
     enc_copy_entries<4>(a, img, pad, f0, n, P0, D, b);
   } else {
-    enc_copy_fields<G, kQ>(a, img, s_dummy + threadIdx.x, pad, f0, n, P0, D);
+    enc_copy_split<GK, GV, kQ>(a, img, s_dummy + threadIdx.x, pad, f0, n, P0, D);
   }
   if (lane == 0) {
     lds_st_u64u(im, D + 16 * n, n);
@@ -1926,6 +1924,9 @@ hipError_t launch_enc_emit(const EncArgs &a, hipStream_t s) {
   const uint32_t g = grid_for(a.nblocks, kEncWaves);
   // G = 8 lanes per span, 2 span groups in flight: G = 16 and kQ = 4 / 8 were
   // slower (profiles/r02_ab/encode_ab.md)
+  // keys in 2-lane groups, values in 8-lane groups, 2 span groups in flight:
+  // (4, 8, 2) / (2, 8, 1) / (4, 8, 4) / (2, 8, 4) and the single pass over
+  // (key, value) span pairs were slower (profiles/r02_ab/encode_ab.md)
   if (!a.entries_in_src) enc_lds_kernel<0><<<g, kEncWaves * kWave, 0, s>>>(a);
   else enc_lds_kernel<1><<<g, kEncWaves * kWave, 0, s>>>(a);
   // blocks past an LDS slot: those listed by enc_lds_kernel when a list is given
