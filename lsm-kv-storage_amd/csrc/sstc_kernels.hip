@@ -1025,11 +1025,22 @@ __device__ __forceinline__ void put_dw(uint8_t *img, uint32_t *dummy, int32_t yy
 
 __device__ __forceinline__ void emit_chunk_clip(uint8_t *img, uint32_t *dummy, u32x4 v, uint32_t nxt, uint32_t r0,
                                                 int32_t y, int32_t lo, int32_t hi, bool first) {
-  put_dw(img, dummy, first ? y - 4 : -64, __builtin_amdgcn_alignbyte(v.x, 0u, r0), lo, hi);
-  put_dw(img, dummy, y, __builtin_amdgcn_alignbyte(v.y, v.x, r0), lo, hi);
-  put_dw(img, dummy, y + 4, __builtin_amdgcn_alignbyte(v.z, v.y, r0), lo, hi);
-  put_dw(img, dummy, y + 8, __builtin_amdgcn_alignbyte(v.w, v.z, r0), lo, hi);
-  put_dw(img, dummy, y + 12, __builtin_amdgcn_alignbyte(nxt, v.w, r0), lo, hi);
+  // dword k = 0..4 at image position y - 4 + 4k (k = 0: chunk 0's extra dword)
+  // meets [lo, hi) iff 0 <= (y - 4 + 4k) - lo + 3 < hi - lo + 3 (one unsigned
+  // compare); a dword that does not goes to the sink, addressed so that the
+  // store's constant offset 4k lands on it
+  const uint32_t t = static_cast<uint32_t>(y - lo - 1), span = static_cast<uint32_t>(hi - lo + 3);
+  uint8_t *b = img + y - 4;
+  uint8_t *sink = reinterpret_cast<uint8_t *>(dummy);
+  const uint32_t d[5] = {__builtin_amdgcn_alignbyte(v.x, 0u, r0), __builtin_amdgcn_alignbyte(v.y, v.x, r0),
+                         __builtin_amdgcn_alignbyte(v.z, v.y, r0), __builtin_amdgcn_alignbyte(v.w, v.z, r0),
+                         __builtin_amdgcn_alignbyte(nxt, v.w, r0)};
+#pragma unroll
+  for (uint32_t k = 0; k < 5; k++) {
+    const bool ok = (k > 0 || first) && t + 4 * k < span;
+    uint8_t *p = ok ? b : sink - 4 * k;
+    *reinterpret_cast<uint32_t *>(p + 4 * k) = d[k];
+  }
 }
 
 // One pass of span copies into a block image (enc_copy_split).  Owner lane
