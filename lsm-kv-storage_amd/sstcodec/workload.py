@@ -252,3 +252,19 @@ def cross_duplicate_inputs(k, n_per, key_space, seed=5, p_shared=0.5, p_delete=0
                     "val_off": np.where(typ == TYPE_DELETED, 0, val_off).astype(np.uint64),
                     "key_src": fixed_keys(idx.astype(np.uint64), key_width), "val_src": val_src})
     return out
+
+
+def config3_lookup_queries(n, seed=7, ssts=8, keys=1_000_000):
+    """Point-lookup queries over the config-3 SSTs (SST s holds k%015d of
+    i*ssts+s): (table per query, key index per query).  Half are present in
+    their table, a quarter belong to another table (absent here), the rest
+    lie past the last key or between keys' ranges of other sizes."""
+    rng = np.random.default_rng(seed)
+    t = rng.integers(0, ssts, n).astype(np.uint32)
+    kind = rng.random(n)
+    i = rng.integers(0, keys, n).astype(np.uint64)
+    own = i * np.uint64(ssts) + t.astype(np.uint64)
+    other = i * np.uint64(ssts) + ((t.astype(np.uint64) + np.uint64(1)) % np.uint64(ssts))
+    past = np.uint64(ssts * keys) + rng.integers(0, 1000, n).astype(np.uint64)
+    k = np.where(kind < 0.5, own, np.where(kind < 0.75, other, past))
+    return t, k

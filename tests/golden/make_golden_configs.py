@@ -76,16 +76,45 @@ def make_case(ref, name, gen, td):
     return case
 
 
+def lookup_case(ref, td, nq=40000):
+    """TableReader::GetValue of the reference over the 8 config-3 SSTs for
+    nq seeded queries (workload.config3_lookup_queries): per query the type,
+    the value length, and one SHA-256 over all returned values in query order."""
+    import numpy as np
+    sets = W.config_inputs(3)
+    paths = []
+    for i, rec in enumerate(sets):
+        p = os.path.join(td, f"in{i}.sst")
+        paths.append((p, ref.table_build(p, rec, 4096)))
+    del sets
+    qt, qk = W.config3_lookup_queries(nq)
+    keys = W.fixed_keys(qk).reshape(-1, 16)
+    types = np.zeros(nq, np.uint32)
+    vlens = np.zeros(nq, np.uint32)
+    vals = [b""] * nq
+    for t, (p, fs) in enumerate(paths):
+        sel = np.flatnonzero(qt == t)
+        ty, vv = ref.table_get(p, fs, [bytes(keys[j]) for j in sel])
+        for j, a, v in zip(sel, ty, vv):
+            types[j] = a
+            vals[j] = v if v is not None else b""
+            vlens[j] = len(vals[j])
+    h = hashlib.sha256(b"".join(vals)).hexdigest()
+    return {"queries": nq, "seed": 7, "types_sha256": hashlib.sha256(types.tobytes()).hexdigest(),
+            "val_len_sha256": hashlib.sha256(vlens.tobytes()).hexdigest(), "values_sha256": h,
+            "found": int((types == 0).sum()), "inputs": [{"file_size": fs} for _, fs in paths]}
+
+
 def main():
     ref = RefLib()
-    names = sys.argv[1:] or list(CASES)
+    names = sys.argv[1:] or list(CASES) + ["lookup_config3"]
     manifest = {}
     if os.path.exists(OUT):
         with open(OUT) as f:
             manifest = json.load(f)
     for name in names:
         with tempfile.TemporaryDirectory() as td:
-            manifest[name] = make_case(ref, name, CASES[name], td)
+            manifest[name] = lookup_case(ref, td) if name == "lookup_config3" else make_case(ref, name, CASES[name], td)
         with open(OUT, "w") as f:
             json.dump(manifest, f, indent=1)
     print("compaction_configs.json written")

@@ -89,3 +89,27 @@ def test_config_full_size_vs_reference(codec, tmp_path, name):
         assert sha(img) == w["sha256"], f"file output {sid} differs from the reference's"
         os.remove(p)
     print(f"{name}: file pipeline -> {len(want)} outputs equal to the reference's", flush=True)
+
+
+@pytest.mark.timeout(300)
+def test_lookup_config3_vs_reference(codec, oracle):
+    """sstc_get_batch at full size: 40 000 seeded point lookups over the 8
+    config-3 SSTs (8 x 151.6 MB resident, block indexes from sstc_open_tables)
+    give the reference TableReader::GetValue's types, value lengths and values
+    (hashes in compaction_configs.json)."""
+    import sstcodec
+    case = CASES["lookup_config3"]
+    tables = [oracle.table_build(r, 4096) for r in W.config_inputs(3)]
+    for t, img in enumerate(tables):
+        assert img.size + 1 == case["inputs"][t]["file_size"]
+    qt, qk = W.config3_lookup_queries(case["queries"], case["seed"])
+    keys = [bytes(k) for k in W.fixed_keys(qk).reshape(-1, 16)]
+    lk = sstcodec.Lookup(codec, tables)
+    typ, vo, vl, _ = lk.get(qt, keys)
+    whole = np.concatenate(tables)
+    del tables
+    vlens = np.where(typ == 0, vl, 0).astype(np.uint32)
+    vals = b"".join(bytes(whole[int(o):int(o) + int(n)]) for o, n, t in zip(vo, vl, typ) if t == 0)
+    assert hashlib.sha256(typ.astype(np.uint32).tobytes()).hexdigest() == case["types_sha256"]
+    assert hashlib.sha256(vlens.tobytes()).hexdigest() == case["val_len_sha256"]
+    assert hashlib.sha256(vals).hexdigest() == case["values_sha256"]

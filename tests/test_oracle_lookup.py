@@ -56,3 +56,33 @@ def test_lookup_live_reference(oracle, reflib):
         for i in range(len(keys)):
             if typ[i] == 0:
                 assert bytes(img[int(vo[i]):int(vo[i]) + int(vl[i])]) == rv[i]
+
+
+def test_lookup_config3_matches_reference(oracle):
+    """40 000 seeded point lookups over the 8 config-3 SSTs (1 M keys each):
+    the oracle's TableReader::GetValue restatement gives the reference's types,
+    value lengths and values (tests/golden/compaction_configs.json)."""
+    import hashlib
+    import json
+    import os
+    from conftest import GOLDEN
+    from sstcodec import workload as W
+    case = json.load(open(os.path.join(GOLDEN, "compaction_configs.json")))["lookup_config3"]
+    qt, qk = W.config3_lookup_queries(case["queries"], case["seed"])
+    keys = W.fixed_keys(qk).reshape(-1, 16)
+    types = np.zeros(len(qt), np.uint32)
+    vlens = np.zeros(len(qt), np.uint32)
+    vals = [b""] * len(qt)
+    for t, rec in enumerate(W.config_inputs(3)):
+        img = oracle.table_build(rec, 4096)
+        assert img.size + 1 == case["inputs"][t]["file_size"]
+        sel = np.flatnonzero(qt == t)
+        ty, vo, vl, _ = oracle.table_get(img, [bytes(keys[j]) for j in sel])
+        for j, a, o, n in zip(sel, ty, vo, vl):
+            types[j] = a
+            if a == 0:
+                vals[j] = bytes(img[int(o):int(o) + int(n)])
+                vlens[j] = n
+    assert hashlib.sha256(types.tobytes()).hexdigest() == case["types_sha256"]
+    assert hashlib.sha256(vlens.tobytes()).hexdigest() == case["val_len_sha256"]
+    assert hashlib.sha256(b"".join(vals)).hexdigest() == case["values_sha256"]
