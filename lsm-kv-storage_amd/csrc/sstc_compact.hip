@@ -107,16 +107,16 @@ __global__ void ck_check_blocks_kernel(const SK *s, const uint64_t *rec_base, ui
 //     them to the splitter's rank among splitters (sum of ceil(c / S)) and
 //     among records (sum of c), and write the co-rank row in sorted order.
 //     Between two consecutive splitter rows a run contributes <= S records.
-//  2. merge: workgroup w takes the records between the first splitter rows
-//     at or after output ranks w * kKWin and (w + 1) * kKWin (< 2 kKWin records),
-//     stages the <= kKWay sub-runs in LDS, and every record's output rank is
-//     its position in its sub-run + its co-ranks in the other sub-runs (LDS
-//     binary searches).  Order = key asc, txn desc, then lower run first, i.e.
-//     the stable pairwise merge of MergeIterator (merge_iterator.cc:34-46).
+//  2. windows: window w holds the records between the first splitter rows at
+//     or after output ranks w * kKWin and (w + 1) * kKWin (< 2 kKWin records);
+//     a thread per window resolves its output position and sub-runs.
+//  3. merge: a workgroup per window stages the <= kKWay sub-runs in LDS and
+//     merges them by a pairwise merge-path tree (ck_mg_merge_kernel).  Order =
+//     key asc, txn desc, then lower run first, i.e. the stable pairwise merge
+//     of MergeIterator (merge_iterator.cc:34-46).
 constexpr uint32_t kKWay = 8;
 constexpr uint32_t kKWin = 512;
 constexpr uint32_t kKRegion = 2 * kKWin;
-constexpr uint32_t kKThreads = 512;
 
 struct KGroup {
   uint64_t start[kKWay + 1]; // absolute run starts; start[nruns] = group end
@@ -209,22 +209,6 @@ __global__ __launch_bounds__(256) void ck_kw_split_kernel(const SK *in, const SK
   if (r == 0) G[row] = sc;
 }
 
-// LDS slot of staged record i: rows of 8 records (256 B = all 64 banks); the
-// column is XOR-swizzled by the row so that lanes ranking consecutive 8-record
-// runs (one row each) do not all hit the same banks.
-__device__ __forceinline__ uint32_t kw_slot(uint32_t i) { return i ^ ((i >> 3) & 7u); }
-
-// kw_before on a staged record: the 16 B prefix (one 16 B LDS read) decides
-// unless it ties
-__device__ __forceinline__ bool kw_before_lds(const SK *tile, uint32_t i, uint32_t ry, const SK &x, uint32_t rx,
-                                              const KeyView &kv) {
-  const SK *y = tile + kw_slot(i);
-  const uint64_t p0 = y->p0, p1 = y->p1;
-  if (p0 != x.p0) return p0 < x.p0;
-  if (p1 != x.p1) return p1 < x.p1;
-  return kw_before(*y, ry, x, rx, kv);
-}
-
 // first splitter row of every merge window: window w starts at the first row
 // whose record rank G is >= w * kKWin (rows are sorted, G increasing)
 __global__ void ck_kw_bounds_kernel(const KGroup *groups, uint32_t ngroups, uint32_t nids, const uint64_t *G,
@@ -244,80 +228,153 @@ __global__ void ck_kw_bounds_kernel(const KGroup *groups, uint32_t ngroups, uint
   for (uint64_t w = w0; w <= w1 && w <= nw; w++) J[gr.wg0 + gr.base + w] = j;
 }
 
-__global__ __launch_bounds__(kKThreads) void ck_kw_merge_kernel(const SK *in, SK *out, const KGroup *groups,
-                                                               uint32_t ngroups, const uint32_t *C,
-                                                               const uint64_t *G, const uint32_t *J, KeyView kv,
-                                                               Abort stop) {
+// one merge window, resolved once per window by a thread (not by the merge
+// workgroup, whose dependent group -> J -> C -> record loads would each stall
+// a whole LDS-holding workgroup): output position, the absolute start of every
+// sub-run and the sub-runs' offsets in the window (off[q] for q > k = n)
+struct __attribute__((aligned(16))) KWin {
+  uint32_t out, n, k, pad;
+  uint32_t src[kKWay];
+  uint32_t off[kKWay + 1];
+  uint32_t pad2[3];
+};
+constexpr uint32_t kKWinWords = sizeof(KWin) / 4;
+
+__global__ void ck_kw_win_kernel(const KGroup *groups, uint32_t ngroups, uint32_t nwin, const uint32_t *C,
+                                 const uint64_t *G, const uint32_t *J, KWin *win, Abort stop) {
+  const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= nwin) return;
+  KWin d{};
+  if (!stop()) { // an aborted job merges nothing (n = 0 in every window)
+    const KGroup &gr = groups[find_group(groups, ngroups, u, [](const KGroup &x) { return x.wg0; })];
+    const uint32_t at = gr.wg0 + gr.base + (u - gr.wg0), k = gr.nruns;
+    const uint32_t j0 = J[at], j1 = J[at + 1];
+    d.k = k;
+    if (j0 != j1) {
+      d.out = static_cast<uint32_t>(gr.start[0] + G[gr.base + j0]);
+      uint32_t acc = 0;
+      for (uint32_t q = 0; q < k; q++) {
+        const uint32_t lo = C[static_cast<uint64_t>(gr.base + j0) * kKWay + q];
+        const uint32_t hi = C[static_cast<uint64_t>(gr.base + j1) * kKWay + q];
+        d.src[q] = static_cast<uint32_t>(gr.start[q] + lo);
+        d.off[q] = acc;
+        acc += hi - lo;
+      }
+      d.n = acc;
+    }
+    for (uint32_t q = k; q <= kKWay; q++) d.off[q] = d.n;
+  }
+  win[u] = d;
+}
+
+__device__ __forceinline__ void load_win(const KWin *win, KWin &s_d) {
+  if (threadIdx.x < kKWinWords)
+    reinterpret_cast<uint32_t *>(&s_d)[threadIdx.x] = reinterpret_cast<const uint32_t *>(win + blockIdx.x)[threadIdx.x];
+  __syncthreads();
+}
+
+// Merge of one window by a pairwise tree in LDS: the
+// staged records stay put; log2(k) levels each merge neighbouring sub-run
+// groups into a permutation of 16-bit slot indices (ping-pong), the first
+// straight from the staged order; the last permutation drives a coalesced
+// copy to the output.  Every thread produces ceil(n / threads) consecutive
+// outputs of a level (all threads busy whatever the window size): one
+// merge-path search for its first output, then a sequential two-head merge
+// with the heads held in registers.  The left group always holds the lower
+// runs, so taking B only when B sorts strictly first gives key asc, txn desc,
+// lower run first (merge_iterator.cc:34-46).
+constexpr uint32_t kMgThreads = 256;
+
+__global__ __launch_bounds__(kMgThreads) void ck_mg_merge_kernel(const SK *in, SK *out, const KWin *win,
+                                                                KeyView kv) {
   __shared__ SK tile[kKRegion];
-  __shared__ uint32_t s_j[2], s_off[kKWay + 1], s_lo[kKWay];
-  if (stop()) return; // uniform over the workgroup
-  const KGroup &gr = groups[find_group(groups, ngroups, blockIdx.x, [](const KGroup &x) { return x.wg0; })];
-  const uint32_t wl = blockIdx.x - gr.wg0, k = gr.nruns;
-  const uint64_t *Gg = G + gr.base;
-  if (threadIdx.x < 2) s_j[threadIdx.x] = J[gr.wg0 + gr.base + wl + threadIdx.x];
-  __syncthreads();
-  const uint32_t j0 = s_j[0], j1 = s_j[1];
-  if (j0 == j1) return;
-  if (threadIdx.x < k) {
-    const uint32_t lo = C[static_cast<uint64_t>(gr.base + j0) * kKWay + threadIdx.x];
-    s_lo[threadIdx.x] = lo;
-    s_off[threadIdx.x + 1] = C[static_cast<uint64_t>(gr.base + j1) * kKWay + threadIdx.x] - lo;
+  __shared__ uint16_t ix[2][kKRegion];
+  __shared__ KWin s_d;
+  load_win(win, s_d);
+  const uint32_t total = s_d.n, k = s_d.k;
+  if (total == 0) return;
+  const uint32_t *s_off = s_d.off;
+  SK *o = out + s_d.out;
+  if (k == 1) {
+    for (uint32_t i = threadIdx.x; i < total; i += kMgThreads) o[i] = in[s_d.src[0] + i];
+    return;
   }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    s_off[0] = 0;
-    for (uint32_t q = 0; q < k; q++) s_off[q + 1] += s_off[q];
-  }
-  __syncthreads();
-  const uint32_t total = s_off[k];
-  for (uint32_t i = threadIdx.x; i < total; i += kKThreads) {
-    uint32_t q = 0;
-    while (s_off[q + 1] <= i) q++;
-    tile[kw_slot(i)] = in[gr.start[q] + s_lo[q] + (i - s_off[q])];
-  }
-  __syncthreads();
-  // every thread ranks kKPer consecutive staged records: along a sub-run the
-  // co-ranks in the other sub-runs are nondecreasing, so after one binary
-  // search per sub-run the cursors gallop forward (interleaved runs: ~2 probes)
-  SK *o = out + gr.start[0] + Gg[j0];
-  constexpr uint32_t kKPer = kKRegion / kKThreads;
-  uint32_t cur[kKWay];
-  uint32_t qprev = kKWay;
-  for (uint32_t e = 0; e < kKPer; e++) {
-    const uint32_t i = threadIdx.x * kKPer + e;
-    if (i >= total) break;
-    uint32_t q = 0;
-    while (s_off[q + 1] <= i) q++;
-    const SK x = tile[kw_slot(i)];
-    uint32_t rank = i - s_off[q];
+  // window layout in registers (uniform): sub-run of a slot by compares,
+  // no dependent LDS probes
+  uint32_t off[kKWay + 1], base[kKWay];
 #pragma unroll
-    for (uint32_t r = 0; r < kKWay; r++) {
-      if (r >= k || r == q) continue;
-      const uint32_t b1 = s_off[r + 1];
-      uint32_t lo = q == qprev ? cur[r] : s_off[r], hi = b1;
-      if (q == qprev) {
-        uint32_t step = 1;
-        for (uint32_t p = lo; p < b1;) {
-          if (!kw_before_lds(tile, p, r, x, q, kv)) {
-            hi = p;
-            break;
-          }
-          lo = p + 1;
-          p = lo + step - 1;
-          step <<= 1;
+  for (uint32_t r = 0; r <= kKWay; r++) off[r] = s_off[r]; // off[q > k] = n
+#pragma unroll
+  for (uint32_t r = 0; r < kKWay; r++) base[r] = s_d.src[r] - off[r];
+  auto run_of = [&](uint32_t x) {
+    uint32_t q = 0;
+#pragma unroll
+    for (uint32_t r = 1; r < kKWay; r++) q += x >= off[r];
+    return q;
+  };
+  auto bound = [&](uint32_t x) { // off[min(x, kKWay)]
+    uint32_t v = off[kKWay];
+#pragma unroll
+    for (uint32_t r = 0; r < kKWay; r++) v = x == r ? off[r] : v;
+    return v;
+  };
+  for (uint32_t i = threadIdx.x; i < total; i += kMgThreads) {
+    const uint32_t q = run_of(i);
+    uint32_t bq = base[0];
+#pragma unroll
+    for (uint32_t r = 1; r < kKWay; r++) bq = q == r ? base[r] : bq;
+    tile[i] = in[bq + i];
+  }
+  __syncthreads();
+  const uint32_t per = (total + kMgThreads - 1) / kMgThreads; // outputs per thread
+  const uint32_t p0 = threadIdx.x * per;
+  uint32_t src = 0;
+  for (uint32_t wd = 1; wd < k; wd <<= 1) {
+    const bool first = wd == 1;
+    const uint16_t *a_ix = ix[src];
+    uint16_t *o_ix = ix[src ^ 1];
+    auto slot = [&](uint32_t x) -> uint32_t { return first ? x : a_ix[x]; };
+    if (p0 < total) {
+      uint32_t m = run_of(p0) & ~(2 * wd - 1);
+      uint32_t lo = bound(m), mid = bound(m + wd), hi = bound(m + 2 * wd);
+      const uint32_t diag = p0 - lo;
+      uint32_t i = diag > hi - mid ? diag - (hi - mid) : 0, ihi = diag < mid - lo ? diag : mid - lo;
+      while (i < ihi) {
+        const uint32_t im = (i + ihi) >> 1;
+        if (!sk_less(tile[slot(mid + diag - 1 - im)], tile[slot(lo + im)], kv)) i = im + 1;
+        else ihi = im;
+      }
+      uint32_t j = diag - i, ai = 0, bi = 0;
+      SK a, b;
+      if (lo + i < mid) a = tile[ai = slot(lo + i)];
+      if (mid + j < hi) b = tile[bi = slot(mid + j)];
+      for (uint32_t e = 0; e < per; e++) {
+        const uint32_t p = p0 + e;
+        if (p >= total) break;
+        while (p == hi) { // the next pair starts inside this thread's outputs
+          m += 2 * wd;
+          lo = hi;
+          mid = bound(m + wd);
+          hi = bound(m + 2 * wd);
+          i = j = 0;
+          if (lo < mid) a = tile[ai = slot(lo)];
+          if (mid < hi) b = tile[bi = slot(mid)];
+        }
+        const bool take_b = lo + i >= mid || (mid + j < hi && sk_less(b, a, kv));
+        o_ix[p] = static_cast<uint16_t>(take_b ? bi : ai);
+        if (take_b) {
+          j++;
+          if (mid + j < hi) b = tile[bi = slot(mid + j)];
+        } else {
+          i++;
+          if (lo + i < mid) a = tile[ai = slot(lo + i)];
         }
       }
-      while (lo < hi) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (kw_before_lds(tile, mid, r, x, q, kv)) lo = mid + 1;
-        else hi = mid;
-      }
-      cur[r] = lo;
-      rank += lo - s_off[r];
     }
-    qprev = q;
-    o[rank] = x;
+    __syncthreads();
+    src ^= 1;
   }
+  for (uint32_t p = threadIdx.x; p < total; p += kMgThreads) o[p] = tile[ix[src][p]];
 }
 
 struct Rec {
@@ -935,13 +992,17 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
         for (size_t p = 0; p < pass_groups.size(); p++) max_j = std::max(max_j, pass_ids[p] + pass_wgs[p] + pass_groups[p]);
         uint32_t *Jm = pool.get<uint32_t>(max_j);
         SK *Sm = pool.get<SK>(max_ids);
+        KWin *Wm = pool.get<KWin>(*std::max_element(pass_wgs.begin(), pass_wgs.end()) + 1);
         size_t at = 0;
         for (size_t p = 0; p < pass_groups.size(); p++) {
           const uint32_t ng = pass_groups[p];
           ck_kw_sample_kernel<<<grid(pass_ids[p]), 256, 0, s>>>(A, d_kg + at, ng, pass_ids[p], Sm, stop);
           ck_kw_split_kernel<<<grid(static_cast<uint64_t>(pass_ids[p]) * 8), 256, 0, s>>>(A, Sm, d_kg + at, ng, pass_ids[p], kv, Cm, Gm, stop);
           ck_kw_bounds_kernel<<<grid(pass_ids[p]), 256, 0, s>>>(d_kg + at, ng, pass_ids[p], Gm, Jm, stop);
-          if (pass_wgs[p]) ck_kw_merge_kernel<<<pass_wgs[p], kKThreads, 0, s>>>(A, B, d_kg + at, ng, Cm, Gm, Jm, kv, stop);
+          if (pass_wgs[p]) {
+            ck_kw_win_kernel<<<grid(pass_wgs[p]), 256, 0, s>>>(d_kg + at, ng, pass_wgs[p], Cm, Gm, Jm, Wm, stop);
+            ck_mg_merge_kernel<<<pass_wgs[p], kMgThreads, 0, s>>>(A, B, Wm, kv);
+          }
           std::swap(A, B);
           at += ng;
         }

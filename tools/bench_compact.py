@@ -54,6 +54,19 @@ def record_sets(args, rank):
                            ranges=args.ranges, key_space=args.key_space)
 
 
+def fixture_name(args, rank):
+    """tests/golden/compaction_configs.json case generated from exactly these inputs, if any."""
+    if args.ranges or (args.ssts, args.keys) != W.CONFIG_DEFAULTS[args.config]:
+        return None
+    if args.config == 3:
+        return "config3_overlap" if args.overlap else "config3"
+    if args.config == 4 and rank == 0:
+        return "config4_rank0"
+    if args.config == 5 and args.key_space == 20000:
+        return "config5"
+    return None
+
+
 def barrier(world):
     if world > 1:
         import torch.distributed as dist
@@ -169,6 +182,10 @@ def run_bench(args, ranks, codec, td):
            "tables_out": nt, "blocks_out": res.blocks_out, "bytes_out": res.bytes_out,
            "device_s_median": med, "device_GiBps_in_all_ranks": all_in / med / 2 ** 30,
            "input_build_s": gen_s, "output_sizes_head": [int(x) + 1 for x in tlen[:min(nt, 4)].cpu().tolist()]}
+    fx = fixture_name(args, rank)
+    if fx:  # full-size fixture of this exact input: the reference's output hashes
+        want = json.load(open(os.path.join(ROOT, "tests", "golden", "compaction_configs.json")))[fx]["outputs_base1"]
+        out["matches_reference_fixture"] = (fx, gpu_hash == [w["sha256"] for w in want])
     if per_rank:
         out["per_rank"] = [{"rank": r, "device_s_median": t, "GiBps_in": b / t / 2 ** 30}
                            for r, (t, b) in enumerate(per_rank)]
