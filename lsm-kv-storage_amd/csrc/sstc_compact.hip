@@ -299,31 +299,17 @@ __global__ __launch_bounds__(kMgThreads) void ck_mg_merge_kernel(const SK *in, S
     for (uint32_t i = threadIdx.x; i < total; i += kMgThreads) o[i] = in[s_d.src[0] + i];
     return;
   }
-  // window layout in registers (uniform): sub-run of a slot by compares,
-  // no dependent LDS probes
-  uint32_t off[kKWay + 1], base[kKWay];
-#pragma unroll
-  for (uint32_t r = 0; r <= kKWay; r++) off[r] = s_off[r]; // off[q > k] = n
-#pragma unroll
-  for (uint32_t r = 0; r < kKWay; r++) base[r] = s_d.src[r] - off[r];
+  // sub-run of a slot, and off[min(x, kKWay)] (off[q > k] = n); probes of the
+  // 9-entry table in LDS measured faster than selects over registers
   auto run_of = [&](uint32_t x) {
     uint32_t q = 0;
-#pragma unroll
-    for (uint32_t r = 1; r < kKWay; r++) q += x >= off[r];
+    while (s_off[q + 1] <= x) q++;
     return q;
   };
-  auto bound = [&](uint32_t x) { // off[min(x, kKWay)]
-    uint32_t v = off[kKWay];
-#pragma unroll
-    for (uint32_t r = 0; r < kKWay; r++) v = x == r ? off[r] : v;
-    return v;
-  };
+  auto bound = [&](uint32_t x) { return s_off[x < kKWay ? x : kKWay]; };
   for (uint32_t i = threadIdx.x; i < total; i += kMgThreads) {
     const uint32_t q = run_of(i);
-    uint32_t bq = base[0];
-#pragma unroll
-    for (uint32_t r = 1; r < kKWay; r++) bq = q == r ? base[r] : bq;
-    tile[i] = in[bq + i];
+    tile[i] = in[s_d.src[q] + (i - s_off[q])];
   }
   __syncthreads();
   const uint32_t per = (total + kMgThreads - 1) / kMgThreads; // outputs per thread
