@@ -573,24 +573,6 @@ __global__ __launch_bounds__(kFtThreads) void ck_compact_tile_kernel(const SK *s
   }
 }
 
-// per record: end of its output table (clamp for block segmentation)
-__global__ void ck_table_end_kernel(const uint64_t *tf, const uint64_t *d_nt, uint64_t m, uint32_t *clamp) {
-  const uint64_t r = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (r > m) return;
-  const uint64_t nt = *d_nt;
-  if (r == m) {
-    clamp[r] = static_cast<uint32_t>(m);
-    return;
-  }
-  uint64_t lo = 0, hi = nt; // last tf <= r
-  while (lo + 1 < hi) {
-    const uint64_t mid = (lo + hi) >> 1;
-    if (tf[mid] <= r) lo = mid;
-    else hi = mid;
-  }
-  clamp[r] = static_cast<uint32_t>(tf[lo + 1]);
-}
-
 // block b: length, meta entry size, table index
 __global__ void ck_block_info_kernel(const uint64_t *bf, uint64_t nb, const uint64_t *Pe, const uint32_t *kl,
                                      const uint64_t *tf, uint64_t nt, uint64_t *blen, uint64_t *msz,
@@ -676,8 +658,9 @@ __global__ __launch_bounds__(256) void ck_meta_kernel(const uint64_t *bf, uint64
                                                       const uint64_t *BL, const uint64_t *MS, const uint64_t *blen,
                                                       const uint64_t *tbf, const uint64_t *toff,
                                                       const uint64_t *tdata, Rec K, const uint8_t *src,
-                                                      uint8_t *dst) {
+                                                      uint8_t *dst, const uint64_t *need, uint64_t cap) {
   __shared__ __attribute__((aligned(16))) uint8_t img[kMetaLds + 16];
+  if (*need > cap) return; // output capacity exceeded: nothing is written
   const uint64_t b0 = static_cast<uint64_t>(blockIdx.x) * 256u;
   const uint64_t bend = b0 + 256u < nb ? b0 + 256u : nb;
   const uint64_t b = b0 + threadIdx.x;
@@ -720,19 +703,26 @@ __global__ __launch_bounds__(256) void ck_meta_kernel(const uint64_t *bf, uint64
 
 // min / max txn of every output table (table_builder.cc:47-49): the encode
 // kernels reduce every block, then one workgroup per table reduces its blocks
+// table min / max txn from the blocks' (footer, table_builder.cc:179-211):
+// kMmSplit workgroups per table each reduce a slice of its blocks to a
+// partial; the footer kernel folds a table's kMmSplit partials (no atomics:
+// same-address atomics from every XCD serialise)
+constexpr uint32_t kMmSplit = 16;
 __global__ __launch_bounds__(256) void ck_tab_minmax_kernel(const uint64_t *tbf, const uint64_t *bmin,
-                                                            const uint64_t *bmax, uint64_t *tmin, uint64_t *tmax) {
+                                                            const uint64_t *bmax, uint64_t *pmin, uint64_t *pmax) {
   __shared__ uint64_t smn[256 / kWave], smx[256 / kWave];
-  const uint64_t t = blockIdx.x;
+  const uint64_t t = blockIdx.x / kMmSplit, g = blockIdx.x % kMmSplit;
+  const uint64_t f = tbf[t], n = tbf[t + 1] - f;
+  const uint64_t b0 = f + n * g / kMmSplit, b1 = f + n * (g + 1) / kMmSplit;
   uint64_t mn = ~0ull, mx = 0;
-  for (uint64_t b = tbf[t] + threadIdx.x; b < tbf[t + 1]; b += 256) {
+  for (uint64_t b = b0 + threadIdx.x; b < b1; b += 256) {
     mn = bmin[b] < mn ? bmin[b] : mn;
     mx = bmax[b] > mx ? bmax[b] : mx;
   }
   for (uint32_t d = kWave / 2; d > 0; d >>= 1) {
-    const uint64_t a = __shfl_xor(mn, d, kWave), c = __shfl_xor(mx, d, kWave);
-    mn = a < mn ? a : mn;
-    mx = c > mx ? c : mx;
+    const uint64_t x = __shfl_xor(mn, d, kWave), y = __shfl_xor(mx, d, kWave);
+    mn = x < mn ? x : mn;
+    mx = y > mx ? y : mx;
   }
   if (lane_id() == 0) {
     smn[threadIdx.x / kWave] = mn;
@@ -744,22 +734,28 @@ __global__ __launch_bounds__(256) void ck_tab_minmax_kernel(const uint64_t *tbf,
       mn = smn[w] < mn ? smn[w] : mn;
       mx = smx[w] > mx ? smx[w] : mx;
     }
-    tmin[t] = mn;
-    tmax[t] = mx;
+    pmin[blockIdx.x] = mn;
+    pmax[blockIdx.x] = mx;
   }
 }
 
 // footer of table t (table_builder.cc:179-211)
 __global__ void ck_footer_kernel(uint64_t nt, const uint64_t *tbf, const uint64_t *toff, const uint64_t *tdata,
-                                 const uint64_t *tmeta, const uint64_t *tmin, const uint64_t *tmax, uint8_t *dst) {
+                                 const uint64_t *tmeta, const uint64_t *tmin, const uint64_t *tmax, uint8_t *dst,
+                                 uint64_t cap) {
   const uint64_t t = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (t >= nt) return;
+  if (t >= nt || toff[nt] > cap) return;
+  uint64_t mn = ~0ull, mx = 0;
+  for (uint32_t g = 0; g < kMmSplit; g++) {
+    mn = tmin[t * kMmSplit + g] < mn ? tmin[t * kMmSplit + g] : mn;
+    mx = tmax[t * kMmSplit + g] > mx ? tmax[t * kMmSplit + g] : mx;
+  }
   uint8_t *p = dst + toff[t] + tdata[t] + tmeta[t];
   put_le(p, tbf[t + 1] - tbf[t], 8);
   put_le(p + 8, tdata[t], 8);
   put_le(p + 16, tmeta[t], 8);
-  put_le(p + 24, tmin[t], 8);
-  put_le(p + 32, tmax[t], 8);
+  put_le(p + 24, mn, 8);
+  put_le(p + 32, mx, 8);
 }
 
 // ------------------------------------------------------------------ host side
@@ -804,12 +800,12 @@ struct Pool {
 
 
 // greedy segmentation of [0, m) by weights whose prefix sums are
-// Pw[i] + add * i (>= threshold closes), optional clamp; the count lands in
-// *dn on the device.
-void segment(Pool &pool, const uint64_t *Pw, uint64_t add, uint64_t m, uint64_t threshold, const uint32_t *clamp,
-             uint64_t *first, uint64_t *dn, hipStream_t s, bool long_segments) {
+// Pw[i] + add * i (>= threshold closes), optionally clamped at ends[0..*nends];
+// the count lands in *dn on the device.
+void segment(Pool &pool, const uint64_t *Pw, uint64_t add, uint64_t m, uint64_t threshold, const uint64_t *ends,
+             const uint64_t *nends, uint64_t *first, uint64_t *dn, hipStream_t s, bool long_segments) {
   uint32_t *J = pool.get<uint32_t>(segment_workspace_u32(m));
-  CK(launch_segment(Pw, m, threshold, J, dn, first, s, clamp, add, long_segments));
+  CK(launch_segment(Pw, m, threshold, J, dn, first, s, ends, nends, add, long_segments));
 }
 
 struct Words {
@@ -877,8 +873,9 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     const uint64_t nws = scan_workspace_elems(nblocks + 1) + 64;
     // Host syncs: (1) per-block record counts (they size every array), (2) the
     // kept count with the sortedness / decode error flags, (3) the table and
-    // block counts, (4) the output size (capacity check before any write),
-    // (5) completion.  Everything else stays on the stream.
+    // block counts, (4) completion with the output size (the capacity check is
+    // on the device: no writer touches d_dst when the output exceeds dst_cap).
+    // Everything else stays on the stream.
     // 1. decode every block
     uint64_t *rb_all = pool.get<uint64_t>(nblocks + 1);
     uint64_t *ws = pool.get<uint64_t>(nws);
@@ -1022,11 +1019,9 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     ck_compact_tile_kernel<<<static_cast<uint32_t>(ftiles), kFtThreads, 0, s>>>(A, n, keep, tsum, totals, RX, KR, Pd,
                                                                              Pe);
     uint64_t *tf = pool.get<uint64_t>(m + 1), *dn = pool.get<uint64_t>(2);
-    segment(pool, Pd, 0, m, table_limit, nullptr, tf, dn, s, true);
-    uint32_t *clamp = pool.get<uint32_t>(m + 1);
-    ck_table_end_kernel<<<grid(m + 1), 256, 0, s>>>(tf, dn, m, clamp);
+    segment(pool, Pd, 0, m, table_limit, nullptr, nullptr, tf, dn, s, true);
     uint64_t *bf = pool.get<uint64_t>(m + 1);
-    segment(pool, Pe, 16, m, block_threshold, clamp, bf, dn + 1, s, false);
+    segment(pool, Pe, 16, m, block_threshold, tf, dn, bf, dn + 1, s, false); // blocks end at table ends
     fetch(arena, s, {dn, dn + 1});
     const uint64_t nt = arena.host[0], nb = arena.host[1];
     if (nt > max_tables) {
@@ -1045,15 +1040,11 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     uint64_t *tbf = pool.get<uint64_t>(nt + 1), *tdata = pool.get<uint64_t>(nt), *tmeta = pool.get<uint64_t>(nt);
     ck_table_info_kernel<<<grid(nt + 1), 256, 0, s>>>(tf, nt, bf, nb, BL, MS, tbf, tdata, tmeta, d_table_len);
     CK(launch_scan(d_table_len, nt, 0, d_table_off, ws2, s)); // d_table_off needs nt + 1 elements
-    fetch(arena, s, {d_table_off + nt});
-    const uint64_t total = arena.host[0];
+    // the output size is checked on the device (every writer below stands down
+    // when it exceeds dst_cap) and by the host after the last sync
+    const uint64_t *need = d_table_off + nt;
     res[2] = nb;
     res[3] = nt;
-    res[4] = total;
-    if (total > dst_cap) {
-      err = "output buffer too small";
-      return SSTC_E_CAPACITY;
-    }
     uint64_t *bo = pool.get<uint64_t>(nb);
     uint32_t *big = pool.get<uint32_t>(nb + 1);
     ck_block_off_kernel<<<grid(nb), 256, 0, s>>>(btab, nb, BL, tbf, d_table_off, bo, big + nb);
@@ -1062,15 +1053,23 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     ea.big = big;
     ea.nbig = big + nb;
     uint64_t *bmin = pool.get<uint64_t>(nb), *bmax = pool.get<uint64_t>(nb);
-    uint64_t *tmin = pool.get<uint64_t>(nt), *tmax = pool.get<uint64_t>(nt);
+    ea.need = need;
+    ea.cap = dst_cap;
+    uint64_t *tmin = pool.get<uint64_t>(nt * kMmSplit), *tmax = pool.get<uint64_t>(nt * kMmSplit);  // per-table partials
     ea.bmin = bmin; // block min / max txn, reduced by the encode kernels
     ea.bmax = bmax;
     CK(launch_enc_emit(ea, s));
-    ck_meta_kernel<<<static_cast<uint32_t>((nb + 255) / 256), 256, 0, s>>>(bf, nb, btab, BL, MS, blen, tbf, d_table_off, tdata, KR, d_src, d_dst);
-    ck_tab_minmax_kernel<<<static_cast<uint32_t>(nt), 256, 0, s>>>(tbf, bmin, bmax, tmin, tmax);
-    ck_footer_kernel<<<grid(nt), 256, 0, s>>>(nt, tbf, d_table_off, tdata, tmeta, tmin, tmax, d_dst);
+    ck_meta_kernel<<<static_cast<uint32_t>((nb + 255) / 256), 256, 0, s>>>(bf, nb, btab, BL, MS, blen, tbf, d_table_off, tdata, KR, d_src, d_dst,
+                                                                          need, dst_cap);
+    ck_tab_minmax_kernel<<<static_cast<uint32_t>(nt * kMmSplit), 256, 0, s>>>(tbf, bmin, bmax, tmin, tmax);
+    ck_footer_kernel<<<grid(nt), 256, 0, s>>>(nt, tbf, d_table_off, tdata, tmeta, tmin, tmax, d_dst, dst_cap);
     CK(hipGetLastError());
-    CK(hipStreamSynchronize(s));
+    fetch(arena, s, {need});
+    res[4] = arena.host[0];
+    if (res[4] > dst_cap) {
+      err = "output buffer too small";
+      return SSTC_E_CAPACITY;
+    }
     return SSTC_OK;
   } catch (const std::exception &e) {
     err = e.what();

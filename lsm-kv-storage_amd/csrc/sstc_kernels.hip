@@ -850,6 +850,7 @@ __device__ void enc_blk_minmax(const EncArgs &a, uint64_t b) {
 
 __global__ __launch_bounds__(kEncThreads) void enc_emit_kernel(EncArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t slot[kEncThreads * 16];
+  if (a.over()) return;
   if (a.big) {
     const uint32_t cnt = *a.nbig;
     for (uint32_t i = blockIdx.x; i < cnt; i += gridDim.x) {
@@ -1152,7 +1153,7 @@ __global__ __launch_bounds__(kEncWaves *kWave) void enc_lds_kernel(EncArgs a) {
   const uint32_t lane = lane_id();
   const uint32_t wg = a.xcd ? xcd_logical_block(blockIdx.x, gridDim.x) : blockIdx.x;
   const uint64_t b = static_cast<uint64_t>(wg) * kEncWaves + wave;
-  if (b >= a.nblocks) return;
+  if (b >= a.nblocks || a.over()) return;
   uint8_t *img = lds + wave * kEncSlot;
   const uint64_t bo = uniform64(a.out_blk_off[b]);
   const uint64_t L64 = uniform64(a.out_blk_len[b]);
@@ -1245,7 +1246,7 @@ __device__ uint64_t seg_next_at(const SegW &W, uint64_t i, uint64_t lim, uint64_
 struct SegArgs {
   const uint64_t *Pw;
   uint64_t add, m, threshold;
-  const uint32_t *clamp;
+  const uint64_t *ends, *nends; // optional clamp: ends[0..*nends], ends[*nends] = m
   uint32_t *J0, *Fx, *Fc; // by record
   uint64_t *win;          // per tile: entry-window size (scanned into node bases)
   uint64_t *first, *d_count;
@@ -1254,17 +1255,30 @@ struct SegArgs {
   uint32_t *tentry;       // cleared here: tiles + 1 entry counters
 };
 
+// index of the first end > i (ends sorted, ends[ne] = m > i)
+__device__ __forceinline__ uint64_t seg_end_index(const uint64_t *ends, uint64_t ne, uint64_t i) {
+  uint64_t lo = 0, hi = ne; // first t in [0, ne] with ends[t] > i
+  while (lo < hi) {
+    const uint64_t mid = (lo + hi) >> 1;
+    if (ends[mid] > i) hi = mid;
+    else lo = mid + 1;
+  }
+  return lo;
+}
+
 __global__ __launch_bounds__(kChThreads) void seg_walk_kernel(SegArgs a) {
   constexpr uint32_t kLw = kChTile + kChMargin;
   __shared__ uint64_t lw[kLw + kLw / 8];
   __shared__ uint32_t jn[kChTile], jc[kChTile];
-  __shared__ uint64_t s_wend;
+  __shared__ uint64_t s_wend, s_t0;
   const uint32_t tid = threadIdx.x;
   const uint64_t c0 = static_cast<uint64_t>(blockIdx.x) * kChTile;
   const uint64_t c1 = c0 + kChTile < a.m ? c0 + kChTile : a.m;
   const uint32_t len = static_cast<uint32_t>(c1 - c0);
   const uint64_t nl = a.m + 1 - c0 < kLw ? a.m + 1 - c0 : kLw;
-  if (tid == 0) {
+  const uint64_t ne = a.ends ? *a.nends : 0;
+  if (tid == 0) { // first table end past the tile start (its search overlaps the window fill)
+    s_t0 = a.ends ? seg_end_index(a.ends, ne, c0) : 0;
     a.tentry[blockIdx.x] = 0;
     if (blockIdx.x == 0) a.tentry[gridDim.x] = 0;
     for (uint64_t z = blockIdx.x; z < a.nz; z += gridDim.x) a.zws[z] = 0;
@@ -1287,16 +1301,28 @@ __global__ __launch_bounds__(kChThreads) void seg_walk_kernel(SegArgs a) {
   const SegW W{a.Pw, lw, a.add, c0, nl};
   if (tid == kChThreads - 1) { // entry window end: J0 of the record before the tile
     const uint64_t i = c0 - 1;
-    s_wend = blockIdx.x ? seg_next_at(W, i, a.clamp ? a.clamp[i] : a.m, a.threshold, i) : c0;
+    uint64_t lim = a.m;
+    if (a.ends) { // first end > c0 - 1: s_t0, or the one before it when it equals c0
+      const uint64_t t = s_t0;
+      lim = t > 0 && a.ends[t - 1] == c0 ? c0 : a.ends[t];
+    }
+    s_wend = blockIdx.x ? seg_next_at(W, i, lim, a.threshold, i) : c0;
   }
   // J0 of kPer consecutive records per thread: gallop for the first, then from
   // the previous answer (J0 is monotone within an output table)
   constexpr uint32_t kPer = kChTile / kChThreads;
   uint64_t lim[kPer];
+  {
+    const uint64_t i0 = c0 + tid * kPer;
+    uint64_t t = s_t0;
+    uint64_t end = a.ends ? a.ends[t] : a.m; // ends[ne] = m: the walks below stop at ne
 #pragma unroll
-  for (uint32_t r = 0; r < kPer; r++) {
-    const uint32_t p = tid * kPer + r;
-    lim[r] = p < len ? (a.clamp ? a.clamp[c0 + p] : a.m) : 0;
+    for (uint32_t r = 0; r < kPer; r++) {
+      const uint64_t i = i0 + r;
+      if (a.ends && i < a.m)
+        while (end <= i) end = a.ends[++t]; // ends[ne] = m > i
+      lim[r] = i < c1 ? end : 0;
+    }
   }
   uint64_t e_prev = 0;
 #pragma unroll
@@ -1978,14 +2004,14 @@ struct SegLayout { // u32 offsets into the segmentation workspace
 uint64_t segment_workspace_u32(uint64_t nrec) { return SegLayout(nrec).total + 2; }
 
 hipError_t launch_segment(const uint64_t *Pw, uint64_t nrec, uint64_t threshold, uint32_t *J,
-                          uint64_t *d_nblocks, uint64_t *blk_first, hipStream_t s, const uint32_t *clamp,
-                          uint64_t add, bool long_segments) {
+                          uint64_t *d_nblocks, uint64_t *blk_first, hipStream_t s, const uint64_t *ends,
+                          const uint64_t *d_nends, uint64_t add, bool long_segments) {
   if (nrec == 0) { // no records: no segment, first[0] = 0
     hipError_t e = hipMemsetAsync(d_nblocks, 0, sizeof(uint64_t), s);
     if (e == hipSuccess) e = hipMemsetAsync(blk_first, 0, sizeof(uint64_t), s);
     return e;
   }
-  if (long_segments && !clamp) {
+  if (long_segments && !ends) {
     seg_hops_kernel<<<1, kWave, 0, s>>>(Pw, add, nrec, threshold, blk_first, d_nblocks);
     return hipGetLastError();
   }
@@ -1995,7 +2021,7 @@ hipError_t launch_segment(const uint64_t *Pw, uint64_t nrec, uint64_t threshold,
   uint64_t *win = U + L.win, *base = U + L.base, *visits = U + L.visits, *sws = U + L.sws;
   uint32_t *tentry = J + L.tentry, *tbefore = J + L.tbefore;
   const uint64_t stride = nrec + 1;
-  SegArgs a{Pw, add, nrec, threshold, clamp, J + L.J0, J + L.Fx, J + L.Fc, win, blk_first, d_nblocks,
+  SegArgs a{Pw, add, nrec, threshold, ends, d_nends, J + L.J0, J + L.Fx, J + L.Fc, win, blk_first, d_nblocks,
             sws, scan_status_words(L.tiles), tentry};
   seg_walk_kernel<<<static_cast<uint32_t>(L.tiles), kChThreads, 0, s>>>(a);
   hipError_t e = launch_scan(win, L.tiles, 0, base, sws, s, true); // base[tiles] = node count

@@ -75,6 +75,10 @@ struct EncArgs {
   uint32_t *big = nullptr, *nbig = nullptr;
   // optional (compaction, entries_in_src): per-block min / max txn
   uint64_t *bmin = nullptr, *bmax = nullptr;
+  // optional capacity guard (compaction): nothing is written when *need > cap
+  const uint64_t *need = nullptr;
+  uint64_t cap = 0;
+  __device__ bool over() const { return need && *need > cap; }
 };
 
 // point lookups (sstc_get.hip)
@@ -124,9 +128,12 @@ hipError_t launch_enc_blocks(const uint64_t *P, const uint64_t *blk_first, uint6
 hipError_t launch_enc_emit(const EncArgs &a, hipStream_t s);
 // greedy segmentation; J = segment_workspace_u32(nrec) u32 of device workspace
 uint64_t segment_workspace_u32(uint64_t nrec);
+// ends: optional sorted segment-end list (a coarser segmentation's starts with
+// its sentinel, e.g. the output tables'): no segment crosses one of them
 hipError_t launch_segment(const uint64_t *Pw, uint64_t nrec, uint64_t threshold, uint32_t *J,
                           uint64_t *d_nblocks, uint64_t *blk_first, hipStream_t s,
-                          const uint32_t *clamp = nullptr, uint64_t add = 0, bool long_segments = false);
+                          const uint64_t *ends = nullptr, const uint64_t *d_nends = nullptr, uint64_t add = 0,
+                          bool long_segments = false);
 
 // persistent device workspace of one context (compaction)
 struct Arena {

@@ -197,3 +197,38 @@ def test_compact_many_entries_per_block(codec, oracle, base):
     assert res.records_kept == kept and len(outs) == len(want)
     for o, w in zip(outs, want):
         assert np.array_equal(o, w)
+
+
+def test_compact_capacity_exceeded_writes_nothing(codec):
+    """sstc_compact with an output buffer one byte short: SSTC_E_CAPACITY, the
+    exact output size in bytes_out (what sstc_compact_files retries with), and
+    not one byte of the buffer written (the writers check the size on the
+    device); the same call with the exact size gives the reference's bytes."""
+    import ctypes
+    import torch
+    from sstcodec._lib import CompactParams, CompactResult
+    g = load_golden("compact_small_base1.npz")
+    ins = [g[f"in{i}"] for i in range(4)]
+    want = [g[k] for k in sorted((k for k in g if k.startswith("out")), key=lambda x: int(x[3:]))]
+    need = sum(w.size for w in want)
+    src = torch.from_numpy(np.concatenate(ins)).to(codec.device)
+    idx = codec.open_tables(src, [f.size for f in ins], strict=True)
+    P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    toff = torch.zeros(65, dtype=torch.int64, device=codec.device)
+    tlen = torch.zeros(64, dtype=torch.int64, device=codec.device)
+    prm = CompactParams(4096, 32 << 20, 1, 0)
+    for cap, rc_want in ((need - 1, -5), (need, 0)):
+        dst = torch.full((need + 64,), 0xA5, dtype=torch.uint8, device=codec.device)
+        res = CompactResult()
+        codec._stream()
+        rc = codec.lib.sstc_compact(codec.h, P(src), P(idx["blk_off"]), P(idx["blk_len"]), int(idx["blk_off"].numel()),
+                                    idx["table_first_block"].ctypes.data_as(ctypes.c_void_p), len(ins),
+                                    ctypes.byref(prm), P(dst), cap, P(toff), P(tlen), 64, ctypes.byref(res))
+        assert rc == rc_want
+        assert res.bytes_out == need
+        d = dst.cpu().numpy()
+        assert (d[need:] == 0xA5).all()
+        if rc:
+            assert (d == 0xA5).all(), "a writer touched the output buffer past its capacity check"
+        else:
+            assert np.array_equal(d[:need], np.concatenate(want))
