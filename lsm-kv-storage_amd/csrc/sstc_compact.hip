@@ -84,8 +84,9 @@ __device__ __forceinline__ bool sk_less(const SK &a, const SK &b, const KeyView 
 // non-empty block against the last record before it, unless it starts a run.
 __global__ void ck_check_blocks_kernel(const SK *s, const uint64_t *rec_base, uint64_t nblocks,
                                        const uint64_t *run_start, uint64_t nruns, KeyView kv,
-                                       unsigned long long *bad, Abort stop) {
+                                       unsigned long long *bad, Abort stop, uint64_t *zws, uint64_t nz) {
   const uint64_t b = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  for (uint64_t z = b; z < nz; z += static_cast<uint64_t>(gridDim.x) * blockDim.x) zws[z] = 0; // filter look-back
   if (b >= nblocks || stop()) return;
   const uint64_t r = rec_base[b];
   if (r == 0 || rec_base[b + 1] == r) return;
@@ -371,10 +372,9 @@ struct Rec {
 
 // Keep / drop (ShouldKeepEntry, compact.cc:324-363) over the merged records,
 // then stream compaction of the survivors with the prefix sums the splits
-// need, in three kernels: per-tile keep flags + sums, one scan of the tile
-// sums, per-tile compaction.  Tile = kFtItems rows of kFtThreads records;
-// a row's records are lane-consecutive so loads and stores coalesce.
-constexpr uint32_t kFtThreads = 256, kFtItems = 16, kFtTile = kFtThreads * kFtItems;
+// need (ck_filter_kernel).  A row = kFtThreads lane-consecutive records, so
+// loads and stores coalesce.
+constexpr uint32_t kFtThreads = 256;
 
 // exclusive scan of three u64 per thread over the workgroup; tot = totals
 __device__ __forceinline__ void wg_scan3(uint64_t (&v)[3], uint64_t (&tot)[3]) {
@@ -407,169 +407,147 @@ __device__ __forceinline__ uint64_t data_bytes(uint32_t kl, uint32_t vl) {
   return static_cast<uint64_t>(kl) + (vl != kNoValue ? vl : 0u);
 }
 
-// keep[i]: the first merged record always; a group head (key differs from the
-// previous record, compact.cc:266-268) if PUT, or if DELETED and not the base
-// level; any other record iff its txn equals its group head's (drop if
-// last_txn > txn).  Txns descend within a group, so a non-head whose txn
+// Keep / drop and survivor compaction in one pass (round 1 used three kernels:
+// flags + tile sums, a scan of the tile sums, compaction): a tile of kFfRows
+// rows keeps its survivors' fields in registers, publishes its three totals
+// (kept records, key+value bytes, entry bytes) through decoupled look-back
+// (one wave per total; ws = [ticket, status[3][tiles]], cleared before the
+// launch), then writes the survivors row by row at their global positions.
+// The merged keys and the side records are read once.
+constexpr uint32_t kFfRows = 8, kFfTile = kFtThreads * kFfRows;
+
+// keep record i: the first merged record always; a group head (key differs
+// from the previous record, compact.cc:266-268) if PUT, or if DELETED and not
+// the base level; any other record iff its txn equals its group head's (drop
+// if last_txn > txn).  Txns descend within a group, so a non-head whose txn
 // differs from its predecessor's is dropped, and an equal one looks back along
 // its run of equal txns (records duplicated across inputs) to the head.
-// tsum[3 t + {0,1,2}] = kept records, their key+value bytes, their entry bytes.
-__global__ __launch_bounds__(kFtThreads) void ck_keep_tile_kernel(const SK *s, uint64_t n, KeyView kv,
-                                                                  uint32_t base_level, uint8_t *keep,
-                                                                  uint64_t *tsum, Abort stop) {
-  if (stop()) return; // uniform over the workgroup; the host rejects the job
+__device__ __forceinline__ uint32_t ff_keep(const SK *s, uint64_t i, const SK &x, const SK &pv, uint32_t ty,
+                                            uint32_t base_level, const KeyView &kv) {
+  if (i == 0) return 1;
+  if (key_cmp(pv.p0, pv.p1, pv.kl, pv.id, x.p0, x.p1, x.kl, x.id, kv) != 0)
+    return ty == kTypePut ? 1u : (base_level ? 0u : 1u);
+  if (x.tx != pv.tx) return 0;
+  for (uint64_t q = i - 1; q > 0; q--) { // run of equal txns back to the group head
+    const SK y = s[q - 1], z = s[q];
+    if (key_cmp(y.p0, y.p1, y.kl, y.id, z.p0, z.p1, z.kl, z.id, kv) != 0) break; // z is the head
+    if (y.tx != z.tx) return 0;
+  }
+  return 1;
+}
+
+__global__ __launch_bounds__(kFtThreads) void ck_filter_kernel(const SK *s, uint64_t n, KeyView kv,
+                                                               uint32_t base_level, Rec out, uint64_t *Pd,
+                                                               uint64_t *Pe, uint64_t *ws, uint64_t *totals,
+                                                               Abort stop) {
+  __shared__ uint64_t s_tile, s_pre[3];
+  if (stop()) return; // uniform over the grid: no ticket drawn, the host rejects the job
+  const uint32_t tid = threadIdx.x, lane = lane_id(), w = tid / kWave;
+  if (tid == 0) {
+    const uint64_t t = __hip_atomic_fetch_add(ws, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (t + 1 == gridDim.x) __hip_atomic_store(ws, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_tile = t;
+  }
+  __syncthreads();
+  const uint64_t tile = s_tile, t0 = tile * kFfTile;
   constexpr uint32_t kGroup = 4; // rows whose loads are in flight together
-  const uint64_t t0 = static_cast<uint64_t>(blockIdx.x) * kFtTile;
-  uint64_t v[3] = {0, 0, 0};
-  for (uint32_t j0 = 0; j0 < kFtItems; j0 += kGroup) {
+  uint32_t km = 0, kl[kFfRows], vl[kFfRows], ty[kFfRows];
+  uint64_t tx[kFfRows], ko[kFfRows];
+  uint64_t sum[3] = {0, 0, 0};
+#pragma unroll
+  for (uint32_t j0 = 0; j0 < kFfRows; j0 += kGroup) {
     SK x[kGroup], pv[kGroup];
 #pragma unroll
     for (uint32_t g = 0; g < kGroup; g++) { // row j: records t0 + 256 j + [0, 256), lane-consecutive
-      const uint64_t i = t0 + static_cast<uint64_t>(j0 + g) * kFtThreads + threadIdx.x;
+      const uint64_t i = t0 + static_cast<uint64_t>(j0 + g) * kFtThreads + tid;
       const uint64_t ic = i < n ? i : n - 1; // clamped, unconditional: the loads stay in flight together
       x[g] = s[ic];
       pv[g] = s[ic ? ic - 1 : 0];
     }
     __builtin_amdgcn_sched_barrier(0);
-    uint32_t kk[kGroup], vl[kGroup], ty[kGroup];
-#pragma unroll
-    for (uint32_t g = 0; g < kGroup; g++) { // the record's 16 B side fields, all rows in flight together
-      const uint64_t i = t0 + static_cast<uint64_t>(j0 + g) * kFtThreads + threadIdx.x;
-      const RecX r = kv.rx[x[g].id]; // unconditional (past n: the last record's)
-      vl[g] = i < n ? r.vl : 0u;
-      ty[g] = i < n ? r.type : 0u;
-    }
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (uint32_t g = 0; g < kGroup; g++) {
-      const uint64_t i = t0 + static_cast<uint64_t>(j0 + g) * kFtThreads + threadIdx.x;
-      uint32_t k = 0;
-      if (i < n) {
-        if (i == 0) {
-          k = 1;
-        } else if (key_cmp(pv[g].p0, pv[g].p1, pv[g].kl, pv[g].id, x[g].p0, x[g].p1, x[g].kl, x[g].id, kv) != 0) {
-          k = ty[g] == kTypePut ? 1u : (base_level ? 0u : 1u);
-        } else if (x[g].tx == pv[g].tx) {
-          k = 1;
-          for (uint64_t q = i - 1; q > 0; q--) { // run of equal txns back to the group head
-            const SK y = s[q - 1], z = s[q];
-            if (key_cmp(y.p0, y.p1, y.kl, y.id, z.p0, z.p1, z.kl, z.id, kv) != 0) break; // z is the head
-            if (y.tx != z.tx) {
-              k = 0;
-              break;
-            }
-          }
-        }
-        keep[i] = static_cast<uint8_t>(k);
-      }
-      kk[g] = k;
-    }
-#pragma unroll
-    for (uint32_t g = 0; g < kGroup; g++)
-      if (kk[g]) {
-        v[0] += 1;
-        v[1] += data_bytes(x[g].kl, vl[g]);
-        v[2] += entry_size(x[g].kl, vl[g]);
-      }
-  }
-  uint64_t tot[3];
-  wg_scan3(v, tot);
-  if (threadIdx.x == 0) {
-    tsum[3 * blockIdx.x] = tot[0];
-    tsum[3 * blockIdx.x + 1] = tot[1];
-    tsum[3 * blockIdx.x + 2] = tot[2];
-  }
-}
-
-// exclusive scan of the tile sums in place (one workgroup); totals[3]
-__global__ __launch_bounds__(kFtThreads) void ck_tile_scan_kernel(uint64_t *tsum, uint64_t tiles, uint64_t *totals) {
-  uint64_t carry[3] = {0, 0, 0};
-  for (uint64_t t0 = 0; t0 < tiles; t0 += kFtThreads) {
-    const uint64_t t = t0 + threadIdx.x;
-    uint64_t v[3];
-#pragma unroll
-    for (int c = 0; c < 3; c++) v[c] = t < tiles ? tsum[3 * t + c] : 0;
-    uint64_t tot[3];
-    wg_scan3(v, tot);
-#pragma unroll
-    for (int c = 0; c < 3; c++) {
-      if (t < tiles) tsum[3 * t + c] = carry[c] + v[c];
-      carry[c] += tot[c];
-    }
-  }
-  if (threadIdx.x == 0)
-    for (int c = 0; c < 3; c++) totals[c] = carry[c];
-}
-
-// the survivors in merge order: record table, Pd = prefix sums of key+value
-// bytes (table split), Pe = prefix sums of entry bytes (block split, encode)
-__global__ __launch_bounds__(kFtThreads) void ck_compact_tile_kernel(const SK *s, uint64_t n, const uint8_t *keep,
-                                                                     const uint64_t *tsum, const uint64_t *totals,
-                                                                     const RecX *rx, Rec out, uint64_t *Pd,
-                                                                     uint64_t *Pe) {
-  constexpr uint32_t kGroup = 4; // rows whose loads are in flight together
-  const uint64_t t0 = static_cast<uint64_t>(blockIdx.x) * kFtTile;
-  uint64_t base[3] = {tsum[3 * blockIdx.x], tsum[3 * blockIdx.x + 1], tsum[3 * blockIdx.x + 2]};
-  for (uint32_t j0 = 0; j0 < kFtItems; j0 += kGroup) {
-    if (t0 + static_cast<uint64_t>(j0) * kFtThreads >= n) break; // uniform over the workgroup
-    uint32_t km = 0, kl[kGroup], vl[kGroup], ty[kGroup];
-    uint64_t tx[kGroup], ko[kGroup];
-    SK x[kGroup];
-    // loads unconditional at clamped indices (a load under a branch is waited
-    // for before the branch joins): flags and keys of all rows, then the side
-    // records, each batch in flight together
-    uint32_t kb[kGroup];
-#pragma unroll
-    for (uint32_t g = 0; g < kGroup; g++) {
-      const uint64_t i = t0 + static_cast<uint64_t>(j0 + g) * kFtThreads + threadIdx.x;
-      const uint64_t ic = i < n ? i : n - 1;
-      kb[g] = keep[ic];
-      x[g] = s[ic];
-    }
-    __builtin_amdgcn_sched_barrier(0);
     RecX rr[kGroup];
 #pragma unroll
-    for (uint32_t g = 0; g < kGroup; g++) rr[g] = rx[x[g].id];
+    for (uint32_t g = 0; g < kGroup; g++) rr[g] = kv.rx[x[g].id]; // unconditional (past n: the last record's)
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (uint32_t g = 0; g < kGroup; g++) {
-      const uint64_t i = t0 + static_cast<uint64_t>(j0 + g) * kFtThreads + threadIdx.x;
-      if (i < n && kb[g]) km |= 1u << g;
-    }
-#pragma unroll
-    for (uint32_t g = 0; g < kGroup; g++) {
-      const bool k = (km >> g) & 1u;
-      const RecX r = k ? rr[g] : RecX{};
-      kl[g] = x[g].kl;
-      tx[g] = x[g].tx;
-      vl[g] = r.vl;
-      ty[g] = r.type;
-      ko[g] = r.ko;
-    }
-#pragma unroll
-    for (uint32_t g = 0; g < kGroup; g++) { // row by row: survivors of a row are lane-consecutive
-      const bool k = (km >> g) & 1u;
-      uint64_t v[3] = {k ? 1ull : 0ull, k ? data_bytes(kl[g], vl[g]) : 0ull, k ? entry_size(kl[g], vl[g]) : 0ull};
-      uint64_t tot[3];
-      wg_scan3(v, tot);
+      const uint32_t j = j0 + g;
+      const uint64_t i = t0 + static_cast<uint64_t>(j) * kFtThreads + tid;
+      const uint32_t k = i < n ? ff_keep(s, i, x[g], pv[g], rr[g].type, base_level, kv) : 0u;
+      km |= k << j;
+      kl[j] = x[g].kl;
+      tx[j] = x[g].tx;
+      vl[j] = rr[g].vl;
+      ty[j] = rr[g].type;
+      ko[j] = rr[g].ko;
       if (k) {
-        const uint64_t q = base[0] + v[0];
-        out.type[q] = static_cast<uint8_t>(ty[g]);
-        out.kl[q] = kl[g];
-        out.vl[q] = vl[g];
-        out.tx[q] = tx[g];
-        out.ko[q] = ko[g];
-        out.vo[q] = ty[g] != kTypeDeleted ? ko[g] + kl[g] + 4 : 0; // decode's val_off
-        Pd[q] = base[1] + v[1];
-        Pe[q] = base[2] + v[2];
+        sum[0] += 1;
+        sum[1] += data_bytes(kl[j], vl[j]);
+        sum[2] += entry_size(kl[j], vl[j]);
       }
-#pragma unroll
-      for (int c = 0; c < 3; c++) base[c] += tot[c];
     }
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    Pd[totals[0]] = totals[1];
-    Pe[totals[0]] = totals[2];
+  uint64_t tot[3];
+  wg_scan3(sum, tot); // only the tile totals are used here
+  if (w < 3) { // wave c: decoupled look-back of total c
+    uint64_t *status = ws + 1 + static_cast<uint64_t>(w) * gridDim.x;
+    const uint64_t total = tot[w];
+    uint64_t prefix = 0;
+    if (tile == 0) {
+      if (lane == 0) __hip_atomic_store(&status[0], kLbInc | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      if (lane == 0) __hip_atomic_store(&status[tile], kLbAgg | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      int64_t p = static_cast<int64_t>(tile) - 1; // window [p - 63, p]
+      uint64_t spins = 0;
+      for (;;) {
+        const int64_t q = p - static_cast<int64_t>(lane);
+        const uint64_t st = q >= 0 ? __hip_atomic_load(&status[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                   : kLbInc;
+        const uint64_t inc = __ballot((st >> 62) == 2);
+        const uint32_t need = inc ? static_cast<uint32_t>(__ffsll(static_cast<long long>(inc))) : kWave;
+        const uint64_t zero = __ballot((st >> 62) == 0 && lane < need);
+        if (zero) {
+          if (++spins > kLbSpinLimit) break; // a predecessor never published: give up (wrong sums, no hang)
+          __builtin_amdgcn_s_sleep(1);
+          continue;
+        }
+        prefix += wave_sum_u64(lane < need ? (st & kLbVal) : 0);
+        if (inc) break;
+        p -= kWave;
+      }
+      if (lane == 0)
+        __hip_atomic_store(&status[tile], kLbInc | (prefix + total), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (lane == 0) s_pre[w] = prefix;
+  }
+  __syncthreads();
+  uint64_t base[3] = {s_pre[0], s_pre[1], s_pre[2]};
+#pragma unroll
+  for (uint32_t j = 0; j < kFfRows; j++) { // row by row: survivors of a row are lane-consecutive
+    const bool k = (km >> j) & 1u;
+    uint64_t v[3] = {k ? 1ull : 0ull, k ? data_bytes(kl[j], vl[j]) : 0ull, k ? entry_size(kl[j], vl[j]) : 0ull};
+    uint64_t rt[3];
+    wg_scan3(v, rt);
+    if (k) {
+      const uint64_t q = base[0] + v[0];
+      out.type[q] = static_cast<uint8_t>(ty[j]);
+      out.kl[q] = kl[j];
+      out.vl[q] = vl[j];
+      out.tx[q] = tx[j];
+      out.ko[q] = ko[j];
+      out.vo[q] = ty[j] != kTypeDeleted ? ko[j] + kl[j] + 4 : 0; // decode's val_off
+      Pd[q] = base[1] + v[1];
+      Pe[q] = base[2] + v[2];
+    }
+#pragma unroll
+    for (int c = 0; c < 3; c++) base[c] += rt[c];
+  }
+  if (tid == 0 && t0 + kFfTile >= n) { // the last tile: grand totals and the closing prefix sums
+    Pd[base[0]] = base[1];
+    Pe[base[0]] = base[2];
+    totals[0] = base[0];
+    totals[1] = base[1];
+    totals[2] = base[2];
   }
 }
 
@@ -932,7 +910,10 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     uint64_t nruns = ntables;
     const uint64_t *rb = d_rs; // run starts, nruns + 1
     const Abort dec_fail{err_count, errs, nullptr}, stop{err_count, errs, bad};
-    ck_check_blocks_kernel<<<grid(nblocks), 256, 0, s>>>(A, rb_all, nblocks, rb, nruns, kv, bad, dec_fail);
+    const uint64_t fftiles = (n + kFfTile - 1) / kFfTile;
+    uint64_t *ffws = pool.get<uint64_t>(1 + 3 * fftiles);
+    ck_check_blocks_kernel<<<grid(nblocks), 256, 0, s>>>(A, rb_all, nblocks, rb, nruns, kv, bad, dec_fail, ffws,
+                                                         1 + 3 * fftiles);
     // k-way merge passes; run boundaries of every pass are known on the host,
     // so all group descriptors go up in one upload (lives until the next sync)
     std::vector<KGroup> kg;
@@ -991,13 +972,14 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
         }
       }
     }
-    // 3. keep / drop: survivor counts and byte sums per tile, one scan
-    const uint64_t ftiles = (n + kFtTile - 1) / kFtTile;
-    uint8_t *keep = pool.get<uint8_t>(n);
-    uint64_t *tsum = pool.get<uint64_t>(3 * ftiles), *totals = pool.get<uint64_t>(3);
-    ck_keep_tile_kernel<<<static_cast<uint32_t>(ftiles), kFtThreads, 0, s>>>(A, n, kv, base_level, keep, tsum,
-                                                                          stop);
-    ck_tile_scan_kernel<<<1, kFtThreads, 0, s>>>(tsum, ftiles, totals);
+    // 3. keep / drop and the survivors gathered in merge order with their
+    // prefix sums (sized by n: the kept count is known after the pass)
+    uint64_t *totals = pool.get<uint64_t>(3);
+    Rec KR{pool.get<uint8_t>(n), pool.get<uint32_t>(n), pool.get<uint32_t>(n), pool.get<uint64_t>(n),
+           pool.get<uint64_t>(n), pool.get<uint64_t>(n)};
+    uint64_t *Pd = pool.get<uint64_t>(n + 1), *Pe = pool.get<uint64_t>(n + 1);
+    ck_filter_kernel<<<static_cast<uint32_t>(fftiles), kFtThreads, 0, s>>>(A, n, kv, base_level, KR, Pd, Pe, ffws,
+                                                                        totals, stop);
     fetch(arena, s, {totals, reinterpret_cast<const uint64_t *>(bad),
                            reinterpret_cast<const uint64_t *>(err_count), errs});
     if (arena.host[2] != arena.host[3]) {
@@ -1010,14 +992,8 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     }
     const uint64_t m = arena.host[0];
     res[1] = m;
-    Rec KR{pool.get<uint8_t>(m), pool.get<uint32_t>(m), pool.get<uint32_t>(m), pool.get<uint64_t>(m),
-           pool.get<uint64_t>(m), pool.get<uint64_t>(m)};
-    // 4. survivors gathered in merge order with their prefix sums; then the
-    // table split (key+value bytes, compact.cc:290) and the block split
+    // 4. the table split (key+value bytes, compact.cc:290) and the block split
     // (entry + offset-entry bytes, table_builder.cc:57-59) clamped at table ends
-    uint64_t *Pd = pool.get<uint64_t>(m + 1), *Pe = pool.get<uint64_t>(m + 1);
-    ck_compact_tile_kernel<<<static_cast<uint32_t>(ftiles), kFtThreads, 0, s>>>(A, n, keep, tsum, totals, RX, KR, Pd,
-                                                                             Pe);
     uint64_t *tf = pool.get<uint64_t>(m + 1), *dn = pool.get<uint64_t>(2);
     segment(pool, Pd, 0, m, table_limit, nullptr, nullptr, tf, dn, s, true);
     uint64_t *bf = pool.get<uint64_t>(m + 1);

@@ -135,6 +135,12 @@ __device__ __forceinline__ uint64_t wave_incl_scan_u64(uint64_t v) {
   return v;
 }
 
+// decoupled look-back status word: 2 flag bits (aggregate / inclusive) | 14-bit
+// epoch | 48 value bits (scan_lookback_kernel, ck_filter_kernel)
+constexpr uint64_t kLbAgg = 1ull << 62, kLbInc = 2ull << 62, kLbVal = (1ull << 48) - 1;
+constexpr uint32_t kLbEpochShift = 48;
+constexpr uint64_t kLbSpinLimit = 1ull << 24; // never reached unless a tile died
+
 __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
 #pragma unroll
   for (uint32_t d = kWave / 2; d > 0; d >>= 1) v += __shfl_xor(v, d, kWave);

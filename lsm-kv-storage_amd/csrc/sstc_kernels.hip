@@ -1774,9 +1774,6 @@ __global__ __launch_bounds__(kScanThreads) void scan_apply_kernel(In in, uint64_
 // already resident; the tile that draws the last ticket resets the counter
 // for the next launch.  ws = [ticket, status[tiles]].
 constexpr uint32_t kLbItems = 16, kLbTile = kScanThreads * kLbItems;
-constexpr uint64_t kLbAgg = 1ull << 62, kLbInc = 2ull << 62, kLbVal = (1ull << 48) - 1;
-constexpr uint32_t kLbEpochShift = 48;
-constexpr uint64_t kLbSpinLimit = 1ull << 24; // never reached unless a tile died
 
 __device__ __forceinline__ uint32_t lb_idx(uint32_t i) { return i + (i >> 4); } // 1 pad per 16
 
