@@ -601,6 +601,60 @@ __global__ void enc_blocks_kernel(const uint64_t *P, const uint64_t *blk_first, 
   }
 }
 
+// Encode offsets without a scan over the records (reduce, scan the blocks,
+// then write): 8 lanes per block sum its entry sizes (block length = entries
+// + 16 per offset entry + the 16 B extra), a device scan of the block lengths
+// gives the block offsets, and enc_prefix_kernel writes P (exclusive prefix
+// of the entry sizes from the first block's first record) block by block.
+// Three short launches instead of the chained 1.8 M-record look-back scan +
+// the closed-form offsets (config 2 encode leg -4.6 us; one kernel with a
+// thread per block and a look-back over 256-block tiles was 20 us slower:
+// profiles/r02_ab/encode_ab.md).
+constexpr uint32_t kBsG = 8;
+
+__global__ __launch_bounds__(256) void enc_bsum_kernel(const uint32_t *kl, const uint32_t *vl,
+                                                       const uint64_t *blk_first, uint64_t nblocks,
+                                                       uint64_t *blk_len, uint32_t *nbig) {
+  const uint64_t t = static_cast<uint64_t>(blockIdx.x) * 256u + threadIdx.x;
+  const uint64_t b = t / kBsG;
+  const uint32_t g = static_cast<uint32_t>(t % kBsG);
+  if (t == 0 && nbig) *nbig = 0; // the large-block list starts empty
+  uint64_t f0 = 0, f1 = 0, sum = 0;
+  if (b < nblocks) {
+    f0 = blk_first[b];
+    f1 = blk_first[b + 1];
+    for (uint64_t r = f0 + g; r < f1; r += kBsG) sum += entry_size(kl[r], vl[r]);
+  }
+#pragma unroll
+  for (uint32_t d = kBsG / 2; d > 0; d >>= 1) sum += __shfl_xor(sum, d, kWave); // stays inside the 8-lane group
+  if (b < nblocks && g == 0) blk_len[b] = sum + 16 * (f1 - f0) + 16;
+}
+
+__global__ __launch_bounds__(256) void enc_prefix_kernel(const uint32_t *kl, const uint32_t *vl,
+                                                         const uint64_t *blk_first, uint64_t nblocks,
+                                                         const uint64_t *blk_off, uint64_t out_base, uint64_t *P) {
+  const uint64_t t = static_cast<uint64_t>(blockIdx.x) * 256u + threadIdx.x;
+  const uint64_t b = t / kBsG;
+  const uint32_t g = static_cast<uint32_t>(t % kBsG);
+  if (b >= nblocks) return; // whole 8-lane groups leave together
+  const uint64_t F0 = blk_first[0], f0 = blk_first[b], f1 = blk_first[b + 1];
+  // entry bytes before the block: its offset minus the offset entries and extras before it
+  uint64_t base = blk_off[b] - out_base - 16 * (f0 - F0) - 16 * b;
+  for (uint64_t r0 = f0; r0 < f1; r0 += kBsG) { // same trip count for the whole group
+    const uint64_t r = r0 + g;
+    const uint64_t sz = r < f1 ? entry_size(kl[r], vl[r]) : 0;
+    uint64_t inc = sz;
+#pragma unroll
+    for (uint32_t d = 1; d < kBsG; d <<= 1) {
+      const uint64_t y = __shfl_up(inc, d, kWave);
+      if (g >= d) inc += y;
+    }
+    if (r < f1) P[r] = base + inc - sz;
+    base += __shfl(inc, static_cast<int>((lane_id() & ~(kBsG - 1)) + kBsG - 1), kWave);
+  }
+  if (b == nblocks - 1 && g == 0) P[f1] = base;
+}
+
 // One workgroup per block; each thread assembles 16-byte output chunks aligned
 // to the destination address.  A chunk that lies inside one key or value span
 // is funnel-shifted from five source dwords; any other chunk is assembled byte
@@ -622,8 +676,10 @@ __device__ __forceinline__ u32x4 load16_unaligned(const uint8_t *p) {
   return v;
 }
 
-__device__ void enc_emit_block(const EncArgs &a, uint64_t b, uint8_t *slot) {
-  const uint32_t tid = threadIdx.x;
+// kT threads (tid = 0..kT-1) encode block b straight to HBM: a workgroup
+// (enc_emit_kernel) or one wave (enc_lds_kernel's blocks past its LDS slot)
+template <uint32_t kT = kEncThreads>
+__device__ void enc_emit_block(const EncArgs &a, uint64_t b, uint8_t *slot, uint32_t tid = threadIdx.x) {
   const uint64_t f0 = a.blk_first[b], f1 = a.blk_first[b + 1];
   const uint64_t n = f1 - f0;
   const uint64_t P0 = a.P[f0];
@@ -635,7 +691,7 @@ __device__ void enc_emit_block(const EncArgs &a, uint64_t b, uint8_t *slot) {
   uint8_t *my = slot + 16 * tid;
 
   const uint64_t c_first = bo >> 4, c_end = (bo + L + 15) >> 4;
-  for (uint64_t c = c_first + tid; c < c_end; c += kEncThreads) {
+  for (uint64_t c = c_first + tid; c < c_end; c += kT) {
     const int64_t x0 = static_cast<int64_t>(16 * c) - static_cast<int64_t>(bo);
     const uint64_t xs = x0 < 0 ? 0 : static_cast<uint64_t>(x0);
     const uint64_t xe = static_cast<uint64_t>(x0 + 16) < L ? static_cast<uint64_t>(x0 + 16) : L;
@@ -1158,8 +1214,14 @@ __global__ __launch_bounds__(kEncWaves *kWave) void enc_lds_kernel(EncArgs a) {
   const uint64_t bo = uniform64(a.out_blk_off[b]);
   const uint64_t L64 = uniform64(a.out_blk_len[b]);
   const uint32_t pad = static_cast<uint32_t>(bo & 15u);
-  if (pad + L64 + 16 > kEncSlot) {       // large block: enc_emit_kernel
-    if (a.big && lane == 0) a.big[atomicAdd(a.nbig, 1u)] = static_cast<uint32_t>(b);
+  if (pad + L64 + 16 > kEncSlot) { // large block
+    if constexpr (kMode == 0) {
+      if (a.big_inline) { // this wave writes it straight to HBM (its LDS image holds the lanes' chunk slots)
+        enc_emit_block<kWave>(a, b, img, lane);
+        return;
+      }
+    }
+    if (a.big && lane == 0) a.big[atomicAdd(a.nbig, 1u)] = static_cast<uint32_t>(b); // enc_emit_kernel
     return;
   }
   const uint32_t L = static_cast<uint32_t>(L64);
@@ -1953,6 +2015,21 @@ hipError_t launch_enc_blocks(const uint64_t *P, const uint64_t *blk_first, uint6
   return hipGetLastError();
 }
 
+hipError_t launch_enc_offsets(const uint32_t *kl, const uint32_t *vl, const uint64_t *blk_first, uint64_t nblocks,
+                              uint64_t out_base, uint64_t *blk_off, uint64_t *blk_len, uint64_t *P, uint32_t *nbig,
+                              uint64_t *ws, hipStream_t s, uint32_t epoch) {
+  if (nblocks == 0) { // blk_first may be NULL
+    enc_blocks_kernel<<<1, 256, 0, s>>>(nullptr, nullptr, 0, out_base, blk_off, blk_len, nbig);
+    return hipGetLastError();
+  }
+  const uint32_t g = grid_for(nblocks * kBsG, 256);
+  enc_bsum_kernel<<<g, 256, 0, s>>>(kl, vl, blk_first, nblocks, blk_len, nbig);
+  hipError_t e = scan_any(ArrIn{blk_len}, nblocks, out_base, blk_off, ws, s, false, epoch);
+  if (e != hipSuccess) return e;
+  enc_prefix_kernel<<<g, 256, 0, s>>>(kl, vl, blk_first, nblocks, blk_off, out_base, P);
+  return hipGetLastError();
+}
+
 hipError_t launch_enc_emit(const EncArgs &a, hipStream_t s) {
   if (!a.nblocks) return hipSuccess;
   const uint32_t g = grid_for(a.nblocks, kEncWaves);
@@ -1964,6 +2041,7 @@ hipError_t launch_enc_emit(const EncArgs &a, hipStream_t s) {
   if (!a.entries_in_src) enc_lds_kernel<0><<<g, kEncWaves * kWave, 0, s>>>(a);
   else enc_lds_kernel<1><<<g, kEncWaves * kWave, 0, s>>>(a);
   // blocks past an LDS slot: those listed by enc_lds_kernel when a list is given
+  if (a.big_inline && !a.entries_in_src) return hipGetLastError();
   const uint64_t cap = a.big ? 512 : 2048;
   enc_emit_kernel<<<static_cast<uint32_t>(a.nblocks < cap ? a.nblocks : cap), kEncThreads, 0, s>>>(a);
   return hipGetLastError();

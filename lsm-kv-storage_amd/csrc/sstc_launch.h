@@ -73,6 +73,9 @@ struct EncArgs {
   // optional: blocks too large for an LDS slot are listed here by enc_lds_kernel
   // (*nbig zeroed by the caller) so enc_emit_kernel visits only them
   uint32_t *big = nullptr, *nbig = nullptr;
+  // records -> blocks (not entries_in_src): enc_lds_kernel's waves encode the
+  // blocks past their LDS slot themselves, no enc_emit_kernel launch
+  uint32_t big_inline = 0;
   // optional (compaction, entries_in_src): per-block min / max txn
   uint64_t *bmin = nullptr, *bmax = nullptr;
   // optional capacity guard (compaction): nothing is written when *need > cap
@@ -125,6 +128,12 @@ hipError_t launch_scan_entry_sizes(const uint32_t *klen, const uint32_t *vlen, u
 // block offsets (nblocks + 1) and sizes of an encode from P (closed form); clears *nbig
 hipError_t launch_enc_blocks(const uint64_t *P, const uint64_t *blk_first, uint64_t nblocks, uint64_t out_base,
                              uint64_t *blk_off, uint64_t *blk_len, uint32_t *nbig, hipStream_t s);
+// the same without a record scan: block lengths by reduction, a scan over the
+// blocks, then P (entry-size prefix, P[blk_first[0]] = 0) written per block;
+// clears *nbig
+hipError_t launch_enc_offsets(const uint32_t *kl, const uint32_t *vl, const uint64_t *blk_first, uint64_t nblocks,
+                              uint64_t out_base, uint64_t *blk_off, uint64_t *blk_len, uint64_t *P, uint32_t *nbig,
+                              uint64_t *ws, hipStream_t s, uint32_t epoch);
 hipError_t launch_enc_emit(const EncArgs &a, hipStream_t s);
 // greedy segmentation; J = segment_workspace_u32(nrec) u32 of device workspace
 uint64_t segment_workspace_u32(uint64_t nrec);
