@@ -232,3 +232,39 @@ def test_compact_capacity_exceeded_writes_nothing(codec):
             assert (d == 0xA5).all(), "a writer touched the output buffer past its capacity check"
         else:
             assert np.array_equal(d[:need], np.concatenate(want))
+
+
+def test_compact_long_keys_many_windows(codec, oracle):
+    """Keys longer than the 16 B sort prefix, all sharing it (every merge
+    comparison falls back to the source bytes), over 10 inputs (two merge
+    passes, many merge windows and filter tiles), overlapping keys across
+    inputs (drops) and one input duplicated (equal (key, txn) runs that the
+    filter walks back through, across tile boundaries)."""
+    rng = np.random.default_rng(5)
+    sets = []
+    txn = 1
+    for t in range(10):
+        n = 3000
+        idx = np.sort(rng.choice(9000, n, replace=False))
+        keys = [b"SHARED-PREFIX-16" + b"%08d" % i + (b"x" * int(i % 7)) for i in idx]  # 24..30 B
+        vals = [bytes(rng.integers(0, 256, int(rng.integers(0, 40)), dtype=np.uint8)) for _ in range(n)]
+        rec = {"type": (rng.random(n) < 0.1).astype(np.uint8),
+               "key_len": np.array([len(k) for k in keys], np.uint32),
+               "val_len": np.array([len(v) for v in vals], np.uint32),
+               "txn": np.arange(txn, txn + n, dtype=np.uint64)[rng.permutation(n)],
+               "key_off": np.cumsum([0] + [len(k) for k in keys[:-1]]).astype(np.uint64),
+               "val_off": np.cumsum([0] + [len(v) for v in vals[:-1]]).astype(np.uint64),
+               "key_src": np.frombuffer(b"".join(keys), np.uint8).copy(),
+               "val_src": np.frombuffer(b"".join(vals) + b"\0", np.uint8).copy()}
+        rec["val_len"][rec["type"] == 1] = 0xFFFFFFFF  # DELETE: no value fields
+        txn += n
+        sets.append(rec)
+    sets[4] = {key: v.copy() for key, v in sets[3].items()}
+    ins = [oracle.table_build(r, 4096) for r in sets]
+    for base in (1, 0):
+        want, kept = oracle.compact(ins, 4096, 150_000, base)
+        outs, res = codec.compact(ins, 4096, 150_000, base)
+        assert res.records_kept == kept
+        assert len(outs) == len(want)
+        for o, w in zip(outs, want):
+            assert np.array_equal(o, w)
