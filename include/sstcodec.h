@@ -225,7 +225,11 @@ typedef struct sstc_compact_result {
  * section, 40 B footer) back to back into d_dst: table t at d_table_off[t]
  * with d_table_len[t] bytes (TableBuilder::GetFileSize() = d_table_len[t] + 1).
  * d_table_off needs max_tables+1 elements.  This call allocates its own
- * workspace and synchronises the stream (output sizes are data dependent). */
+ * workspace and synchronises the stream (output sizes are data dependent).
+ * Output larger than dst_cap: SSTC_E_CAPACITY with result->bytes_out = the
+ * exact size needed and not one byte of d_dst written (every writer checks
+ * the size on the device); more tables than max_tables: SSTC_E_CAPACITY
+ * before any write to d_dst. */
 int sstc_compact(sstc_ctx *ctx, const uint8_t *d_src, const uint64_t *d_blk_off, const uint64_t *d_blk_len,
                  uint64_t nblocks, const uint64_t *h_table_first_block, uint32_t ntables,
                  const sstc_compact_params *params, uint8_t *d_dst, uint64_t dst_cap, uint64_t *d_table_off,
