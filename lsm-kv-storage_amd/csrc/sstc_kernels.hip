@@ -608,8 +608,8 @@ __global__ void enc_blocks_kernel(const uint64_t *P, const uint64_t *blk_first, 
 // of the entry sizes from the first block's first record) block by block.
 // Three short launches instead of the chained 1.8 M-record look-back scan +
 // the closed-form offsets (config 2 encode leg -4.6 us; one kernel with a
-// thread per block and a look-back over 256-block tiles was 20 us slower:
-// profiles/r02_ab/encode_ab.md).
+// thread per block and a look-back over 256-block tiles was 20 us slower, 5 us
+// slower with the tile's entry sizes staged in LDS: profiles/r02_ab/encode_ab.md).
 constexpr uint32_t kBsG = 8;
 
 __global__ __launch_bounds__(256) void enc_bsum_kernel(const uint32_t *kl, const uint32_t *vl,
