@@ -1265,7 +1265,7 @@ __global__ __launch_bounds__(kEncWaves *kWave) void enc_lds_kernel(EncArgs a) {
 // Few long segments (output tables): seg_hops_kernel, one workgroup hopping
 // along the chain with a 4096-ary search of W per hop.
 // ---------------------------------------------------------------------------
-constexpr uint32_t kChTile = 2048, kChThreads = 256, kChMargin = 256;
+constexpr uint32_t kChTile = 1024, kChThreads = 256, kChMargin = 256;
 constexpr uint32_t kSegRadix = 8;
 constexpr uint32_t kNoNode = 0xFFFFFFFFu;
 
