@@ -617,7 +617,7 @@ __device__ __forceinline__ void put_le(uint8_t *p, uint64_t v, int n) {
 // Entries are assembled in LDS by a thread per block, then every table run of
 // the workgroup's 256 blocks is written with aligned 16 B stores (byte stores
 // straight to HBM from 256 threads at a 56 B stride cost ~10x more).
-constexpr uint32_t kMetaLds = 32768;
+constexpr uint32_t kMetaLds = 24576; // 256 entries of keys up to 32 B (32 KiB: 4 workgroups per CU, 48 -> 45 us at 16 KiB)
 __device__ __forceinline__ void meta_entry(uint8_t *p, uint64_t b, const uint64_t *bf, const uint32_t *btab,
                                            const uint64_t *BL, const uint64_t *blen, const uint64_t *tbf, Rec K,
                                            const uint8_t *src) {
