@@ -1835,7 +1835,7 @@ __global__ __launch_bounds__(kScanThreads) void scan_apply_kernel(In in, uint64_
 // Tiles are numbered by a ticket counter so every tile a workgroup waits on is
 // already resident; the tile that draws the last ticket resets the counter
 // for the next launch.  ws = [ticket, status[tiles]].
-constexpr uint32_t kLbItems = 16, kLbTile = kScanThreads * kLbItems;
+constexpr uint32_t kLbItems = 16;
 
 __device__ __forceinline__ uint32_t lb_idx(uint32_t i) { return i + (i >> 4); } // 1 pad per 16
 
@@ -1975,7 +1975,11 @@ hipError_t launch_decode(const DecArgs &a, hipStream_t s) {
 // sized for the smallest tile any scan uses (kScanThreads x 4 items)
 uint64_t scan_workspace_elems(uint64_t n) { return (n + 4 * kScanThreads - 1) / (4 * kScanThreads) + 2; }
 
-uint64_t scan_status_words(uint64_t n) { return n <= kScanTile ? 0 : (n + kLbTile - 1) / kLbTile + 1; }
+// u64 array scans (block counts, block lengths, segmentation node counts):
+// kArrItems per thread (16 / 8 / 4: the three block-level scans of config 3
+// took 28.4 / 20.9 / 25.9 us); the entry-size scan keeps kLbItems
+constexpr uint32_t kArrItems = 8, kArrTile = kScanThreads * kArrItems;
+uint64_t scan_status_words(uint64_t n) { return n <= kScanTile ? 0 : (n + kArrTile - 1) / kArrTile + 1; }
 
 template <class In, uint32_t kItems = kLbItems>
 static hipError_t scan_any(In in, uint64_t n, uint64_t carry_in, uint64_t *out, uint64_t *ws, hipStream_t s,
@@ -1999,7 +2003,7 @@ static hipError_t scan_any(In in, uint64_t n, uint64_t carry_in, uint64_t *out, 
 
 hipError_t launch_scan(const uint64_t *in, uint64_t n, uint64_t carry_in, uint64_t *out, uint64_t *ws,
                        hipStream_t s, bool ws_zeroed, uint32_t epoch) {
-  return scan_any(ArrIn{in}, n, carry_in, out, ws, s, ws_zeroed, epoch);
+  return scan_any<ArrIn, kArrItems>(ArrIn{in}, n, carry_in, out, ws, s, ws_zeroed, epoch);
 }
 
 hipError_t launch_scan_entry_sizes(const uint32_t *klen, const uint32_t *vlen, uint64_t nrec, uint64_t add,
