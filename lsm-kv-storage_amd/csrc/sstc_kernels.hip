@@ -2028,7 +2028,7 @@ hipError_t launch_enc_offsets(const uint32_t *kl, const uint32_t *vl, const uint
   }
   const uint32_t g = grid_for(nblocks * kBsG, 256);
   enc_bsum_kernel<<<g, 256, 0, s>>>(kl, vl, blk_first, nblocks, blk_len, nbig);
-  hipError_t e = scan_any(ArrIn{blk_len}, nblocks, out_base, blk_off, ws, s, false, epoch);
+  hipError_t e = scan_any<ArrIn, kArrItems>(ArrIn{blk_len}, nblocks, out_base, blk_off, ws, s, false, epoch);
   if (e != hipSuccess) return e;
   enc_prefix_kernel<<<g, 256, 0, s>>>(kl, vl, blk_first, nblocks, blk_off, out_base, P);
   return hipGetLastError();
