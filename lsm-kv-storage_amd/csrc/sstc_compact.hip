@@ -254,16 +254,21 @@ __global__ void ck_kw_win_kernel(const KGroup *groups, uint32_t ngroups, uint32_
     if (j0 != j1) {
       d.out = static_cast<uint32_t>(gr.start[0] + G[gr.base + j0]);
       uint32_t acc = 0;
-      for (uint32_t q = 0; q < k; q++) {
-        const uint32_t lo = C[static_cast<uint64_t>(gr.base + j0) * kKWay + q];
-        const uint32_t hi = C[static_cast<uint64_t>(gr.base + j1) * kKWay + q];
-        d.src[q] = static_cast<uint32_t>(gr.start[q] + lo);
-        d.off[q] = acc;
-        acc += hi - lo;
+#pragma unroll
+      for (uint32_t q = 0; q < kKWay; q++) { // static indices: d stays in registers
+        if (q < k) {
+          const uint32_t lo = C[static_cast<uint64_t>(gr.base + j0) * kKWay + q];
+          const uint32_t hi = C[static_cast<uint64_t>(gr.base + j1) * kKWay + q];
+          d.src[q] = static_cast<uint32_t>(gr.start[q] + lo);
+          d.off[q] = acc;
+          acc += hi - lo;
+        }
       }
       d.n = acc;
     }
-    for (uint32_t q = k; q <= kKWay; q++) d.off[q] = d.n;
+#pragma unroll
+    for (uint32_t q = 0; q <= kKWay; q++)
+      if (q >= k) d.off[q] = d.n;
   }
   win[u] = d;
 }
