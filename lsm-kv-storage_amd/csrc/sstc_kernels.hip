@@ -821,6 +821,38 @@ __device__ __forceinline__ void copy_span(uint8_t *dp, const uint8_t *sp, uint64
   for (uintptr_t x = ce + t; x < d1; x += nt) dp[x - d0] = sp[x - d0];
 }
 
+// The same by one wave (enc_lds_kernel<1>'s blocks past its LDS slot when
+// big_inline): entries one after another, each by the 64 lanes.
+__device__ void enc_emit_block_entries_wave(const EncArgs &a, uint64_t b) {
+  const uint32_t lane = lane_id();
+  const uint64_t f0 = a.blk_first[b], f1 = a.blk_first[b + 1];
+  const uint64_t n = f1 - f0;
+  const uint64_t P0 = a.P[f0];
+  const uint64_t D = a.P[f1] - P0;
+  uint8_t *blk = a.dst + a.out_blk_off[b];
+  for (uint64_t i = 0; i < n; i++) {
+    const uint64_t r = f0 + i;
+    const uint64_t o = a.P[r] - P0, sz = a.P[r + 1] - a.P[r];
+    copy_span(blk + o, a.key_src + a.in.key_off[r] - 5, sz - 8, lane, kWave);
+    if (lane < 8) blk[o + sz - 8 + lane] = static_cast<uint8_t>(a.in.txn[r] >> (8 * lane));
+  }
+  for (uint64_t i = lane; i < n; i += kWave) {
+    const uint64_t st = a.P[f0 + i] - P0, sz = a.P[f0 + i + 1] - a.P[f0 + i];
+    uint8_t *q = blk + D + 16 * i;
+    for (int j = 0; j < 8; j++) {
+      q[j] = static_cast<uint8_t>(st >> (8 * j));
+      q[8 + j] = static_cast<uint8_t>(sz >> (8 * j));
+    }
+  }
+  if (lane == 0) {
+    uint8_t *q = blk + D + 16 * n;
+    for (int j = 0; j < 8; j++) {
+      q[j] = static_cast<uint8_t>(n >> (8 * j));
+      q[8 + j] = static_cast<uint8_t>(D >> (8 * j));
+    }
+  }
+}
+
 __device__ void enc_emit_block_entries(const EncArgs &a, uint64_t b) {
   __shared__ uint32_t s_big[kBigList];
   __shared__ uint32_t s_nbig;
@@ -1215,11 +1247,31 @@ __global__ __launch_bounds__(kEncWaves *kWave) void enc_lds_kernel(EncArgs a) {
   const uint64_t L64 = uniform64(a.out_blk_len[b]);
   const uint32_t pad = static_cast<uint32_t>(bo & 15u);
   if (pad + L64 + 16 > kEncSlot) { // large block
-    if constexpr (kMode == 0) {
-      if (a.big_inline) { // this wave writes it straight to HBM (its LDS image holds the lanes' chunk slots)
-        enc_emit_block<kWave>(a, b, img, lane);
-        return;
+    if (a.big_inline) { // this wave writes it straight to HBM
+      if constexpr (kMode == 0) {
+        enc_emit_block<kWave>(a, b, img, lane); // its LDS image holds the lanes' chunk slots
+      } else {
+        enc_emit_block_entries_wave(a, b);
+        if (a.bmin) { // the block's min / max txn (table footer), reduced by the wave
+          const uint64_t f0 = a.blk_first[b], f1 = a.blk_first[b + 1];
+          uint64_t mn = ~0ull, mx = 0;
+          for (uint64_t r = f0 + lane; r < f1; r += kWave) {
+            const uint64_t x = a.in.txn[r];
+            mn = x < mn ? x : mn;
+            mx = x > mx ? x : mx;
+          }
+          for (uint32_t d = kWave / 2; d > 0; d >>= 1) {
+            const uint64_t x = __shfl_xor(mn, d, kWave), y = __shfl_xor(mx, d, kWave);
+            mn = x < mn ? x : mn;
+            mx = y > mx ? y : mx;
+          }
+          if (lane == 0) {
+            a.bmin[b] = mn;
+            a.bmax[b] = mx;
+          }
+        }
       }
+      return;
     }
     if (a.big && lane == 0) a.big[atomicAdd(a.nbig, 1u)] = static_cast<uint32_t>(b); // enc_emit_kernel
     return;
@@ -2045,7 +2097,7 @@ hipError_t launch_enc_emit(const EncArgs &a, hipStream_t s) {
   if (!a.entries_in_src) enc_lds_kernel<0><<<g, kEncWaves * kWave, 0, s>>>(a);
   else enc_lds_kernel<1><<<g, kEncWaves * kWave, 0, s>>>(a);
   // blocks past an LDS slot: those listed by enc_lds_kernel when a list is given
-  if (a.big_inline && !a.entries_in_src) return hipGetLastError();
+  if (a.big_inline) return hipGetLastError();
   // (a 512-workgroup grid over the list: config 5 275 us, 2048: 208 us)
   const uint64_t cap = 2048;
   enc_emit_kernel<<<static_cast<uint32_t>(a.nblocks < cap ? a.nblocks : cap), kEncThreads, 0, s>>>(a);

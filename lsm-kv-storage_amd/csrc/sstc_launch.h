@@ -73,8 +73,8 @@ struct EncArgs {
   // optional: blocks too large for an LDS slot are listed here by enc_lds_kernel
   // (*nbig zeroed by the caller) so enc_emit_kernel visits only them
   uint32_t *big = nullptr, *nbig = nullptr;
-  // records -> blocks (not entries_in_src): enc_lds_kernel's waves encode the
-  // blocks past their LDS slot themselves, no enc_emit_kernel launch
+  // enc_lds_kernel's waves encode the blocks past their LDS slot themselves
+  // (records -> blocks and compaction alike), no enc_emit_kernel launch
   uint32_t big_inline = 0;
   // optional (compaction, entries_in_src): per-block min / max txn
   uint64_t *bmin = nullptr, *bmax = nullptr;
