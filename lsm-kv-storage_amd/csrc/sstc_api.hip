@@ -304,9 +304,13 @@ int sstc_encode_blocks(sstc_ctx *c, const uint8_t *d_key_src, const uint8_t *d_v
   // P (entry-size prefix) per block, then the block images
   uint32_t ep = 0;
   if (int r = next_epoch(c, ep)) return r;
+  // entry offsets inside each block's wave (p_in_kernel): no P pass
+  // (config-2 encode leg 134.7 -> 127.7 us against the P pass, profiles/r02_ab/encode_ab.md)
   SSTC_HIP(sstc::launch_enc_offsets(in.key_len, in.val_len, d_blk_first, nblocks, out_base, d_out_blk_off,
-                                    d_out_blk_len, c->P, c->blist, c->scan_ws, c->stream, ep), "block offsets");
+                                    d_out_blk_len, nullptr, c->blist, c->scan_ws, c->stream, ep),
+           "block offsets");
   sstc::EncArgs a{d_key_src, d_val_src, in, d_blk_first, nblocks, c->P, d_out_blk_off, d_out_blk_len, d_dst};
+  a.p_in_kernel = 1; // c->P: workspace for the blocks past an LDS slot
   a.nbig = c->blist;
   a.big = c->blist + 1;
   a.big_inline = 1; // blocks past an LDS slot encoded by their own wave (Zipf 64 KiB set: 329 -> 236 us)

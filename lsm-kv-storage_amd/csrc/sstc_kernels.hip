@@ -683,10 +683,13 @@ __device__ void enc_emit_block(const EncArgs &a, uint64_t b, uint8_t *slot, uint
   const uint64_t f0 = a.blk_first[b], f1 = a.blk_first[b + 1];
   const uint64_t n = f1 - f0;
   const uint64_t P0 = a.P[f0];
-  const uint64_t D = a.P[f1] - P0;
   const uint64_t bo = a.out_blk_off[b];
   const uint64_t L = a.out_blk_len[b];
   if ((bo & 15) + L + 16 <= kEncSlot) return; // encoded by enc_lds_kernel
+  // entry bytes from the block length (P[f1] is not read: with p_in_kernel it
+  // belongs to the next block's wave)
+  const uint64_t D = L - 16 * n - 16;
+  auto Pr = [&](uint64_t x) { return x < f1 ? a.P[x] - P0 : D; }; // entry offset, x in [f0, f1]
   uint8_t *dst = a.dst;
   uint8_t *my = slot + 16 * tid;
 
@@ -738,7 +741,7 @@ __device__ void enc_emit_block(const EncArgs &a, uint64_t b, uint8_t *slot, uint
         }
       } else if (x < D + 16 * n) {
         const uint64_t i = (x - D) >> 4, j = (x - D) & 15;
-        const uint64_t val = j < 8 ? a.P[f0 + i] - P0 : a.P[f0 + i + 1] - a.P[f0 + i];
+        const uint64_t val = j < 8 ? Pr(f0 + i) : Pr(f0 + i + 1) - Pr(f0 + i);
         v = static_cast<uint32_t>(val >> (8 * (j & 7))) & 0xFFu;
       } else {
         const uint64_t j = x - D - 16 * n;
@@ -1205,14 +1208,25 @@ __device__ __forceinline__ void enc_copy_split(const EncArgs &a, uint8_t *img, u
   const uint32_t lane = lane_id();
   uint8_t *im = img + pad;
   const u32x4 *safe = reinterpret_cast<const u32x4 *>(a.P); // a valid address for masked-off loads
+  uint32_t carry = 0; // p_in_kernel: entry bytes of the rounds before
   for (uint32_t c0 = 0; c0 < n; c0 += kWave) {
     const uint32_t nc = n - c0 < kWave ? n - c0 : kWave;
     const uint64_t r = f0 + c0 + (lane < nc ? lane : 0u);
-    const uint64_t pr = a.P[r], pr1 = a.P[r + 1];
+    const bool on = lane < nc;
+    uint32_t o, sz;
+    if (a.p_in_kernel) { // offsets by a wave scan of the entry sizes (no P pass over HBM)
+      const uint32_t kl0 = a.in.key_len[r], vl0 = a.in.val_len[r];
+      sz = on ? static_cast<uint32_t>(entry_size(kl0, vl0)) : 0u;
+      const uint32_t inc = wave_incl_scan_u32(sz);
+      o = carry + inc - sz;
+      carry += __shfl(inc, kWave - 1, kWave);
+    } else {
+      const uint64_t pr = a.P[r], pr1 = a.P[r + 1];
+      o = static_cast<uint32_t>(pr - P0);
+      sz = static_cast<uint32_t>(pr1 - pr);
+    }
     const uint32_t kl = a.in.key_len[r], vl = a.in.val_len[r], ty = a.in.type[r];
     const uint64_t ko = a.in.key_off[r], vo = a.in.val_off[r], tx = a.in.txn[r];
-    const uint32_t o = static_cast<uint32_t>(pr - P0), sz = static_cast<uint32_t>(pr1 - pr);
-    const bool on = lane < nc;
     copy_spans<GK, kQ>(a.key_src, img, dummy, nc, ko, on ? kl : 0u, pad + o + 5, safe);
     const uint32_t vlen = on && vl != kNoValue ? vl : 0u;
     copy_spans<GV, kQ>(a.val_src, img, dummy, nc, vlen ? vo : 0ull, vlen, pad + o + 9 + kl, safe);
@@ -1229,6 +1243,25 @@ __device__ __forceinline__ void enc_copy_split(const EncArgs &a, uint8_t *img, u
       lds_st_u64u(im, D + 16 * (c0 + lane) + 8, sz);
     }
   }
+}
+
+// p_in_kernel, a block past its LDS slot: its wave writes the block-relative
+// entry offsets P[f0 .. f1) (a workspace no other block touches) for
+// enc_emit_block, which reads them back from other lanes
+__device__ void enc_wave_offsets(const EncArgs &a, uint64_t b) {
+  uint64_t *P = const_cast<uint64_t *>(a.P);
+  const uint32_t lane = lane_id();
+  const uint64_t f0 = a.blk_first[b], n = a.blk_first[b + 1] - f0;
+  uint64_t carry = 0;
+  for (uint64_t c0 = 0; c0 < n; c0 += kWave) {
+    const bool on = c0 + lane < n;
+    const uint64_t r = f0 + c0 + (on ? lane : 0u);
+    const uint64_t sz = on ? entry_size(a.in.key_len[r], a.in.val_len[r]) : 0ull;
+    const uint64_t inc = wave_incl_scan_u64(sz);
+    if (on) P[r] = carry + inc - sz;
+    carry += __shfl(inc, kWave - 1, kWave);
+  }
+  __threadfence_block(); // the stores complete before any lane of the wave reads them (same CU)
 }
 
 // kMode 0: two arenas (key spans in groups of GK lanes, then value spans in
@@ -1249,6 +1282,7 @@ __global__ __launch_bounds__(kEncWaves *kWave) void enc_lds_kernel(EncArgs a) {
   if (pad + L64 + 16 > kEncSlot) { // large block
     if (a.big_inline) { // this wave writes it straight to HBM
       if constexpr (kMode == 0) {
+        if (a.p_in_kernel) enc_wave_offsets(a, b);
         enc_emit_block<kWave>(a, b, img, lane); // its LDS image holds the lanes' chunk slots
       } else {
         enc_emit_block_entries_wave(a, b);
@@ -1279,8 +1313,9 @@ __global__ __launch_bounds__(kEncWaves *kWave) void enc_lds_kernel(EncArgs a) {
   const uint32_t L = static_cast<uint32_t>(L64);
   const uint64_t f0 = uniform64(a.blk_first[b]);
   const uint32_t n = static_cast<uint32_t>(uniform64(a.blk_first[b + 1]) - f0);
-  const uint64_t P0 = uniform64(a.P[f0]);
-  const uint32_t D = static_cast<uint32_t>(uniform64(a.P[f0 + n]) - P0);
+  const uint64_t P0 = kMode == 0 && a.p_in_kernel ? 0ull : uniform64(a.P[f0]);
+  const uint32_t D = kMode == 0 && a.p_in_kernel ? L - 16u * n - 16u
+                                                 : static_cast<uint32_t>(uniform64(a.P[f0 + n]) - P0);
   uint8_t *im = img + pad; // image byte 0 == block byte 0
 
   if constexpr (kMode == 1) {
@@ -2082,7 +2117,7 @@ hipError_t launch_enc_offsets(const uint32_t *kl, const uint32_t *vl, const uint
   enc_bsum_kernel<<<g, 256, 0, s>>>(kl, vl, blk_first, nblocks, blk_len, nbig);
   hipError_t e = scan_any<ArrIn, kArrItems>(ArrIn{blk_len}, nblocks, out_base, blk_off, ws, s, false, epoch);
   if (e != hipSuccess) return e;
-  enc_prefix_kernel<<<g, 256, 0, s>>>(kl, vl, blk_first, nblocks, blk_off, out_base, P);
+  if (P) enc_prefix_kernel<<<g, 256, 0, s>>>(kl, vl, blk_first, nblocks, blk_off, out_base, P);
   return hipGetLastError();
 }
 

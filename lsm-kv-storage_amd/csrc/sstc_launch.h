@@ -64,7 +64,7 @@ struct EncArgs {
   sstc_records in;
   const uint64_t *blk_first;
   uint64_t nblocks;
-  const uint64_t *P; // exclusive scan of entry sizes, nrec+1
+  const uint64_t *P; // exclusive scan of entry sizes, nrec+1 (see p_in_kernel)
   const uint64_t *out_blk_off;
   const uint64_t *out_blk_len;
   uint8_t *dst;
@@ -81,6 +81,10 @@ struct EncArgs {
   // optional capacity guard (compaction): nothing is written when *need > cap
   const uint64_t *need = nullptr;
   uint64_t cap = 0;
+  // records -> blocks (mode 0): the entry offsets are scanned inside the block's
+  // wave (P is not read); P is then a workspace the wave fills with block-
+  // relative offsets for a block past its LDS slot (entries [f0, f1) only)
+  uint32_t p_in_kernel = 0;
   __device__ bool over() const { return need && *need > cap; }
 };
 
@@ -129,8 +133,8 @@ hipError_t launch_scan_entry_sizes(const uint32_t *klen, const uint32_t *vlen, u
 hipError_t launch_enc_blocks(const uint64_t *P, const uint64_t *blk_first, uint64_t nblocks, uint64_t out_base,
                              uint64_t *blk_off, uint64_t *blk_len, uint32_t *nbig, hipStream_t s);
 // the same without a record scan: block lengths by reduction, a scan over the
-// blocks, then P (entry-size prefix, P[blk_first[0]] = 0) written per block;
-// clears *nbig
+// blocks, then P (entry-size prefix, P[blk_first[0]] = 0) written per block
+// unless P is null (EncArgs::p_in_kernel); clears *nbig
 hipError_t launch_enc_offsets(const uint32_t *kl, const uint32_t *vl, const uint64_t *blk_first, uint64_t nblocks,
                               uint64_t out_base, uint64_t *blk_off, uint64_t *blk_len, uint64_t *P, uint32_t *nbig,
                               uint64_t *ws, hipStream_t s, uint32_t epoch);
