@@ -796,22 +796,29 @@ struct Words {
   uint32_t n;
 };
 
-__global__ void ck_pack_kernel(Words w, uint64_t *out) {
+// words w, then arr[0..narr), to the pinned host words; then the sequence
+// number at out[flag] once every word has landed (the host spins on it)
+__global__ __launch_bounds__(256) void ck_pack_kernel(Words w, const uint64_t *arr, uint64_t narr, uint64_t *out,
+                                                      uint64_t seq, uint64_t flag) {
   if (threadIdx.x < w.n) out[threadIdx.x] = *w.p[threadIdx.x];
+  for (uint64_t i = threadIdx.x; i < narr; i += 256) out[w.n + i] = arr[i];
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(out + flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // run starts (record index of every input table's first block) to the device
-// and to the pinned host words; thread 0 also snapshots the context's decode
+// (fetched to the host by the pack kernel); thread 0 also snapshots the context's decode
 // error counter and clears the unsorted count for this job
 __global__ void ck_run_starts_kernel(const uint64_t *rec_base, const uint64_t *tfb, uint64_t n, uint64_t *out,
-                                     uint64_t *host, const unsigned long long *err_count, uint64_t *errs,
+                                     const unsigned long long *err_count, uint64_t *errs,
                                      unsigned long long *bad) {
   const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (i == 0) {
     *errs = *err_count;
     *bad = 0;
   }
-  if (i < n) out[i] = host[i] = rec_base[tfb[i]];
+  if (i < n) out[i] = rec_base[tfb[i]];
 }
 
 // pinned, device-mapped, coherent host words: kernels store the job's few
@@ -831,16 +838,38 @@ void ensure_host(Arena &arena, uint64_t words) {
     arena.host_dev = nullptr;
     throw std::runtime_error("pinned host words");
   }
+  memset(arena.host, 0, cap * sizeof(uint64_t)); // no stale word can equal a sequence number
   arena.host_cap = cap;
 }
 
-// device words -> pinned host words: one pack kernel, one sync
-void fetch(Arena &arena, hipStream_t s, std::initializer_list<const uint64_t *> src) {
-  ensure_host(arena, 64);
+// device words (+ an optional array after them) -> pinned host words: one
+// pack kernel, then the host spins on the sequence word the kernel stores
+// last instead of a stream synchronize (each of the job's mid-job syncs cost
+// ~20-35 us of idle GPU with hipStreamSynchronize); `complete` also waits for
+// the stream to drain (the job's last fetch: the call returns with its work done)
+void fetch(Arena &arena, hipStream_t s, std::initializer_list<const uint64_t *> src, const uint64_t *arr = nullptr,
+           uint64_t narr = 0, bool complete = false) {
+  ensure_host(arena, 8 + narr + 1);
   Words w{};
   for (const uint64_t *p : src) w.p[w.n++] = p;
-  ck_pack_kernel<<<1, 64, 0, s>>>(w, arena.host_dev);
-  CK(hipStreamSynchronize(s));
+  const uint64_t flag = arena.host_cap - 1, seq = ++arena.seq;
+  ck_pack_kernel<<<1, 256, 0, s>>>(w, arr, narr, arena.host_dev, seq, flag);
+  CK(hipGetLastError());
+  if (complete) {
+    CK(hipStreamSynchronize(s));
+    return;
+  }
+  for (uint64_t it = 1;; it++) {
+    if (__atomic_load_n(arena.host + flag, __ATOMIC_ACQUIRE) == seq) return;
+    if ((it & 255) == 0) { // a failed stream never stores the word
+      const hipError_t q = hipStreamQuery(s);
+      if (q == hipSuccess) {
+        if (__atomic_load_n(arena.host + flag, __ATOMIC_ACQUIRE) == seq) return;
+        throw std::runtime_error("pack kernel finished without its sequence word");
+      }
+      if (q != hipErrorNotReady) throw std::runtime_error(hipGetErrorString(q));
+    }
+  }
 }
 
 } // namespace
@@ -869,10 +898,8 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     unsigned long long *bad = reinterpret_cast<unsigned long long *>(pool.get<uint64_t>(1));
     // record index of every input table's first record (its run start)
     CK(hipMemcpyAsync(d_tfb, h_tfb, (ntables + 1) * 8, hipMemcpyHostToDevice, s));
-    ensure_host(arena, ntables + 1);
-    ck_run_starts_kernel<<<grid(ntables + 1), 256, 0, s>>>(rb_all, d_tfb, ntables + 1, d_rs, arena.host_dev,
-                                                           err_count, errs, bad);
-    CK(hipStreamSynchronize(s));
+    ck_run_starts_kernel<<<grid(ntables + 1), 256, 0, s>>>(rb_all, d_tfb, ntables + 1, d_rs, err_count, errs, bad);
+    fetch(arena, s, {}, d_rs, ntables + 1);
     std::vector<uint64_t> run_start(arena.host, arena.host + ntables + 1);
     const uint64_t n = run_start[ntables];
     res[0] = n;
@@ -1046,7 +1073,7 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     ck_tab_minmax_kernel<<<static_cast<uint32_t>(nt * kMmSplit), 256, 0, s>>>(tbf, bmin, bmax, tmin, tmax);
     ck_footer_kernel<<<grid(nt), 256, 0, s>>>(nt, tbf, d_table_off, tdata, tmeta, tmin, tmax, d_dst, dst_cap);
     CK(hipGetLastError());
-    fetch(arena, s, {need});
+    fetch(arena, s, {need}, nullptr, 0, true);
     res[4] = arena.host[0];
     if (res[4] > dst_cap) {
       err = "output buffer too small";

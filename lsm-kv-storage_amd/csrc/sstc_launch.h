@@ -155,6 +155,7 @@ struct Arena {
   uint64_t *host = nullptr;     // pinned host words: the job's few device -> host reads
   uint64_t *host_dev = nullptr; // the same words as mapped into the device
   uint64_t host_cap = 0;
+  uint64_t seq = 0; // sequence word of the last host fetch (sstc_compact.hip fetch)
 };
 
 int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, const uint8_t *d_src,

@@ -8,5 +8,5 @@ tail -1 gpurun_out/cc/pytest.log
 for c in ${CONFIGS:-3 4}; do
   timeout -k 10 300 rocprofv3 --kernel-trace -d gpurun_out/cc/t$c -o trace --output-format csv -- python3 tools/bench_compact.py --config $c --steps 5 --no-ref --no-files > gpurun_out/cc/b$c.log 2>&1 || { echo "bench $c failed"; tail -20 gpurun_out/cc/b$c.log; exit 4; }
   echo "== config $c $(grep -o '"device_s_median": [0-9.e-]*' gpurun_out/cc/b$c.log) $(grep -o '"matches_reference_fixture": [^]]*' gpurun_out/cc/b$c.log)"
-  python3 tools/trace_compact.py $(find gpurun_out/cc/t$c -name "*kernel_trace.csv" | head -1) > gpurun_out/cc/k$c.txt; head -14 gpurun_out/cc/k$c.txt; tail -1 gpurun_out/cc/k$c.txt
+  python3 tools/trace_compact.py $(find gpurun_out/cc/t$c -name "*kernel_trace.csv" | head -1) > gpurun_out/cc/k$c.txt; grep -A8 "kernel sum" gpurun_out/cc/k$c.txt
 done
