@@ -369,7 +369,7 @@ __global__ __launch_bounds__(kMgThreads) void ck_mg_merge_kernel(const SK *in, S
   for (uint32_t p = threadIdx.x; p < total; p += kMgThreads) o[p] = tile[ix[src][p]];
 }
 
-struct Rec {
+struct Rec { // survivor columns (vl / vo null in the compaction job: unused by its encode)
   uint8_t *type;
   uint32_t *kl, *vl;
   uint64_t *tx, *ko, *vo;
@@ -537,10 +537,11 @@ __global__ __launch_bounds__(kFtThreads) void ck_filter_kernel(const SK *s, uint
       const uint64_t q = base[0] + v[0];
       out.type[q] = static_cast<uint8_t>(ty[j]);
       out.kl[q] = kl[j];
-      out.vl[q] = vl[j];
       out.tx[q] = tx[j];
       out.ko[q] = ko[j];
-      out.vo[q] = ty[j] != kTypeDeleted ? ko[j] + kl[j] + 4 : 0; // decode's val_off
+      // no value length / offset columns: the entry is copied whole from its
+      // input block (enc_lds_kernel<1>), which only reads type, key length,
+      // txn and key offset (12 B per survivor fewer written)
       Pd[q] = base[1] + v[1];
       Pe[q] = base[2] + v[2];
     }
@@ -1007,8 +1008,8 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     // 3. keep / drop and the survivors gathered in merge order with their
     // prefix sums (sized by n: the kept count is known after the pass)
     uint64_t *totals = pool.get<uint64_t>(3);
-    Rec KR{pool.get<uint8_t>(n), pool.get<uint32_t>(n), pool.get<uint32_t>(n), pool.get<uint64_t>(n),
-           pool.get<uint64_t>(n), pool.get<uint64_t>(n)};
+    Rec KR{pool.get<uint8_t>(n), pool.get<uint32_t>(n), nullptr, pool.get<uint64_t>(n), pool.get<uint64_t>(n),
+           nullptr}; // vl / vo: not needed by the whole-entry encode
     uint64_t *Pd = pool.get<uint64_t>(n + 1), *Pe = pool.get<uint64_t>(n + 1);
     ck_filter_kernel<<<static_cast<uint32_t>(fftiles), kFtThreads, 0, s>>>(A, n, kv, base_level, KR, Pd, Pe, ffws,
                                                                         totals, stop);
