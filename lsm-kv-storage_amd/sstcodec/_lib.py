@@ -8,7 +8,8 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 PKG_ROOT = os.path.dirname(HERE)
-LIB_PATH = os.path.join(PKG_ROOT, "lib", "libsstcodec.so")
+# SSTC_LIB_PATH: an A/B build of the same library (tools/ab_*.sh); default the in-tree build
+LIB_PATH = os.environ.get("SSTC_LIB_PATH") or os.path.join(PKG_ROOT, "lib", "libsstcodec.so")
 HEADER = os.path.join(os.path.dirname(PKG_ROOT), "include", "sstcodec.h")
 
 SSTC_OK = 0
