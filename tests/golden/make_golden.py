@@ -108,6 +108,8 @@ def main():
     ref = RefLib()
     if sys.argv[1:] == ["ties"]:
         return tie_fixtures(ref)
+    if sys.argv[1:] == ["compaction"]:
+        return compaction_fixtures(ref)
 
     # 1. tests/test_block.cc:57-138 (BasicEncode) and :140-187 (EdgeCasesEncode)
     basic = records_from_list([(0, b"apple", b"value1", 12345), (0, b"apply", b"success", 9876),
@@ -175,6 +177,11 @@ COMPACTION_CASES = [
     # config 5 shape: Zipf(1.1) values clamped to [8 B, 64 KiB]
     # (entries far above the 4 KiB block threshold), ~50 % key overlap, 10 % DELETE
     ("zipf", 4, 600, 1200, 65536, 4 << 20, True, {"vmin": 8, "zipf": 1.1, "p_delete": 0.1}),
+    # the other end of SST_BLOCK_SIZE's valid range (db/config.cc:89-94): 32 KiB
+    # blocks of ~100 small entries (past the encode's LDS slot: the large-block
+    # path) and 16 KiB blocks with overlapping keys and DELETEs
+    ("blk32k", 6, 3000, 9000, 300, 600_000, True, {"block_threshold": 32768}),
+    ("blk16k", 5, 2500, 4000, 900, 1 << 20, True, {"block_threshold": 16384, "p_delete": 0.2}),
 ]
 
 
@@ -185,21 +192,23 @@ def compaction_fixtures(ref):
     case is stored byte for byte, the others as SHA-256 + GetFileSize()."""
     manifest = {}
     for name, k, n, ks, vmax, limit, distinct, gen in COMPACTION_CASES:
+        gen = dict(gen)
+        T = gen.pop("block_threshold", 4096)
         sets = W.compaction_inputs(k, n, ks, vmax=vmax, distinct=distinct, **gen)
         with tempfile.TemporaryDirectory() as td:
             ins = []
             for i, rec in enumerate(sets):
                 p = os.path.join(td, f"in{i}.sst")
-                fs = ref.table_build(p, rec, 4096)
+                fs = ref.table_build(p, rec, T)
                 ins.append((p, fs))
             case = {"k": k, "n_per": n, "key_space": ks, "vmax": vmax, "table_limit": limit,
-                    "distinct": distinct, "block_threshold": 4096, "gen": gen,
+                    "distinct": distinct, "block_threshold": T, "gen": gen,
                     "inputs": [{"sha256": hashlib.sha256(open(p, "rb").read()).hexdigest(), "file_size": fs}
                                for p, fs in ins]}
             for base in (1, 0):
                 od = os.path.join(td, f"out{base}")
                 os.makedirs(od)
-                outs = ref_compact(ins, od, 4096, limit, base)
+                outs = ref_compact(ins, od, T, limit, base)
                 case[f"outputs_base{base}"] = [
                     {"sha256": hashlib.sha256(open(p, "rb").read()).hexdigest(), "file_size": fs}
                     for p, fs in outs]

@@ -32,10 +32,10 @@ def write(tmp_path, files):
     return args
 
 
-def run_loop(tmp_path, files, limit, base):
+def run_loop(tmp_path, files, limit, base, block_size=4096):
     od = tmp_path / f"out{base}"
     od.mkdir(exist_ok=True)
-    r = subprocess.run([EXE, str(od), "4096", str(limit), str(base)] + write(tmp_path, files), capture_output=True,
+    r = subprocess.run([EXE, str(od), str(block_size), str(limit), str(base)] + write(tmp_path, files), capture_output=True,
                        text=True, timeout=120)
     assert r.returncode == 0, r.stderr
     outs = []
@@ -57,7 +57,7 @@ def test_cpp_compact_loop_matches_reference(oracle, tmp_path, name, base):
     sets = W.compaction_inputs(case["k"], case["n_per"], case["key_space"], vmax=case["vmax"],
                                distinct=case["distinct"], **case.get("gen", {}))
     files = [oracle.table_build(r, case["block_threshold"]) for r in sets]
-    outs = run_loop(tmp_path, files, case["table_limit"], base)
+    outs = run_loop(tmp_path, files, case["table_limit"], base, case["block_threshold"])
     want = case[f"outputs_base{base}"]
     assert len(outs) == len(want)
     for (img, fs), w in zip(outs, want):
