@@ -953,11 +953,35 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     std::vector<uint32_t> pass_groups, pass_ids, pass_wgs;
     {
       std::vector<uint64_t> cur = run_start;
+      // passes: ceil(log8 runs), each pass as narrow as that allows (the
+      // splitter search grows with k^2): 128 runs merge as 4, 4, 8 instead of
+      // 8, 8, 2 (config 4 splitters 310 -> 257 us, merge unchanged)
+      auto passes_for = [](size_t runs) {
+        uint32_t p = 0;
+        for (size_t c = 1; c < runs; c *= kKWay) p++;
+        return p;
+      };
       while (cur.size() > 2) {
         std::vector<uint64_t> next;
         uint32_t ids = 0, wgs = 0, ng = 0;
-        for (size_t r0 = 0; r0 + 1 < cur.size(); r0 += kKWay) {
-          const uint32_t k = static_cast<uint32_t>(std::min<size_t>(kKWay, cur.size() - 1 - r0));
+        size_t way = kKWay;
+        {
+          const size_t runs = cur.size() - 1;
+          const uint32_t P = passes_for(runs);
+          // the largest power of two <= runs^(1/P), doubled until the
+          // remaining passes still suffice (128 runs: 4, 4, 8 instead of 8, 8, 2)
+          size_t w = 2;
+          while (w * 2 <= kKWay) {
+            size_t pw = 1;
+            for (uint32_t q = 0; q < P; q++) pw *= w * 2;
+            if (pw > runs) break;
+            w *= 2;
+          }
+          while (w < kKWay && passes_for((runs + w - 1) / w) + 1 > P) w *= 2;
+          way = w;
+        }
+        for (size_t r0 = 0; r0 + 1 < cur.size(); r0 += way) {
+          const uint32_t k = static_cast<uint32_t>(std::min<size_t>(way, cur.size() - 1 - r0));
           KGroup g{};
           g.nruns = k;
           g.stride = kKWin / k;
