@@ -381,32 +381,6 @@ struct Rec { // survivor columns (vl / vo null in the compaction job: unused by 
 // loads and stores coalesce.
 constexpr uint32_t kFtThreads = 256;
 
-// exclusive scan of three u64 per thread over the workgroup; tot = totals
-__device__ __forceinline__ void wg_scan3(uint64_t (&v)[3], uint64_t (&tot)[3]) {
-  __shared__ uint64_t sw[3][kFtThreads / kWave];
-  const uint32_t lane = lane_id(), w = threadIdx.x / kWave;
-  uint64_t inc[3];
-#pragma unroll
-  for (int c = 0; c < 3; c++) {
-    inc[c] = wave_incl_scan_u64(v[c]);
-    if (lane == kWave - 1) sw[c][w] = inc[c];
-  }
-  __syncthreads();
-#pragma unroll
-  for (int c = 0; c < 3; c++) {
-    uint64_t base = 0, t = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < kFtThreads / kWave; k++) {
-      const uint64_t x = sw[c][k];
-      if (k < w) base += x;
-      t += x;
-    }
-    v[c] = base + inc[c] - v[c];
-    tot[c] = t;
-  }
-  __syncthreads();
-}
-
 // data_size increment (table_builder.cc:55)
 __device__ __forceinline__ uint64_t data_bytes(uint32_t kl, uint32_t vl) {
   return static_cast<uint64_t>(kl) + (vl != kNoValue ? vl : 0u);
@@ -458,7 +432,6 @@ __global__ __launch_bounds__(kFtThreads) void ck_filter_kernel(const SK *s, uint
   constexpr uint32_t kGroup = 4; // rows whose loads are in flight together
   uint32_t km = 0, kl[kFfRows], vl[kFfRows], ty[kFfRows];
   uint64_t tx[kFfRows], ko[kFfRows];
-  uint64_t sum[3] = {0, 0, 0};
 #pragma unroll
   for (uint32_t j0 = 0; j0 < kFfRows; j0 += kGroup) {
     SK x[kGroup], pv[kGroup];
@@ -485,18 +458,30 @@ __global__ __launch_bounds__(kFtThreads) void ck_filter_kernel(const SK *s, uint
       vl[j] = rr[g].vl;
       ty[j] = rr[g].type;
       ko[j] = rr[g].ko;
-      if (k) {
-        sum[0] += 1;
-        sum[1] += data_bytes(kl[j], vl[j]);
-        sum[2] += entry_size(kl[j], vl[j]);
-      }
     }
   }
-  uint64_t tot[3];
-  wg_scan3(sum, tot); // only the tile totals are used here
+  // per row and wave: kept count and the two byte sums by wave reductions,
+  // exchanged once through LDS for the whole tile (one barrier instead of two
+  // per row of a workgroup scan)
+  __shared__ uint64_t s_row[kFfRows][kFtThreads / kWave][3];
+#pragma unroll
+  for (uint32_t j = 0; j < kFfRows; j++) {
+    const bool k = (km >> j) & 1u;
+    const uint64_t c = static_cast<uint64_t>(__popcll(__ballot(k)));
+    const uint64_t d = wave_sum_u64(k ? data_bytes(kl[j], vl[j]) : 0ull);
+    const uint64_t e = wave_sum_u64(k ? entry_size(kl[j], vl[j]) : 0ull);
+    if (lane == 0) {
+      s_row[j][w][0] = c;
+      s_row[j][w][1] = d;
+      s_row[j][w][2] = e;
+    }
+  }
+  __syncthreads();
   if (w < 3) { // wave c: decoupled look-back of total c
     uint64_t *status = ws + 1 + static_cast<uint64_t>(w) * gridDim.x;
-    const uint64_t total = tot[w];
+    constexpr uint32_t kRW = kFfRows * (kFtThreads / kWave);
+    const uint64_t total =
+        wave_sum_u64(lane < kRW ? s_row[lane / (kFtThreads / kWave)][lane % (kFtThreads / kWave)][w] : 0ull);
     uint64_t prefix = 0;
     if (tile == 0) {
       if (lane == 0) __hip_atomic_store(&status[0], kLbInc | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -530,11 +515,23 @@ __global__ __launch_bounds__(kFtThreads) void ck_filter_kernel(const SK *s, uint
 #pragma unroll
   for (uint32_t j = 0; j < kFfRows; j++) { // row by row: survivors of a row are lane-consecutive
     const bool k = (km >> j) & 1u;
-    uint64_t v[3] = {k ? 1ull : 0ull, k ? data_bytes(kl[j], vl[j]) : 0ull, k ? entry_size(kl[j], vl[j]) : 0ull};
-    uint64_t rt[3];
-    wg_scan3(v, rt);
-    if (k) {
-      const uint64_t q = base[0] + v[0];
+    uint64_t off[3] = {base[0], base[1], base[2]}, rt[3] = {0, 0, 0};
+#pragma unroll
+    for (uint32_t x = 0; x < kFtThreads / kWave; x++) { // waves before this one in the row
+#pragma unroll
+      for (int c = 0; c < 3; c++) {
+        const uint64_t y = s_row[j][x][c];
+        off[c] += x < w ? y : 0ull;
+        rt[c] += y;
+      }
+    }
+    const uint64_t bal = __ballot(k);
+    const uint32_t rank = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(bal >> 32),
+                                                    __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(bal), 0u));
+    const uint64_t dv = k ? data_bytes(kl[j], vl[j]) : 0ull, ev = k ? entry_size(kl[j], vl[j]) : 0ull;
+    const uint64_t dincl = wave_incl_scan_u64(dv), eincl = wave_incl_scan_u64(ev);
+    const uint64_t q = off[0] + rank;
+    if (k && q < n) { // (q < n holds by construction; the bound guards the stores)
       out.type[q] = static_cast<uint8_t>(ty[j]);
       out.kl[q] = kl[j];
       out.tx[q] = tx[j];
@@ -542,15 +539,17 @@ __global__ __launch_bounds__(kFtThreads) void ck_filter_kernel(const SK *s, uint
       // no value length / offset columns: the entry is copied whole from its
       // input block (enc_lds_kernel<1>), which only reads type, key length,
       // txn and key offset (12 B per survivor fewer written)
-      Pd[q] = base[1] + v[1];
-      Pe[q] = base[2] + v[2];
+      Pd[q] = off[1] + dincl - dv;
+      Pe[q] = off[2] + eincl - ev;
     }
 #pragma unroll
     for (int c = 0; c < 3; c++) base[c] += rt[c];
   }
   if (tid == 0 && t0 + kFfTile >= n) { // the last tile: grand totals and the closing prefix sums
-    Pd[base[0]] = base[1];
-    Pe[base[0]] = base[2];
+    if (base[0] <= n) {
+      Pd[base[0]] = base[1];
+      Pe[base[0]] = base[2];
+    }
     totals[0] = base[0];
     totals[1] = base[1];
     totals[2] = base[2];
