@@ -824,6 +824,63 @@ __device__ __forceinline__ void copy_span(uint8_t *dp, const uint8_t *sp, uint64
   for (uintptr_t x = ce + t; x < d1; x += nt) dp[x - d0] = sp[x - d0];
 }
 
+// copy_span by one wave with kU chunks per lane in flight: the right-hand
+// source chunk of lane l's funnel shift is lane l + 1's own chunk (a shuffle),
+// for lane 63 lane 0's chunk of the next group (a broadcast), and after the
+// last group one extra chunk every lane loads (the same address): one load per
+// 16 B instead of two.  kU = 4 (config 5 encode 232 -> 224 us); kU = 8 is
+// faster on config 5 (210 us) but its 98 VGPRs cost enc_lds_kernel<1> a wave
+// per SIMD: config 3 encode 500 -> 624 us (profiles/r02_ab/encode_ab.md)
+constexpr uint32_t kWaveSpanUnroll = 4;
+template <uint32_t kU>
+__device__ __forceinline__ void copy_span_wave(uint8_t *dp, const uint8_t *sp, uint64_t len) {
+  const uint32_t lane = lane_id();
+  const uintptr_t d0 = reinterpret_cast<uintptr_t>(dp), d1 = d0 + len;
+  const uintptr_t cb = (d0 + 15) & ~static_cast<uintptr_t>(15), ce = d1 & ~static_cast<uintptr_t>(15);
+  if (cb >= ce) {
+    for (uint64_t x = lane; x < len; x += kWave) dp[x] = sp[x];
+    return;
+  }
+  const uint64_t nch = (ce - cb) >> 4;
+  const uint8_t *s0 = sp + (cb - d0);
+  const uint32_t sh = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(s0) & 15u);
+  const u32x4 *sa = reinterpret_cast<const u32x4 *>(s0 - sh);
+  u32x4 *da = reinterpret_cast<u32x4 *>(cb);
+  for (uint64_t k0 = 0; k0 < nch; k0 += static_cast<uint64_t>(kWave) * kU) {
+    u32x4 v[kU + 1];
+#pragma unroll
+    for (uint32_t u = 0; u < kU; u++) { // clamped at nch: sa[nch] is inside the read allowance
+      const uint64_t k = k0 + static_cast<uint64_t>(u) * kWave + lane;
+      v[u] = sa[k < nch ? k : nch];
+    }
+    const uint64_t kn = k0 + static_cast<uint64_t>(kU) * kWave;
+    v[kU] = sa[kn < nch ? kn : nch];
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (uint32_t u = 0; u < kU; u++) {
+      u32x4 nx;
+      nx.x = __shfl_down(v[u].x, 1u, kWave);
+      nx.y = __shfl_down(v[u].y, 1u, kWave);
+      nx.z = __shfl_down(v[u].z, 1u, kWave);
+      nx.w = __shfl_down(v[u].w, 1u, kWave);
+      u32x4 nl;
+      if (u + 1 < kU) {
+        nl.x = __shfl(v[u + 1].x, 0, kWave);
+        nl.y = __shfl(v[u + 1].y, 0, kWave);
+        nl.z = __shfl(v[u + 1].z, 0, kWave);
+        nl.w = __shfl(v[u + 1].w, 0, kWave);
+      } else {
+        nl = v[kU];
+      }
+      if (lane == kWave - 1) nx = nl;
+      const uint64_t k = k0 + static_cast<uint64_t>(u) * kWave + lane;
+      if (k < nch) __builtin_nontemporal_store(funnel16(v[u], nx, sh), da + k);
+    }
+  }
+  for (uintptr_t x = d0 + lane; x < cb; x += kWave) dp[x - d0] = sp[x - d0];
+  for (uintptr_t x = ce + lane; x < d1; x += kWave) dp[x - d0] = sp[x - d0];
+}
+
 // The same by one wave (enc_lds_kernel<1>'s blocks past its LDS slot when
 // big_inline): entries one after another, each by the 64 lanes.
 __device__ void enc_emit_block_entries_wave(const EncArgs &a, uint64_t b) {
@@ -836,7 +893,7 @@ __device__ void enc_emit_block_entries_wave(const EncArgs &a, uint64_t b) {
   for (uint64_t i = 0; i < n; i++) {
     const uint64_t r = f0 + i;
     const uint64_t o = a.P[r] - P0, sz = a.P[r + 1] - a.P[r];
-    copy_span(blk + o, a.key_src + a.in.key_off[r] - 5, sz - 8, lane, kWave);
+    copy_span_wave<kWaveSpanUnroll>(blk + o, a.key_src + a.in.key_off[r] - 5, sz - 8);
     if (lane < 8) blk[o + sz - 8 + lane] = static_cast<uint8_t>(a.in.txn[r] >> (8 * lane));
   }
   for (uint64_t i = lane; i < n; i += kWave) {
