@@ -460,7 +460,13 @@ int sstc_compact(sstc_ctx *c, const uint8_t *d_src, const uint64_t *d_blk_off, c
   result->blocks_out = res[2];
   result->tables_out = res[3];
   result->bytes_out = res[4];
-  if (rc != SSTC_OK) return fail(rc, ("sstc_compact: " + err).c_str());
+  if (rc != SSTC_OK) {
+    // an error return can follow a mid-job fetch, which waits on the pack
+    // kernel's sequence word rather than the stream: drain it so the call
+    // returns with the stream idle, as documented
+    (void)hipStreamSynchronize(c->stream);
+    return fail(rc, ("sstc_compact: " + err).c_str());
+  }
   return SSTC_OK;
 }
 
