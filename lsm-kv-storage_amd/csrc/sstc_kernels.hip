@@ -1203,7 +1203,8 @@ __device__ __forceinline__ void emit_chunk_clip(uint8_t *img, uint32_t *dummy, u
 // span.  kQ span groups are loaded before any is stored.
 template <uint32_t G, uint32_t kQ>
 __device__ __forceinline__ void copy_spans(const uint8_t *base, uint8_t *img, uint32_t *dummy, uint32_t nspan,
-                                           uint64_t my_off, uint32_t my_len, uint32_t my_ds, const u32x4 *safe) {
+                                           uint64_t my_off, uint32_t my_len, uint32_t my_ds, const u32x4 *safe,
+                                           u32x4 *tbl) {
   constexpr uint32_t kS = kWave / G;
   const uint32_t lane = lane_id();
   const uint32_t g = lane % G, sub = lane / G;
@@ -1211,6 +1212,11 @@ __device__ __forceinline__ void copy_spans(const uint8_t *base, uint8_t *img, ui
   const uint32_t my_nch = my_len ? ((static_cast<uint32_t>(my_addr & 15u) + my_len + 15u) >> 4) : 0u;
   const bool longs = __any(my_nch > G); // wave-uniform
   const int32_t no = -(1 << 30);
+  // the owners' span tuples in the wave's LDS table: one 16 B broadcast read
+  // per span group instead of four shuffles (config-2 encode leg -1 %,
+  // profiles/r02_ab/encode_ab.md)
+  tbl[lane] = u32x4{static_cast<uint32_t>(my_off), static_cast<uint32_t>(my_off >> 32), my_len, my_ds};
+  wave_lds_sync();
   for (uint32_t p0 = 0; p0 < nspan; p0 += kS * kQ) {
     u32x4 v[kQ];
     const uint8_t *sp_[kQ];
@@ -1219,10 +1225,10 @@ __device__ __forceinline__ void copy_spans(const uint8_t *base, uint8_t *img, ui
     for (uint32_t q = 0; q < kQ; q++) {
       const uint32_t i = p0 + q * kS + sub;
       const int sl = static_cast<int>(i & 63u);
-      const uint32_t olo = __shfl(static_cast<uint32_t>(my_off), sl, kWave);
-      const uint32_t ohi = __shfl(static_cast<uint32_t>(my_off >> 32), sl, kWave);
-      len_[q] = __shfl(my_len, sl, kWave); // 0 for owners >= nspan
-      ds_[q] = __shfl(my_ds, sl, kWave);
+      const u32x4 t = tbl[sl];
+      const uint32_t olo = t.x, ohi = t.y;
+      len_[q] = t.z; // 0 for owners >= nspan
+      ds_[q] = t.w;
       sp_[q] = base + ((static_cast<uint64_t>(ohi) << 32) | olo);
       const uint32_t mis = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(sp_[q]) & 15u);
       const uint32_t nch = len_[q] ? (mis + len_[q] + 15u) >> 4 : 0u;
@@ -1261,7 +1267,7 @@ __device__ __forceinline__ void copy_spans(const uint8_t *base, uint8_t *img, ui
 // the header fields, txn and offset entry (block_builder.cc:36-93).
 template <uint32_t GK, uint32_t GV, uint32_t kQ>
 __device__ __forceinline__ void enc_copy_split(const EncArgs &a, uint8_t *img, uint32_t *dummy, uint32_t pad,
-                                               uint64_t f0, uint32_t n, uint64_t P0, uint32_t D) {
+                                               uint64_t f0, uint32_t n, uint64_t P0, uint32_t D, u32x4 *tbl) {
   const uint32_t lane = lane_id();
   uint8_t *im = img + pad;
   const u32x4 *safe = reinterpret_cast<const u32x4 *>(a.P); // a valid address for masked-off loads
@@ -1284,9 +1290,9 @@ __device__ __forceinline__ void enc_copy_split(const EncArgs &a, uint8_t *img, u
     }
     const uint32_t kl = a.in.key_len[r], vl = a.in.val_len[r], ty = a.in.type[r];
     const uint64_t ko = a.in.key_off[r], vo = a.in.val_off[r], tx = a.in.txn[r];
-    copy_spans<GK, kQ>(a.key_src, img, dummy, nc, ko, on ? kl : 0u, pad + o + 5, safe);
+    copy_spans<GK, kQ>(a.key_src, img, dummy, nc, ko, on ? kl : 0u, pad + o + 5, safe, tbl);
     const uint32_t vlen = on && vl != kNoValue ? vl : 0u;
-    copy_spans<GV, kQ>(a.val_src, img, dummy, nc, vlen ? vo : 0ull, vlen, pad + o + 9 + kl, safe);
+    copy_spans<GV, kQ>(a.val_src, img, dummy, nc, vlen ? vo : 0ull, vlen, pad + o + 9 + kl, safe, tbl);
     if (on) { // header fields, txn, offset entry (after both span passes)
       im[o] = static_cast<uint8_t>(ty);
 #pragma unroll
@@ -1327,6 +1333,7 @@ template <uint32_t kMode, uint32_t GK = 2, uint32_t GV = 8, uint32_t kQ = 2>
 __global__ __launch_bounds__(kEncWaves *kWave) void enc_lds_kernel(EncArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kEncSlotWaves * kEncSlot];
   __shared__ uint32_t s_dummy[kMode == 0 ? kEncWaves * kWave : 1]; // per-lane sink of clipped stores
+  __shared__ u32x4 s_tbl[kMode == 0 ? kEncWaves * kWave : 1]; // span tuples (copy_spans)
   const uint32_t wave = uniform(threadIdx.x / kWave);
   const uint32_t lane = lane_id();
   const uint32_t wg = a.xcd ? xcd_logical_block(blockIdx.x, gridDim.x) : blockIdx.x;
@@ -1378,7 +1385,8 @@ __global__ __launch_bounds__(kEncWaves *kWave) void enc_lds_kernel(EncArgs a) {
   if constexpr (kMode == 1) {
     enc_copy_entries<4>(a, img, pad, f0, n, P0, D, b);
   } else {
-    enc_copy_split<GK, GV, kQ>(a, img, s_dummy + threadIdx.x, pad, f0, n, P0, D);
+    enc_copy_split<GK, GV, kQ>(a, img, s_dummy + threadIdx.x, pad, f0, n, P0, D,
+                               s_tbl + wave * kWave);
   }
   if (lane == 0) {
     lds_st_u64u(im, D + 16 * n, n);
