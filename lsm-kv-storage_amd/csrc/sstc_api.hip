@@ -25,8 +25,6 @@ struct sstc_ctx {
   void *counters = nullptr;                 // 64 B: error counter
   unsigned long long *err_count = nullptr;  // 1
   uint64_t *scan_ws = nullptr;              // cap_scan
-  uint32_t *blist = nullptr;                // cap_blist: encode's large-block list (count, then ids)
-  uint64_t cap_blist = 0;
   uint64_t *P = nullptr;                    // cap_records + 1
   uint32_t *jump = nullptr;                 // cap_jump
   sstc::Arena arena;                        // compaction workspace
@@ -194,7 +192,7 @@ int sstc_ctx_destroy(sstc_ctx *c) {
   }
   if (c->switch_ev) (void)hipEventDestroy(c->switch_ev);
   for (void *p : {c->counters, c->arena.base,
-                  static_cast<void *>(c->scan_ws), static_cast<void *>(c->blist),
+                  static_cast<void *>(c->scan_ws),
                   static_cast<void *>(c->P), static_cast<void *>(c->jump)})
     if (p) (void)hipFree(p);
   delete c;
@@ -298,22 +296,19 @@ int sstc_encode_blocks(sstc_ctx *c, const uint8_t *d_key_src, const uint8_t *d_v
   if (int r = bind_device(c)) return r;
   if (nblocks >= 0xFFFFFFFFull) return fail(SSTC_E_INVALID_ARG, "too many blocks for one call");
   if (int r = ensure_records(c, nrec)) return r;
-  if (int r = grow(c, c->blist, c->cap_blist, nblocks + 2, "block list")) return r;
   if (int r = ensure_scan(c, nblocks + 1)) return r; // the block-length scan's workspace
   // block lengths (entry sizes summed per block), their scan = block offsets,
   // P (entry-size prefix) per block, then the block images
   uint32_t ep = 0;
   if (int r = next_epoch(c, ep)) return r;
-  // entry offsets inside each block's wave (p_in_kernel): no P pass
-  // (config-2 encode leg 134.7 -> 127.7 us against the P pass, profiles/r02_ab/encode_ab.md)
+  // block lengths and offsets; the entry offsets are scanned inside each
+  // block's wave (no P pass: config-2 encode leg 134.7 -> 127.7 us,
+  // profiles/r02_ab/encode_ab.md); c->P is the workspace of the blocks past an
+  // LDS slot, which their own wave encodes (Zipf 64 KiB set 329 -> 236 us)
   SSTC_HIP(sstc::launch_enc_offsets(in.key_len, in.val_len, d_blk_first, nblocks, out_base, d_out_blk_off,
-                                    d_out_blk_len, nullptr, c->blist, c->scan_ws, c->stream, ep),
+                                    d_out_blk_len, c->scan_ws, c->stream, ep),
            "block offsets");
   sstc::EncArgs a{d_key_src, d_val_src, in, d_blk_first, nblocks, c->P, d_out_blk_off, d_out_blk_len, d_dst};
-  a.p_in_kernel = 1; // c->P: workspace for the blocks past an LDS slot
-  a.nbig = c->blist;
-  a.big = c->blist + 1;
-  a.big_inline = 1; // blocks past an LDS slot encoded by their own wave (Zipf 64 KiB set: 329 -> 236 us)
   SSTC_HIP(sstc::launch_enc_emit(a, c->stream), "emit kernel");
   return SSTC_OK;
 }

@@ -605,9 +605,8 @@ __global__ void ck_table_info_kernel(const uint64_t *tf, uint64_t nt, const uint
 }
 
 __global__ void ck_block_off_kernel(const uint32_t *btab, uint64_t nb, const uint64_t *BL, const uint64_t *tbf,
-                                    const uint64_t *toff, uint64_t *bo, uint32_t *nbig) {
+                                    const uint64_t *toff, uint64_t *bo) {
   const uint64_t b = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (b == 0) *nbig = 0; // the encode's large-block list starts empty
   if (b >= nb) return;
   const uint32_t t = btab[b];
   bo[b] = toff[t] + (BL[b] - BL[tbf[t]]);
@@ -1078,14 +1077,11 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     res[2] = nb;
     res[3] = nt;
     uint64_t *bo = pool.get<uint64_t>(nb);
-    uint32_t *big = pool.get<uint32_t>(nb + 1);
-    ck_block_off_kernel<<<grid(nb), 256, 0, s>>>(btab, nb, BL, tbf, d_table_off, bo, big + nb);
+    ck_block_off_kernel<<<grid(nb), 256, 0, s>>>(btab, nb, BL, tbf, d_table_off, bo);
     // 6. encode blocks, meta entries, footers
     EncArgs ea{d_src, d_src, sstc_records{KR.type, KR.kl, KR.vl, KR.tx, KR.ko, KR.vo}, bf, nb, Pe, bo, blen, d_dst, 1};
-    ea.big = big;
-    ea.nbig = big + nb;
     uint64_t *bmin = pool.get<uint64_t>(nb), *bmax = pool.get<uint64_t>(nb);
-    ea.big_inline = 1; // blocks past an LDS slot encoded by the wave that met them (config 5 319 -> 233 us)
+    // blocks past an LDS slot are encoded by the wave that met them (config 5 319 -> 233 us)
     ea.need = need;
     ea.cap = dst_cap;
     uint64_t *tmin = pool.get<uint64_t>(nt * kMmSplit), *tmax = pool.get<uint64_t>(nt * kMmSplit);  // per-table partials

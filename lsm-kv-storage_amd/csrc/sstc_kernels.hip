@@ -578,47 +578,26 @@ __global__ __launch_bounds__(kDecWaves *kWave) void decode_kernel(DecArgs a) {
 // ---------------------------------------------------------------------------
 // Encode: records -> blocks.
 // ---------------------------------------------------------------------------
-// Block sizes and offsets of an encode in closed form: block b holds records
-// [f_b, f_b+1), its bytes are the entries (P = exclusive scan of the entry
-// sizes) + 16 per offset entry + the 16 B extra (block_builder.cc:79-109), so
-// off[b] = out_base + P[f_b] - P[f_0] + 16 (f_b - f_0) + 16 b -- no second scan.
-// off[nblocks] = end of the last block.  Also clears the large-block list.
-__global__ void enc_blocks_kernel(const uint64_t *P, const uint64_t *blk_first, uint64_t nblocks, uint64_t out_base,
-                                  uint64_t *blk_off, uint64_t *blk_len, uint32_t *nbig) {
-  const uint64_t b = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (b == 0 && nbig) *nbig = 0;
-  if (b > nblocks) return;
-  if (nblocks == 0) { // blk_first may be NULL
-    blk_off[0] = out_base;
-    return;
-  }
-  const uint64_t f0 = blk_first[0], fb = blk_first[b];
-  const uint64_t p0 = P[f0], pb = P[fb];
-  blk_off[b] = out_base + (pb - p0) + 16 * (fb - f0) + 16 * b;
-  if (b < nblocks) {
-    const uint64_t f1 = blk_first[b + 1];
-    blk_len[b] = (P[f1] - pb) + 16 * (f1 - fb) + 16;
-  }
-}
+// an encode of no blocks: the offset array's closing entry only
+__global__ void enc_none_kernel(uint64_t out_base, uint64_t *blk_off) { blk_off[0] = out_base; }
 
-// Encode offsets without a scan over the records (reduce, scan the blocks,
-// then write): 8 lanes per block sum its entry sizes (block length = entries
-// + 16 per offset entry + the 16 B extra), a device scan of the block lengths
-// gives the block offsets, and enc_prefix_kernel writes P (exclusive prefix
-// of the entry sizes from the first block's first record) block by block.
-// Three short launches instead of the chained 1.8 M-record look-back scan +
-// the closed-form offsets (config 2 encode leg -4.6 us; one kernel with a
-// thread per block and a look-back over 256-block tiles was 20 us slower, 5 us
-// slower with the tile's entry sizes staged in LDS: profiles/r02_ab/encode_ab.md).
+// Encode offsets without a scan over the records: 8 lanes per block sum its
+// entry sizes (block length = entries + 16 per offset entry + the 16 B extra)
+// and a device scan of the block lengths gives the block offsets; the entry
+// offsets inside a block are scanned by the block's own wave in
+// enc_lds_kernel<0>.  Replaced the chained 1.8 M-record look-back scan + the
+// closed-form offsets (config 2 encode leg -4.6 us; one kernel with a thread
+// per block and a look-back over 256-block tiles was 20 us slower, 5 us slower
+// with the tile's entry sizes staged in LDS; the P pass of enc_prefix 7 us:
+// profiles/r02_ab/encode_ab.md).
 constexpr uint32_t kBsG = 8;
 
 __global__ __launch_bounds__(256) void enc_bsum_kernel(const uint32_t *kl, const uint32_t *vl,
                                                        const uint64_t *blk_first, uint64_t nblocks,
-                                                       uint64_t *blk_len, uint32_t *nbig) {
+                                                       uint64_t *blk_len) {
   const uint64_t t = static_cast<uint64_t>(blockIdx.x) * 256u + threadIdx.x;
   const uint64_t b = t / kBsG;
   const uint32_t g = static_cast<uint32_t>(t % kBsG);
-  if (t == 0 && nbig) *nbig = 0; // the large-block list starts empty
   uint64_t f0 = 0, f1 = 0, sum = 0;
   if (b < nblocks) {
     f0 = blk_first[b];
@@ -628,31 +607,6 @@ __global__ __launch_bounds__(256) void enc_bsum_kernel(const uint32_t *kl, const
 #pragma unroll
   for (uint32_t d = kBsG / 2; d > 0; d >>= 1) sum += __shfl_xor(sum, d, kWave); // stays inside the 8-lane group
   if (b < nblocks && g == 0) blk_len[b] = sum + 16 * (f1 - f0) + 16;
-}
-
-__global__ __launch_bounds__(256) void enc_prefix_kernel(const uint32_t *kl, const uint32_t *vl,
-                                                         const uint64_t *blk_first, uint64_t nblocks,
-                                                         const uint64_t *blk_off, uint64_t out_base, uint64_t *P) {
-  const uint64_t t = static_cast<uint64_t>(blockIdx.x) * 256u + threadIdx.x;
-  const uint64_t b = t / kBsG;
-  const uint32_t g = static_cast<uint32_t>(t % kBsG);
-  if (b >= nblocks) return; // whole 8-lane groups leave together
-  const uint64_t F0 = blk_first[0], f0 = blk_first[b], f1 = blk_first[b + 1];
-  // entry bytes before the block: its offset minus the offset entries and extras before it
-  uint64_t base = blk_off[b] - out_base - 16 * (f0 - F0) - 16 * b;
-  for (uint64_t r0 = f0; r0 < f1; r0 += kBsG) { // same trip count for the whole group
-    const uint64_t r = r0 + g;
-    const uint64_t sz = r < f1 ? entry_size(kl[r], vl[r]) : 0;
-    uint64_t inc = sz;
-#pragma unroll
-    for (uint32_t d = 1; d < kBsG; d <<= 1) {
-      const uint64_t y = __shfl_up(inc, d, kWave);
-      if (g >= d) inc += y;
-    }
-    if (r < f1) P[r] = base + inc - sz;
-    base += __shfl(inc, static_cast<int>((lane_id() & ~(kBsG - 1)) + kBsG - 1), kWave);
-  }
-  if (b == nblocks - 1 && g == 0) P[f1] = base;
 }
 
 // One workgroup per block; each thread assembles 16-byte output chunks aligned
@@ -676,8 +630,9 @@ __device__ __forceinline__ u32x4 load16_unaligned(const uint8_t *p) {
   return v;
 }
 
-// kT threads (tid = 0..kT-1) encode block b straight to HBM: a workgroup
-// (enc_emit_kernel) or one wave (enc_lds_kernel's blocks past its LDS slot)
+// kT threads (tid = 0..kT-1) encode block b straight to HBM (one wave:
+// enc_lds_kernel's records -> blocks past its LDS slot; P holds the block's
+// relative entry offsets, written by enc_wave_offsets)
 template <uint32_t kT = kEncThreads>
 __device__ void enc_emit_block(const EncArgs &a, uint64_t b, uint8_t *slot, uint32_t tid = threadIdx.x) {
   const uint64_t f0 = a.blk_first[b], f1 = a.blk_first[b + 1];
@@ -686,8 +641,8 @@ __device__ void enc_emit_block(const EncArgs &a, uint64_t b, uint8_t *slot, uint
   const uint64_t bo = a.out_blk_off[b];
   const uint64_t L = a.out_blk_len[b];
   if ((bo & 15) + L + 16 <= kEncSlot) return; // encoded by enc_lds_kernel
-  // entry bytes from the block length (P[f1] is not read: with p_in_kernel it
-  // belongs to the next block's wave)
+  // entry bytes from the block length (P[f1] is not read: in mode 0 it belongs
+  // to the next block's wave)
   const uint64_t D = L - 16 * n - 16;
   auto Pr = [&](uint64_t x) { return x < f1 ? a.P[x] - P0 : D; }; // entry offset, x in [f0, f1]
   uint8_t *dst = a.dst;
@@ -760,15 +715,12 @@ __device__ void enc_emit_block(const EncArgs &a, uint64_t b, uint8_t *slot, uint
 
 
 // Large block of a compaction (records decoded from blocks held in key_src):
-// every entry is already its own encoding in its input block, so the
-// workgroup copies whole entries.  An entry of at least kBigEntry bytes is
-// copied by all threads: each 16 B destination chunk (aligned) is funnel-
-// shifted from two aligned 16 B source chunks (the source / destination skew
-// is constant along the entry), kEmitUnroll chunks per thread in flight; the
-// partial chunks at its ends and the txn (the compat reader may have changed
-// it) go byte by byte.  Smaller entries are copied the same way by one wave
-// each.  Then the offset section and the extra.
-constexpr uint32_t kBigEntry = 2048, kEmitUnroll = 4, kBigList = 256;
+// every entry is already its own encoding in its input block, so the wave
+// that met the block copies whole entries: each 16 B destination chunk
+// (aligned) is funnel-shifted from two aligned 16 B source chunks (the source
+// / destination skew is constant along the entry); the partial chunks at its
+// ends and the txn (the compat reader may have changed it) go byte by byte.
+// Then the offset section and the extra.
 
 __device__ __forceinline__ u32x4 funnel16(const u32x4 &v0, const u32x4 &v1, uint32_t s) {
   const uint32_t w[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
@@ -787,48 +739,13 @@ __device__ __forceinline__ u32x4 funnel16(const u32x4 &v0, const u32x4 &v1, uint
   return out;
 }
 
-// copy len bytes sp -> dp (both unaligned) with threads t of nt: aligned 16 B
-// destination chunks funnel-shifted from aligned source chunks, kEmitUnroll
-// chunks per thread in flight, the partial chunks at both ends byte by byte.
-// The source may be read up to 31 B past sp + len (inside its block: the txn
-// and the offset section follow every entry).
-__device__ __forceinline__ void copy_span(uint8_t *dp, const uint8_t *sp, uint64_t len, uint32_t t, uint32_t nt) {
-  const uintptr_t d0 = reinterpret_cast<uintptr_t>(dp), d1 = d0 + len;
-  const uintptr_t cb = (d0 + 15) & ~static_cast<uintptr_t>(15), ce = d1 & ~static_cast<uintptr_t>(15);
-  if (cb >= ce) {
-    for (uint64_t x = t; x < len; x += nt) dp[x] = sp[x];
-    return;
-  }
-  const uint64_t nch = (ce - cb) >> 4;
-  const uint8_t *s0 = sp + (cb - d0); // source byte of the first full chunk
-  const uint32_t sh = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(s0) & 15u);
-  const u32x4 *sa = reinterpret_cast<const u32x4 *>(s0 - sh);
-  u32x4 *da = reinterpret_cast<u32x4 *>(cb);
-  for (uint64_t k0 = 0; k0 < nch; k0 += static_cast<uint64_t>(nt) * kEmitUnroll) {
-    u32x4 v0[kEmitUnroll], v1[kEmitUnroll];
-#pragma unroll
-    for (uint32_t u = 0; u < kEmitUnroll; u++) { // clamped, unconditional: all loads in flight together
-      const uint64_t k = k0 + static_cast<uint64_t>(u) * nt + t;
-      const uint64_t kc = k < nch ? k : nch - 1;
-      v0[u] = sa[kc];
-      v1[u] = sa[kc + 1]; // <= 16 B past the last full chunk (inside the allowance)
-    }
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (uint32_t u = 0; u < kEmitUnroll; u++) {
-      const uint64_t k = k0 + static_cast<uint64_t>(u) * nt + t;
-      if (k < nch) __builtin_nontemporal_store(funnel16(v0[u], v1[u], sh), da + k);
-    }
-  }
-  for (uintptr_t x = d0 + t; x < cb; x += nt) dp[x - d0] = sp[x - d0];
-  for (uintptr_t x = ce + t; x < d1; x += nt) dp[x - d0] = sp[x - d0];
-}
-
 // copy_span by one wave with kU chunks per lane in flight: the right-hand
 // source chunk of lane l's funnel shift is lane l + 1's own chunk (a shuffle),
 // for lane 63 lane 0's chunk of the next group (a broadcast), and after the
 // last group one extra chunk every lane loads (the same address): one load per
-// 16 B instead of two.  kU = 4 (config 5 encode 232 -> 224 us); kU = 8 is
+// 16 B instead of two.  The source may be read up to 31 B past sp + len
+// (inside its block: the txn and the offset section follow every entry).
+// kU = 4 (config 5 encode 232 -> 224 us); kU = 8 is
 // faster on config 5 (210 us) but its 98 VGPRs cost enc_lds_kernel<1> a wave
 // per SIMD: config 3 encode 500 -> 624 us (profiles/r02_ab/encode_ab.md)
 constexpr uint32_t kWaveSpanUnroll = 4;
@@ -881,8 +798,8 @@ __device__ __forceinline__ void copy_span_wave(uint8_t *dp, const uint8_t *sp, u
   for (uintptr_t x = ce + lane; x < d1; x += kWave) dp[x - d0] = sp[x - d0];
 }
 
-// The same by one wave (enc_lds_kernel<1>'s blocks past its LDS slot when
-// big_inline): entries one after another, each by the 64 lanes.
+// A compaction block past the LDS slot of the enc_lds_kernel<1> wave that met
+// it: entries one after another, each copied by the 64 lanes.
 __device__ void enc_emit_block_entries_wave(const EncArgs &a, uint64_t b) {
   const uint32_t lane = lane_id();
   const uint64_t f0 = a.blk_first[b], f1 = a.blk_first[b + 1];
@@ -911,104 +828,6 @@ __device__ void enc_emit_block_entries_wave(const EncArgs &a, uint64_t b) {
       q[8 + j] = static_cast<uint8_t>(D >> (8 * j));
     }
   }
-}
-
-__device__ void enc_emit_block_entries(const EncArgs &a, uint64_t b) {
-  __shared__ uint32_t s_big[kBigList];
-  __shared__ uint32_t s_nbig;
-  const uint32_t tid = threadIdx.x, lane = lane_id(), wave = tid / kWave;
-  const uint64_t f0 = a.blk_first[b], f1 = a.blk_first[b + 1];
-  const uint64_t n = f1 - f0;
-  const uint64_t P0 = a.P[f0];
-  const uint64_t D = a.P[f1] - P0;
-  uint8_t *blk = a.dst + a.out_blk_off[b];
-  for (uint64_t r0 = 0; r0 < n; r0 += kBigList) { // entries in batches (a batch's big list fits LDS)
-    if (tid == 0) s_nbig = 0;
-    __syncthreads();
-    const uint64_t r1 = r0 + kBigList < n ? r0 + kBigList : n;
-    // entries below kBigEntry: a wave each (span copy + the txn)
-    for (uint64_t i = r0 + wave; i < r1; i += kEncThreads / kWave) {
-      const uint64_t r = f0 + i;
-      const uint64_t o = a.P[r] - P0, sz = a.P[r + 1] - a.P[r];
-      if (sz >= kBigEntry) {
-        if (lane == 0) s_big[atomicAdd(&s_nbig, 1u)] = static_cast<uint32_t>(i);
-        continue;
-      }
-      copy_span(blk + o, a.key_src + a.in.key_off[r] - 5, sz - 8, lane, kWave);
-      if (lane < 8) blk[o + sz - 8 + lane] = static_cast<uint8_t>(a.in.txn[r] >> (8 * lane));
-    }
-    __syncthreads();
-    const uint32_t nbig = s_nbig;
-    for (uint32_t e = 0; e < nbig; e++) { // large entries: the whole workgroup each
-      const uint64_t r = f0 + s_big[e];
-      const uint64_t o = a.P[r] - P0, sz = a.P[r + 1] - a.P[r];
-      copy_span(blk + o, a.key_src + a.in.key_off[r] - 5, sz - 8, tid, kEncThreads);
-      if (tid < 8) blk[o + sz - 8 + tid] = static_cast<uint8_t>(a.in.txn[r] >> (8 * tid));
-    }
-    __syncthreads();
-  }
-  // offset section (start, size per entry) and the extra (block_builder.cc:79-109)
-  for (uint64_t i = tid; i < n; i += kEncThreads) {
-    const uint64_t st = a.P[f0 + i] - P0, sz = a.P[f0 + i + 1] - a.P[f0 + i];
-    uint8_t *q = blk + D + 16 * i;
-    for (int j = 0; j < 8; j++) {
-      q[j] = static_cast<uint8_t>(st >> (8 * j));
-      q[8 + j] = static_cast<uint8_t>(sz >> (8 * j));
-    }
-  }
-  if (tid == 0) {
-    uint8_t *q = blk + D + 16 * n;
-    for (int j = 0; j < 8; j++) {
-      q[j] = static_cast<uint8_t>(n >> (8 * j));
-      q[8 + j] = static_cast<uint8_t>(D >> (8 * j));
-    }
-  }
-}
-
-// min / max txn of block b by the whole workgroup (large blocks)
-__device__ void enc_blk_minmax(const EncArgs &a, uint64_t b) {
-  __shared__ uint64_t smn[kEncThreads / kWave], smx[kEncThreads / kWave];
-  const uint64_t f0 = a.blk_first[b], f1 = a.blk_first[b + 1];
-  uint64_t mn = ~0ull, mx = 0;
-  for (uint64_t r = f0 + threadIdx.x; r < f1; r += kEncThreads) {
-    const uint64_t x = a.in.txn[r];
-    mn = x < mn ? x : mn;
-    mx = x > mx ? x : mx;
-  }
-  for (uint32_t d = kWave / 2; d > 0; d >>= 1) {
-    const uint64_t x = __shfl_xor(mn, d, kWave), y = __shfl_xor(mx, d, kWave);
-    mn = x < mn ? x : mn;
-    mx = y > mx ? y : mx;
-  }
-  if (lane_id() == 0) {
-    smn[threadIdx.x / kWave] = mn;
-    smx[threadIdx.x / kWave] = mx;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    for (uint32_t w = 1; w < kEncThreads / kWave; w++) {
-      mn = smn[w] < mn ? smn[w] : mn;
-      mx = smx[w] > mx ? smx[w] : mx;
-    }
-    a.bmin[b] = mn;
-    a.bmax[b] = mx;
-  }
-  __syncthreads();
-}
-
-__global__ __launch_bounds__(kEncThreads) void enc_emit_kernel(EncArgs a) {
-  __shared__ __attribute__((aligned(16))) uint8_t slot[kEncThreads * 16];
-  if (a.over()) return;
-  if (a.big) {
-    const uint32_t cnt = *a.nbig;
-    for (uint32_t i = blockIdx.x; i < cnt; i += gridDim.x) {
-      if (a.entries_in_src) enc_emit_block_entries(a, a.big[i]);
-      else enc_emit_block(a, a.big[i], slot);
-      if (a.bmin) enc_blk_minmax(a, a.big[i]);
-    }
-    return;
-  }
-  for (uint64_t b = blockIdx.x; b < a.nblocks; b += gridDim.x) enc_emit_block(a, b, slot);
 }
 
 
@@ -1271,24 +1090,17 @@ __device__ __forceinline__ void enc_copy_split(const EncArgs &a, uint8_t *img, u
   const uint32_t lane = lane_id();
   uint8_t *im = img + pad;
   const u32x4 *safe = reinterpret_cast<const u32x4 *>(a.P); // a valid address for masked-off loads
-  uint32_t carry = 0; // p_in_kernel: entry bytes of the rounds before
+  uint32_t carry = 0; // entry bytes of the rounds before
   for (uint32_t c0 = 0; c0 < n; c0 += kWave) {
     const uint32_t nc = n - c0 < kWave ? n - c0 : kWave;
     const uint64_t r = f0 + c0 + (lane < nc ? lane : 0u);
     const bool on = lane < nc;
-    uint32_t o, sz;
-    if (a.p_in_kernel) { // offsets by a wave scan of the entry sizes (no P pass over HBM)
-      const uint32_t kl0 = a.in.key_len[r], vl0 = a.in.val_len[r];
-      sz = on ? static_cast<uint32_t>(entry_size(kl0, vl0)) : 0u;
-      const uint32_t inc = wave_incl_scan_u32(sz);
-      o = carry + inc - sz;
-      carry += __shfl(inc, kWave - 1, kWave);
-    } else {
-      const uint64_t pr = a.P[r], pr1 = a.P[r + 1];
-      o = static_cast<uint32_t>(pr - P0);
-      sz = static_cast<uint32_t>(pr1 - pr);
-    }
     const uint32_t kl = a.in.key_len[r], vl = a.in.val_len[r], ty = a.in.type[r];
+    // entry offsets by a wave scan of the entry sizes (no P pass over HBM)
+    const uint32_t sz = on ? static_cast<uint32_t>(entry_size(kl, vl)) : 0u;
+    const uint32_t inc = wave_incl_scan_u32(sz);
+    const uint32_t o = carry + inc - sz;
+    carry += __shfl(inc, kWave - 1, kWave);
     const uint64_t ko = a.in.key_off[r], vo = a.in.val_off[r], tx = a.in.txn[r];
     copy_spans<GK, kQ>(a.key_src, img, dummy, nc, ko, on ? kl : 0u, pad + o + 5, safe, tbl);
     const uint32_t vlen = on && vl != kNoValue ? vl : 0u;
@@ -1308,7 +1120,7 @@ __device__ __forceinline__ void enc_copy_split(const EncArgs &a, uint8_t *img, u
   }
 }
 
-// p_in_kernel, a block past its LDS slot: its wave writes the block-relative
+// mode 0, a block past its LDS slot: its wave writes the block-relative
 // entry offsets P[f0 .. f1) (a workspace no other block touches) for
 // enc_emit_block, which reads them back from other lanes
 __device__ void enc_wave_offsets(const EncArgs &a, uint64_t b) {
@@ -1344,9 +1156,9 @@ __global__ __launch_bounds__(kEncWaves *kWave) void enc_lds_kernel(EncArgs a) {
   const uint64_t L64 = uniform64(a.out_blk_len[b]);
   const uint32_t pad = static_cast<uint32_t>(bo & 15u);
   if (pad + L64 + 16 > kEncSlot) { // large block
-    if (a.big_inline) { // this wave writes it straight to HBM
+    { // this wave writes it straight to HBM
       if constexpr (kMode == 0) {
-        if (a.p_in_kernel) enc_wave_offsets(a, b);
+        enc_wave_offsets(a, b);
         enc_emit_block<kWave>(a, b, img, lane); // its LDS image holds the lanes' chunk slots
       } else {
         enc_emit_block_entries_wave(a, b);
@@ -1369,17 +1181,15 @@ __global__ __launch_bounds__(kEncWaves *kWave) void enc_lds_kernel(EncArgs a) {
           }
         }
       }
-      return;
     }
-    if (a.big && lane == 0) a.big[atomicAdd(a.nbig, 1u)] = static_cast<uint32_t>(b); // enc_emit_kernel
     return;
   }
   const uint32_t L = static_cast<uint32_t>(L64);
   const uint64_t f0 = uniform64(a.blk_first[b]);
   const uint32_t n = static_cast<uint32_t>(uniform64(a.blk_first[b + 1]) - f0);
-  const uint64_t P0 = kMode == 0 && a.p_in_kernel ? 0ull : uniform64(a.P[f0]);
-  const uint32_t D = kMode == 0 && a.p_in_kernel ? L - 16u * n - 16u
-                                                 : static_cast<uint32_t>(uniform64(a.P[f0 + n]) - P0);
+  // mode 0 scans its entry offsets in the wave (P0 unused); L = D + 16 n + 16
+  const uint64_t P0 = kMode == 0 ? 0ull : uniform64(a.P[f0]);
+  const uint32_t D = L - 16u * n - 16u;
   uint8_t *im = img + pad; // image byte 0 == block byte 0
 
   if constexpr (kMode == 1) {
@@ -2164,26 +1974,15 @@ hipError_t launch_scan_entry_sizes(const uint32_t *klen, const uint32_t *vlen, u
   return scan_any(EntryIn{klen, vlen, add}, nrec, 0, out, ws, s, false, epoch);
 }
 
-hipError_t launch_enc_blocks(const uint64_t *P, const uint64_t *blk_first, uint64_t nblocks, uint64_t out_base,
-                             uint64_t *blk_off, uint64_t *blk_len, uint32_t *nbig, hipStream_t s) {
-  enc_blocks_kernel<<<grid_for(nblocks + 1, 256), 256, 0, s>>>(P, blk_first, nblocks, out_base, blk_off, blk_len,
-                                                              nbig);
-  return hipGetLastError();
-}
-
 hipError_t launch_enc_offsets(const uint32_t *kl, const uint32_t *vl, const uint64_t *blk_first, uint64_t nblocks,
-                              uint64_t out_base, uint64_t *blk_off, uint64_t *blk_len, uint64_t *P, uint32_t *nbig,
-                              uint64_t *ws, hipStream_t s, uint32_t epoch) {
+                              uint64_t out_base, uint64_t *blk_off, uint64_t *blk_len, uint64_t *ws, hipStream_t s,
+                              uint32_t epoch) {
   if (nblocks == 0) { // blk_first may be NULL
-    enc_blocks_kernel<<<1, 256, 0, s>>>(nullptr, nullptr, 0, out_base, blk_off, blk_len, nbig);
+    enc_none_kernel<<<1, 1, 0, s>>>(out_base, blk_off);
     return hipGetLastError();
   }
-  const uint32_t g = grid_for(nblocks * kBsG, 256);
-  enc_bsum_kernel<<<g, 256, 0, s>>>(kl, vl, blk_first, nblocks, blk_len, nbig);
-  hipError_t e = scan_any<ArrIn, kArrItems>(ArrIn{blk_len}, nblocks, out_base, blk_off, ws, s, false, epoch);
-  if (e != hipSuccess) return e;
-  if (P) enc_prefix_kernel<<<g, 256, 0, s>>>(kl, vl, blk_first, nblocks, blk_off, out_base, P);
-  return hipGetLastError();
+  enc_bsum_kernel<<<grid_for(nblocks * kBsG, 256), 256, 0, s>>>(kl, vl, blk_first, nblocks, blk_len);
+  return scan_any<ArrIn, kArrItems>(ArrIn{blk_len}, nblocks, out_base, blk_off, ws, s, false, epoch);
 }
 
 hipError_t launch_enc_emit(const EncArgs &a, hipStream_t s) {
@@ -2196,11 +1995,9 @@ hipError_t launch_enc_emit(const EncArgs &a, hipStream_t s) {
   // (key, value) span pairs were slower (profiles/r02_ab/encode_ab.md)
   if (!a.entries_in_src) enc_lds_kernel<0><<<g, kEncWaves * kWave, 0, s>>>(a);
   else enc_lds_kernel<1><<<g, kEncWaves * kWave, 0, s>>>(a);
-  // blocks past an LDS slot: those listed by enc_lds_kernel when a list is given
-  if (a.big_inline) return hipGetLastError();
-  // (a 512-workgroup grid over the list: config 5 275 us, 2048: 208 us)
-  const uint64_t cap = 2048;
-  enc_emit_kernel<<<static_cast<uint32_t>(a.nblocks < cap ? a.nblocks : cap), kEncThreads, 0, s>>>(a);
+  // blocks past an LDS slot are encoded by the wave that met them (a listed
+  // pass by a workgroup per block was slower: Zipf set 329 -> 236 us, config 5
+  // 319 -> 233 us; profiles/r02_ab/)
   return hipGetLastError();
 }
 

@@ -64,27 +64,20 @@ struct EncArgs {
   sstc_records in;
   const uint64_t *blk_first;
   uint64_t nblocks;
-  const uint64_t *P; // exclusive scan of entry sizes, nrec+1 (see p_in_kernel)
+  // mode 1 (entries_in_src): exclusive scan of the entry sizes, nrec + 1;
+  // mode 0: a workspace (nrec + 1) the wave of a block past its LDS slot fills
+  // with the block-relative entry offsets (other blocks scan them in the wave)
+  const uint64_t *P;
   const uint64_t *out_blk_off;
   const uint64_t *out_blk_len;
   uint8_t *dst;
   uint32_t entries_in_src = 0; // records decoded from blocks in key_src (== val_src)
   uint32_t xcd = 0;
-  // optional: blocks too large for an LDS slot are listed here by enc_lds_kernel
-  // (*nbig zeroed by the caller) so enc_emit_kernel visits only them
-  uint32_t *big = nullptr, *nbig = nullptr;
-  // enc_lds_kernel's waves encode the blocks past their LDS slot themselves
-  // (records -> blocks and compaction alike), no enc_emit_kernel launch
-  uint32_t big_inline = 0;
   // optional (compaction, entries_in_src): per-block min / max txn
   uint64_t *bmin = nullptr, *bmax = nullptr;
   // optional capacity guard (compaction): nothing is written when *need > cap
   const uint64_t *need = nullptr;
   uint64_t cap = 0;
-  // records -> blocks (mode 0): the entry offsets are scanned inside the block's
-  // wave (P is not read); P is then a workspace the wave fills with block-
-  // relative offsets for a block past its LDS slot (entries [f0, f1) only)
-  uint32_t p_in_kernel = 0;
   __device__ bool over() const { return need && *need > cap; }
 };
 
@@ -129,15 +122,11 @@ hipError_t launch_scan(const uint64_t *in, uint64_t n, uint64_t carry_in, uint64
 // out = exclusive scan of the entry sizes (+ add) of records (klen, vlen)
 hipError_t launch_scan_entry_sizes(const uint32_t *klen, const uint32_t *vlen, uint64_t nrec, uint64_t add,
                                    uint64_t *out, uint64_t *ws, hipStream_t s, uint32_t epoch);
-// block offsets (nblocks + 1) and sizes of an encode from P (closed form); clears *nbig
-hipError_t launch_enc_blocks(const uint64_t *P, const uint64_t *blk_first, uint64_t nblocks, uint64_t out_base,
-                             uint64_t *blk_off, uint64_t *blk_len, uint32_t *nbig, hipStream_t s);
-// the same without a record scan: block lengths by reduction, a scan over the
-// blocks, then P (entry-size prefix, P[blk_first[0]] = 0) written per block
-// unless P is null (EncArgs::p_in_kernel); clears *nbig
+// block offsets (nblocks + 1) and lengths of a records -> blocks encode: block
+// lengths by reduction over each block's records, then a scan over the blocks
 hipError_t launch_enc_offsets(const uint32_t *kl, const uint32_t *vl, const uint64_t *blk_first, uint64_t nblocks,
-                              uint64_t out_base, uint64_t *blk_off, uint64_t *blk_len, uint64_t *P, uint32_t *nbig,
-                              uint64_t *ws, hipStream_t s, uint32_t epoch);
+                              uint64_t out_base, uint64_t *blk_off, uint64_t *blk_len, uint64_t *ws, hipStream_t s,
+                              uint32_t epoch);
 hipError_t launch_enc_emit(const EncArgs &a, hipStream_t s);
 // greedy segmentation; J = segment_workspace_u32(nrec) u32 of device workspace
 uint64_t segment_workspace_u32(uint64_t nrec);
