@@ -143,6 +143,20 @@ __device__ __forceinline__ uint32_t find_group(const KGroup *g, uint32_t ng, uin
   return lo;
 }
 
+// kw_before(*yp, ry, x, rx) reading only y's 16 B key prefix unless it equals
+// x's: a prefix that differs decides the order whatever the runs.  The
+// splitter search is bound by its probe bytes, not by the probe chain (an
+// 8-ary search was 2x slower): config 3 splitters 92 -> 89 us, config 4
+// 259 -> 241 us (profiles/r02_ab/merge_ab.md)
+__device__ __forceinline__ bool kw_before_at(const SK *yp, uint32_t ry, const SK &x, uint32_t rx, const KeyView &kv) {
+  const u32x4 h = *reinterpret_cast<const u32x4 *>(yp);
+  const uint64_t p0 = static_cast<uint64_t>(h.x) | (static_cast<uint64_t>(h.y) << 32);
+  const uint64_t p1 = static_cast<uint64_t>(h.z) | (static_cast<uint64_t>(h.w) << 32);
+  if (p0 != x.p0) return p0 < x.p0;
+  if (p1 != x.p1) return p1 < x.p1;
+  return kw_before(*yp, ry, x, rx, kv);
+}
+
 // the splitter records of a pass gathered by splitter id (run-major, sorted
 // within each run): the co-rank searches first run over this compact array
 // (a few MiB, cache resident) and only the last log2(S) probes touch the runs
@@ -185,14 +199,14 @@ __global__ __launch_bounds__(256) void ck_kw_split_kernel(const SK *in, const SK
         uint32_t slo = 0, shi = gr.sbase[r + 1] - gr.sbase[r];
         while (slo < shi) {
           const uint32_t mid = (slo + shi) >> 1;
-          if (kw_before(rsmp[mid], r, x, q, kv)) slo = mid + 1;
+          if (kw_before_at(rsmp + mid, r, x, q, kv)) slo = mid + 1;
           else shi = mid;
         }
         uint64_t lo = slo ? static_cast<uint64_t>(slo - 1) * S + 1 : 0;
         uint64_t hi = static_cast<uint64_t>(slo) * S < len ? static_cast<uint64_t>(slo) * S : len;
         while (lo < hi) {
           const uint64_t mid = (lo + hi) >> 1;
-          if (kw_before(in[rs + mid], r, x, q, kv)) lo = mid + 1;
+          if (kw_before_at(in + rs + mid, r, x, q, kv)) lo = mid + 1;
           else hi = mid;
         }
         c = lo;
