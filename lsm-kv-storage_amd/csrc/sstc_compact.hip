@@ -305,6 +305,28 @@ __device__ __forceinline__ void load_win(const KWin *win, KWin &s_d) {
 // lower run first (merge_iterator.cc:34-46).
 constexpr uint32_t kMgThreads = 256;
 
+// merge-order compares that read a record's 16 B key prefix from LDS first and
+// its other 16 B only when the prefixes tie (a differing prefix decides the
+// order: key_cmp compares p0, p1 first)
+struct MgPf {
+  uint64_t p0, p1;
+};
+__device__ __forceinline__ MgPf mg_pf(const SK *tile, uint32_t s) {
+  const u32x4 h = *reinterpret_cast<const u32x4 *>(tile + s);
+  return {static_cast<uint64_t>(h.x) | (static_cast<uint64_t>(h.y) << 32),
+          static_cast<uint64_t>(h.z) | (static_cast<uint64_t>(h.w) << 32)};
+}
+// record at slot sa (prefix a) before the record at slot sb (prefix b)
+__device__ __forceinline__ bool mg_less_pf(const SK *tile, uint32_t sa, const MgPf &a, uint32_t sb, const MgPf &b,
+                                           const KeyView &kv) {
+  if (a.p0 != b.p0) return a.p0 < b.p0;
+  if (a.p1 != b.p1) return a.p1 < b.p1;
+  return sk_less(tile[sa], tile[sb], kv);
+}
+__device__ __forceinline__ bool mg_less(const SK *tile, uint32_t sa, uint32_t sb, const KeyView &kv) {
+  return mg_less_pf(tile, sa, mg_pf(tile, sa), sb, mg_pf(tile, sb), kv);
+}
+
 __global__ __launch_bounds__(kMgThreads) void ck_mg_merge_kernel(const SK *in, SK *out, const KWin *win,
                                                                 KeyView kv) {
   __shared__ SK tile[kKRegion];
@@ -347,13 +369,13 @@ __global__ __launch_bounds__(kMgThreads) void ck_mg_merge_kernel(const SK *in, S
       uint32_t i = diag > hi - mid ? diag - (hi - mid) : 0, ihi = diag < mid - lo ? diag : mid - lo;
       while (i < ihi) {
         const uint32_t im = (i + ihi) >> 1;
-        if (!sk_less(tile[slot(mid + diag - 1 - im)], tile[slot(lo + im)], kv)) i = im + 1;
+        if (!mg_less(tile, slot(mid + diag - 1 - im), slot(lo + im), kv)) i = im + 1;
         else ihi = im;
       }
       uint32_t j = diag - i, ai = 0, bi = 0;
-      SK a, b;
-      if (lo + i < mid) a = tile[ai = slot(lo + i)];
-      if (mid + j < hi) b = tile[bi = slot(mid + j)];
+      MgPf a{0, 0}, b{0, 0}; // the heads' key prefixes (the rest is read from LDS on a prefix tie)
+      if (lo + i < mid) a = mg_pf(tile, ai = slot(lo + i));
+      if (mid + j < hi) b = mg_pf(tile, bi = slot(mid + j));
       for (uint32_t e = 0; e < per; e++) {
         const uint32_t p = p0 + e;
         if (p >= total) break;
@@ -363,17 +385,17 @@ __global__ __launch_bounds__(kMgThreads) void ck_mg_merge_kernel(const SK *in, S
           mid = bound(m + wd);
           hi = bound(m + 2 * wd);
           i = j = 0;
-          if (lo < mid) a = tile[ai = slot(lo)];
-          if (mid < hi) b = tile[bi = slot(mid)];
+          if (lo < mid) a = mg_pf(tile, ai = slot(lo));
+          if (mid < hi) b = mg_pf(tile, bi = slot(mid));
         }
-        const bool take_b = lo + i >= mid || (mid + j < hi && sk_less(b, a, kv));
+        const bool take_b = lo + i >= mid || (mid + j < hi && mg_less_pf(tile, bi, b, ai, a, kv));
         o_ix[p] = static_cast<uint16_t>(take_b ? bi : ai);
         if (take_b) {
           j++;
-          if (mid + j < hi) b = tile[bi = slot(mid + j)];
+          if (mid + j < hi) b = mg_pf(tile, bi = slot(mid + j));
         } else {
           i++;
-          if (lo + i < mid) a = tile[ai = slot(lo + i)];
+          if (lo + i < mid) a = mg_pf(tile, ai = slot(lo + i));
         }
       }
     }
