@@ -33,7 +33,12 @@ threads (the job's CPU share), each pinned to its own CPU; generous, the
 reference compacts on one thread.
 
 legs (N=1): decode alone and encode alone over the same blocks, each with its
-own roofline sub-object.
+own roofline sub-object; compact = BASELINE config 3 (8 SSTs x 1 M records)
+through the device compaction job sstc_compact, verified against the
+reference's output hashes, with its own roofline and reference CPU baseline.
+
+Input pin: the GPU-built block buffer is hashed and must equal the reference
+BlockBuilder's encoding of the same records (tests/golden/bench_inputs.json).
 """
 import argparse
 import json
@@ -74,6 +79,27 @@ def make_blocks(codec, dev, nblocks, rank):
     src, off, ln = codec.encode(table, ksrc, vsrc, first)
     del table, ksrc, vsrc
     return src, off[:-1].contiguous(), ln.contiguous()
+
+
+def input_pin(src, nblocks, rank):
+    """SHA-256 of the GPU-built input buffer against the reference BlockBuilder's
+    encoding of the same records (tests/golden/bench_inputs.json, made by
+    tests/golden/make_golden_bench.py from /root/reference/sstable/block_builder.cc).
+    Returns True / False, or None when no fixture covers (rank, nblocks)."""
+    import hashlib
+    try:
+        with open(os.path.join(ROOT, "tests", "golden", "bench_inputs.json")) as f:
+            cases = json.load(f)["cases"]
+    except (OSError, ValueError, KeyError):
+        return None
+    want = [c["sha256"] for c in cases if c["rank"] == rank and c["blocks"] == nblocks]
+    if not want:
+        return None
+    h = hashlib.sha256()
+    step = 64 << 20
+    for lo in range(0, src.numel(), step):
+        h.update(src[lo:lo + step].cpu().numpy().tobytes())
+    return h.hexdigest() == want[0]
 
 
 def time_roundtrip(codec, src, dst, off, ln, steps, warmup, stream, ranks):
@@ -319,6 +345,9 @@ def hbm_variant(codec, dev, nblocks, steps=10):
     span of `steps` back-to-back launches / steps; identity checked."""
     import ctypes
     src, off, ln = make_blocks(codec, dev, nblocks, 0)
+    pinned = input_pin(src, nblocks, 0)
+    if pinned is False:
+        raise SystemExit("1 GiB variant: GPU-built blocks differ from the reference BlockBuilder's")
     dst = torch.empty_like(src)
     out_len = torch.empty(nblocks, dtype=torch.int64, device=dev)
     status = torch.empty(nblocks, dtype=torch.int32, device=dev)
@@ -344,7 +373,7 @@ def hbm_variant(codec, dev, nblocks, steps=10):
     cp = copy_peak(codec, dev, (alg // 2 + 15) // 16 * 16)
     return {"copy_peak_GBps": round(cp, 1), "frac_of_copy_peak": round(achieved / cp, 4), "blocks": nblocks, "input_bytes": nblocks * BLOCK_BYTES, "launch_ms_events": round(ms, 5),
             "GiBps_in": round(nblocks * BLOCK_BYTES / (ms * 1e-3) / 2 ** 30, 1), "achieved_GBps": round(achieved, 1),
-            "frac": round(achieved / HBM_PEAK_GBPS, 4), "verified": ok,
+            "frac": round(achieved / HBM_PEAK_GBPS, 4), "verified": ok, "input_sha256_equals_reference": pinned,
             "why": "4x config 2 so the working set exceeds the 256 MiB Infinity Cache (HBM-bound)"}
 
 
@@ -467,6 +496,137 @@ def codec_legs(codec, dev, stream, src, off, ln, steps):
                           f"{nrec} x 33 B SoA read", ok_enc)}
 
 
+def read_compact_traffic(workload):
+    """HBM bytes per sstc_compact call from the PMC passes of
+    tools/pmc_compact_job.sh (profiles/pmc_compact.json), or None."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "pmc_compact.json")) as f:
+            d = json.load(f)
+        if d.get("workload") == workload:
+            return float(d["hbm_bytes_per_call"])
+    except (OSError, ValueError, KeyError):
+        pass
+    return None
+
+
+def compact_leg(codec, dev, stream, steps, cpu_ref=True):
+    """BASELINE config 3 -- the compaction hot path north_star replaces
+    (db/compact.cc:232-322): 8 SSTs x 1 M records (16 B keys, 100 B values,
+    disjoint interleave) resident in HBM -> sstc_compact (decode, k-way merge,
+    keep/drop, 32 MiB table split, 4 KiB block split, encode, meta, footers) ->
+    28 output SSTs in HBM.  Inputs are written by the flush-path
+    sstc::TableBuilder and must hash to the reference TableBuilder's files;
+    every output must hash to the reference's compaction
+    (tests/golden/compaction_configs.json "config3").  Time = median of
+    `steps` calls, each bracketed by device syncs (the job makes host fetches
+    inside), plus the HIP-event span on the codec's stream.  Roofline: the job
+    must read every input byte once and write every output byte once:
+    algorithmic bytes = input + output bytes.  cpu_baseline: the reference's
+    own MergeIterator + TableReaderIterator + TableBuilder under the
+    DoCompactJob loop (oracle/_ref/ref_compact, 1 thread, files incl. fsync)
+    on the same input files, once."""
+    import ctypes
+    import hashlib
+    import shutil
+    import subprocess
+    import tempfile
+    from sstcodec._lib import CompactParams, CompactResult
+    from sstcodec.table import build_table
+    fx = json.load(open(os.path.join(ROOT, "tests", "golden", "compaction_configs.json")))["config3"]
+    td = tempfile.mkdtemp(prefix="sstc_bench_c3_", dir=os.environ.get("TMPDIR", "/tmp"))
+    try:
+        files, paths = [], []
+        inputs_ok = True
+        for i, rec in enumerate(W.config_inputs(3)):
+            p = os.path.join(td, f"in{i}.sst")
+            fs, _ = build_table(codec, p, rec, 4096)
+            img = np.fromfile(p, np.uint8)
+            inputs_ok &= (fs == fx["inputs"][i]["file_size"] and
+                          hashlib.sha256(img.tobytes()).hexdigest() == fx["inputs"][i]["sha256"])
+            files.append(img)
+            paths.append((p, fs))
+        if not inputs_ok:
+            raise SystemExit("compact leg: input SSTs differ from the reference TableBuilder's")
+        src = torch.from_numpy(np.concatenate(files)).to(dev)
+        sizes = [f.size for f in files]
+        del files
+        idx = codec.open_tables(src, sizes, strict=True)
+        bo, bl, h_tfb = idx["blk_off"], idx["blk_len"], idx["table_first_block"]
+        cap = int(src.numel()) + (1 << 20)
+        dst = torch.empty(cap, dtype=torch.uint8, device=dev)
+        max_t = 1 << 12
+        toff = torch.zeros(max_t + 1, dtype=torch.int64, device=dev)
+        tlen = torch.zeros(max_t, dtype=torch.int64, device=dev)
+        prm = CompactParams(4096, 32 << 20, 1, 0)
+        res = CompactResult()
+        P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+
+        def run():
+            codec._stream()
+            check(codec.lib.sstc_compact(codec.h, P(src), P(bo), P(bl), int(bo.numel()),
+                                         h_tfb.ctypes.data_as(ctypes.c_void_p), len(sizes), ctypes.byref(prm),
+                                         P(dst), cap, P(toff), P(tlen), max_t, ctypes.byref(res)), "sstc_compact")
+
+        for _ in range(2):
+            run()
+        torch.cuda.synchronize()
+        walls, evs = [], []
+        for _ in range(steps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            e0.record(stream)
+            run()
+            e1.record(stream)
+            torch.cuda.synchronize()
+            walls.append(time.perf_counter() - t0)
+            evs.append(e0.elapsed_time(e1) * 1e-3)
+        nt = res.tables_out
+        o = toff[: nt + 1].cpu().numpy()
+        d = dst[: int(o[nt])].cpu().numpy()
+        got = [(hashlib.sha256(d[int(o[t]):int(o[t + 1])].tobytes()).hexdigest(), int(o[t + 1] - o[t]) + 1)
+               for t in range(nt)]
+        ok = got == [(w["sha256"], w["file_size"]) for w in fx["outputs_base1"]]
+        in_bytes, out_bytes = int(src.numel()), int(o[nt])
+        del src, dst, d
+        torch.cuda.empty_cache()
+        t = float(np.median(walls))
+        alg = in_bytes + out_bytes
+        traffic = read_compact_traffic("config3")
+        leg = {"workload": "config3: 8 SSTs x 1 M records (16 B keys, 100 B values) -> 28 SSTs, sstc_compact, "
+                           "device-resident", "steps": steps, "ms_median": round(t * 1e3, 4),
+               "ms_events_median": round(float(np.median(evs)) * 1e3, 4),
+               "GiBps_in": round(in_bytes / t / 2 ** 30, 1), "records_in": res.records_in,
+               "records_kept": res.records_kept, "tables_out": nt, "input_bytes": in_bytes, "output_bytes": out_bytes,
+               "verified_vs_reference": ok, "inputs_equal_reference": inputs_ok,
+               "roofline": {"bound": "hbm", "achieved": round(alg / t / 1e9, 1), "peak": HBM_PEAK_GBPS,
+                            "unit": "GB/s", "frac": round(alg / t / 1e9 / HBM_PEAK_GBPS, 4),
+                            "traffic": traffic, "alg_bytes_per_call": alg,
+                            "alg": "input bytes read once + output bytes written once (a copy's traffic)",
+                            "kernel": "sstc_compact (whole job, ~30 kernels; wall time incl. its host syncs)"}}
+        if not ok:
+            raise SystemExit("compact leg: outputs differ from the reference's compaction: timing invalid")
+        ref = os.path.join(ROOT, "oracle", "_ref", "ref_compact")
+        if cpu_ref and os.path.exists(ref):
+            od = os.path.join(td, "ref_out")
+            os.makedirs(od)
+            cpu = current_cpu()
+            t0 = time.perf_counter()
+            r = subprocess.run([ref, od, "4096", str(32 << 20), "1"] + [x for p, fs in paths for x in (p, str(fs))],
+                               capture_output=True, text=True, preexec_fn=lambda: os.sched_setaffinity(0, {cpu}))
+            el = time.perf_counter() - t0
+            if r.returncode == 0:
+                leg["cpu_baseline"] = {
+                    "value": round(in_bytes / el / 2 ** 30, 3), "unit": "GiB/s", "seconds": round(el, 3),
+                    "cores": 1, "kind": "reference", "pinned_cpu": cpu,
+                    "sample": "the whole config-3 job once: the reference's MergeIterator + TableReaderIterator "
+                              "+ TableBuilder under the DoCompactJob loop (oracle/_ref/ref_compact), input files "
+                              "page-cache-hot, outputs written + fsync'd like the reference"}
+        return leg
+    finally:
+        shutil.rmtree(td, ignore_errors=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1, help="ranks (one per GPU); >1 launches them itself")
@@ -478,6 +638,8 @@ def main():
     ap.add_argument("--no-e2e", action="store_true", help="skip the host->device->host rate")
     ap.add_argument("--no-hbm-variant", action="store_true", help="skip the 4x (1 GiB, HBM-bound) measurement")
     ap.add_argument("--no-legs", action="store_true", help="skip the decode-only / encode-only legs")
+    ap.add_argument("--no-compact", action="store_true", help="skip the config-3 compaction leg")
+    ap.add_argument("--compact-steps", type=int, default=10)
     ap.add_argument("--plumbing", action="store_true",
                     help="CPU-only launcher check (gloo, host copy as the step): NOT a measurement")
     args = ap.parse_args()
@@ -499,6 +661,9 @@ def main():
     src, off, ln = make_blocks(codec, dev, nb, rank)
     torch.cuda.synchronize()
     assert int(ln.min()) == BLOCK_BYTES == int(ln.max())
+    pinned = input_pin(src, nb, rank)
+    if pinned is False:
+        raise SystemExit("GPU-built input blocks differ from the reference BlockBuilder's: timing invalid")
     dst = torch.empty_like(src)
 
     wall, per_launch, out_len, status = time_roundtrip(codec, src, dst, off, ln, args.steps, args.warmup,
@@ -534,6 +699,7 @@ def main():
             "dtype": "u8",
             "data": "synthetic (uniform 16 B keys k%015d / 100 B splitmix64 values, blocks built on GPU by "
                     "the codec's encoder; identity round trip verified)",
+            "input_sha256_equals_reference_blockbuilder": pinned,
             "config": {"workload": "config2: batch decode+re-encode of 65536 x 4188 B device-resident "
                                    "blocks per GPU (28 PUTs each), fused rt_kernel",
                        "blocks_per_gpu": nb, "block_bytes": BLOCK_BYTES, "records_per_gpu": nb * PER_BLOCK,
@@ -554,6 +720,9 @@ def main():
             out["roofline"]["frac_of_copy_peak"] = round(achieved / cp, 4)
             if not args.no_legs:
                 out["legs"] = codec_legs(codec, dev, stream, src, off, ln, max(10, args.steps // 2))
+            if not args.no_compact:
+                out.setdefault("legs", {})["compact"] = compact_leg(codec, dev, stream, args.compact_steps,
+                                                                     not args.no_cpu_baseline)
             if not args.no_hbm_variant:
                 out["roofline"]["hbm_1gib"] = hbm_variant(codec, dev, 4 * nb)
             if not args.no_e2e:

@@ -15,6 +15,7 @@
 
 #include <cerrno>
 #include <cstring>
+#include <map>
 #include <memory>
 #include <stdexcept>
 
@@ -179,11 +180,13 @@ void TableBuilder::FlushBlock() {
   block_size_ = 0;
 }
 
+extern "C" int sstc__ctx_device(const sstc_ctx *ctx); // sstc_api.hip: the device a context is bound to
+
 namespace {
-// per-host-thread staging reused across Finish() calls (flush / compaction
-// threads each build many SSTs): one pinned host buffer and one device buffer,
-// grown when needed, so a Finish makes no allocation in steady state and its
-// copies run from / into pinned memory
+// per-host-thread, per-device staging reused across Finish() calls (flush /
+// compaction threads each build many SSTs): one pinned host buffer and one
+// device buffer on the context's device, grown when needed, so a Finish makes
+// no allocation in steady state and its copies run from / into pinned memory
 struct Staging {
   uint8_t *host = nullptr, *dev = nullptr;
   uint64_t host_cap = 0, dev_cap = 0;
@@ -215,7 +218,20 @@ struct Staging {
     return dev;
   }
 };
-thread_local Staging g_stage;
+thread_local std::map<int, Staging> g_stage; // device -> staging
+
+// makes `dev` current for the scope and restores the caller's device
+struct DeviceScope {
+  int prev = -1;
+  explicit DeviceScope(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (dev >= 0 && dev != prev && hipSetDevice(dev) != hipSuccess) throw std::runtime_error("hipSetDevice failed");
+  }
+  ~DeviceScope() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
 
 uint64_t align256(uint64_t x) { return (x + 255) & ~uint64_t(255); }
 } // namespace
@@ -239,7 +255,12 @@ void TableBuilder::Finish() {
                  o_vals = align256(o_keys + keys_.size()), in_bytes = align256(o_vals + vals_.size());
   const uint64_t o_dst = in_bytes, o_off = align256(o_dst + data_bytes), o_len = align256(o_off + 8 * (nb + 1)),
                  dev_bytes = align256(o_len + 8 * nb + 8);
-  uint8_t *h = g_stage.Host(std::max(in_bytes, file_bytes) + 16 * nb + 16);
+  // the staging lives on the context's device, whatever device the calling
+  // thread has current (the encode kernel runs on the context's device)
+  const int dev = sstc__ctx_device(ctx_);
+  DeviceScope on_ctx_device(dev);
+  Staging &stage = g_stage[dev];
+  uint8_t *h = stage.Host(std::max(in_bytes, file_bytes) + 16 * nb + 16);
   std::vector<uint64_t> blk_off(nb + 1), blk_len(nb);
   if (nb) {
     std::memcpy(h + o_type, type_.data(), n);
@@ -251,7 +272,7 @@ void TableBuilder::Finish() {
     std::memcpy(h + o_first, blk_first_.data(), 8 * (nb + 1));
     std::memcpy(h + o_keys, keys_.data(), keys_.size());
     std::memcpy(h + o_vals, vals_.data(), vals_.size());
-    uint8_t *d = g_stage.Dev(dev_bytes);
+    uint8_t *d = stage.Dev(dev_bytes);
     if (hipMemcpy(d, h, in_bytes, hipMemcpyHostToDevice) != hipSuccess) throw std::runtime_error("hipMemcpy H2D failed");
     sstc_records rec{d + o_type, reinterpret_cast<uint32_t *>(d + o_kl), reinterpret_cast<uint32_t *>(d + o_vl),
                      reinterpret_cast<uint64_t *>(d + o_txn), reinterpret_cast<uint64_t *>(d + o_ko),

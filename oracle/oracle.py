@@ -244,6 +244,40 @@ def ref_compact(paths_and_sizes, out_dir, block_threshold=4096, table_limit=32 <
     return out
 
 
+REF_PICK_COMPACT = os.path.join(HERE, "_ref", "ref_pick_compact")
+COMPACT_DROPIN = os.path.join(HERE, "_ref", "compact_dropin")
+
+
+def table_key_range(rec):
+    """(smallest, largest) key of a sorted record set (what VersionEdit::AddNewFiles
+    records for a flushed table, db_impl.cc:430-436)."""
+    n = len(rec["type"])
+    ko, kl, src = rec["key_off"], rec["key_len"], rec["key_src"]
+    first = bytes(src[int(ko[0]):int(ko[0]) + int(kl[0])])
+    last = bytes(src[int(ko[n - 1]):int(ko[n - 1]) + int(kl[n - 1])])
+    return first, last
+
+
+def ref_pick_compact(inputs, db_dir, block_threshold=4096, table_limit=32 << 20, exe=REF_PICK_COMPACT, env=None):
+    """Run the reference's Compact::PickCompact (db/compact.cc compiled
+    unchanged, oracle/ref_pick_compact.cc) over L0 tables 1..k.
+    inputs: [(path, file_size, smallest_key_bytes, largest_key_bytes)].
+    Returns (picked table ids, [(path, GetFileSize(), smallest, largest)])."""
+    args = [exe, db_dir, str(block_threshold), str(table_limit)]
+    for p, s, lo, hi in inputs:
+        args += [p, str(int(s)), lo.hex() or "-", hi.hex() or "-"]
+    r = subprocess.run(args, check=True, capture_output=True, text=True, env=env)
+    picked, out = [], []
+    for line in r.stdout.strip().splitlines():
+        f = line.split(" ")
+        if f[0] == "in":
+            picked.append(int(f[1]))
+        elif f[0] == "out":
+            unhex = lambda h: b"" if h == "-" else bytes.fromhex(h)  # noqa: E731
+            out.append((f[1], int(f[2]), unhex(f[3]), unhex(f[4])))
+    return picked, out
+
+
 class RefLib:
     """oracle/_ref/libsstref.so: the reference's own sstable code."""
 

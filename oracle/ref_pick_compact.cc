@@ -1,0 +1,185 @@
+// ref_pick_compact.cc — runs the REFERENCE's own Compact::PickCompact
+// (/root/reference/db/compact.cc, compiled unchanged) over given L0 SSTs
+// (TEST INFRASTRUCTURE ONLY).
+//
+// db/db_impl.cc cannot be compiled here (it includes the empty
+// third_party/rapidjson submodule), and compact.cc / version*.cc /
+// table_reader_cache.cc reach DBImpl only through seven accessors, so this TU
+// defines exactly those plus the constructor/destructor,
+// mirroring db/db_impl.cc:54-83,240-245,600-624 minus the memtable, the
+// transaction manager and the trash-file thread, which compaction never
+// touches.
+//
+// The same TU is linked twice by oracle/Makefile:
+//   _ref/ref_pick_compact  against the reference's own sstable/table_builder.cc:
+//                          the as-written compaction, INCLUDING the dangling
+//                          `std::string_view last_current_key` of
+//                          compact.cc:250,266-268;
+//   _ref/compact_dropin    with include/dropin/ first on the include path, so
+//                          db/compact.cc (unchanged) builds its outputs with
+//                          sstc::TableBuilder (GPU encode, libsstcodec.so):
+//                          the drop-in of INTEGRATION.md, demonstrated.
+//
+// usage: <exe> <db_dir> <block_size> <table_limit> [<file> <file_size> <smallest_hex> <largest_hex>]...
+//   The inputs become L0 tables 1..k (table 1 = oldest), db_dir receives the
+//   outputs "<id>.sst" (ids k+1, ...).  Prints one line per input the job
+//   picked ("in <table_id>") and one per output ("out <path> <GetFileSize()>
+//   <smallest_hex> <largest_hex>"), in VersionEdit order.
+#include "common/base_iterator.h"
+#include "common/thread_pool.h"
+#include "db/base_memtable.h"
+#include "db/compact.h"
+#include "db/config.h"
+#include "db/db_impl.h"
+#include "db/version.h"
+#include "db/version_edit.h"
+#include "db/version_manager.h"
+#include "io/base_file.h"
+#include "mvcc/transaction.h"
+#include "mvcc/transaction_manager.h"
+#include "sstable/block_reader_cache.h"
+#include "sstable/table_reader_cache.h"
+
+#include <cstdio>
+#include <cstdlib>
+#include <filesystem>
+#include <fstream>
+#include <string>
+#include <unistd.h>
+
+namespace fs = std::filesystem;
+
+namespace {
+std::string g_db_path;
+uint64_t g_block_size = 4096, g_table_limit = 32ull << 20, g_first_id = 1;
+
+// db/config.cc:37-53 reads <cwd>/../tests/test_config.toml
+std::unique_ptr<kvs::db::Config> MakeConfig() {
+  char tmpl[] = "/tmp/sstref_pickXXXXXX";
+  if (!mkdtemp(tmpl)) std::exit(3);
+  fs::path root(tmpl);
+  fs::create_directories(root / "tests");
+  fs::create_directories(root / "run");
+  {
+    std::ofstream t(root / "tests" / "test_config.toml");
+    t << "[lsm]\nLSM_PER_MEM_SIZE_LIMIT = " << g_table_limit << "\nMAX_IMMUTABLE_MEMTABLES_IN_MEMORY = 4\n"
+      << "SST_BLOCK_SIZE = " << g_block_size << "\nLSM_SST_NUM_LEVELS = 7\n"
+      << "LVL0_COMPACTION_TRIGGER = 6\n[cache]\nTOTAL_BG_THREADS = 12\n"
+      << "TOTAL_TABLES_CACHE = 1000\nTOTAL_BLOCKS_EACH_CACHE = 20000\nTOTAL_BLOCKS_CACHE = 5\n";
+  }
+  fs::path old = fs::current_path();
+  fs::current_path(root / "run");
+  auto cfg = std::make_unique<kvs::db::Config>(true);
+  fs::current_path(old);
+  fs::remove_all(root);
+  return cfg;
+}
+
+std::string Unhex(const char *h) {
+  std::string s;
+  if (h[0] == '-') return s;
+  for (size_t i = 0; h[i] && h[i + 1]; i += 2) s.push_back(static_cast<char>(std::stoi(std::string(h + i, 2), nullptr, 16)));
+  return s;
+}
+
+std::string Hex(std::string_view k) {
+  std::string h;
+  char b[3];
+  for (unsigned char c : k) {
+    std::snprintf(b, sizeof b, "%02x", c);
+    h += b;
+  }
+  return h.empty() ? std::string("-") : h;
+}
+} // namespace
+
+namespace kvs {
+namespace db {
+
+// db/db_impl.cc:54-75 (memtable, transaction manager and trash thread omitted)
+DBImpl::DBImpl(bool is_testing)
+    : db_path_(g_db_path), next_sstable_id_(g_first_id), memtable_version_(1), sequence_number_(0),
+      config_(MakeConfig()), background_compaction_scheduled_(false),
+      thread_pool_(std::make_unique<kvs::ThreadPool>(config_->GetTotalBackGroundThreads())),
+      table_reader_cache_(std::make_unique<sstable::TableReaderCache>(this, thread_pool_.get())),
+      block_cache_thread_pool_(std::make_unique<kvs::ThreadPool>(config_->GetTotalBlocksCache())),
+      version_manager_(std::make_unique<VersionManager>(this, thread_pool_.get())) {
+  (void)is_testing;
+  for (int i = 0; i < config_->GetTotalBlocksCache(); i++) {
+    block_reader_cache_.emplace_back(std::make_unique<sstable::BlockReaderCache>(
+        config_->GetTotalBlocksCache(), block_cache_thread_pool_.get()));
+  }
+}
+
+// db/db_impl.cc:77-83
+DBImpl::~DBImpl() {
+  block_reader_cache_.clear();
+  table_reader_cache_.reset();
+  shutdown_ = true;
+  trash_files_cv_.notify_one();
+}
+
+// db/db_impl.cc:240-245
+void DBImpl::WakeupBgThreadToCleanupFiles(std::string_view filename) const {
+  std::scoped_lock rwlock(trash_files_mutex_);
+  trash_files_.push(std::string(filename));
+  trash_files_cv_.notify_one();
+}
+
+// db/db_impl.cc:600-624
+uint64_t DBImpl::GetNextSSTId() { return next_sstable_id_.fetch_add(1); }
+const Config *DBImpl::GetConfig() const { return config_.get(); }
+const VersionManager *DBImpl::GetVersionManager() const { return version_manager_.get(); }
+std::string DBImpl::GetDBPath() const { return db_path_; }
+const std::vector<std::unique_ptr<sstable::BlockReaderCache>> &DBImpl::GetBlockReaderCache() const {
+  return block_reader_cache_;
+}
+const sstable::TableReaderCache *DBImpl::GetTableReaderCache() const { return table_reader_cache_.get(); }
+
+} // namespace db
+} // namespace kvs
+
+int main(int argc, char **argv) {
+  if (argc < 4 || (argc - 4) % 4) {
+    std::fprintf(stderr, "usage: %s db_dir block_size table_limit [file size smallest_hex largest_hex]...\n",
+                 argv[0]);
+    return 2;
+  }
+  g_db_path = std::string(argv[1]);
+  if (g_db_path.back() != '/') g_db_path += '/';
+  g_block_size = std::strtoull(argv[2], nullptr, 10);
+  g_table_limit = std::strtoull(argv[3], nullptr, 10);
+  const int k = (argc - 4) / 4;
+  g_first_id = static_cast<uint64_t>(k) + 1;
+
+  // a DBImpl that is never destroyed: the reference tears its caches down
+  // while their pool threads may still run (db_impl.cc:77-83); the process
+  // exits through _exit once the outputs are on disk.
+  auto *db = new kvs::db::DBImpl(true);
+  auto *vm = const_cast<kvs::db::VersionManager *>(db->GetVersionManager());
+  const int levels = db->GetConfig()->GetSSTNumLvels();
+
+  // the first edit only creates the initial version (whose
+  // scores would pick the last level); the second one adds the L0 inputs and
+  // gives level 0 the score |L0| / trigger (version_manager.cc:200-203).
+  vm->ApplyNewChanges(std::make_unique<kvs::db::VersionEdit>(levels));
+  auto add = std::make_unique<kvs::db::VersionEdit>(levels);
+  for (int i = 0; i < k; i++) {
+    char **a = argv + 4 + 4 * i;
+    add->AddNewFiles(static_cast<kvs::SSTId>(i + 1), 0, std::strtoull(a[1], nullptr, 10), Unhex(a[2]), Unhex(a[3]),
+                     std::string(a[0]));
+  }
+  vm->ApplyNewChanges(std::move(add));
+
+  const kvs::db::Version *version = vm->GetLatestVersion();
+  kvs::db::VersionEdit out_edit(levels);
+  kvs::db::Compact compact(db->GetBlockReaderCache(), db->GetTableReaderCache(), version, &out_edit, db);
+  const bool ok = compact.PickCompact(); // db/compact.cc:35-52 -> DoL0L1Compact -> DoCompactJob
+  for (const auto &del : out_edit.GetImmutableDeletedFiles()) std::printf("in %llu\n", (unsigned long long)del.first);
+  for (const auto &level_files : out_edit.GetImmutableNewFiles())
+    for (const auto &m : level_files)
+      std::printf("out %s %llu %s %s\n", m->filename.c_str(), (unsigned long long)m->file_size,
+                  Hex(m->smallest_key).c_str(), Hex(m->largest_key).c_str());
+  std::fflush(stdout);
+  _exit(ok ? 0 : 1);
+}

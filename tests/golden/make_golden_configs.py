@@ -38,6 +38,8 @@ CASES = {
     "config3": {"config": 3},
     "config3_overlap": {"config": 3, "overlap": True},
     "config4_rank0": {"config": 4, "rank": 0},
+    # the other seven shards of config 4 (1024 SSTs, 128 per GPU): ranks 1-7
+    **{f"config4_rank{r}": {"config": 4, "rank": r} for r in range(1, 8)},
     "config5": {"config": 5},
 }
 

@@ -1,9 +1,11 @@
 """GPU parity: the HIP kernels (through the C-ABI) against the oracle and the
 reference's golden fixtures.  Bit-exact everywhere (integer/byte work)."""
+import os
+
 import numpy as np
 import pytest
 import torch
-from conftest import BLOCK_SETS, REC_KEYS, golden_records, load_golden
+from conftest import BLOCK_SETS, GOLDEN, REC_KEYS, golden_records, load_golden
 from sstcodec import workload as W
 
 pytestmark = pytest.mark.gpu
@@ -250,12 +252,20 @@ def uniform_blocks(codec, nblocks, seed=1):
 
 
 def test_config2_full_size_properties(codec, oracle):
-    """65 536 x 4188 B blocks: encode(GPU) -> round trip -> identity; decode ->
-    records equal the generator's; a sample of blocks equal the oracle's."""
+    """65 536 x 4188 B blocks (bench.py's rank-0 input): encode(GPU) -> the
+    whole buffer hashes to the reference BlockBuilder's encoding of the same
+    records (tests/golden/bench_inputs.json) -> round trip -> identity; decode
+    -> records equal the generator's; a sample of blocks equal the oracle's."""
+    import hashlib
+    import json
     nb = 65536
     rec, src, off, ln = uniform_blocks(codec, nb)
     torch.cuda.synchronize()
     assert int(ln.min()) == int(ln.max()) == 4188 and src.numel() == nb * 4188
+    pins = json.load(open(os.path.join(GOLDEN, "bench_inputs.json")))["cases"]
+    want_sha = [c["sha256"] for c in pins if c["rank"] == 0 and c["blocks"] == nb][0]
+    assert hashlib.sha256(src.cpu().numpy().tobytes()).hexdigest() == want_sha, \
+        "GPU-encoded config-2 buffer differs from the reference BlockBuilder's"
     dst, out_len, status = codec.roundtrip(src, off, ln, txn_mode=0)
     torch.cuda.synchronize()
     assert bool((status[:nb] == 0).all()) and bool((out_len[:nb] == 4188).all())

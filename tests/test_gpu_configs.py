@@ -113,3 +113,36 @@ def test_lookup_config3_vs_reference(codec, oracle):
     assert hashlib.sha256(typ.astype(np.uint32).tobytes()).hexdigest() == case["types_sha256"]
     assert hashlib.sha256(vlens.tobytes()).hexdigest() == case["val_len_sha256"]
     assert hashlib.sha256(vals).hexdigest() == case["values_sha256"]
+
+
+@pytest.mark.timeout(900)
+def test_config4_all_shards_vs_reference(codec, tmp_path):
+    """BASELINE config 4 whole: 1024 SSTs, 128 per GPU.  Ranks 1-7's shards
+    (rank 0 is test_config_full_size_vs_reference) run one after another on
+    this GPU through the same device job each rank runs in bench
+    (tools/bench_compact.py --config 4): inputs written by sstc::TableBuilder
+    and hash-checked against the reference TableBuilder's files, every output
+    SST's SHA-256 and GetFileSize() equal to the reference's compaction of
+    that shard (compaction_configs.json config4_rank1..7)."""
+    import torch
+    from sstcodec.table import build_table
+    for rank in range(1, 8):
+        case = CASES[f"config4_rank{rank}"]
+        imgs = []
+        for i, rec in enumerate(W.config_inputs(**case["gen"])):
+            p = str(tmp_path / f"r{rank}_in{i}.sst")
+            fs, _ = build_table(codec, p, rec, case["block_threshold"])
+            img = np.fromfile(p, np.uint8)
+            os.remove(p)
+            w = case["inputs"][i]
+            assert fs == w["file_size"] and sha(img) == w["sha256"], f"rank {rank} input {i}"
+            imgs.append(img)
+        outs, res = codec.compact(imgs, case["block_threshold"], case["table_limit"], 1)
+        del imgs
+        want = case["outputs_base1"]
+        assert res.tables_out == len(outs) == len(want)
+        for t, (o, w) in enumerate(zip(outs, want)):
+            assert o.size + 1 == w["file_size"] and sha(o) == w["sha256"], f"rank {rank} output {t}"
+        del outs
+        torch.cuda.empty_cache()
+        print(f"config4 rank {rank}: 128 inputs -> {len(want)} outputs equal to the reference's", flush=True)
