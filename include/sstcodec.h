@@ -56,6 +56,7 @@ extern "C" {
 #define SSTC_E_NOMEM -3
 #define SSTC_E_NO_DEVICE -4
 #define SSTC_E_CAPACITY -5 /* workspace too small: call sstc_ctx_reserve */
+#define SSTC_E_INTERNAL -6 /* a device-side consistency check of a job failed: nothing was written */
 
 /* per-block status, d_block_status[b] */
 #define SSTC_BLK_OK 0

@@ -133,6 +133,15 @@ uint32_t sstc_version(void) { return SSTC_ABI_VERSION; }
 // through sstc_last_error_string
 int sstc__fail(int code, const char *what) { return fail(code, what); }
 int sstc__ctx_device(const sstc_ctx *c) { return c ? c->device : -1; }
+
+// test hook (not in the public header): corrupt the next compaction jobs'
+// filter output on the device (sstc::Arena::fault) so the job's consistency
+// guard can be exercised; 0 turns it off
+int sstc__ctx_set_fault(sstc_ctx *c, uint32_t fault) {
+  if (!c) return SSTC_E_INVALID_ARG;
+  c->arena.fault = fault;
+  return SSTC_OK;
+}
 int sstc__ctx_sync(sstc_ctx *c) {
   if (!c || bind_device(c)) return SSTC_E_NO_DEVICE;
   return hipStreamSynchronize(c->stream) == hipSuccess ? SSTC_OK : SSTC_E_HIP;

@@ -84,9 +84,19 @@ __device__ __forceinline__ bool sk_less(const SK &a, const SK &b, const KeyView 
 // non-empty block against the last record before it, unless it starts a run.
 __global__ void ck_check_blocks_kernel(const SK *s, const uint64_t *rec_base, uint64_t nblocks,
                                        const uint64_t *run_start, uint64_t nruns, KeyView kv,
-                                       unsigned long long *bad, Abort stop, uint64_t *zws, uint64_t nz) {
+                                       unsigned long long *bad, Abort stop, uint64_t *zws, uint64_t nz,
+                                       const uint64_t *blk_off, const uint64_t *blk_len,
+                                       unsigned long long *src_end) {
   const uint64_t b = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   for (uint64_t z = b; z < nz; z += static_cast<uint64_t>(gridDim.x) * blockDim.x) zws[z] = 0; // filter look-back
+  { // end of the source bytes the blocks span: the bound of every entry the encode copies
+    uint64_t e = b < nblocks ? blk_off[b] + blk_len[b] : 0;
+    for (uint32_t d = kWave / 2; d > 0; d >>= 1) {
+      const uint64_t y = __shfl_xor(e, d, kWave);
+      e = y > e ? y : e;
+    }
+    if (lane_id() == 0 && e) atomicMax(src_end, static_cast<unsigned long long>(e));
+  }
   if (b >= nblocks || stop()) return;
   const uint64_t r = rec_base[b];
   if (r == 0 || rec_base[b + 1] == r) return;
@@ -456,26 +466,44 @@ constexpr uint32_t kFfRows = 8, kFfTile = kFtThreads * kFfRows;
 // from the previous record, compact.cc:266-268) if PUT, or if DELETED and not
 // the base level; any other record iff its txn equals its group head's (drop
 // if last_txn > txn).  Txns descend within a group, so a non-head whose txn
-// differs from its predecessor's is dropped, and an equal one looks back along
-// its run of equal txns (records duplicated across inputs) to the head.
+// differs from its predecessor's is dropped; an equal one (records duplicated
+// across inputs) finds its group head by galloping back over equal keys and
+// compares txns: O(log distance) per record, so a long run of equal
+// (key, txn) records costs n log n, not the n^2 of a walk back record by record.
+__device__ __forceinline__ bool ff_same_key(const SK &a, const SK &b, const KeyView &kv) {
+  return key_cmp(a.p0, a.p1, a.kl, a.id, b.p0, b.p1, b.kl, b.id, kv) == 0;
+}
 __device__ __forceinline__ uint32_t ff_keep(const SK *s, uint64_t i, const SK &x, const SK &pv, uint32_t ty,
                                             uint32_t base_level, const KeyView &kv) {
   if (i == 0) return 1;
-  if (key_cmp(pv.p0, pv.p1, pv.kl, pv.id, x.p0, x.p1, x.kl, x.id, kv) != 0)
-    return ty == kTypePut ? 1u : (base_level ? 0u : 1u);
+  if (!ff_same_key(pv, x, kv)) return ty == kTypePut ? 1u : (base_level ? 0u : 1u);
   if (x.tx != pv.tx) return 0;
-  for (uint64_t q = i - 1; q > 0; q--) { // run of equal txns back to the group head
-    const SK y = s[q - 1], z = s[q];
-    if (key_cmp(y.p0, y.p1, y.kl, y.id, z.p0, z.p1, z.kl, z.id, kv) != 0) break; // z is the head
-    if (y.tx != z.tx) return 0;
+  // group head = first record of x's key group: s[hi] has x's key, s[lo] not
+  // (or lo = -1 past the start)
+  uint64_t hi = i - 1;
+  int64_t lo = -1;
+  for (uint64_t step = 1;; step <<= 1) {
+    if (hi == 0) break;
+    const uint64_t p = hi > step ? hi - step : 0;
+    if (ff_same_key(s[p], x, kv)) {
+      hi = p;
+    } else {
+      lo = static_cast<int64_t>(p);
+      break;
+    }
   }
-  return 1;
+  while (lo + 1 < static_cast<int64_t>(hi)) {
+    const uint64_t mid = static_cast<uint64_t>((lo + static_cast<int64_t>(hi)) >> 1);
+    if (ff_same_key(s[mid], x, kv)) hi = mid;
+    else lo = static_cast<int64_t>(mid);
+  }
+  return s[hi].tx == x.tx ? 1u : 0u;
 }
 
 __global__ __launch_bounds__(kFtThreads) void ck_filter_kernel(const SK *s, uint64_t n, KeyView kv,
                                                                uint32_t base_level, Rec out, uint64_t *Pd,
                                                                uint64_t *Pe, uint64_t *ws, uint64_t *totals,
-                                                               Abort stop) {
+                                                               Abort stop, unsigned long long *guard) {
   __shared__ uint64_t s_tile, s_pre[3];
   if (stop()) return; // uniform over the grid: no ticket drawn, the host rejects the job
   const uint32_t tid = threadIdx.x, lane = lane_id(), w = tid / kWave;
@@ -501,8 +529,16 @@ __global__ __launch_bounds__(kFtThreads) void ck_filter_kernel(const SK *s, uint
     }
     __builtin_amdgcn_sched_barrier(0);
     RecX rr[kGroup];
+    bool bad_id = false; // a merged record id out of range (never, unless the merge is wrong)
 #pragma unroll
-    for (uint32_t g = 0; g < kGroup; g++) rr[g] = kv.rx[x[g].id]; // unconditional (past n: the last record's)
+    for (uint32_t g = 0; g < kGroup; g++) {
+      bad_id |= x[g].id >= n || pv[g].id >= n;
+      rr[g] = kv.rx[x[g].id < n ? x[g].id : 0u]; // unconditional (past n: the last record's)
+    }
+    if (__any(bad_id)) { // no key compare may follow such an id: the job is rejected
+      if (lane == 0) atomicOr(guard, kGuardMergeId);
+      for (uint32_t g = 0; g < kGroup; g++) x[g].id = pv[g].id = 0;
+    }
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (uint32_t g = 0; g < kGroup; g++) {
@@ -679,6 +715,17 @@ __device__ __forceinline__ void put_le(uint8_t *p, uint64_t v, int n) {
 // the workgroup's 256 blocks is written with aligned 16 B stores (byte stores
 // straight to HBM from 256 threads at a 56 B stride cost ~10x more).
 constexpr uint32_t kMetaLds = 24576; // 256 entries of keys up to 32 B (32 KiB: 4 workgroups per CU, 48 -> 45 us at 16 KiB)
+// the entry's key sources inside the source bytes and its keys within the
+// reference's key limit (block_builder.cc:38); false sets the guard
+__device__ __forceinline__ bool meta_entry_ok(uint64_t b, const uint64_t *bf, Rec K, const uint64_t *src_end,
+                                              unsigned long long *guard) {
+  const uint64_t f = bf[b], l = bf[b + 1] - 1, e = *src_end;
+  const uint32_t fk = K.kl[f], lk = K.kl[l];
+  const bool ok = f <= l && fk <= kMaxKey && lk <= kMaxKey && K.ko[f] <= e && fk <= e - K.ko[f] && K.ko[l] <= e &&
+                  lk <= e - K.ko[l];
+  if (!ok) atomicOr(guard, kGuardMeta);
+  return ok;
+}
 __device__ __forceinline__ void meta_entry(uint8_t *p, uint64_t b, const uint64_t *bf, const uint32_t *btab,
                                            const uint64_t *BL, const uint64_t *blen, const uint64_t *tbf, Rec K,
                                            const uint8_t *src) {
@@ -697,27 +744,38 @@ __global__ __launch_bounds__(256) void ck_meta_kernel(const uint64_t *bf, uint64
                                                       const uint64_t *BL, const uint64_t *MS, const uint64_t *blen,
                                                       const uint64_t *tbf, const uint64_t *toff,
                                                       const uint64_t *tdata, Rec K, const uint8_t *src,
-                                                      uint8_t *dst, const uint64_t *need, uint64_t cap) {
+                                                      uint8_t *dst, const uint64_t *need, uint64_t cap,
+                                                      const uint64_t *src_end, unsigned long long *guard) {
   __shared__ __attribute__((aligned(16))) uint8_t img[kMetaLds + 16];
   if (*need > cap) return; // output capacity exceeded: nothing is written
   const uint64_t b0 = static_cast<uint64_t>(blockIdx.x) * 256u;
   const uint64_t bend = b0 + 256u < nb ? b0 + 256u : nb;
   const uint64_t b = b0 + threadIdx.x;
   const uint64_t m0 = MS[b0];
+  // a table's meta section must end inside the output buffer
+  auto in_cap = [&](uint64_t t, uint64_t at, uint64_t len) {
+    const uint64_t o = toff[t] + tdata[t] + at;
+    const bool ok = o <= cap && len <= cap - o;
+    if (!ok) atomicOr(guard, kGuardMeta);
+    return ok;
+  };
   if (MS[bend] - m0 > kMetaLds) {  // long keys: direct per-thread writes
-    if (b < bend) {
+    if (b < bend && meta_entry_ok(b, bf, K, src_end, guard)) {
       const uint32_t t = btab[b];
-      meta_entry(dst + toff[t] + tdata[t] + (MS[b] - MS[tbf[t]]), b, bf, btab, BL, blen, tbf, K, src);
+      if (in_cap(t, MS[b] - MS[tbf[t]], MS[b + 1] - MS[b]))
+        meta_entry(dst + toff[t] + tdata[t] + (MS[b] - MS[tbf[t]]), b, bf, btab, BL, blen, tbf, K, src);
     }
     return;
   }
-  if (b < bend) meta_entry(img + (MS[b] - m0), b, bf, btab, BL, blen, tbf, K, src);
-  __syncthreads();
+  const bool ok = b >= bend || meta_entry_ok(b, bf, K, src_end, guard);
+  if (b < bend && ok) meta_entry(img + (MS[b] - m0), b, bf, btab, BL, blen, tbf, K, src);
+  if (__syncthreads_or(!ok)) return; // a bad entry: the workgroup writes nothing
   for (uint64_t bs = b0; bs < bend;) {  // one run per output table touched
     const uint32_t t = btab[bs];
     const uint64_t be = tbf[t + 1] < bend ? tbf[t + 1] : bend;
     const uint32_t l0 = static_cast<uint32_t>(MS[bs] - m0);
     const int64_t len = static_cast<int64_t>(MS[be] - MS[bs]);
+    if (!in_cap(t, MS[bs] - MS[tbf[t]], static_cast<uint64_t>(len))) return; // uniform
     uint8_t *g = dst + toff[t] + tdata[t] + (MS[bs] - MS[tbf[t]]);
     const uint32_t pad = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(g) & 15u);
     const uint32_t nchunk = static_cast<uint32_t>((pad + len + 15) >> 4);
@@ -781,9 +839,14 @@ __global__ __launch_bounds__(256) void ck_tab_minmax_kernel(const uint64_t *tbf,
 // footer of table t (table_builder.cc:179-211)
 __global__ void ck_footer_kernel(uint64_t nt, const uint64_t *tbf, const uint64_t *toff, const uint64_t *tdata,
                                  const uint64_t *tmeta, const uint64_t *tmin, const uint64_t *tmax, uint8_t *dst,
-                                 uint64_t cap) {
+                                 uint64_t cap, unsigned long long *guard) {
   const uint64_t t = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (t >= nt || toff[nt] > cap) return;
+  const uint64_t at = toff[t] + tdata[t] + tmeta[t];
+  if (at < toff[t] || at > cap || cap - at < 40) { // the footer must end inside the output buffer
+    atomicOr(guard, kGuardFooter);
+    return;
+  }
   uint64_t mn = ~0ull, mx = 0;
   for (uint32_t g = 0; g < kMmSplit; g++) {
     mn = tmin[t * kMmSplit + g] < mn ? tmin[t * kMmSplit + g] : mn;
@@ -868,11 +931,13 @@ __global__ __launch_bounds__(256) void ck_pack_kernel(Words w, const uint64_t *a
 // error counter and clears the unsorted count for this job
 __global__ void ck_run_starts_kernel(const uint64_t *rec_base, const uint64_t *tfb, uint64_t n, uint64_t *out,
                                      const unsigned long long *err_count, uint64_t *errs,
-                                     unsigned long long *bad) {
+                                     unsigned long long *bad, unsigned long long *guard) {
   const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (i == 0) {
     *errs = *err_count;
     *bad = 0;
+    guard[0] = 0; // consistency-guard bits
+    guard[1] = 0; // source end (ck_check_blocks_kernel)
   }
   if (i < n) out[i] = rec_base[tfb[i]];
 }
@@ -952,9 +1017,14 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     CK(launch_count(d_src, d_blk_off, d_blk_len, nblocks, rb_all, s, ws));
     CK(launch_scan(rb_all, nblocks, 0, rb_all, ws, s, true));
     unsigned long long *bad = reinterpret_cast<unsigned long long *>(pool.get<uint64_t>(1));
+    // consistency guard: [0] bits set by any check of the job, [1] the end of
+    // the source bytes its blocks span (both cleared by ck_run_starts_kernel)
+    unsigned long long *guard = reinterpret_cast<unsigned long long *>(pool.get<uint64_t>(2));
+    const uint64_t *src_end = reinterpret_cast<const uint64_t *>(guard + 1);
     // record index of every input table's first record (its run start)
     CK(hipMemcpyAsync(d_tfb, h_tfb, (ntables + 1) * 8, hipMemcpyHostToDevice, s));
-    ck_run_starts_kernel<<<grid(ntables + 1), 256, 0, s>>>(rb_all, d_tfb, ntables + 1, d_rs, err_count, errs, bad);
+    ck_run_starts_kernel<<<grid(ntables + 1), 256, 0, s>>>(rb_all, d_tfb, ntables + 1, d_rs, err_count, errs, bad,
+                                                           guard);
     fetch(arena, s, {}, d_rs, ntables + 1);
     std::vector<uint64_t> run_start(arena.host, arena.host + ntables + 1);
     const uint64_t n = run_start[ntables];
@@ -1001,7 +1071,7 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     const uint64_t fftiles = (n + kFfTile - 1) / kFfTile;
     uint64_t *ffws = pool.get<uint64_t>(1 + 3 * fftiles);
     ck_check_blocks_kernel<<<grid(nblocks), 256, 0, s>>>(A, rb_all, nblocks, rb, nruns, kv, bad, dec_fail, ffws,
-                                                         1 + 3 * fftiles);
+                                                         1 + 3 * fftiles, d_blk_off, d_blk_len, guard + 1);
     // k-way merge passes; run boundaries of every pass are known on the host,
     // so all group descriptors go up in one upload (lives until the next sync)
     std::vector<KGroup> kg;
@@ -1091,9 +1161,12 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
            nullptr}; // vl / vo: not needed by the whole-entry encode
     uint64_t *Pd = pool.get<uint64_t>(n + 1), *Pe = pool.get<uint64_t>(n + 1);
     ck_filter_kernel<<<static_cast<uint32_t>(fftiles), kFtThreads, 0, s>>>(A, n, kv, base_level, KR, Pd, Pe, ffws,
-                                                                        totals, stop);
+                                                                        totals, stop, guard);
+    if (arena.fault == 1) CK(hipMemsetAsync(KR.ko, 0xFF, n * sizeof(uint64_t), s)); // test: bad key offsets
+    if (arena.fault == 2) CK(hipMemsetAsync(Pe, 0x5A, (n + 1) * sizeof(uint64_t), s)); // test: bad prefix sums
     fetch(arena, s, {totals, reinterpret_cast<const uint64_t *>(bad),
-                           reinterpret_cast<const uint64_t *>(err_count), errs});
+                           reinterpret_cast<const uint64_t *>(err_count), errs,
+                           reinterpret_cast<const uint64_t *>(guard)});
     if (arena.host[2] != arena.host[3]) {
       err = "an input block failed to decode";
       return SSTC_E_INVALID_ARG;
@@ -1101,6 +1174,10 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     if (arena.host[1]) {
       err = "input SST records are not sorted (key asc, txn desc)";
       return SSTC_E_INVALID_ARG;
+    }
+    if (arena.host[4]) {
+      err = "device consistency check failed after the merge (merged record ids out of range)";
+      return SSTC_E_INTERNAL;
     }
     const uint64_t m = arena.host[0];
     res[1] = m;
@@ -1144,14 +1221,24 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     uint64_t *tmin = pool.get<uint64_t>(nt * kMmSplit), *tmax = pool.get<uint64_t>(nt * kMmSplit);  // per-table partials
     ea.bmin = bmin; // block min / max txn, reduced by the encode kernels
     ea.bmax = bmax;
+    ea.src_end = src_end;
+    ea.guard = guard;
     CK(launch_enc_emit(ea, s));
     ck_meta_kernel<<<static_cast<uint32_t>((nb + 255) / 256), 256, 0, s>>>(bf, nb, btab, BL, MS, blen, tbf, d_table_off, tdata, KR, d_src, d_dst,
-                                                                          need, dst_cap);
+                                                                          need, dst_cap, src_end, guard);
     ck_tab_minmax_kernel<<<static_cast<uint32_t>(nt * kMmSplit), 256, 0, s>>>(tbf, bmin, bmax, tmin, tmax);
-    ck_footer_kernel<<<grid(nt), 256, 0, s>>>(nt, tbf, d_table_off, tdata, tmeta, tmin, tmax, d_dst, dst_cap);
+    ck_footer_kernel<<<grid(nt), 256, 0, s>>>(nt, tbf, d_table_off, tdata, tmeta, tmin, tmax, d_dst, dst_cap, guard);
     CK(hipGetLastError());
-    fetch(arena, s, {need}, nullptr, 0, true);
+    fetch(arena, s, {need, reinterpret_cast<const uint64_t *>(guard)}, nullptr, 0, true);
     res[4] = arena.host[0];
+    if (arena.host[1]) {
+      err = "device consistency check failed (guard bits 0x" + [](uint64_t v) {
+        char b[24];
+        snprintf(b, sizeof b, "%llx", static_cast<unsigned long long>(v));
+        return std::string(b);
+      }(arena.host[1]) + "): the output is incomplete";
+      return SSTC_E_INTERNAL;
+    }
     if (res[4] > dst_cap) {
       err = "output buffer too small";
       return SSTC_E_CAPACITY;

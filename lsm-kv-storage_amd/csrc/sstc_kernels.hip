@@ -714,6 +714,20 @@ __device__ void enc_emit_block(const EncArgs &a, uint64_t b, uint8_t *slot, uint
 }
 
 
+// the consistency guard of one record of a compaction block (EncArgs::guard):
+// inside the block image, at least its header + key, its source inside
+// [5, *src_end).  Compaction only; true when unguarded.
+__device__ __forceinline__ bool enc1_entry_ok(const EncArgs &a, uint64_t o, uint64_t sz, uint32_t kl, uint64_t ko,
+                                              uint64_t D) {
+  if (!a.guard) return true;
+  const uint64_t e = *a.src_end;
+  return o <= D && sz <= D - o && kl <= kMaxKey && sz >= 13ull + kl && ko >= 5 && ko - 5 <= e && sz <= e - (ko - 5);
+}
+__device__ __forceinline__ bool enc1_block_ok(const EncArgs &a, uint64_t bo, uint64_t L, uint64_t n) {
+  if (!a.guard) return true;
+  return L >= 16 * n + 16 && bo <= a.cap && L <= a.cap - bo;
+}
+
 // Large block of a compaction (records decoded from blocks held in key_src):
 // every entry is already its own encoding in its input block, so the wave
 // that met the block copies whole entries: each 16 B destination chunk
@@ -800,12 +814,21 @@ __device__ __forceinline__ void copy_span_wave(uint8_t *dp, const uint8_t *sp, u
 
 // A compaction block past the LDS slot of the enc_lds_kernel<1> wave that met
 // it: entries one after another, each copied by the 64 lanes.
-__device__ void enc_emit_block_entries_wave(const EncArgs &a, uint64_t b) {
+__device__ bool enc_emit_block_entries_wave(const EncArgs &a, uint64_t b) {
   const uint32_t lane = lane_id();
   const uint64_t f0 = a.blk_first[b], f1 = a.blk_first[b + 1];
   const uint64_t n = f1 - f0;
   const uint64_t P0 = a.P[f0];
   const uint64_t D = a.P[f1] - P0;
+  if (a.guard) { // every entry checked before the first byte goes out
+    bool bad = !enc1_block_ok(a, a.out_blk_off[b], a.out_blk_len[b], n) || a.out_blk_len[b] != D + 16 * n + 16;
+    for (uint64_t r = f0 + lane; r < f1 && !bad; r += kWave)
+      bad = !enc1_entry_ok(a, a.P[r] - P0, a.P[r + 1] - a.P[r], a.in.key_len[r], a.in.key_off[r], D);
+    if (__any(bad)) {
+      if (lane == 0) atomicOr(a.guard, kGuardEntry);
+      return false;
+    }
+  }
   uint8_t *blk = a.dst + a.out_blk_off[b];
   for (uint64_t i = 0; i < n; i++) {
     const uint64_t r = f0 + i;
@@ -828,6 +851,7 @@ __device__ void enc_emit_block_entries_wave(const EncArgs &a, uint64_t b) {
       q[8 + j] = static_cast<uint8_t>(D >> (8 * j));
     }
   }
+  return true;
 }
 
 
@@ -894,7 +918,7 @@ __device__ __forceinline__ void emit_chunk(uint8_t *img, u32x4 v, uint32_t nxt, 
 // lane per record writes type + key length (the first 5 bytes), the txn (the
 // last 8; the compat reader may have changed it) and the offset entry.
 template <uint32_t kCopyQ>
-__device__ __forceinline__ void enc_copy_entries(const EncArgs &a, uint8_t *img, uint32_t pad, uint64_t f0,
+__device__ __forceinline__ bool enc_copy_entries(const EncArgs &a, uint8_t *img, uint32_t pad, uint64_t f0,
                                                  uint32_t n, uint64_t P0, uint32_t D, uint64_t b) {
   const uint32_t lane = lane_id();
   const uint32_t g = lane & 15u, sub = lane >> 4;
@@ -912,6 +936,10 @@ __device__ __forceinline__ void enc_copy_entries(const EncArgs &a, uint8_t *img,
       my_tx = a.in.txn[r];
       my_kl = a.in.key_len[r];
       my_ty = a.in.type[r];
+    }
+    if (__any(lane < nc && !enc1_entry_ok(a, my_o, my_sz, my_kl, my_ko, D))) { // the block is not written
+      if (lane == 0) atomicOr(a.guard, kGuardEntry);
+      return false;
     }
     for (uint32_t p0 = 0; p0 < nc; p0 += 4 * kCopyQ) {
       u32x4 v[kCopyQ];
@@ -975,6 +1003,7 @@ __device__ __forceinline__ void enc_copy_entries(const EncArgs &a, uint8_t *img,
       a.bmax[b] = tmax;
     }
   }
+  return true;
 }
 
 // Chunk c of a span (16 aligned source bytes v + the first dword of chunk c+1)
@@ -1161,7 +1190,7 @@ __global__ __launch_bounds__(kEncWaves *kWave) void enc_lds_kernel(EncArgs a) {
         enc_wave_offsets(a, b);
         enc_emit_block<kWave>(a, b, img, lane); // its LDS image holds the lanes' chunk slots
       } else {
-        enc_emit_block_entries_wave(a, b);
+        if (!enc_emit_block_entries_wave(a, b)) return;
         if (a.bmin) { // the block's min / max txn (table footer), reduced by the wave
           const uint64_t f0 = a.blk_first[b], f1 = a.blk_first[b + 1];
           uint64_t mn = ~0ull, mx = 0;
@@ -1193,7 +1222,11 @@ __global__ __launch_bounds__(kEncWaves *kWave) void enc_lds_kernel(EncArgs a) {
   uint8_t *im = img + pad; // image byte 0 == block byte 0
 
   if constexpr (kMode == 1) {
-    enc_copy_entries<4>(a, img, pad, f0, n, P0, D, b);
+    if (!enc1_block_ok(a, bo, L64, n) || (a.guard && uniform64(a.P[f0 + n]) - P0 != D)) {
+      if (lane == 0) atomicOr(a.guard, kGuardBlockRange);
+      return;
+    }
+    if (!enc_copy_entries<4>(a, img, pad, f0, n, P0, D, b)) return;
   } else {
     enc_copy_split<GK, GV, kQ>(a, img, s_dummy + threadIdx.x, pad, f0, n, P0, D,
                                s_tbl + wave * kWave);

@@ -79,7 +79,17 @@ struct EncArgs {
   const uint64_t *need = nullptr;
   uint64_t cap = 0;
   __device__ bool over() const { return need && *need > cap; }
+  // optional consistency guard (compaction, mode 1): every block's output range
+  // must lie in [0, cap), every entry inside its block image (offset + size
+  // <= data bytes, size >= its header + key) and its source inside
+  // [5, *src_end); a block that fails is not written and sets *guard
+  const uint64_t *src_end = nullptr;
+  unsigned long long *guard = nullptr;
 };
+
+// consistency-guard bits of the compaction job (sstc_compact.hip)
+constexpr unsigned long long kGuardMergeId = 1, kGuardEntry = 2, kGuardBlockRange = 4, kGuardMeta = 8,
+                             kGuardFooter = 16;
 
 // point lookups (sstc_get.hip)
 struct GetArgs {
@@ -145,6 +155,10 @@ struct Arena {
   uint64_t *host_dev = nullptr; // the same words as mapped into the device
   uint64_t host_cap = 0;
   uint64_t seq = 0; // sequence word of the last host fetch (sstc_compact.hip fetch)
+  // fault injection for tests (sstc__ctx_set_fault): corrupts the compaction
+  // job's filter output on the device so its consistency guard can be tested
+  // (1: survivor key offsets, 2: entry prefix sums); 0 in production
+  uint32_t fault = 0;
 };
 
 int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, const uint8_t *d_src,

@@ -63,6 +63,8 @@ class FilesTiming(ctypes.Structure):
                 ("store_s", ctypes.c_double), ("total_s", ctypes.c_double)]
 
 
+SSTC_E_INTERNAL = -6  # include/sstcodec.h: a device-side consistency check failed
+
 SSTC_TAB_OK, SSTC_TAB_BAD_FOOTER, SSTC_TAB_BAD_META, SSTC_TAB_BAD_BLOCK, SSTC_TAB_TOO_LARGE = 0, 1, 2, 3, 4
 
 
@@ -105,6 +107,7 @@ def load():
         "sstc_roundtrip_host": (ctypes.c_int, [c_vp, c_vp, c_vp, c_u64, c_vp, c_vp, c_u64, c_u32, c_u64, c_vp,
                                                c_vp]),
         "sstc_copy_probe": (ctypes.c_int, [c_vp, c_vp, c_vp, c_u64]),
+        "sstc__ctx_set_fault": (ctypes.c_int, [c_vp, c_u32]),  # test hook (sstc_api.hip), not in the header
         "sstc_open_tables": (ctypes.c_int, [c_vp, c_vp, c_u64, c_vp, c_vp, c_u32, c_u64, c_vp, c_vp, c_vp, c_vp,
                                             c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
         "sstc_pipe_create": (ctypes.c_int, [c_vp, c_u32, P(c_vp)]),

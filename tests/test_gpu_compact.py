@@ -268,3 +268,53 @@ def test_compact_long_keys_many_windows(codec, oracle):
         assert len(outs) == len(want)
         for o, w in zip(outs, want):
             assert np.array_equal(o, w)
+
+
+@pytest.mark.parametrize("fault", [1, 2])
+@pytest.mark.parametrize("case", ["mixed", "zipf"])
+def test_compact_guard_rejects_corrupted_filter_output(codec, oracle, fault, case):
+    """Downstream of the keep / drop filter, the encode, meta and footer
+    kernels index with device-produced offsets (survivor key offsets, entry
+    prefix sums).  With the filter output deliberately corrupted on the device
+    (test hook sstc__ctx_set_fault: 1 = survivor key offsets 0xFF.., 2 = entry
+    prefix sums garbage), the job's consistency guard must reject it
+    (SSTC_E_INTERNAL) without an out-of-range access, and the context must stay
+    usable.  'zipf' has blocks past the encode's LDS slot (the large-block
+    path)."""
+    import sstcodec
+    if case == "zipf":
+        sets = W.compaction_inputs(4, 600, 1200, seed=5, vmax=65536, vmin=8, zipf=1.1, p_delete=0.1)
+    else:
+        sets = W.compaction_inputs(4, 3000, 8000, seed=9, vmax=300, p_delete=0.1)
+    ins = [oracle.table_build(r, 4096) for r in sets]
+    want, _ = oracle.compact(ins, 4096, 4 << 20, 1)
+    assert codec.lib.sstc__ctx_set_fault(codec.h, fault) == 0
+    try:
+        with pytest.raises(sstcodec.SstcError, match=r"\(-6\).*consistency"):
+            codec.compact(ins, 4096, 4 << 20, 1)
+    finally:
+        codec.lib.sstc__ctx_set_fault(codec.h, 0)
+    outs, _ = codec.compact(ins, 4096, 4 << 20, 1)
+    assert len(outs) == len(want) and all(np.array_equal(o, w) for o, w in zip(outs, want))
+
+
+@pytest.mark.timeout(120)
+def test_compact_long_equal_runs(codec, oracle):
+    """Runs of identical (key, txn) records far longer than the inputs count
+    (ShouldKeepEntry keeps them all: last_txn == txn, compact.cc:357-362): the
+    keep test finds a record's group head by galloping, O(log run) per record
+    (a walk back over the run was O(run^2) in total)."""
+    n = 60_000
+    sets = []
+    for t in range(3):
+        rec = W.uniform_records(n, key_index=np.zeros(n, np.uint64), seed=t + 1, value_len=20)
+        rec["txn"][:] = 77  # one key, one txn, every record
+        sets.append(rec)
+    extra = W.uniform_records(1000, key_index=np.arange(1, 1001, dtype=np.uint64), seed=9, value_len=20,
+                              txn_start=10)
+    sets.append(extra)
+    ins = [oracle.table_build(r, 4096) for r in sets]
+    want, kept = oracle.compact(ins, 4096, 1 << 20, 1)
+    outs, res = codec.compact(ins, 4096, 1 << 20, 1)
+    assert res.records_kept == kept == 3 * n + 1000
+    assert len(outs) == len(want) and all(np.array_equal(o, w) for o, w in zip(outs, want))

@@ -77,6 +77,9 @@ def test_live_ref_compact(oracle):
 
 
 CONFIGS = {k: v for k, v in json.load(open(os.path.join(GOLDEN, "compaction_configs.json"))).items() if "gen" in v}
+# config 4's eight shards are alike: the CPU suite pins ranks 0 and 7 against
+# the oracle (every shard runs through the HIP path in test_gpu_configs.py)
+CONFIGS = {k: v for k, v in CONFIGS.items() if not k.startswith("config4_rank") or k in ("config4_rank0", "config4_rank7")}
 
 
 @pytest.mark.parametrize("name", sorted(CONFIGS))
