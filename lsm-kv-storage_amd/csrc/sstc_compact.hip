@@ -541,15 +541,11 @@ __global__ __launch_bounds__(kFtThreads) void ck_filter_kernel(const SK *s, uint
   __shared__ uint64_t s_tile, s_pre[3];
   if (stop()) return; // uniform over the grid: no ticket drawn, the host rejects the job
   const uint32_t tid = threadIdx.x, lane = lane_id(), w = tid / kWave;
-#ifdef SSTC_AB_NOTICKET
-  if (tid == 0) s_tile = blockIdx.x;
-#else
   if (tid == 0) {
     const uint64_t t = __hip_atomic_fetch_add(ws, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (t + 1 == gridDim.x) __hip_atomic_store(ws, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     s_tile = t;
   }
-#endif
   __syncthreads();
   const uint64_t tile = s_tile, t0 = tile * kFfTile;
   constexpr uint32_t kGroup = 4; // rows whose loads are in flight together
@@ -677,267 +673,6 @@ __global__ __launch_bounds__(kFtThreads) void ck_filter_kernel(const SK *s, uint
     for (int c = 0; c < 3; c++) base[c] += rt[c];
   }
   if (tid == 0 && t0 + kFfTile >= n) { // the last tile: grand totals and the closing prefix sums
-    if (base[0] <= n) {
-      Pd[base[0]] = base[1];
-      Pe[base[0]] = base[2];
-    }
-    totals[0] = base[0];
-    totals[1] = base[1];
-    totals[2] = base[2];
-  }
-}
-
-// The last merge pass fused with keep / drop and survivor compaction: the
-// merged window never goes back to HBM (config 3: 256 MB written by the merge
-// and read again by the filter).  One workgroup per window, windows taken by
-// ticket in output order (the decoupled look-back of the survivor totals
-// waits only on windows already running):
-//   1. the window's sub-runs staged in LDS and merged (mg_window_merge, as
-//      ck_mg_merge_kernel), plus the record just before the window in merge
-//      order (the last of the k records preceding the sub-runs);
-//   2. ShouldKeepEntry (compact.cc:324-363) per output position from its LDS
-//      neighbour; an equal-txn duplicate finds its group head by galloping
-//      back in the window, or -- when its key group started in an earlier
-//      window -- the head's txn as the largest txn of the key among the
-//      records before the window (each run's first record of the key);
-//   3. the window's kept count / key+value bytes / entry bytes through a
-//      decoupled look-back over windows, then the survivors' columns and
-//      prefix sums written at their global positions (ck_filter_kernel's
-//      outputs, so everything after it is unchanged).
-constexpr uint32_t kMfRows = kKRegion / kMgThreads; // output positions per thread
-
-// the largest txn of x's key among the records of the pass's runs that come
-// before the window (run q's first record of the key before src[q] has run
-// q's largest txn of it): the group head's txn when x's key group began in an
-// earlier window.  O(k log run) reads; only for duplicates of equal txn at a
-// window's start.
-__device__ uint64_t mf_head_txn_before(const SK *in, const KGroup &gr, const KWin &d, const SK &x,
-                                       const KeyView &kv) {
-  uint64_t best = 0;
-  for (uint32_t q = 0; q < d.k; q++) {
-    const uint64_t s0 = gr.start[q], e = d.src[q];
-    if (e <= s0 || !ff_same_key(in[e - 1], x, kv)) continue;
-    uint64_t hi = e - 1; // in[hi] has x's key; in[lo] not (lo = s0 - 1: none)
-    int64_t lo = static_cast<int64_t>(s0) - 1;
-    for (uint64_t step = 1;; step <<= 1) {
-      if (hi == s0) break;
-      const uint64_t p = hi - s0 > step ? hi - step : s0;
-      if (ff_same_key(in[p], x, kv)) {
-        hi = p;
-      } else {
-        lo = static_cast<int64_t>(p);
-        break;
-      }
-    }
-    while (lo + 1 < static_cast<int64_t>(hi)) {
-      const uint64_t mid = static_cast<uint64_t>((lo + static_cast<int64_t>(hi)) >> 1);
-      if (ff_same_key(in[mid], x, kv)) hi = mid;
-      else lo = static_cast<int64_t>(mid);
-    }
-    best = in[hi].tx > best ? in[hi].tx : best;
-  }
-  return best;
-}
-
-__global__ __launch_bounds__(kMgThreads) void ck_mg_filter_kernel(const SK *in, const KWin *win, const KGroup *groups,
-                                                                  KeyView kv, uint64_t n, uint32_t base_level,
-                                                                  Rec out, uint64_t *Pd, uint64_t *Pe, uint64_t *ws,
-                                                                  uint64_t *totals, Abort stop,
-                                                                  unsigned long long *guard) {
-  __shared__ MgTile tile;
-  __shared__ uint16_t ix[2][kKRegion];
-  __shared__ KWin s_d;
-  __shared__ SK s_pred;
-  __shared__ uint32_t s_has_pred;
-  __shared__ uint64_t s_tile, s_pre[3];
-  __shared__ uint64_t s_row[kMfRows][kMgThreads / kWave][3];
-  if (stop()) return; // uniform over the grid: no ticket drawn, the host rejects the job
-  const uint32_t tid = threadIdx.x, lane = lane_id(), w = tid / kWave;
-#ifdef SSTC_AB_NOTICKET
-  if (tid == 0) s_tile = blockIdx.x;
-#else
-  if (tid == 0) { // windows by ticket in output order: a window's look-back waits only on running windows
-    const uint64_t t = __hip_atomic_fetch_add(ws, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (t + 1 == gridDim.x) __hip_atomic_store(ws, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_tile = t;
-  }
-#endif
-  __syncthreads();
-  const uint64_t wi = s_tile;
-  if (tid < kKWinWords)
-    reinterpret_cast<uint32_t *>(&s_d)[tid] = reinterpret_cast<const uint32_t *>(win + wi)[tid];
-  __syncthreads();
-  const KGroup &gr = groups[0]; // the last pass merges one group
-  const uint32_t total = s_d.n;
-  if (tid == 0) { // the record before the window in merge order: the last of the runs' predecessors
-    uint64_t bpos = ~0ull;
-    uint32_t bq = 0;
-    for (uint32_t q = 0; q < s_d.k; q++) {
-      const uint64_t e = s_d.src[q];
-      if (total == 0 || e <= gr.start[q]) continue;
-      if (bpos == ~0ull || kw_before(in[bpos], bq, in[e - 1], q, kv)) {
-        bpos = e - 1;
-        bq = q;
-      }
-    }
-    if (bpos != ~0ull) s_pred = in[bpos];
-    s_has_pred = bpos != ~0ull;
-  }
-  const int res = total ? mg_window_merge(in, tile, ix, s_d, kv) : -1; // barriers inside (total is uniform)
-  __syncthreads();
-  auto slot_at = [&](uint32_t p) -> uint32_t { return res < 0 ? p : ix[res][p]; };
-  uint32_t km = 0, kl[kMfRows], vl[kMfRows], ty[kMfRows];
-  uint64_t tx[kMfRows], ko[kMfRows];
-  bool bad_id = false;
-  // every row's side record (a 16 B gather by record id) in flight before the
-  // keep tests that need their types
-  RecX rr[kMfRows];
-#pragma unroll
-  for (uint32_t j = 0; j < kMfRows; j++) {
-    const uint32_t p = j * kMgThreads + tid;
-    const uint32_t id = p < total ? tile.rs[slot_at(p)].w : 0u; // SortKey.id
-    bad_id |= p < total && id >= n;
-    rr[j] = kv.rx[id < n ? id : 0u];
-  }
-#pragma unroll
-  for (uint32_t j = 0; j < kMfRows; j++) {
-    const uint32_t p = j * kMgThreads + tid;
-    kl[j] = vl[j] = ty[j] = 0;
-    tx[j] = ko[j] = 0;
-    if (p >= total) continue;
-    const SK x = tile.get(slot_at(p));
-    uint32_t keep;
-    if (x.id >= n) {
-      keep = 0;
-    } else if (s_d.out + p == 0) {
-      keep = 1; // the first merged record (compact.cc:336-339)
-    } else {
-      const SK pv = p ? tile.get(slot_at(p - 1)) : s_pred;
-      if (!ff_same_key(pv, x, kv)) {
-        keep = rr[j].type == kTypePut ? 1u : (base_level ? 0u : 1u);
-      } else if (x.tx != pv.tx) {
-        keep = 0;
-      } else { // equal txn: the group head's txn decides (galloping back in the window)
-        int64_t lo = -1;
-        uint32_t hi = p ? p - 1 : 0;
-        if (p) {
-          for (uint32_t step = 1;; step <<= 1) {
-            if (hi == 0) break;
-            const uint32_t q = hi > step ? hi - step : 0;
-            if (ff_same_key(tile.get(slot_at(q)), x, kv)) {
-              hi = q;
-            } else {
-              lo = q;
-              break;
-            }
-          }
-          while (lo + 1 < static_cast<int64_t>(hi)) {
-            const uint32_t mid = static_cast<uint32_t>((lo + static_cast<int64_t>(hi)) >> 1);
-            if (ff_same_key(tile.get(slot_at(mid)), x, kv)) hi = mid;
-            else lo = mid;
-          }
-        }
-        const bool in_window = p && (lo >= 0 || !s_has_pred || !ff_same_key(s_pred, x, kv));
-        const uint64_t htx = in_window ? tile.get(slot_at(hi)).tx : mf_head_txn_before(in, gr, s_d, x, kv);
-        keep = htx == x.tx ? 1u : 0u;
-      }
-    }
-    km |= keep << j;
-    kl[j] = x.kl;
-    tx[j] = x.tx;
-    vl[j] = rr[j].vl;
-    ty[j] = rr[j].type;
-    ko[j] = rr[j].ko;
-  }
-  if (__syncthreads_or(bad_id)) { // no output from a window with an impossible record id
-    if (tid == 0) atomicOr(guard, kGuardMergeId);
-    km = 0;
-  }
-  // per row and wave: kept count and the two byte sums, exchanged once through LDS
-#pragma unroll
-  for (uint32_t j = 0; j < kMfRows; j++) {
-    const bool k = (km >> j) & 1u;
-    const uint64_t c = static_cast<uint64_t>(__popcll(__ballot(k)));
-    const uint64_t d = wave_sum_u64(k ? data_bytes(kl[j], vl[j]) : 0ull);
-    const uint64_t e = wave_sum_u64(k ? entry_size(kl[j], vl[j]) : 0ull);
-    if (lane == 0) {
-      s_row[j][w][0] = c;
-      s_row[j][w][1] = d;
-      s_row[j][w][2] = e;
-    }
-  }
-  __syncthreads();
-#ifdef SSTC_AB_NOLB
-  if (w < 3 && lane == 0) s_pre[w] = 0;
-  if (false) {
-#else
-  if (w < 3) { // wave c: decoupled look-back of total c over the windows
-#endif
-    uint64_t *status = ws + 1 + static_cast<uint64_t>(w) * gridDim.x;
-    constexpr uint32_t kRW = kMfRows * (kMgThreads / kWave);
-    const uint64_t tot =
-        wave_sum_u64(lane < kRW ? s_row[lane / (kMgThreads / kWave)][lane % (kMgThreads / kWave)][w] : 0ull);
-    uint64_t prefix = 0;
-    if (wi == 0) {
-      if (lane == 0) __hip_atomic_store(&status[0], kLbInc | tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      if (lane == 0) __hip_atomic_store(&status[wi], kLbAgg | tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      int64_t pp = static_cast<int64_t>(wi) - 1; // window [pp - 63, pp]
-      uint64_t spins = 0;
-      for (;;) {
-        const int64_t q = pp - static_cast<int64_t>(lane);
-        const uint64_t st = q >= 0 ? __hip_atomic_load(&status[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                   : kLbInc;
-        const uint64_t inc = __ballot((st >> 62) == 2);
-        const uint32_t need = inc ? static_cast<uint32_t>(__ffsll(static_cast<long long>(inc))) : kWave;
-        const uint64_t zero = __ballot((st >> 62) == 0 && lane < need);
-        if (zero) {
-          if (++spins > kLbSpinLimit) break; // a predecessor never published: give up (wrong sums, no hang)
-          __builtin_amdgcn_s_sleep(1);
-          continue;
-        }
-        prefix += wave_sum_u64(lane < need ? (st & kLbVal) : 0);
-        if (inc) break;
-        pp -= kWave;
-      }
-      if (lane == 0)
-        __hip_atomic_store(&status[wi], kLbInc | (prefix + tot), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if (lane == 0) s_pre[w] = prefix;
-  }
-  __syncthreads();
-  uint64_t base[3] = {s_pre[0], s_pre[1], s_pre[2]};
-#pragma unroll
-  for (uint32_t j = 0; j < kMfRows; j++) { // row by row: survivors of a row are lane-consecutive
-    const bool k = (km >> j) & 1u;
-    uint64_t off[3] = {base[0], base[1], base[2]}, rt[3] = {0, 0, 0};
-#pragma unroll
-    for (uint32_t x = 0; x < kMgThreads / kWave; x++) { // waves before this one in the row
-#pragma unroll
-      for (int c = 0; c < 3; c++) {
-        const uint64_t y = s_row[j][x][c];
-        off[c] += x < w ? y : 0ull;
-        rt[c] += y;
-      }
-    }
-    const uint64_t bal = __ballot(k);
-    const uint32_t rank = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(bal >> 32),
-                                                    __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(bal), 0u));
-    const uint64_t dv = k ? data_bytes(kl[j], vl[j]) : 0ull, ev = k ? entry_size(kl[j], vl[j]) : 0ull;
-    const uint64_t dincl = wave_incl_scan_u64(dv), eincl = wave_incl_scan_u64(ev);
-    const uint64_t q = off[0] + rank;
-    if (k && q < n) { // (q < n holds by construction; the bound guards the stores)
-      out.type[q] = static_cast<uint8_t>(ty[j]);
-      out.kl[q] = kl[j];
-      out.tx[q] = tx[j];
-      out.ko[q] = ko[j];
-      Pd[q] = off[1] + dincl - dv;
-      Pe[q] = off[2] + eincl - ev;
-    }
-#pragma unroll
-    for (int c = 0; c < 3; c++) base[c] += rt[c];
-  }
-  if (tid == 0 && wi + 1 == gridDim.x) { // the last window: grand totals and the closing prefix sums
     if (base[0] <= n) {
       Pd[base[0]] = base[1];
       Pe[base[0]] = base[2];
@@ -1368,13 +1103,12 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     const uint64_t *rb = d_rs; // run starts, nruns + 1
     const Abort dec_fail{err_count, errs, nullptr}, stop{err_count, errs, bad};
     const uint64_t fftiles = (n + kFfTile - 1) / kFfTile;
-    uint64_t *ffws = nullptr; // look-back words of the filter (fused into the last merge pass when there is one)
+    uint64_t *ffws = nullptr; // look-back words of the filter
     // survivors of the keep / drop filter (sized by n: the kept count is known after it)
     uint64_t *totals = pool.get<uint64_t>(3);
     Rec KR{pool.get<uint8_t>(n), pool.get<uint32_t>(n), nullptr, pool.get<uint64_t>(n), pool.get<uint64_t>(n),
            nullptr}; // vl / vo: not needed by the whole-entry encode
     uint64_t *Pd = pool.get<uint64_t>(n + 1), *Pe = pool.get<uint64_t>(n + 1);
-    bool fused = false; // the filter ran inside the last merge pass
     // k-way merge passes; run boundaries of every pass are known on the host,
     // so all group descriptors go up in one upload (lives until the next sync)
     std::vector<KGroup> kg;
@@ -1431,12 +1165,10 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
         pass_wgs.push_back(wgs);
         cur = std::move(next);
       }
-      // the filter's look-back status words (its tiles, or the last pass's
-      // windows when it runs fused into that pass), cleared by the check kernel
-      const uint64_t lb_tiles = std::max<uint64_t>(fftiles, kg.empty() ? 0 : pass_wgs.back());
-      ffws = pool.get<uint64_t>(1 + 3 * lb_tiles);
+      // the filter's look-back status words, cleared by the check kernel
+      ffws = pool.get<uint64_t>(1 + 3 * fftiles);
       ck_check_blocks_kernel<<<grid(nblocks), 256, 0, s>>>(A, rb_all, nblocks, rb, nruns, kv, bad, dec_fail, ffws,
-                                                           1 + 3 * lb_tiles, d_blk_off, d_blk_len, guard + 1);
+                                                           1 + 3 * fftiles, d_blk_off, d_blk_len, guard + 1);
       if (!kg.empty()) {
         KGroup *d_kg = pool.get<KGroup>(kg.size());
         CK(hipMemcpyAsync(d_kg, kg.data(), kg.size() * sizeof(KGroup), hipMemcpyHostToDevice, s));
@@ -1454,30 +1186,19 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
           ck_kw_sample_kernel<<<grid(pass_ids[p]), 256, 0, s>>>(A, d_kg + at, ng, pass_ids[p], Sm, stop);
           ck_kw_split_kernel<<<grid(static_cast<uint64_t>(pass_ids[p]) * 8), 256, 0, s>>>(A, Sm, d_kg + at, ng, pass_ids[p], kv, Cm, Gm, stop);
           ck_kw_bounds_kernel<<<grid(pass_ids[p]), 256, 0, s>>>(d_kg + at, ng, pass_ids[p], Gm, Jm, stop);
-#ifdef SSTC_AB_UNFUSED
-          const bool last = false;
-#else
-          const bool last = p + 1 == pass_groups.size();
-#endif
           if (pass_wgs[p]) {
             ck_kw_win_kernel<<<grid(pass_wgs[p]), 256, 0, s>>>(d_kg + at, ng, pass_wgs[p], Cm, Gm, Jm, Wm, stop);
-            if (last) // merged records go straight into the keep / drop + survivor compaction
-              ck_mg_filter_kernel<<<pass_wgs[p], kMgThreads, 0, s>>>(A, Wm, d_kg + at, kv, n, base_level, KR, Pd,
-                                                                      Pe, ffws, totals, stop, guard);
-            else
-              ck_mg_merge_kernel<<<pass_wgs[p], kMgThreads, 0, s>>>(A, B, Wm, kv);
-            fused = last;
+            ck_mg_merge_kernel<<<pass_wgs[p], kMgThreads, 0, s>>>(A, B, Wm, kv);
           }
-          if (!last) std::swap(A, B);
+          std::swap(A, B);
           at += ng;
         }
       }
     }
     // 3. keep / drop and the survivors gathered in merge order with their
     // prefix sums (sized by n: the kept count is known after the pass)
-    if (!fused)
-      ck_filter_kernel<<<static_cast<uint32_t>(fftiles), kFtThreads, 0, s>>>(A, n, kv, base_level, KR, Pd, Pe,
-                                                                          ffws, totals, stop, guard);
+    ck_filter_kernel<<<static_cast<uint32_t>(fftiles), kFtThreads, 0, s>>>(A, n, kv, base_level, KR, Pd, Pe, ffws,
+                                                                        totals, stop, guard);
     if (arena.fault == 1) CK(hipMemsetAsync(KR.ko, 0xFF, n * sizeof(uint64_t), s)); // test: bad key offsets
     if (arena.fault == 2) CK(hipMemsetAsync(Pe, 0x5A, (n + 1) * sizeof(uint64_t), s)); // test: bad prefix sums
     fetch(arena, s, {totals, reinterpret_cast<const uint64_t *>(bad),
