@@ -26,8 +26,10 @@ for c in ("FETCH_SIZE", "WRITE_SIZE"):
     start = max(i for i, r in enumerate(rows) if "count_kernel" in r["Kernel_Name"])
     tot = 0.0
     for r in rows[start:]:
+        if r["Kernel_Name"].startswith("__amd_rocclr"):  # the caller's copies after the call, not the job
+            continue
         v = float(r["Counter_Value"]) * 1024 * (2 if c == "FETCH_SIZE" else 1)
-        k = r["Kernel_Name"].split("(")[0].replace("sstc::(anonymous namespace)::", "").replace("sstc::", "")
+        k = r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("sstc::", "").split("(")[0]
         per.setdefault(k, {}).setdefault(c, 0.0)
         per[k][c] += v
         tot += v
