@@ -104,6 +104,12 @@ const char *sstc_last_error_string(void);
 int sstc_ctx_create(int device, void *stream, sstc_ctx **out);
 int sstc_ctx_destroy(sstc_ctx *ctx);
 int sstc_ctx_set_stream(sstc_ctx *ctx, void *stream);
+/* The current stream must still be alive when sstc_ctx_set_stream switches
+ * away from it (an event is recorded on it).  A caller about to destroy the
+ * context's stream synchronizes it and calls sstc_ctx_drop_stream first: the
+ * context forgets it without recording anything on it and runs on the null
+ * stream until the next sstc_ctx_set_stream. */
+int sstc_ctx_drop_stream(sstc_ctx *ctx);
 /* Pre-size the workspace for up to max_blocks blocks and max_records records. */
 int sstc_ctx_reserve(sstc_ctx *ctx, uint64_t max_blocks, uint64_t max_records);
 /* Synchronise the stream; return the number of blocks that failed since the

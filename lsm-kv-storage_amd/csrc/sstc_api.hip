@@ -134,6 +134,14 @@ uint32_t sstc_version(void) { return SSTC_ABI_VERSION; }
 int sstc__fail(int code, const char *what) { return fail(code, what); }
 int sstc__ctx_device(const sstc_ctx *c) { return c ? c->device : -1; }
 
+// test hook (not in the public header): the context's scan epoch, to run scans
+// across the 14-bit wrap of next_epoch without 16 k calls first
+int sstc__ctx_set_scan_epoch(sstc_ctx *c, uint32_t epoch) {
+  if (!c || epoch >= sstc::kScanEpochs) return SSTC_E_INVALID_ARG;
+  c->scan_epoch = epoch;
+  return SSTC_OK;
+}
+
 // test hook (not in the public header): corrupt the next compaction jobs'
 // filter output on the device (sstc::Arena::fault) so the job's consistency
 // guard can be exercised; 0 turns it off
@@ -221,6 +229,12 @@ int sstc_ctx_set_stream(sstc_ctx *c, void *stream) {
   SSTC_HIP(hipEventRecord(c->switch_ev, c->stream), "stream switch: record on the old stream");
   SSTC_HIP(hipStreamWaitEvent(ns, c->switch_ev, 0), "stream switch: new stream waits");
   c->stream = ns;
+  return SSTC_OK;
+}
+
+int sstc_ctx_drop_stream(sstc_ctx *c) {
+  if (!c) return fail(SSTC_E_INVALID_ARG, "ctx is NULL");
+  c->stream = nullptr; // the caller synchronized it: nothing is recorded on it
   return SSTC_OK;
 }
 

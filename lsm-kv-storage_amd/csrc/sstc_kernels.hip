@@ -189,10 +189,15 @@ __device__ __forceinline__ void store_window(const uint8_t *img, uint8_t *gd, ui
     if (lo >= keep_lo && lo + 16 <= keep_hi) {
       const u32x4 v = *reinterpret_cast<const u32x4 *>(img + 16 * c);
       __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(gd + lo));
-    } else {
+    } else { // an edge chunk shared with a neighbouring block: only this block's bytes,
+             // as dwords where they are dword-aligned (back-to-back 4188 B blocks: always)
       const int64_t x0 = lo < keep_lo ? keep_lo : lo;
       const int64_t x1 = lo + 16 < keep_hi ? lo + 16 : keep_hi;
-      for (int64_t x = x0; x < x1; x++) gd[x] = img[x - base];
+      int64_t x = x0;
+      for (; x < x1 && (x & 3); x++) gd[x] = img[x - base];
+      for (; x + 4 <= x1; x += 4)
+        *reinterpret_cast<uint32_t *>(gd + x) = *reinterpret_cast<const uint32_t *>(img + (x - base));
+      for (; x < x1; x++) gd[x] = img[x - base];
     }
   }
 }
@@ -282,6 +287,41 @@ __device__ __forceinline__ void rt_small(const RtArgs &a, uint64_t b, uint8_t *i
   const uint64_t doff = uniform64(rd.u64(L - 8));
   uint32_t st = check_extra(L, n, doff);
   if (st != kBlkOk) return rt_report(a, b, st, 0);
+  if (n <= kWave) { // one entry per lane: parse, validate and regenerate in one pass
+    uint8_t *wimg = img + pad;
+    const uint32_t i = lane, nn = static_cast<uint32_t>(n), dd = static_cast<uint32_t>(doff);
+    Entry e{};
+    uint64_t s = 0;
+    if (i < nn) {
+      s = rd.u64(dd + 16ull * i);
+      e = parse_entry(rd, s, doff, a.txn_mode);
+    }
+    const uint64_t bad = __ballot(e.code != kBlkOk);
+    if (bad) return rt_report(a, b, __shfl(e.code, __ffsll(static_cast<long long>(bad)) - 1, kWave), 0);
+    const uint32_t sz = static_cast<uint32_t>(e.size); // < L < 2^32
+    const uint32_t incl = wave_incl_scan_u32(sz);
+    const uint32_t data = __shfl(incl, kWave - 1, kWave);
+    const bool canon = doff + 16 * n + 16 == L && data == doff && !__any(i < nn && s != incl - sz);
+    const bool qk = i < nn && a.txn_mode == 0u && e.type != kTypeDeleted && e.vlen == 0u;
+    if (!canon) {
+      const uint64_t out_len = data + 16 * n + 16;
+      if (out_len > L) return rt_report(a, b, kBlkNoRoom, 0);
+      rt_repack_wave(a, a.src + off, a.dst + off, n, doff, data, img);
+      return rt_report(a, b, kBlkOk, out_len);
+    }
+    if (i < nn) { // offset entry (start = scan = stored start, size recomputed), compat txn
+      lds_st_u64u(wimg, dd + 16u * i, incl - sz);
+      lds_st_u64u(wimg, dd + 16u * i + 8u, sz);
+      if (qk) lds_st_u64u(wimg, static_cast<uint32_t>(s) + 9u + e.klen, e.txn);
+    }
+    if (lane == 0) { // extra: n, data bytes (== doff)
+      lds_st_u64u(wimg, L - 16, n);
+      lds_st_u64u(wimg, L - 8, data);
+    }
+    wave_lds_sync();
+    store_window(img, a.dst + (off - pad), (pad + L + 15u) >> 4, 0, pad, pad + L);
+    return rt_report(a, b, kBlkOk, L);
+  }
   const Pass1 p = rt_pass1(rd, L, n, doff, a.txn_mode);
   if (p.st != kBlkOk) return rt_report(a, b, p.st, 0);
   if (!p.canon) {
@@ -425,13 +465,106 @@ __global__ __launch_bounds__(kRtWaves *kWave, 8) void rt_kernel(RtArgs a) {
   uint32_t L, pad;
   const uint32_t cls = rt_classify(a, b, off, L, pad);
   if (cls == 0) {
+#ifdef SSTC_RT_VGPR
+    { // A/B: stage through VGPRs (non-temporal 16 B loads, then LDS stores)
+      const uint32_t nch = (pad + L + 15u) >> 4;
+      const u32x4 *g = reinterpret_cast<const u32x4 *>(a.src + (off - pad));
+      u32x4 v[kRtSlot / 16 / kWave + 1];
+#pragma unroll
+      for (uint32_t k = 0; k < kRtSlot / 16 / kWave + 1; k++) {
+        const uint32_t c = k * kWave + lane_id();
+        if (c < nch) v[k] = __builtin_nontemporal_load(g + c);
+      }
+#pragma unroll
+      for (uint32_t k = 0; k < kRtSlot / 16 / kWave + 1; k++) {
+        const uint32_t c = k * kWave + lane_id();
+        if (c < nch) *reinterpret_cast<u32x4 *>(img + 16 * c) = v[k];
+      }
+      wave_lds_sync();
+    }
+#else
     rt_stage<1>(a.src + (off - pad), img, (pad + L + 15u) >> 4);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
     rt_small(a, b, img, off, L, pad);
   } else if (cls == 1) {
     rt_large(a, b, img, off, L, pad);
   }
 }
+
+#ifdef SSTC_RT_MODE
+// A/B variants (not shipped unless measured faster): persistent waves looping
+// over blocks.  Mode 1: one LDS slot per wave; the next block's LDS-DMA is
+// issued right after the current block's store phase has read the slot, so the
+// wave's stores of block i and loads of block i+1 are in flight together (no
+// vmcnt wait on the stores alone).  Mode 2: two slots per wave; block i+1's
+// DMA is issued BEFORE block i is parsed (the wait for block i then counts
+// only block i+1's DMA instructions as allowed outstanding).
+__device__ __forceinline__ void rt_wait_vm_le(uint32_t k) { // s_waitcnt vmcnt(k), k <= 5 (immediate)
+  switch (k) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+  }
+}
+
+__global__ __launch_bounds__(kRtWaves *kWave, 8) void rt_persist_kernel(RtArgs a) {
+  constexpr uint32_t kSlots = SSTC_RT_MODE == 2 ? 2 : 1;
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kRtWaves * kSlots * kRtSlot];
+  const uint32_t wave = uniform(threadIdx.x / kWave);
+  const uint64_t W = static_cast<uint64_t>(gridDim.x) * kRtWaves;
+  uint8_t *slot0 = lds + wave * kSlots * kRtSlot;
+  uint64_t b = static_cast<uint64_t>(blockIdx.x) * kRtWaves + wave;
+  if constexpr (kSlots == 1) {
+    for (; b < a.nblocks; b += W) {
+      uint64_t off;
+      uint32_t L, pad;
+      const uint32_t cls = rt_classify(a, b, off, L, pad);
+      if (cls == 0) {
+        rt_stage<1>(a.src + (off - pad), slot0, (pad + L + 15u) >> 4);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // this DMA (and the previous block's stores before it)
+        rt_small(a, b, slot0, off, L, pad);
+      } else if (cls == 1) {
+        rt_large(a, b, slot0, off, L, pad);
+      }
+    }
+  } else {
+    // prologue: stage the first small block
+    uint64_t off = 0;
+    uint32_t L = 0, pad = 0, cls = 2, cur = 0;
+    if (b < a.nblocks) {
+      cls = rt_classify(a, b, off, L, pad);
+      if (cls == 0) rt_stage<1>(a.src + (off - pad), slot0, (pad + L + 15u) >> 4);
+    }
+    for (; b < a.nblocks; b += W) {
+      // next block's DMA into the other slot before this one is parsed
+      const uint64_t nb = b + W;
+      uint64_t noff = 0;
+      uint32_t nL = 0, npad = 0, ncls = 2, nk = 0;
+      uint8_t *img = slot0 + cur * kRtSlot, *nimg = slot0 + (cur ^ 1u) * kRtSlot;
+      if (nb < a.nblocks) {
+        ncls = rt_classify(a, nb, noff, nL, npad);
+        if (ncls == 0) nk = rt_stage<1>(a.src + (noff - npad), nimg, (npad + nL + 15u) >> 4);
+      }
+      if (cls == 0) {
+        rt_wait_vm_le(nk); // this block's DMA (issued before the next one's) has landed
+        rt_small(a, b, img, off, L, pad);
+      } else if (cls == 1) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // rt_large restages through its slot
+        rt_large(a, b, img, off, L, pad);
+      }
+      off = noff;
+      L = nL;
+      pad = npad;
+      cls = ncls;
+      cur ^= 1u;
+    }
+  }
+}
+#endif
 
 // ---------------------------------------------------------------------------
 // Decode to the record table.
@@ -1949,7 +2082,15 @@ hipError_t launch_roundtrip(const RtArgs &a, hipStream_t s) {
   // (256 MiB, Infinity-Cache resident) but -2.5 % on 1 GiB (profiles/r01_ab_xcd.log)
   // (persistent waves looping over blocks in one slot, and storing the staged
   // block before the parse, were both slower: profiles/r02_ab/rt_ab.md)
+#ifdef SSTC_RT_MODE
+  if (a.nblocks) {
+    const uint32_t per_cu = SSTC_RT_MODE == 2 ? 4u : 8u; // workgroups per CU the LDS allows
+    const uint32_t g = std::min<uint64_t>(grid_for(a.nblocks, kRtWaves), static_cast<uint64_t>(a.num_cus) * per_cu);
+    rt_persist_kernel<<<g, kRtWaves * kWave, 0, s>>>(a);
+  }
+#else
   if (a.nblocks) rt_kernel<<<grid_for(a.nblocks, kRtWaves), kRtWaves * kWave, 0, s>>>(a);
+#endif
   return hipGetLastError();
 }
 

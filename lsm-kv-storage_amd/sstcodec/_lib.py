@@ -91,6 +91,7 @@ def load():
         "sstc_ctx_create": (ctypes.c_int, [ctypes.c_int, c_vp, P(c_vp)]),
         "sstc_ctx_destroy": (ctypes.c_int, [c_vp]),
         "sstc_ctx_set_stream": (ctypes.c_int, [c_vp, c_vp]),
+        "sstc_ctx_drop_stream": (ctypes.c_int, [c_vp]),
         "sstc_ctx_reserve": (ctypes.c_int, [c_vp, c_u64, c_u64]),
         "sstc_ctx_error_count": (ctypes.c_int, [c_vp, P(c_u64)]),
         "sstc_ctx_reset_errors": (ctypes.c_int, [c_vp]),
@@ -107,7 +108,8 @@ def load():
         "sstc_roundtrip_host": (ctypes.c_int, [c_vp, c_vp, c_vp, c_u64, c_vp, c_vp, c_u64, c_u32, c_u64, c_vp,
                                                c_vp]),
         "sstc_copy_probe": (ctypes.c_int, [c_vp, c_vp, c_vp, c_u64]),
-        "sstc__ctx_set_fault": (ctypes.c_int, [c_vp, c_u32]),  # test hook (sstc_api.hip), not in the header
+        "sstc__ctx_set_fault": (ctypes.c_int, [c_vp, c_u32]),  # test hooks (sstc_api.hip), not in the header
+        "sstc__ctx_set_scan_epoch": (ctypes.c_int, [c_vp, c_u32]),
         "sstc_open_tables": (ctypes.c_int, [c_vp, c_vp, c_u64, c_vp, c_vp, c_u32, c_u64, c_vp, c_vp, c_vp, c_vp,
                                             c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
         "sstc_pipe_create": (ctypes.c_int, [c_vp, c_u32, P(c_vp)]),

@@ -111,3 +111,14 @@ def test_build_provenance_matches_tree():
     spec.loader.exec_module(b)
     ok, bad = b.tree_matches_build()
     assert ok, f"library built from other sources than the tree's: {bad[:5]}"
+
+
+def test_in_tree_library_is_the_one_loaded():
+    """SSTC_LIB_PATH (the A/B scripts' override) must not leak into a test run:
+    the provenance test checks the in-tree build, so the tests must load it."""
+    import os
+    from sstcodec import _lib
+    intree = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(_lib.__file__))), "lib",
+                          "libsstcodec.so")
+    assert os.path.realpath(_lib.LIB_PATH) == os.path.realpath(intree), \
+        f"SSTC_LIB_PATH={os.environ.get('SSTC_LIB_PATH')} overrides the in-tree library in a test run"

@@ -1,6 +1,7 @@
-"""A/B of rt_kernel variants (SSTC_RT_VARIANT, one process each): HIP-event
-time of sstc_roundtrip_blocks at config 2 (65 536 blocks) and 4x (1 GiB),
-identity checked.   python tools/ab_rt.py 0,4,8"""
+"""A/B of rt_kernel variants, one process each: HIP-event time of
+sstc_roundtrip_blocks at config 2 (65 536 blocks) and 4x (1 GiB), identity
+checked.  A variant is a library build lsm-kv-storage_amd/lib/ab/<name>/
+(tools/ab_build.sh) or 'cur' (the tree's).   python tools/ab_rt.py cur,p1,p2 [rounds]"""
 import json
 import os
 import subprocess
@@ -34,9 +35,13 @@ for nb in (65536, 262144):
 print(json.dumps(out))
 '''
 res = {}
-for v in sys.argv[1].split(","):
-    r = subprocess.run([sys.executable, "-c", CHILD, ROOT], env=dict(os.environ, SSTC_RT_VARIANT=v),
-                       capture_output=True, text=True, timeout=300)
+rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 1
+for v in sys.argv[1].split(",") * rounds:
+    env = dict(os.environ)
+    env.pop("SSTC_LIB_PATH", None)
+    if v != "cur":
+        env["SSTC_LIB_PATH"] = os.path.join(ROOT, "lsm-kv-storage_amd", "lib", "ab", v, "libsstcodec.so")
+    r = subprocess.run([sys.executable, "-c", CHILD, ROOT], env=env, capture_output=True, text=True, timeout=300)
     line = [x for x in r.stdout.splitlines() if x.startswith("{")]
     res[v] = json.loads(line[-1]) if line else {"error": r.stderr[-800:]}
     print(v, res[v], flush=True)
