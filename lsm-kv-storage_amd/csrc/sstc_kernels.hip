@@ -465,106 +465,14 @@ __global__ __launch_bounds__(kRtWaves *kWave, 8) void rt_kernel(RtArgs a) {
   uint32_t L, pad;
   const uint32_t cls = rt_classify(a, b, off, L, pad);
   if (cls == 0) {
-#ifdef SSTC_RT_VGPR
-    { // A/B: stage through VGPRs (non-temporal 16 B loads, then LDS stores)
-      const uint32_t nch = (pad + L + 15u) >> 4;
-      const u32x4 *g = reinterpret_cast<const u32x4 *>(a.src + (off - pad));
-      u32x4 v[kRtSlot / 16 / kWave + 1];
-#pragma unroll
-      for (uint32_t k = 0; k < kRtSlot / 16 / kWave + 1; k++) {
-        const uint32_t c = k * kWave + lane_id();
-        if (c < nch) v[k] = __builtin_nontemporal_load(g + c);
-      }
-#pragma unroll
-      for (uint32_t k = 0; k < kRtSlot / 16 / kWave + 1; k++) {
-        const uint32_t c = k * kWave + lane_id();
-        if (c < nch) *reinterpret_cast<u32x4 *>(img + 16 * c) = v[k];
-      }
-      wave_lds_sync();
-    }
-#else
     rt_stage<1>(a.src + (off - pad), img, (pad + L + 15u) >> 4);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
     rt_small(a, b, img, off, L, pad);
   } else if (cls == 1) {
     rt_large(a, b, img, off, L, pad);
   }
 }
 
-#ifdef SSTC_RT_MODE
-// A/B variants (not shipped unless measured faster): persistent waves looping
-// over blocks.  Mode 1: one LDS slot per wave; the next block's LDS-DMA is
-// issued right after the current block's store phase has read the slot, so the
-// wave's stores of block i and loads of block i+1 are in flight together (no
-// vmcnt wait on the stores alone).  Mode 2: two slots per wave; block i+1's
-// DMA is issued BEFORE block i is parsed (the wait for block i then counts
-// only block i+1's DMA instructions as allowed outstanding).
-__device__ __forceinline__ void rt_wait_vm_le(uint32_t k) { // s_waitcnt vmcnt(k), k <= 5 (immediate)
-  switch (k) {
-    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
-    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
-    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
-    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
-    default: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
-  }
-}
-
-__global__ __launch_bounds__(kRtWaves *kWave, 8) void rt_persist_kernel(RtArgs a) {
-  constexpr uint32_t kSlots = SSTC_RT_MODE == 2 ? 2 : 1;
-  __shared__ __attribute__((aligned(16))) uint8_t lds[kRtWaves * kSlots * kRtSlot];
-  const uint32_t wave = uniform(threadIdx.x / kWave);
-  const uint64_t W = static_cast<uint64_t>(gridDim.x) * kRtWaves;
-  uint8_t *slot0 = lds + wave * kSlots * kRtSlot;
-  uint64_t b = static_cast<uint64_t>(blockIdx.x) * kRtWaves + wave;
-  if constexpr (kSlots == 1) {
-    for (; b < a.nblocks; b += W) {
-      uint64_t off;
-      uint32_t L, pad;
-      const uint32_t cls = rt_classify(a, b, off, L, pad);
-      if (cls == 0) {
-        rt_stage<1>(a.src + (off - pad), slot0, (pad + L + 15u) >> 4);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // this DMA (and the previous block's stores before it)
-        rt_small(a, b, slot0, off, L, pad);
-      } else if (cls == 1) {
-        rt_large(a, b, slot0, off, L, pad);
-      }
-    }
-  } else {
-    // prologue: stage the first small block
-    uint64_t off = 0;
-    uint32_t L = 0, pad = 0, cls = 2, cur = 0;
-    if (b < a.nblocks) {
-      cls = rt_classify(a, b, off, L, pad);
-      if (cls == 0) rt_stage<1>(a.src + (off - pad), slot0, (pad + L + 15u) >> 4);
-    }
-    for (; b < a.nblocks; b += W) {
-      // next block's DMA into the other slot before this one is parsed
-      const uint64_t nb = b + W;
-      uint64_t noff = 0;
-      uint32_t nL = 0, npad = 0, ncls = 2, nk = 0;
-      uint8_t *img = slot0 + cur * kRtSlot, *nimg = slot0 + (cur ^ 1u) * kRtSlot;
-      if (nb < a.nblocks) {
-        ncls = rt_classify(a, nb, noff, nL, npad);
-        if (ncls == 0) nk = rt_stage<1>(a.src + (noff - npad), nimg, (npad + nL + 15u) >> 4);
-      }
-      if (cls == 0) {
-        rt_wait_vm_le(nk); // this block's DMA (issued before the next one's) has landed
-        rt_small(a, b, img, off, L, pad);
-      } else if (cls == 1) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); // rt_large restages through its slot
-        rt_large(a, b, img, off, L, pad);
-      }
-      off = noff;
-      L = nL;
-      pad = npad;
-      cls = ncls;
-      cur ^= 1u;
-    }
-  }
-}
-#endif
 
 // ---------------------------------------------------------------------------
 // Decode to the record table.
@@ -2080,17 +1988,10 @@ hipError_t launch_copy_probe(const uint8_t *src, uint8_t *dst, uint64_t n16, hip
 hipError_t launch_roundtrip(const RtArgs &a, hipStream_t s) {
   // blocks in dispatch order: the XCD-grouped order measured +3 % at config 2
   // (256 MiB, Infinity-Cache resident) but -2.5 % on 1 GiB (profiles/r01_ab_xcd.log)
-  // (persistent waves looping over blocks in one slot, and storing the staged
-  // block before the parse, were both slower: profiles/r02_ab/rt_ab.md)
-#ifdef SSTC_RT_MODE
-  if (a.nblocks) {
-    const uint32_t per_cu = SSTC_RT_MODE == 2 ? 4u : 8u; // workgroups per CU the LDS allows
-    const uint32_t g = std::min<uint64_t>(grid_for(a.nblocks, kRtWaves), static_cast<uint64_t>(a.num_cus) * per_cu);
-    rt_persist_kernel<<<g, kRtWaves * kWave, 0, s>>>(a);
-  }
-#else
+  // (persistent waves looping over blocks in one or two slots, staging through
+  // VGPRs instead of LDS-DMA, and storing the staged block before the parse
+  // were all slower: profiles/r02_ab/rt_ab.md, profiles/r03_ab/rt_1gib.md)
   if (a.nblocks) rt_kernel<<<grid_for(a.nblocks, kRtWaves), kRtWaves * kWave, 0, s>>>(a);
-#endif
   return hipGetLastError();
 }
 
