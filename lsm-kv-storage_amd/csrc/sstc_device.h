@@ -55,7 +55,13 @@ __device__ __forceinline__ uint32_t xcd_logical_block(uint32_t i, uint32_t n) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + k;
 }
 
-// ---- LDS image reads (image is padded by >= 16 bytes past its last byte) ----
+// ---- LDS image reads / writes at arbitrary byte offsets ---------------------
+// Reads: aligned dwords + v_alignbyte (the image is padded by >= 16 bytes past
+// its last byte).  gfx950 runs LDS in unaligned mode (the compiler's default
+// target features unaligned-access-mode + unaligned-ds-access), but single
+// unaligned ds_read_b32 / b64 measured slower in the LDS-bound round trip
+// (profiles/r03_ab/unaligned_lds.md).  Writes: one ds_write_b32 / b64 at any
+// alignment (replacing up to 8 byte stores).
 __device__ __forceinline__ uint32_t lds_u8(const uint8_t *img, uint32_t off) { return img[off]; }
 
 __device__ __forceinline__ uint32_t lds_u32u(const uint8_t *img, uint32_t off) {
@@ -71,16 +77,11 @@ __device__ __forceinline__ uint64_t lds_u64u(const uint8_t *img, uint32_t off) {
   return (static_cast<uint64_t>(hi) << 32) | lo;
 }
 
-// Unaligned LDS stores.  `aligned4` must be wave-uniform for good code.
 __device__ __forceinline__ void lds_st_u64u(uint8_t *img, uint32_t off, uint64_t v) {
-  if ((off & 3u) == 0) {
-    uint32_t *w = reinterpret_cast<uint32_t *>(img + off);
-    w[0] = static_cast<uint32_t>(v);
-    w[1] = static_cast<uint32_t>(v >> 32);
-  } else {
-#pragma unroll
-    for (int j = 0; j < 8; j++) img[off + j] = static_cast<uint8_t>(v >> (8 * j));
-  }
+  __builtin_memcpy(img + off, &v, 8);
+}
+__device__ __forceinline__ void lds_st_u32u(uint8_t *img, uint32_t off, uint32_t v) {
+  __builtin_memcpy(img + off, &v, 4);
 }
 
 // ---- global reads at arbitrary byte offsets ---------------------------------

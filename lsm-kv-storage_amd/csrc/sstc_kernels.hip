@@ -953,9 +953,11 @@ __device__ __forceinline__ void emit_chunk(uint8_t *img, u32x4 v, uint32_t nxt, 
 // image is assembled by copying whole entries.  16 lanes per entry, each loads
 // one ALIGNED 16 B source chunk (one dwordx4 per lane instead of five dword
 // loads) and funnel-shifts it, with the first dword of its right neighbour's
-// chunk, into the dword-aligned LDS image; kCopyQ entry quads are loaded
-// before any is written so a lane has kCopyQ wide loads in flight.  Dwords
-// that straddle an entry's ends are left to the record pass that follows:
+// chunk, into the dword-aligned LDS image (aligned stores: unaligned dword
+// stores of the source dwords measured 501 -> 679 us at config 3); kCopyQ
+// entry quads are loaded before any is written so a lane has kCopyQ wide
+// loads in flight.  Dwords that straddle an entry's ends are left to the
+// record pass that follows:
 // lane per record writes type + key length (the first 5 bytes), the txn (the
 // last 8; the compat reader may have changed it) and the offset entry.
 template <uint32_t kCopyQ>
@@ -1020,13 +1022,11 @@ __device__ __forceinline__ bool enc_copy_entries(const EncArgs &a, uint8_t *img,
       }
     }
     wave_lds_sync();
-    if (lane < nc) {
+    if (lane < nc) { // type + key length (the first 5 bytes), the txn (the last 8), the offset entry
       uint8_t *e = img + pad + my_o;
       e[0] = static_cast<uint8_t>(my_ty);
-#pragma unroll
-      for (int j = 0; j < 4; j++) e[1 + j] = static_cast<uint8_t>(my_kl >> (8 * j));
-#pragma unroll
-      for (int j = 0; j < 8; j++) e[my_sz - 8 + j] = static_cast<uint8_t>(my_tx >> (8 * j));
+      lds_st_u32u(e, 1, my_kl);
+      lds_st_u64u(e, my_sz - 8, my_tx);
       lds_st_u64u(img, pad + D + 16 * (c0 + lane), my_o);
       lds_st_u64u(img, pad + D + 16 * (c0 + lane) + 8, my_sz);
       tmin = my_tx < tmin ? my_tx : tmin;
@@ -1047,37 +1047,26 @@ __device__ __forceinline__ bool enc_copy_entries(const EncArgs &a, uint8_t *img,
   return true;
 }
 
-// Chunk c of a span (16 aligned source bytes v + the first dword of chunk c+1)
-// into the image: dwords j = 0..3 at y + 16 c + 4 j, plus for chunk 0 the dword
-// before (its top bytes are the span's first bytes when the skew r0 moves them
-// there).  Every dword that meets [lo, hi) is stored whole, the others go to a
-// per-lane dummy word (no branches): a dword at an end of the span also
+// Chunk c of a span: the 16 ALIGNED source bytes v hold the span's bytes from
+// offset 16 c - mis on, so source dword j belongs at image position y + 4 j
+// (y = span image position - mis + 16 c: any alignment, one unaligned
+// ds_write_b32 per dword -- gfx950 runs LDS in unaligned mode, see
+// sstc_device.h).  Every dword that meets [lo, hi) is stored whole, the others
+// go to a per-lane sink word (no branches): a dword at an end of the span also
 // overwrites up to 3 bytes beyond it, which always belong to the entry's own
 // header fields (klen before a key, vlen after it or before a value, txn after
 // the last field: block_builder.cc:36-77) -- the record pass that follows
-// rewrites every header byte, so it must run after the spans.
-__device__ __forceinline__ void put_dw(uint8_t *img, uint32_t *dummy, int32_t yy, uint32_t v, int32_t lo, int32_t hi) {
-  uint32_t *p = (yy + 4 > lo && yy < hi) ? reinterpret_cast<uint32_t *>(img + yy) : dummy;
-  *p = v;
-}
-
-__device__ __forceinline__ void emit_chunk_clip(uint8_t *img, uint32_t *dummy, u32x4 v, uint32_t nxt, uint32_t r0,
-                                                int32_t y, int32_t lo, int32_t hi, bool first) {
-  // dword k = 0..4 at image position y - 4 + 4k (k = 0: chunk 0's extra dword)
-  // meets [lo, hi) iff 0 <= (y - 4 + 4k) - lo + 3 < hi - lo + 3 (one unsigned
-  // compare); a dword that does not goes to the sink, addressed so that the
-  // store's constant offset 4k lands on it
-  const uint32_t t = static_cast<uint32_t>(y - lo - 1), span = static_cast<uint32_t>(hi - lo + 3);
-  uint8_t *b = img + y - 4;
-  uint8_t *sink = reinterpret_cast<uint8_t *>(dummy);
-  const uint32_t d[5] = {__builtin_amdgcn_alignbyte(v.x, 0u, r0), __builtin_amdgcn_alignbyte(v.y, v.x, r0),
-                         __builtin_amdgcn_alignbyte(v.z, v.y, r0), __builtin_amdgcn_alignbyte(v.w, v.z, r0),
-                         __builtin_amdgcn_alignbyte(nxt, v.w, r0)};
+// rewrites every header field, so it must run after the spans.  (Replaced a
+// funnel shift of every dword with its neighbour lane's first dword.)
+__device__ __forceinline__ void emit_chunk_ua(uint8_t *img, uint32_t *dummy, u32x4 v, int32_t y, int32_t lo,
+                                              int32_t hi) {
+  // dword j at y + 4 j meets [lo, hi) iff 0 <= y + 4 j - lo + 3 < hi - lo + 3 (one unsigned compare)
+  const uint32_t t = static_cast<uint32_t>(y - lo + 3), span = static_cast<uint32_t>(hi - lo + 3);
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-  for (uint32_t k = 0; k < 5; k++) {
-    const bool ok = (k > 0 || first) && t + 4 * k < span;
-    uint8_t *p = ok ? b : sink - 4 * k;
-    *reinterpret_cast<uint32_t *>(p + 4 * k) = d[k];
+  for (uint32_t j = 0; j < 4; j++) {
+    uint8_t *p = t + 4 * j < span ? img + y + 4 * static_cast<int32_t>(j) : reinterpret_cast<uint8_t *>(dummy);
+    __builtin_memcpy(p, &w[j], 4);
   }
 }
 
@@ -1085,11 +1074,9 @@ __device__ __forceinline__ void emit_chunk_clip(uint8_t *img, uint32_t *dummy, u
 // i < nspan holds span i = (offset into `base`, length, image position).
 // Spans are copied by groups of G lanes, 64 / G spans per wave instruction:
 // lane g of a group loads the ALIGNED 16 B source chunk g (chunks g + G,
-// g + 2G, ... in further rounds, only when some span needs them), funnel-
-// shifts it with the first dword of chunk g + 1 (its right neighbour's, by a
-// width-64 shuffle; the group's last lane loads it) into dword-aligned LDS
-// stores (emit_chunk_clip), so the loads are 16 B per lane and coalesced per
-// span.  kQ span groups are loaded before any is stored.
+// g + 2G, ... in further rounds, only when some span needs them) and stores its
+// dwords at their image positions (emit_chunk_ua), so the loads are 16 B per
+// lane and coalesced per span.  kQ span groups are loaded before any is stored.
 template <uint32_t G, uint32_t kQ>
 __device__ __forceinline__ void copy_spans(const uint8_t *base, uint8_t *img, uint32_t *dummy, uint32_t nspan,
                                            uint64_t my_off, uint32_t my_len, uint32_t my_ds, const u32x4 *safe,
@@ -1129,20 +1116,13 @@ __device__ __forceinline__ void copy_spans(const uint8_t *base, uint8_t *img, ui
       const uint32_t len = len_[q], ds = ds_[q];
       const uint32_t nch = len ? (mis + len + 15u) >> 4 : 0u;
       const uint8_t *A = sp_[q] - mis;
-      const uint32_t r0 = (mis - ds) & 3u;
-      const int32_t y = static_cast<int32_t>(ds) - static_cast<int32_t>(mis) + static_cast<int32_t>(r0);
+      const int32_t y = static_cast<int32_t>(ds) - static_cast<int32_t>(mis);
       const int32_t lo = static_cast<int32_t>(ds), hi = static_cast<int32_t>(ds + len);
-      uint32_t nx = __shfl_down(v[q].x, 1u, kWave);
-      if (g == G - 1) nx = 0u;
-      if (longs && g == G - 1) nx = G < nch ? *reinterpret_cast<const uint32_t *>(A + 16 * G) : 0u;
-      emit_chunk_clip(img, dummy, v[q], nx, r0, y + 16 * static_cast<int32_t>(g), g < nch ? lo : no,
-                      g < nch ? hi : no, g == 0);
+      emit_chunk_ua(img, dummy, v[q], y + 16 * static_cast<int32_t>(g), g < nch ? lo : no, g < nch ? hi : no);
       if (longs) {
         for (uint32_t c = g + G; c - g < nch; c += G) {
           const u32x4 w = c < nch ? *reinterpret_cast<const u32x4 *>(A + 16 * c) : u32x4{0u, 0u, 0u, 0u};
-          uint32_t nx2 = __shfl_down(w.x, 1u, kWave);
-          if (g == G - 1) nx2 = c + 1 < nch ? *reinterpret_cast<const uint32_t *>(A + 16 * (c + 1)) : 0u;
-          if (c < nch) emit_chunk_clip(img, dummy, w, nx2, r0, y + 16 * static_cast<int32_t>(c), lo, hi, false);
+          if (c < nch) emit_chunk_ua(img, dummy, w, y + 16 * static_cast<int32_t>(c), lo, hi);
         }
       }
     }
@@ -1153,7 +1133,8 @@ __device__ __forceinline__ void copy_spans(const uint8_t *base, uint8_t *img, ui
 // copies, each with its own group size: GK lanes per key (2: a 16 B key is one
 // or two chunks, 32 keys per wave instruction), GV per value (8: a 100 B value
 // is 7-8 chunks).  A round takes 64 records; the lane per record then writes
-// the header fields, txn and offset entry (block_builder.cc:36-93).
+// the header fields, txn and offset entry (block_builder.cc:36-93), each field
+// one unaligned LDS store.
 template <uint32_t GK, uint32_t GV, uint32_t kQ>
 __device__ __forceinline__ void enc_copy_split(const EncArgs &a, uint8_t *img, uint32_t *dummy, uint32_t pad,
                                                uint64_t f0, uint32_t n, uint64_t P0, uint32_t D, u32x4 *tbl) {
@@ -1177,14 +1158,10 @@ __device__ __forceinline__ void enc_copy_split(const EncArgs &a, uint8_t *img, u
     copy_spans<GV, kQ>(a.val_src, img, dummy, nc, vlen ? vo : 0ull, vlen, pad + o + 9 + kl, safe, tbl);
     if (on) { // header fields, txn, offset entry (after both span passes)
       im[o] = static_cast<uint8_t>(ty);
-#pragma unroll
-      for (int j = 0; j < 4; j++) im[o + 1 + j] = static_cast<uint8_t>(kl >> (8 * j));
-      uint8_t *vp = vl != kNoValue ? im + o + 5 + kl : reinterpret_cast<uint8_t *>(dummy);
-#pragma unroll
-      for (int j = 0; j < 4; j++) vp[j] = static_cast<uint8_t>(vl >> (8 * j));
-#pragma unroll
-      for (int j = 0; j < 8; j++) im[o + sz - 8 + j] = static_cast<uint8_t>(tx >> (8 * j));
-      lds_st_u64u(im, D + 16 * (c0 + lane), o); // D & 3 is wave-uniform
+      lds_st_u32u(im, o + 1, kl);
+      lds_st_u32u(vl != kNoValue ? im : reinterpret_cast<uint8_t *>(dummy), vl != kNoValue ? o + 5 + kl : 0u, vl);
+      lds_st_u64u(im, o + sz - 8, tx);
+      lds_st_u64u(im, D + 16 * (c0 + lane), o);
       lds_st_u64u(im, D + 16 * (c0 + lane) + 8, sz);
     }
   }
