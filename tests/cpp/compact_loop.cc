@@ -15,11 +15,14 @@
 //
 // prints "path smallest_key_hex largest_key_hex GetFileSize()" per output.
 //
-//   sstc_compact_loop --readers [file size]...
+//   sstc_compact_loop --readers dump_path [file size]...
 //
 // checks TableReader::CreateAndSetupDataForBlockReader (one block per call)
 // and CreateAndSetupDataForBlockReaders (all blocks, one call) against the
-// TableReaderIterator stream, record by record, and Seek(); prints
+// TableReaderIterator stream, record by record, and Seek(); writes the
+// records to dump_path (per record: u8 type, u64 txn, u32 key length, key,
+// u8 value-non-null, u32 value length, value) for comparison with the
+// reference's own BlockReaderIterator (tests/readers_util.py); prints
 // "readers ok <records>".
 #include <cstdio>
 #include <cstdlib>
@@ -92,7 +95,11 @@ using namespace kvs;
 
 static int check_readers(int argc, char **argv) {
   uint64_t total = 0;
-  for (int i = 2; i + 1 < argc; i += 2) {
+  std::FILE *dump = std::fopen(argv[2], "wb");
+  if (!dump) return 4;
+  std::unique_ptr<std::FILE, int (*)(std::FILE *)> closer(dump, std::fclose);
+  auto put = [&](const void *p, size_t n) { std::fwrite(p, 1, n, dump); };
+  for (int i = 3; i + 1 < argc; i += 2) {
     auto tr = sstc::TableReader::Create(std::string(argv[i]), 1, std::strtoull(argv[i + 1], nullptr, 10));
     if (!tr) return 4;
     std::vector<std::pair<sstc::BlockOffset, uint64_t>> blocks;
@@ -111,6 +118,13 @@ static int check_readers(int argc, char **argv) {
               (r->GetValue(e).data() == nullptr) != (it.GetValue().data() == nullptr))
             return 7;
         }
+        const uint8_t ty = static_cast<uint8_t>(it.GetType());
+        const uint64_t tx = it.GetTransactionId();
+        const std::string_view k = it.GetKey(), v = it.GetValue();
+        const uint32_t kl = static_cast<uint32_t>(k.size()), vl = static_cast<uint32_t>(v.size());
+        const uint8_t has = v.data() != nullptr;
+        put(&ty, 1), put(&tx, 8), put(&kl, 4), put(k.data(), kl), put(&has, 1), put(&vl, 4);
+        if (vl) put(v.data(), vl);
         total++;
       }
     }

@@ -81,12 +81,30 @@ def test_cpp_compact_loop_ties_match_reference(tmp_path, name, base):
 def test_cpp_block_readers_and_iterator(oracle, tmp_path):
     """CreateAndSetupDataForBlockReader (one block per call) and the batched
     form against the TableReaderIterator stream, record by record (DELETE ->
-    null value view, empty PUT value -> non-null view), plus Seek."""
-    rec = W.mixed_records(3000, seed=5)
-    order = np.lexsort((np.arange(3000), [bytes(rec["key_src"][int(o):int(o) + int(k)])
-                                          for o, k in zip(rec["key_off"], rec["key_len"])]))
-    rec = {k: (v[order] if v.size == 3000 else v) for k, v in rec.items()}
+    null value view, empty PUT value -> non-null view), plus Seek; the records
+    the product read must be the REFERENCE's decode of the same files
+    (TableReader index + BlockReaderIterator, tests/golden/readers_ref.json by
+    make_golden_readers.py; live through oracle/_ref when it is built)."""
+    from readers_util import reader_records, ref_stream
+    want = json.load(open(os.path.join(GOLDEN, "readers_ref.json")))
+    rec = reader_records()
     files = [oracle.table_build(rec, 4096), oracle.table_build(rec, 32768)]
-    r = subprocess.run([EXE, "--readers"] + write(tmp_path, files), capture_output=True, text=True, timeout=120)
+    for f, bs in zip(files, ("4096", "32768")):  # the reference TableBuilder's bytes
+        assert hashlib.sha256(f.tobytes()).hexdigest() == want[bs]["file_sha256"]
+    dump = tmp_path / "records.bin"
+    r = subprocess.run([EXE, "--readers", str(dump)] + write(tmp_path, files), capture_output=True, text=True,
+                       timeout=120)
     assert r.returncode == 0, (r.returncode, r.stderr)
     assert r.stdout.strip() == f"readers ok {2 * 3000}"
+    got = dump.read_bytes()
+    n0 = want["4096"]["stream_bytes"]
+    assert len(got) == n0 + want["32768"]["stream_bytes"]
+    for part, bs in ((got[:n0], "4096"), (got[n0:], "32768")):
+        assert hashlib.sha256(part).hexdigest() == want[bs]["stream_sha256"]
+    from oracle import REF_SO, RefLib
+    if os.path.exists(REF_SO):
+        ref = RefLib()
+        parts = []
+        for i, f in enumerate(files):
+            parts.append(ref_stream(ref, str(tmp_path / f"in{i}.sst"), f)[0])
+        assert got == b"".join(parts)
