@@ -116,23 +116,35 @@ __device__ __forceinline__ uint64_t g_u64u(const uint8_t *p) {
 }
 
 // ---- wave-level primitives (wave64) -----------------------------------------
+// Inclusive scan by DPP (no LDS round trips): row_shr 1 / 2 / 4 / 8 inside each
+// 16-lane row (a lane whose source is outside its row keeps the identity, 0),
+// then row_bcast:15 into rows 1 and 3 and row_bcast:31 into rows 2 and 3.
 __device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v) {
-  const uint32_t lane = lane_id();
-#pragma unroll
-  for (uint32_t d = 1; d < kWave; d <<= 1) {
-    const uint32_t t = __shfl_up(v, d, kWave);
-    if (lane >= d) v += t;
-  }
+  v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x111, 0xf, 0xf, false));
+  v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x112, 0xf, 0xf, false));
+  v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x114, 0xf, 0xf, false));
+  v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x118, 0xf, 0xf, false));
+  v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x142, 0xa, 0xf, false));
+  v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x143, 0xc, 0xf, false));
   return v;
 }
 
-__device__ __forceinline__ uint64_t wave_incl_scan_u64(uint64_t v) {
-  const uint32_t lane = lane_id();
-#pragma unroll
-  for (uint32_t d = 1; d < kWave; d <<= 1) {
-    const uint64_t t = __shfl_up(v, d, kWave);
-    if (lane >= d) v += t;
-  }
+template <int kCtrl, int kRowMask>
+__device__ __forceinline__ uint64_t dpp_u64(uint64_t v) { // lanes the DPP does not write read 0
+  const uint32_t lo = static_cast<uint32_t>(
+      __builtin_amdgcn_update_dpp(0, static_cast<int>(static_cast<uint32_t>(v)), kCtrl, kRowMask, 0xf, false));
+  const uint32_t hi = static_cast<uint32_t>(
+      __builtin_amdgcn_update_dpp(0, static_cast<int>(static_cast<uint32_t>(v >> 32)), kCtrl, kRowMask, 0xf, false));
+  return (static_cast<uint64_t>(hi) << 32) | lo;
+}
+
+__device__ __forceinline__ uint64_t wave_incl_scan_u64(uint64_t v) { // as wave_incl_scan_u32
+  v += dpp_u64<0x111, 0xf>(v);
+  v += dpp_u64<0x112, 0xf>(v);
+  v += dpp_u64<0x114, 0xf>(v);
+  v += dpp_u64<0x118, 0xf>(v);
+  v += dpp_u64<0x142, 0xa>(v);
+  v += dpp_u64<0x143, 0xc>(v);
   return v;
 }
 

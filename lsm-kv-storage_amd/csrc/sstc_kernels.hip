@@ -1129,12 +1129,83 @@ __device__ __forceinline__ void copy_spans(const uint8_t *base, uint8_t *img, ui
   }
 }
 
-// Records -> block image with the keys and the values in two passes of span
-// copies, each with its own group size: GK lanes per key (2: a 16 B key is one
-// or two chunks, 32 keys per wave instruction), GV per value (8: a 100 B value
-// is 7-8 chunks).  A round takes 64 records; the lane per record then writes
-// the header fields, txn and offset entry (block_builder.cc:36-93), each field
-// one unaligned LDS store.
+// Keys and values of up to 32 records with every source load of the round in
+// flight together: the key spans (2-lane groups, one load per lane) and the
+// value spans (8-lane groups, four loads per lane) are issued before any is
+// stored, so a block of <= 32 records waits on one HBM round trip for its
+// entry bytes instead of three (keys, then two rounds of values).  The span
+// tuples go through the wave's one LDS table: key tuples, read, then value
+// tuples (LDS operations of a wave complete in order).  Spans longer than the
+// group (keys > 2 chunks, values > 8) finish in a loop, as in copy_spans.
+__device__ __forceinline__ void copy_kv_spans(const EncArgs &a, uint8_t *img, uint32_t *dummy, uint32_t p0,
+                                              uint64_t ko, uint32_t kl, uint32_t dsk, uint64_t vo, uint32_t vl,
+                                              uint32_t dsv, const u32x4 *safe, u32x4 *tbl) {
+  constexpr uint32_t GK = 2, GV = 8, kQV = 4;
+  const uint32_t lane = lane_id();
+  const int32_t no = -(1 << 30);
+  const uint32_t gk = lane % GK, gv = lane % GV;
+  const uint32_t kbase = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(a.key_src));
+  const uint32_t vbase = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(a.val_src));
+  const bool longk = __any(kl && (((kbase + static_cast<uint32_t>(ko)) & 15u) + kl + 15u) >> 4 > GK);
+  const bool longv = __any(vl && (((vbase + static_cast<uint32_t>(vo)) & 15u) + vl + 15u) >> 4 > GV);
+  const uint32_t kown = (p0 + lane / GK) & 63u;
+  // keys: record p0 + lane / 2 (its tuple, then the value tuples, through the one table)
+  tbl[lane] = u32x4{static_cast<uint32_t>(ko), static_cast<uint32_t>(ko >> 32), kl, dsk};
+  wave_lds_sync();
+  const u32x4 tk = tbl[kown];
+  const uint32_t misk = (kbase + tk.x) & 15u;
+  const uint32_t nchk = tk.z ? (misk + tk.z + 15u) >> 4 : 0u;
+  const u32x4 vk = *(gk < nchk ? reinterpret_cast<const u32x4 *>(
+                                     a.key_src + ((static_cast<uint64_t>(tk.y) << 32) | tk.x) - misk + 16 * gk)
+                               : safe);
+  const uint32_t dk = tk.w, lk = tk.z;
+  wave_lds_sync();
+  tbl[lane] = u32x4{static_cast<uint32_t>(vo), static_cast<uint32_t>(vo >> 32), vl, dsv};
+  wave_lds_sync();
+  u32x4 vv[kQV];
+#pragma unroll
+  for (uint32_t q = 0; q < kQV; q++) {
+    const u32x4 t = tbl[(p0 + q * (kWave / GV) + lane / GV) & 63u];
+    const uint32_t mis = (vbase + t.x) & 15u;
+    const uint32_t nch = t.z ? (mis + t.z + 15u) >> 4 : 0u;
+    vv[q] = *(gv < nch ? reinterpret_cast<const u32x4 *>(a.val_src + ((static_cast<uint64_t>(t.y) << 32) | t.x) -
+                                                         mis + 16 * gv)
+                       : safe);
+  }
+  __builtin_amdgcn_sched_barrier(0); // every load above is issued before the stores below
+  { // key stores
+    const int32_t y = static_cast<int32_t>(dk) - static_cast<int32_t>(misk);
+    const int32_t lo = static_cast<int32_t>(dk), hi = static_cast<int32_t>(dk + lk);
+    emit_chunk_ua(img, dummy, vk, y + 16 * static_cast<int32_t>(gk), gk < nchk ? lo : no, gk < nchk ? hi : no);
+    if (longk) { // rare: the owner's key offset by shuffle (the table holds the value tuples now)
+      const uint64_t kok = __shfl(ko, static_cast<int>(kown), kWave);
+      const uint8_t *A = a.key_src + kok - misk;
+      for (uint32_t c = gk + GK; c - gk < nchk; c += GK) {
+        const u32x4 w = c < nchk ? *reinterpret_cast<const u32x4 *>(A + 16 * c) : u32x4{0u, 0u, 0u, 0u};
+        if (c < nchk) emit_chunk_ua(img, dummy, w, y + 16 * static_cast<int32_t>(c), lo, hi);
+      }
+    }
+  }
+#pragma unroll
+  for (uint32_t q = 0; q < kQV; q++) { // value stores (tuples re-read: fewer live registers)
+    const u32x4 t = tbl[(p0 + q * (kWave / GV) + lane / GV) & 63u];
+    const uint32_t mis = (vbase + t.x) & 15u, len = t.z, ds = t.w;
+    const uint32_t nch = len ? (mis + len + 15u) >> 4 : 0u;
+    const int32_t y = static_cast<int32_t>(ds) - static_cast<int32_t>(mis);
+    const int32_t lo = static_cast<int32_t>(ds), hi = static_cast<int32_t>(ds + len);
+    emit_chunk_ua(img, dummy, vv[q], y + 16 * static_cast<int32_t>(gv), gv < nch ? lo : no, gv < nch ? hi : no);
+    if (longv) {
+      const uint8_t *A = a.val_src + ((static_cast<uint64_t>(t.y) << 32) | t.x) - mis;
+      for (uint32_t c = gv + GV; c - gv < nch; c += GV) {
+        const u32x4 w = c < nch ? *reinterpret_cast<const u32x4 *>(A + 16 * c) : u32x4{0u, 0u, 0u, 0u};
+        if (c < nch) emit_chunk_ua(img, dummy, w, y + 16 * static_cast<int32_t>(c), lo, hi);
+      }
+    }
+  }
+}
+
+constexpr bool kFusedKV = true;
+
 template <uint32_t GK, uint32_t GV, uint32_t kQ>
 __device__ __forceinline__ void enc_copy_split(const EncArgs &a, uint8_t *img, uint32_t *dummy, uint32_t pad,
                                                uint64_t f0, uint32_t n, uint64_t P0, uint32_t D, u32x4 *tbl) {
@@ -1153,9 +1224,15 @@ __device__ __forceinline__ void enc_copy_split(const EncArgs &a, uint8_t *img, u
     const uint32_t o = carry + inc - sz;
     carry += __shfl(inc, kWave - 1, kWave);
     const uint64_t ko = a.in.key_off[r], vo = a.in.val_off[r], tx = a.in.txn[r];
-    copy_spans<GK, kQ>(a.key_src, img, dummy, nc, ko, on ? kl : 0u, pad + o + 5, safe, tbl);
     const uint32_t vlen = on && vl != kNoValue ? vl : 0u;
-    copy_spans<GV, kQ>(a.val_src, img, dummy, nc, vlen ? vo : 0ull, vlen, pad + o + 9 + kl, safe, tbl);
+    if (kFusedKV) { // every load of a 32-record sub-round in flight at once
+      for (uint32_t p0 = 0; p0 < nc; p0 += 32)
+        copy_kv_spans(a, img, dummy, p0, on ? ko : 0ull, on ? kl : 0u, pad + o + 5, vlen ? vo : 0ull, vlen,
+                      pad + o + 9 + kl, safe, tbl);
+    } else {
+      copy_spans<GK, kQ>(a.key_src, img, dummy, nc, ko, on ? kl : 0u, pad + o + 5, safe, tbl);
+      copy_spans<GV, kQ>(a.val_src, img, dummy, nc, vlen ? vo : 0ull, vlen, pad + o + 9 + kl, safe, tbl);
+    }
     if (on) { // header fields, txn, offset entry (after both span passes)
       im[o] = static_cast<uint8_t>(ty);
       lds_st_u32u(im, o + 1, kl);
