@@ -82,32 +82,46 @@ __device__ __forceinline__ bool sk_less(const SK &a, const SK &b, const KeyView 
 // table_builder.h:77): decode_kernel checks each record against its
 // predecessor in the same block; this kernel checks the first record of every
 // non-empty block against the last record before it, unless it starts a run.
-__global__ void ck_check_blocks_kernel(const SK *s, const uint64_t *rec_base, uint64_t nblocks,
+// Grid-stride over the blocks with a capped grid: the source-end bound is one
+// same-address atomic per workgroup (per wave with one block per thread, the
+// serialized atomics took config 3 18 -> 64 us, config 4 -> 104 us).
+constexpr uint32_t kCheckGrid = 512;
+__global__ __launch_bounds__(256) void ck_check_blocks_kernel(const SK *s, const uint64_t *rec_base, uint64_t nblocks,
                                        const uint64_t *run_start, uint64_t nruns, KeyView kv,
                                        unsigned long long *bad, Abort stop, uint64_t *zws, uint64_t nz,
                                        const uint64_t *blk_off, const uint64_t *blk_len,
                                        unsigned long long *src_end) {
-  const uint64_t b = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  for (uint64_t z = b; z < nz; z += static_cast<uint64_t>(gridDim.x) * blockDim.x) zws[z] = 0; // filter look-back
-  { // end of the source bytes the blocks span: the bound of every entry the encode copies
-    uint64_t e = b < nblocks ? blk_off[b] + blk_len[b] : 0;
-    for (uint32_t d = kWave / 2; d > 0; d >>= 1) {
-      const uint64_t y = __shfl_xor(e, d, kWave);
-      e = y > e ? y : e;
+  __shared__ uint64_t s_end[256 / kWave];
+  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+  const uint64_t t0 = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  for (uint64_t z = t0; z < nz; z += stride) zws[z] = 0; // filter look-back
+  const bool go = !stop();
+  uint64_t e = 0; // end of the source bytes the blocks span: the bound of every entry the encode copies
+  for (uint64_t b = t0; b < nblocks; b += stride) {
+    const uint64_t x = blk_off[b] + blk_len[b];
+    e = x > e ? x : e;
+    if (!go) continue;
+    const uint64_t r = rec_base[b];
+    if (r == 0 || rec_base[b + 1] == r) continue;
+    uint64_t lo = 0, hi = nruns; // run containing r: last run_start <= r
+    while (lo + 1 < hi) {
+      const uint64_t mid = (lo + hi) >> 1;
+      if (run_start[mid] <= r) lo = mid;
+      else hi = mid;
     }
-    if (lane_id() == 0 && e) atomicMax(src_end, static_cast<unsigned long long>(e));
+    if (run_start[lo] == r) continue; // first record of its run
+    if (sk_less(s[r], s[r - 1], kv)) atomicAdd(bad, 1ull);
   }
-  if (b >= nblocks || stop()) return;
-  const uint64_t r = rec_base[b];
-  if (r == 0 || rec_base[b + 1] == r) return;
-  uint64_t lo = 0, hi = nruns; // run containing r: last run_start <= r
-  while (lo + 1 < hi) {
-    const uint64_t mid = (lo + hi) >> 1;
-    if (run_start[mid] <= r) lo = mid;
-    else hi = mid;
+  for (uint32_t d = kWave / 2; d > 0; d >>= 1) {
+    const uint64_t y = __shfl_xor(e, d, kWave);
+    e = y > e ? y : e;
   }
-  if (run_start[lo] == r) return; // first record of its run
-  if (sk_less(s[r], s[r - 1], kv)) atomicAdd(bad, 1ull);
+  if (lane_id() == 0) s_end[threadIdx.x / kWave] = e;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (uint32_t w = 1; w < 256 / kWave; w++) e = s_end[w] > e ? s_end[w] : e;
+    if (e) atomicMax(src_end, static_cast<unsigned long long>(e));
+  }
 }
 
 // k-way merge pass: every group of up to kKWay consecutive sorted runs is
@@ -320,88 +334,110 @@ __global__ void ck_kw_win_kernel(const KGroup *groups, uint32_t ngroups, uint32_
   win[u] = d;
 }
 
-__device__ __forceinline__ void load_win(const KWin *win, KWin &s_d) {
-  if (threadIdx.x < kKWinWords)
-    reinterpret_cast<uint32_t *>(&s_d)[threadIdx.x] = reinterpret_cast<const uint32_t *>(win + blockIdx.x)[threadIdx.x];
-  __syncthreads();
-}
 
-// Merge of one window by a pairwise tree in LDS: the
-// staged records stay put; log2(k) levels each merge neighbouring sub-run
-// groups into a permutation of 16-bit slot indices (ping-pong), the first
-// straight from the staged order; the last permutation drives a coalesced
-// copy to the output.  Every thread produces ceil(n / threads) consecutive
-// outputs of a level (all threads busy whatever the window size): one
-// merge-path search for its first output, then a sequential two-head merge
-// with the heads held in registers.  The left group always holds the lower
-// runs, so taking B only when B sorts strictly first gives key asc, txn desc,
-// lower run first (merge_iterator.cc:34-46).
+// Merge of one window by a pairwise tree in LDS: the staged key prefixes stay
+// put; log2(k) levels each merge neighbouring sub-run groups into a
+// permutation of 16-bit slot indices (ping-pong), the first straight from the
+// staged order; the last permutation drives a coalesced copy to the output.
+// Every thread produces ceil(n / threads) consecutive outputs of a level (all
+// threads busy whatever the window size): one merge-path search for its first
+// output, then a sequential two-head merge with the heads' prefixes in
+// registers.  The left group always holds the lower runs, so taking B only
+// when B sorts strictly first gives key asc, txn desc, lower run first
+// (merge_iterator.cc:34-46).
 constexpr uint32_t kMgThreads = 256;
 
-// merge-order compares that read a record's 16 B key prefix from LDS first and
-// its other 16 B only when the prefixes tie (a differing prefix decides the
-// order: key_cmp compares p0, p1 first)
-struct MgPf {
+struct MgPf { // a record's 16 B big-endian key prefix
   uint64_t p0, p1;
 };
-// the window's records in LDS as two planes of 16 B (key prefixes, then txn /
-// key length / id): the prefix reads that dominate the merge stride 16 B (16
-// start bank groups instead of 8 for packed 32 B records; config 4 merge
-// 799 / 827 -> 786 / 793 us, config 3 unchanged)
-struct MgTile {
-  u32x4 pf[kKRegion], rs[kKRegion];
-  __device__ __forceinline__ u32x4 h0(uint32_t s) const { return pf[s]; }
-  __device__ __forceinline__ u32x4 h1(uint32_t s) const { return rs[s]; }
-  __device__ __forceinline__ void put(uint32_t s, const SK &r) {
-    const u32x4 *v = reinterpret_cast<const u32x4 *>(&r);
-    pf[s] = v[0];
-    rs[s] = v[1];
+
+// Only the 16 B key-prefix plane is in LDS (20 KiB per workgroup: 8
+// workgroups per CU; the round-2 tile of whole 32 B records held 37 KB, 4 per
+// CU, and merged config 3 in 206 us vs 167 us, config 4 797 vs 677 us -- the
+// merge is bound by its dependent LDS / load chains, so resident workgroups
+// are what hides them; profiles/r03_ab/merge_pf.md).  The rest of a record (txn, key length, id) is read
+// from the input -- L2-hot, the window staged it moments before -- only on a
+// prefix tie and for the output copy.  The descriptor stays in scalar
+// registers (no LDS copy): sub-run of a slot and its source index by selects.
+struct MgDesc {
+  // sub-run starts in the window (o8 = n; o_q = n for q >= k) and the source
+  // index offsets (slot x of sub-run q is record x + b_q).  Every field read
+  // goes through u() (readfirstlane: a no-op on these uniform values) -- a
+  // select chain over plain field loads is folded into one load at a selected
+  // offset, which pins the descriptor in scratch memory
+  uint32_t o0, o1, o2, o3, o4, o5, o6, o7, o8;
+  uint32_t b0, b1, b2, b3, b4, b5, b6, b7;
+  static __device__ __forceinline__ uint32_t u(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+  __device__ __forceinline__ uint32_t run_of(uint32_t x) const {
+    return (x >= o1) + (x >= o2) + (x >= o3) + (x >= o4) + (x >= o5) + (x >= o6) + (x >= o7);
   }
-  __device__ __forceinline__ SK get(uint32_t s) const {
-    SK r;
-    u32x4 *v = reinterpret_cast<u32x4 *>(&r);
-    v[0] = h0(s);
-    v[1] = h1(s);
+  __device__ __forceinline__ uint32_t gidx(uint32_t x) const {
+    uint32_t b = u(b0);
+    b = x >= o1 ? u(b1) : b;
+    b = x >= o2 ? u(b2) : b;
+    b = x >= o3 ? u(b3) : b;
+    b = x >= o4 ? u(b4) : b;
+    b = x >= o5 ? u(b5) : b;
+    b = x >= o6 ? u(b6) : b;
+    b = x >= o7 ? u(b7) : b;
+    return x + b;
+  }
+  __device__ __forceinline__ uint32_t bound(uint32_t q) const { // o_min(q, 8)
+    uint32_t r = u(o8); // ordered compares: equality selects become a table lookup
+    r = q <= 7 ? u(o7) : r;
+    r = q <= 6 ? u(o6) : r;
+    r = q <= 5 ? u(o5) : r;
+    r = q <= 4 ? u(o4) : r;
+    r = q <= 3 ? u(o3) : r;
+    r = q <= 2 ? u(o2) : r;
+    r = q <= 1 ? u(o1) : r;
+    r = q == 0 ? u(o0) : r;
     return r;
   }
 };
-__device__ __forceinline__ MgPf mg_pf(const MgTile &tile, uint32_t s) {
-  const u32x4 h = tile.h0(s);
-  return {static_cast<uint64_t>(h.x) | (static_cast<uint64_t>(h.y) << 32),
-          static_cast<uint64_t>(h.z) | (static_cast<uint64_t>(h.w) << 32)};
-}
-// record at slot sa (prefix a) before the record at slot sb (prefix b)
-__device__ __forceinline__ bool mg_less_pf(const MgTile &tile, uint32_t sa, const MgPf &a, uint32_t sb,
-                                           const MgPf &b, const KeyView &kv) {
-  if (a.p0 != b.p0) return a.p0 < b.p0;
-  if (a.p1 != b.p1) return a.p1 < b.p1;
-  return sk_less(tile.get(sa), tile.get(sb), kv);
-}
-__device__ __forceinline__ bool mg_less(const MgTile &tile, uint32_t sa, uint32_t sb, const KeyView &kv) {
-  return mg_less_pf(tile, sa, mg_pf(tile, sa), sb, mg_pf(tile, sb), kv);
-}
+static_assert(kKWay == 8, "MgDesc holds 8 sub-runs");
 
-// Stage window s_d's sub-runs in `tile` and merge them into the slot
-// permutation ix[result][0, n); result -1: the staged order is the merged
-// order (k == 1).  Called by every thread of the workgroup (barriers inside).
-__device__ __forceinline__ int mg_window_merge(const SK *in, MgTile &tile, uint16_t (*ix)[kKRegion], const KWin &s_d,
-                                               const KeyView &kv) {
-  const uint32_t total = s_d.n, k = s_d.k;
-  const uint32_t *s_off = s_d.off;
-  // sub-run of a slot, and off[min(x, kKWay)] (off[q > k] = n); probes of the
-  // 9-entry table in LDS measured faster than selects over registers
-  auto run_of = [&](uint32_t x) {
-    uint32_t q = 0;
-    while (s_off[q + 1] <= x) q++;
-    return q;
-  };
-  auto bound = [&](uint32_t x) { return s_off[x < kKWay ? x : kKWay]; };
-  for (uint32_t i = threadIdx.x; i < total; i += kMgThreads) {
-    const uint32_t q = run_of(i);
-    tile.put(i, in[s_d.src[q] + (i - s_off[q])]);
+__global__ __launch_bounds__(kMgThreads) void ck_mg_merge_kernel(const SK *__restrict__ in, SK *__restrict__ out,
+                                                                   const KWin *__restrict__ win, KeyView kv) {
+  __shared__ u32x4 pf[kKRegion];
+  __shared__ uint16_t ix[2][kKRegion];
+  const KWin *w = win + blockIdx.x;
+  const uint32_t total = __builtin_amdgcn_readfirstlane(w->n), k = __builtin_amdgcn_readfirstlane(w->k);
+  if (total == 0) return;
+  SK *o = out + __builtin_amdgcn_readfirstlane(w->out);
+  MgDesc d;
+#define SSTC_MG_LD(q) \
+  d.o##q = __builtin_amdgcn_readfirstlane(w->off[q]);
+  SSTC_MG_LD(0) SSTC_MG_LD(1) SSTC_MG_LD(2) SSTC_MG_LD(3) SSTC_MG_LD(4) SSTC_MG_LD(5) SSTC_MG_LD(6) SSTC_MG_LD(7)
+  SSTC_MG_LD(8)
+#undef SSTC_MG_LD
+#define SSTC_MG_LD(q) \
+  d.b##q = __builtin_amdgcn_readfirstlane(w->src[q]) - d.o##q;
+  SSTC_MG_LD(0) SSTC_MG_LD(1) SSTC_MG_LD(2) SSTC_MG_LD(3) SSTC_MG_LD(4) SSTC_MG_LD(5) SSTC_MG_LD(6) SSTC_MG_LD(7)
+#undef SSTC_MG_LD
+  if (k == 1) {
+    for (uint32_t i = threadIdx.x; i < total; i += kMgThreads) o[i] = in[d.b0 + i];
+    return;
   }
+  for (uint32_t i = threadIdx.x; i < total; i += kMgThreads)
+    pf[i] = *reinterpret_cast<const u32x4 *>(in + d.gidx(i));
   __syncthreads();
-  if (k == 1) return -1;
+  auto pfx = [&](uint32_t sl) __attribute__((always_inline)) -> MgPf {
+    const u32x4 h = pf[sl];
+    return {static_cast<uint64_t>(h.x) | (static_cast<uint64_t>(h.y) << 32),
+            static_cast<uint64_t>(h.z) | (static_cast<uint64_t>(h.w) << 32)};
+  };
+  // slot sa (prefix a) before slot sb (prefix b); the whole records on a tie
+  auto less = [&](uint32_t sa, const MgPf &a, uint32_t sb, const MgPf &b) __attribute__((always_inline)) {
+    if (a.p0 != b.p0) return a.p0 < b.p0;
+    if (a.p1 != b.p1) return a.p1 < b.p1;
+    // the records' second halves (txn, key length, id) from the input
+    const u32x4 ra = reinterpret_cast<const u32x4 *>(in + d.gidx(sa))[1];
+    const u32x4 rb = reinterpret_cast<const u32x4 *>(in + d.gidx(sb))[1];
+    const int c = key_cmp(a.p0, a.p1, ra.z, ra.w, b.p0, b.p1, rb.z, rb.w, kv);
+    return c < 0 || (c == 0 && (static_cast<uint64_t>(ra.x) | (static_cast<uint64_t>(ra.y) << 32)) >
+                                   (static_cast<uint64_t>(rb.x) | (static_cast<uint64_t>(rb.y) << 32)));
+  };
   const uint32_t per = (total + kMgThreads - 1) / kMgThreads; // outputs per thread
   const uint32_t p0 = threadIdx.x * per;
   uint32_t src = 0;
@@ -409,65 +445,49 @@ __device__ __forceinline__ int mg_window_merge(const SK *in, MgTile &tile, uint1
     const bool first = wd == 1;
     const uint16_t *a_ix = ix[src];
     uint16_t *o_ix = ix[src ^ 1];
-    auto slot = [&](uint32_t x) -> uint32_t { return first ? x : a_ix[x]; };
+    auto slot = [&](uint32_t x) __attribute__((always_inline)) -> uint32_t { return first ? x : a_ix[x]; };
     if (p0 < total) {
-      uint32_t m = run_of(p0) & ~(2 * wd - 1);
-      uint32_t lo = bound(m), mid = bound(m + wd), hi = bound(m + 2 * wd);
+      uint32_t m = d.run_of(p0) & ~(2 * wd - 1);
+      uint32_t lo = d.bound(m), mid = d.bound(m + wd), hi = d.bound(m + 2 * wd);
       const uint32_t diag = p0 - lo;
       uint32_t i = diag > hi - mid ? diag - (hi - mid) : 0, ihi = diag < mid - lo ? diag : mid - lo;
       while (i < ihi) {
         const uint32_t im = (i + ihi) >> 1;
-        if (!mg_less(tile, slot(mid + diag - 1 - im), slot(lo + im), kv)) i = im + 1;
+        const uint32_t sb = slot(mid + diag - 1 - im), sa = slot(lo + im);
+        if (!less(sb, pfx(sb), sa, pfx(sa))) i = im + 1;
         else ihi = im;
       }
       uint32_t j = diag - i, ai = 0, bi = 0;
-      MgPf a{0, 0}, b{0, 0}; // the heads' key prefixes (the rest is read from LDS on a prefix tie)
-      if (lo + i < mid) a = mg_pf(tile, ai = slot(lo + i));
-      if (mid + j < hi) b = mg_pf(tile, bi = slot(mid + j));
+      MgPf a{0, 0}, b{0, 0};
+      if (lo + i < mid) a = pfx(ai = slot(lo + i));
+      if (mid + j < hi) b = pfx(bi = slot(mid + j));
       for (uint32_t e = 0; e < per; e++) {
         const uint32_t p = p0 + e;
         if (p >= total) break;
         while (p == hi) { // the next pair starts inside this thread's outputs
           m += 2 * wd;
           lo = hi;
-          mid = bound(m + wd);
-          hi = bound(m + 2 * wd);
+          mid = d.bound(m + wd);
+          hi = d.bound(m + 2 * wd);
           i = j = 0;
-          if (lo < mid) a = mg_pf(tile, ai = slot(lo));
-          if (mid < hi) b = mg_pf(tile, bi = slot(mid));
+          if (lo < mid) a = pfx(ai = slot(lo));
+          if (mid < hi) b = pfx(bi = slot(mid));
         }
-        const bool take_b = lo + i >= mid || (mid + j < hi && mg_less_pf(tile, bi, b, ai, a, kv));
+        const bool take_b = lo + i >= mid || (mid + j < hi && less(bi, b, ai, a));
         o_ix[p] = static_cast<uint16_t>(take_b ? bi : ai);
         if (take_b) {
           j++;
-          if (mid + j < hi) b = mg_pf(tile, bi = slot(mid + j));
+          if (mid + j < hi) b = pfx(bi = slot(mid + j));
         } else {
           i++;
-          if (lo + i < mid) a = mg_pf(tile, ai = slot(lo + i));
+          if (lo + i < mid) a = pfx(ai = slot(lo + i));
         }
       }
     }
     __syncthreads();
     src ^= 1;
   }
-  return static_cast<int>(src);
-}
-
-__global__ __launch_bounds__(kMgThreads) void ck_mg_merge_kernel(const SK *in, SK *out, const KWin *win,
-                                                                KeyView kv) {
-  __shared__ MgTile tile;
-  __shared__ uint16_t ix[2][kKRegion];
-  __shared__ KWin s_d;
-  load_win(win, s_d);
-  const uint32_t total = s_d.n, k = s_d.k;
-  if (total == 0) return;
-  SK *o = out + s_d.out;
-  if (k == 1) {
-    for (uint32_t i = threadIdx.x; i < total; i += kMgThreads) o[i] = in[s_d.src[0] + i];
-    return;
-  }
-  const int src = mg_window_merge(in, tile, ix, s_d, kv);
-  for (uint32_t p = threadIdx.x; p < total; p += kMgThreads) o[p] = tile.get(ix[src][p]);
+  for (uint32_t p = threadIdx.x; p < total; p += kMgThreads) o[p] = in[d.gidx(ix[src][p])];
 }
 
 struct Rec { // survivor columns (vl / vo null in the compaction job: unused by its encode)
@@ -1167,7 +1187,7 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
       }
       // the filter's look-back status words, cleared by the check kernel
       ffws = pool.get<uint64_t>(1 + 3 * fftiles);
-      ck_check_blocks_kernel<<<grid(nblocks), 256, 0, s>>>(A, rb_all, nblocks, rb, nruns, kv, bad, dec_fail, ffws,
+      ck_check_blocks_kernel<<<std::min<uint32_t>(std::max<uint32_t>(grid(std::max<uint64_t>(nblocks, 1ull + 3 * fftiles)), 1u), kCheckGrid), 256, 0, s>>>(A, rb_all, nblocks, rb, nruns, kv, bad, dec_fail, ffws,
                                                            1 + 3 * fftiles, d_blk_off, d_blk_len, guard + 1);
       if (!kg.empty()) {
         KGroup *d_kg = pool.get<KGroup>(kg.size());
