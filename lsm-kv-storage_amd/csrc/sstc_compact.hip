@@ -300,7 +300,6 @@ struct __attribute__((aligned(16))) KWin {
   uint32_t off[kKWay + 1];
   uint32_t pad2[3];
 };
-constexpr uint32_t kKWinWords = sizeof(KWin) / 4;
 
 __global__ void ck_kw_win_kernel(const KGroup *groups, uint32_t ngroups, uint32_t nwin, const uint32_t *C,
                                  const uint64_t *G, const uint32_t *J, KWin *win, Abort stop) {
