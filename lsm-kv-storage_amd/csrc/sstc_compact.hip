@@ -418,8 +418,19 @@ __global__ __launch_bounds__(kMgThreads) void ck_mg_merge_kernel(const SK *__res
     for (uint32_t i = threadIdx.x; i < total; i += kMgThreads) o[i] = in[d.b0 + i];
     return;
   }
-  for (uint32_t i = threadIdx.x; i < total; i += kMgThreads)
-    pf[i] = *reinterpret_cast<const u32x4 *>(in + d.gidx(i));
+  // slot i = tid + 256 j is staged by this thread: its prefix into LDS, its
+  // second half (txn, key length, id) kept in registers for the output
+  constexpr uint32_t kPer = kKRegion / kMgThreads;
+  u32x4 rest[kPer];
+#pragma unroll
+  for (uint32_t j = 0; j < kPer; j++) {
+    const uint32_t i = threadIdx.x + j * kMgThreads;
+    if (i < total) {
+      const u32x4 *r = reinterpret_cast<const u32x4 *>(in + d.gidx(i));
+      pf[i] = r[0];
+      rest[j] = r[1];
+    }
+  }
   __syncthreads();
   auto pfx = [&](uint32_t sl) __attribute__((always_inline)) -> MgPf {
     const u32x4 h = pf[sl];
@@ -486,7 +497,21 @@ __global__ __launch_bounds__(kMgThreads) void ck_mg_merge_kernel(const SK *__res
     __syncthreads();
     src ^= 1;
   }
-  for (uint32_t p = threadIdx.x; p < total; p += kMgThreads) o[p] = in[d.gidx(ix[src][p])];
+  // output: the inverse permutation, then every thread writes its own staged
+  // records at their merged positions (prefix from LDS, second half from its
+  // registers) -- reading the records again from the input after the merge
+  // doubled the kernel's fetch (the window's lines had left L2)
+  for (uint32_t p = threadIdx.x; p < total; p += kMgThreads) ix[src ^ 1][ix[src][p]] = static_cast<uint16_t>(p);
+  __syncthreads();
+#pragma unroll
+  for (uint32_t j = 0; j < kPer; j++) {
+    const uint32_t i = threadIdx.x + j * kMgThreads;
+    if (i < total) {
+      u32x4 *q = reinterpret_cast<u32x4 *>(o + ix[src ^ 1][i]);
+      q[0] = pf[i];
+      q[1] = rest[j];
+    }
+  }
 }
 
 struct Rec { // survivor columns (vl / vo null in the compaction job: unused by its encode)
