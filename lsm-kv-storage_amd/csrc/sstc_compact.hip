@@ -793,37 +793,56 @@ __device__ __forceinline__ void put_le(uint8_t *p, uint64_t v, int n) {
 // the workgroup's 256 blocks is written with aligned 16 B stores (byte stores
 // straight to HBM from 256 threads at a 56 B stride cost ~10x more).
 constexpr uint32_t kMetaLds = 24576; // 256 entries of keys up to 32 B (32 KiB: 4 workgroups per CU, 48 -> 45 us at 16 KiB)
-// the entry's key sources inside the source bytes and its keys within the
-// reference's key limit (block_builder.cc:38); false sets the guard
-__device__ __forceinline__ bool meta_entry_ok(uint64_t b, const uint64_t *bf, Rec K, const uint64_t *src_end,
-                                              unsigned long long *guard) {
-  const uint64_t f = bf[b], l = bf[b + 1] - 1, e = *src_end;
-  const uint32_t fk = K.kl[f], lk = K.kl[l];
-  const bool ok = f <= l && fk <= kMaxKey && lk <= kMaxKey && K.ko[f] <= e && fk <= e - K.ko[f] && K.ko[l] <= e &&
-                  lk <= e - K.ko[l];
+// The entry's keys are read back from the block the encode just wrote (its
+// first entry at the block start, its last found through the block's extra
+// and offset section: three lines per block, vs. gathering both keys and
+// their lengths / offsets from the survivor columns and the input: config 3
+// fetched 324 MB for 16 MB of entries).  MKeys: where the two keys are.
+struct MKeys {
+  const uint8_t *k0, *k1;
+  uint32_t fk, lk;
+};
+// the block's keys inside the block (the encode guard has checked every entry
+// against its block image) and the entry size the layout used (MS)
+__device__ __forceinline__ bool meta_keys(uint64_t b, const uint64_t *bo, const uint64_t *blen, const uint64_t *MS,
+                                          const uint8_t *dst, uint64_t cap, unsigned long long *guard, MKeys &m) {
+  const uint64_t o = bo[b], L = blen[b];
+  bool ok = o <= cap && L <= cap - o && L >= 32;
+  if (ok) {
+    const uint8_t *blk = dst + o;
+    const uint64_t n = g_u64u(blk + L - 16), doff = g_u64u(blk + L - 8);
+    ok = n >= 1 && doff <= L - 16 && n <= (L - 16 - doff) / 16;
+    if (ok) {
+      const uint64_t lo = g_u64u(blk + doff + 16 * (n - 1));
+      m.fk = g_u32u(blk + 1);
+      ok = lo + 5 <= doff && m.fk <= kMaxKey && 5ull + m.fk <= doff;
+      if (ok) {
+        m.lk = g_u32u(blk + lo + 1);
+        m.k0 = blk + 5;
+        m.k1 = blk + lo + 5;
+        ok = m.lk <= kMaxKey && lo + 5 + m.lk <= doff && MS[b + 1] - MS[b] == 24ull + m.fk + m.lk;
+      }
+    }
+  }
   if (!ok) atomicOr(guard, kGuardMeta);
   return ok;
 }
-__device__ __forceinline__ void meta_entry(uint8_t *p, uint64_t b, const uint64_t *bf, const uint32_t *btab,
-                                           const uint64_t *BL, const uint64_t *blen, const uint64_t *tbf, Rec K,
-                                           const uint8_t *src) {
+__device__ __forceinline__ void meta_entry(uint8_t *p, uint64_t b, const uint32_t *btab, const uint64_t *BL,
+                                           const uint64_t *blen, const uint64_t *tbf, const MKeys &m) {
   const uint32_t t = btab[b];
-  const uint64_t f = bf[b], l = bf[b + 1] - 1;
-  const uint32_t fk = K.kl[f], lk = K.kl[l];
-  put_le(p, fk, 4);
-  for (uint32_t j = 0; j < fk; j++) p[4 + j] = src[K.ko[f] + j];
-  put_le(p + 4 + fk, lk, 4);
-  for (uint32_t j = 0; j < lk; j++) p[8 + fk + j] = src[K.ko[l] + j];
-  put_le(p + 8 + fk + lk, BL[b] - BL[tbf[t]], 8);
-  put_le(p + 16 + fk + lk, blen[b], 8);
+  put_le(p, m.fk, 4);
+  for (uint32_t j = 0; j < m.fk; j++) p[4 + j] = m.k0[j];
+  put_le(p + 4 + m.fk, m.lk, 4);
+  for (uint32_t j = 0; j < m.lk; j++) p[8 + m.fk + j] = m.k1[j];
+  put_le(p + 8 + m.fk + m.lk, BL[b] - BL[tbf[t]], 8);
+  put_le(p + 16 + m.fk + m.lk, blen[b], 8);
 }
 
-__global__ __launch_bounds__(256) void ck_meta_kernel(const uint64_t *bf, uint64_t nb, const uint32_t *btab,
+__global__ __launch_bounds__(256) void ck_meta_kernel(const uint64_t *bo, uint64_t nb, const uint32_t *btab,
                                                       const uint64_t *BL, const uint64_t *MS, const uint64_t *blen,
                                                       const uint64_t *tbf, const uint64_t *toff,
-                                                      const uint64_t *tdata, Rec K, const uint8_t *src,
-                                                      uint8_t *dst, const uint64_t *need, uint64_t cap,
-                                                      const uint64_t *src_end, unsigned long long *guard) {
+                                                      const uint64_t *tdata, uint8_t *dst, const uint64_t *need,
+                                                      uint64_t cap, unsigned long long *guard) {
   __shared__ __attribute__((aligned(16))) uint8_t img[kMetaLds + 16];
   if (*need > cap) return; // output capacity exceeded: nothing is written
   const uint64_t b0 = static_cast<uint64_t>(blockIdx.x) * 256u;
@@ -837,16 +856,17 @@ __global__ __launch_bounds__(256) void ck_meta_kernel(const uint64_t *bf, uint64
     if (!ok) atomicOr(guard, kGuardMeta);
     return ok;
   };
+  MKeys mk{};
   if (MS[bend] - m0 > kMetaLds) {  // long keys: direct per-thread writes
-    if (b < bend && meta_entry_ok(b, bf, K, src_end, guard)) {
+    if (b < bend && meta_keys(b, bo, blen, MS, dst, cap, guard, mk)) {
       const uint32_t t = btab[b];
       if (in_cap(t, MS[b] - MS[tbf[t]], MS[b + 1] - MS[b]))
-        meta_entry(dst + toff[t] + tdata[t] + (MS[b] - MS[tbf[t]]), b, bf, btab, BL, blen, tbf, K, src);
+        meta_entry(dst + toff[t] + tdata[t] + (MS[b] - MS[tbf[t]]), b, btab, BL, blen, tbf, mk);
     }
     return;
   }
-  const bool ok = b >= bend || meta_entry_ok(b, bf, K, src_end, guard);
-  if (b < bend && ok) meta_entry(img + (MS[b] - m0), b, bf, btab, BL, blen, tbf, K, src);
+  const bool ok = b >= bend || meta_keys(b, bo, blen, MS, dst, cap, guard, mk);
+  if (b < bend && ok) meta_entry(img + (MS[b] - m0), b, btab, BL, blen, tbf, mk);
   if (__syncthreads_or(!ok)) return; // a bad entry: the workgroup writes nothing
   for (uint64_t bs = b0; bs < bend;) {  // one run per output table touched
     const uint32_t t = btab[bs];
@@ -1305,8 +1325,8 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     ea.src_end = src_end;
     ea.guard = guard;
     CK(launch_enc_emit(ea, s));
-    ck_meta_kernel<<<static_cast<uint32_t>((nb + 255) / 256), 256, 0, s>>>(bf, nb, btab, BL, MS, blen, tbf, d_table_off, tdata, KR, d_src, d_dst,
-                                                                          need, dst_cap, src_end, guard);
+    ck_meta_kernel<<<static_cast<uint32_t>((nb + 255) / 256), 256, 0, s>>>(bo, nb, btab, BL, MS, blen, tbf, d_table_off,
+                                                                          tdata, d_dst, need, dst_cap, guard);
     ck_tab_minmax_kernel<<<static_cast<uint32_t>(nt * kMmSplit), 256, 0, s>>>(tbf, bmin, bmax, tmin, tmax);
     ck_footer_kernel<<<grid(nt), 256, 0, s>>>(nt, tbf, d_table_off, tdata, tmeta, tmin, tmax, d_dst, dst_cap, guard);
     CK(hipGetLastError());
