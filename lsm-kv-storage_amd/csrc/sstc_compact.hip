@@ -727,13 +727,38 @@ __global__ __launch_bounds__(kFtThreads) void ck_filter_kernel(const SK *s, uint
   }
 }
 
+// The output table and block counts stay on the device (dn[0], dn[1]): the
+// layout kernels run on host-side upper bounds (nt_max, nb_max: every table
+// but the last holds >= table_limit key+value bytes, every block but a
+// table's last >= block_threshold entry + offset bytes), so the job needs no
+// host fetch between the split and the encode (it cost 12-36 us of idle GPU).
+// Array slots past the real counts are zero (the scans over the bounds then
+// end at the real totals); counts past the bounds (a corrupt split, or more
+// tables than max_tables) make every layout / encode kernel stand down.
+struct Lay {
+  const uint64_t *dn;
+  uint64_t nt_max, nb_max;
+  __device__ __forceinline__ uint64_t nt() const { return dn[0]; }
+  __device__ __forceinline__ uint64_t nb() const { return dn[1]; }
+  __device__ __forceinline__ bool ok() const { return dn[0] <= nt_max && dn[1] <= nb_max; }
+};
+
 // block b: length, meta entry size, table index
-__global__ void ck_block_info_kernel(const uint64_t *bf, uint64_t nb, const uint64_t *Pe, const uint32_t *kl,
-                                     const uint64_t *tf, uint64_t nt, uint64_t *blen, uint64_t *msz,
-                                     uint32_t *btab, uint64_t *zws, uint64_t nz) {
+__global__ void ck_block_info_kernel(const uint64_t *bf, Lay L, const uint64_t *Pe, const uint32_t *kl,
+                                     const uint64_t *tf, uint64_t *blen, uint64_t *msz, uint32_t *btab,
+                                     uint64_t *zws, uint64_t nz, unsigned long long *guard) {
   const uint64_t b = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (b < nz) zws[b] = 0; // look-back status words of the two block scans that follow
-  if (b >= nb) return;
+  if (b >= L.nb_max) return;
+  const bool ok = L.ok();
+  const uint64_t nb = L.nb(), nt = L.nt();
+  if (!ok || b >= nb) { // past the real blocks: zero (the scans over nb_max stay exact)
+    blen[b] = 0;
+    msz[b] = 0;
+    btab[b] = 0;
+    if (!ok && b == 0) atomicOr(guard, kGuardLayout);
+    return;
+  }
   const uint64_t f0 = bf[b], f1 = bf[b + 1];
   blen[b] = (Pe[f1] - Pe[f0]) + 16 * (f1 - f0) + 16;
   msz[b] = 24ull + kl[f0] + kl[f1 - 1]; // AddIndexBlockEntry, table_builder.cc:101-145
@@ -747,11 +772,21 @@ __global__ void ck_block_info_kernel(const uint64_t *bf, uint64_t nb, const uint
 }
 
 // table t: first block index, data / meta bytes, total
-__global__ void ck_table_info_kernel(const uint64_t *tf, uint64_t nt, const uint64_t *bf, uint64_t nb,
-                                     const uint64_t *BL, const uint64_t *MS, uint64_t *tbf, uint64_t *tdata,
-                                     uint64_t *tmeta, uint64_t *tlen) {
+__global__ void ck_table_info_kernel(const uint64_t *tf, Lay L, const uint64_t *bf, const uint64_t *BL,
+                                     const uint64_t *MS, uint64_t *tbf, uint64_t *tdata, uint64_t *tmeta,
+                                     uint64_t *tlen) {
   const uint64_t t = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (t > nt) return;
+  if (t > L.nt_max) return;
+  const uint64_t nt = L.nt(), nb = L.nb();
+  if (!L.ok() || t > nt) { // past the real tables: zero lengths (the table scan over nt_max stays exact)
+    if (t < L.nt_max) {
+      tlen[t] = 0;
+      tdata[t] = 0;
+      tmeta[t] = 0;
+    }
+    tbf[t] = L.ok() ? nb : 0;
+    return;
+  }
   // block starting at record tf[t] (every table start is a block start)
   uint64_t lo = 0, hi = nb + 1;
   const uint64_t r = tf[t];
@@ -775,10 +810,10 @@ __global__ void ck_table_info_kernel(const uint64_t *tf, uint64_t nt, const uint
   tlen[t] = tdata[t] + tmeta[t] + 40;
 }
 
-__global__ void ck_block_off_kernel(const uint32_t *btab, uint64_t nb, const uint64_t *BL, const uint64_t *tbf,
+__global__ void ck_block_off_kernel(const uint32_t *btab, Lay L, const uint64_t *BL, const uint64_t *tbf,
                                     const uint64_t *toff, uint64_t *bo) {
   const uint64_t b = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (b >= nb) return;
+  if (b >= L.nb_max || !L.ok() || b >= L.nb()) return;
   const uint32_t t = btab[b];
   bo[b] = toff[t] + (BL[b] - BL[tbf[t]]);
 }
@@ -838,14 +873,16 @@ __device__ __forceinline__ void meta_entry(uint8_t *p, uint64_t b, const uint32_
   put_le(p + 16 + m.fk + m.lk, blen[b], 8);
 }
 
-__global__ __launch_bounds__(256) void ck_meta_kernel(const uint64_t *bo, uint64_t nb, const uint32_t *btab,
+__global__ __launch_bounds__(256) void ck_meta_kernel(const uint64_t *bo, Lay L, const uint32_t *btab,
                                                       const uint64_t *BL, const uint64_t *MS, const uint64_t *blen,
                                                       const uint64_t *tbf, const uint64_t *toff,
                                                       const uint64_t *tdata, uint8_t *dst, const uint64_t *need,
                                                       uint64_t cap, unsigned long long *guard) {
   __shared__ __attribute__((aligned(16))) uint8_t img[kMetaLds + 16];
-  if (*need > cap) return; // output capacity exceeded: nothing is written
+  if (*need > cap || !L.ok()) return; // output capacity exceeded / corrupt layout: nothing is written
+  const uint64_t nb = L.nb();
   const uint64_t b0 = static_cast<uint64_t>(blockIdx.x) * 256u;
+  if (b0 >= nb) return;
   const uint64_t bend = b0 + 256u < nb ? b0 + 256u : nb;
   const uint64_t b = b0 + threadIdx.x;
   const uint64_t m0 = MS[b0];
@@ -903,10 +940,11 @@ __global__ __launch_bounds__(256) void ck_meta_kernel(const uint64_t *bo, uint64
 // partial; the footer kernel folds a table's kMmSplit partials (no atomics:
 // same-address atomics from every XCD serialise)
 constexpr uint32_t kMmSplit = 16;
-__global__ __launch_bounds__(256) void ck_tab_minmax_kernel(const uint64_t *tbf, const uint64_t *bmin,
+__global__ __launch_bounds__(256) void ck_tab_minmax_kernel(const uint64_t *tbf, Lay L, const uint64_t *bmin,
                                                             const uint64_t *bmax, uint64_t *pmin, uint64_t *pmax) {
   __shared__ uint64_t smn[256 / kWave], smx[256 / kWave];
   const uint64_t t = blockIdx.x / kMmSplit, g = blockIdx.x % kMmSplit;
+  if (!L.ok() || t >= L.nt()) return; // uniform over the workgroup
   const uint64_t f = tbf[t], n = tbf[t + 1] - f;
   const uint64_t b0 = f + n * g / kMmSplit, b1 = f + n * (g + 1) / kMmSplit;
   uint64_t mn = ~0ull, mx = 0;
@@ -935,10 +973,12 @@ __global__ __launch_bounds__(256) void ck_tab_minmax_kernel(const uint64_t *tbf,
 }
 
 // footer of table t (table_builder.cc:179-211)
-__global__ void ck_footer_kernel(uint64_t nt, const uint64_t *tbf, const uint64_t *toff, const uint64_t *tdata,
+__global__ void ck_footer_kernel(Lay L, const uint64_t *tbf, const uint64_t *toff, const uint64_t *tdata,
                                  const uint64_t *tmeta, const uint64_t *tmin, const uint64_t *tmax, uint8_t *dst,
                                  uint64_t cap, unsigned long long *guard) {
   const uint64_t t = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (!L.ok()) return;
+  const uint64_t nt = L.nt();
   if (t >= nt || toff[nt] > cap) return;
   const uint64_t at = toff[t] + tdata[t] + tmeta[t];
   if (at < toff[t] || at > cap || cap - at < 40) { // the footer must end inside the output buffer
@@ -1267,7 +1307,7 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     if (arena.fault == 2) CK(hipMemsetAsync(Pe, 0x5A, (n + 1) * sizeof(uint64_t), s)); // test: bad prefix sums
     fetch(arena, s, {totals, reinterpret_cast<const uint64_t *>(bad),
                            reinterpret_cast<const uint64_t *>(err_count), errs,
-                           reinterpret_cast<const uint64_t *>(guard)});
+                           reinterpret_cast<const uint64_t *>(guard), totals + 1, totals + 2});
     if (arena.host[2] != arena.host[3]) {
       err = "an input block failed to decode";
       return SSTC_E_INVALID_ARG;
@@ -1288,50 +1328,56 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     segment(pool, Pd, 0, m, table_limit, nullptr, nullptr, tf, dn, s, true);
     uint64_t *bf = pool.get<uint64_t>(m + 1);
     segment(pool, Pe, 16, m, block_threshold, tf, dn, bf, dn + 1, s, false); // blocks end at table ends
-    fetch(arena, s, {dn, dn + 1});
-    const uint64_t nt = arena.host[0], nb = arena.host[1];
-    if (nt > max_tables) {
-      err = "more output tables than max_tables";
-      return SSTC_E_CAPACITY;
-    }
-    // 5. layout
-    uint64_t *blen = pool.get<uint64_t>(nb), *msz = pool.get<uint64_t>(nb);
-    uint32_t *btab = pool.get<uint32_t>(nb);
-    const uint64_t nzb = scan_status_words(nb); // <= nb
+    // 5. layout over the count bounds (no host fetch: see Lay)
+    const uint64_t tl = table_limit ? table_limit : 1, bt = block_threshold ? block_threshold : 1;
+    const uint64_t kv_bytes = arena.host[5], entry_bytes = arena.host[6];
+    const uint64_t nt_max = std::max<uint64_t>(1, std::min<uint64_t>({m, kv_bytes / tl + 1, max_tables}));
+    const uint64_t nb_max = std::max<uint64_t>(1, std::min<uint64_t>(m, (entry_bytes + 16 * m) / bt + nt_max));
+    const Lay L{dn, nt_max, nb_max};
+    uint64_t *blen = pool.get<uint64_t>(nb_max), *msz = pool.get<uint64_t>(nb_max);
+    uint32_t *btab = pool.get<uint32_t>(nb_max);
+    const uint64_t nzb = scan_status_words(nb_max); // <= nb_max
     uint64_t *ws3 = pool.get<uint64_t>(2 * nzb);
-    ck_block_info_kernel<<<grid(nb), 256, 0, s>>>(bf, nb, Pe, KR.kl, tf, nt, blen, msz, btab, ws3, 2 * nzb);
-    uint64_t *BL = pool.get<uint64_t>(nb + 1), *MS = pool.get<uint64_t>(nb + 1);
-    CK(launch_scan(blen, nb, 0, BL, ws3, s, true));
-    CK(launch_scan(msz, nb, 0, MS, ws3 + nzb, s, true));
-    uint64_t *tbf = pool.get<uint64_t>(nt + 1), *tdata = pool.get<uint64_t>(nt), *tmeta = pool.get<uint64_t>(nt);
-    ck_table_info_kernel<<<grid(nt + 1), 256, 0, s>>>(tf, nt, bf, nb, BL, MS, tbf, tdata, tmeta, d_table_len);
-    CK(launch_scan(d_table_len, nt, 0, d_table_off, ws2, s)); // d_table_off needs nt + 1 elements
+    ck_block_info_kernel<<<grid(nb_max), 256, 0, s>>>(bf, L, Pe, KR.kl, tf, blen, msz, btab, ws3, 2 * nzb, guard);
+    uint64_t *BL = pool.get<uint64_t>(nb_max + 1), *MS = pool.get<uint64_t>(nb_max + 1);
+    CK(launch_scan(blen, nb_max, 0, BL, ws3, s, true));
+    CK(launch_scan(msz, nb_max, 0, MS, ws3 + nzb, s, true));
+    uint64_t *tbf = pool.get<uint64_t>(nt_max + 1), *tdata = pool.get<uint64_t>(nt_max),
+             *tmeta = pool.get<uint64_t>(nt_max);
+    ck_table_info_kernel<<<grid(nt_max + 1), 256, 0, s>>>(tf, L, bf, BL, MS, tbf, tdata, tmeta, d_table_len);
+    CK(launch_scan(d_table_len, nt_max, 0, d_table_off, ws2, s)); // nt_max + 1 <= max_tables + 1 elements
     // the output size is checked on the device (every writer below stands down
     // when it exceeds dst_cap) and by the host after the last sync
-    const uint64_t *need = d_table_off + nt;
-    res[2] = nb;
-    res[3] = nt;
-    uint64_t *bo = pool.get<uint64_t>(nb);
-    ck_block_off_kernel<<<grid(nb), 256, 0, s>>>(btab, nb, BL, tbf, d_table_off, bo);
+    const uint64_t *need = d_table_off + nt_max; // = d_table_off[nt]: the lengths past nt are zero
+    uint64_t *bo = pool.get<uint64_t>(nb_max);
+    ck_block_off_kernel<<<grid(nb_max), 256, 0, s>>>(btab, L, BL, tbf, d_table_off, bo);
     // 6. encode blocks, meta entries, footers
-    EncArgs ea{d_src, d_src, sstc_records{KR.type, KR.kl, KR.vl, KR.tx, KR.ko, KR.vo}, bf, nb, Pe, bo, blen, d_dst, 1};
-    uint64_t *bmin = pool.get<uint64_t>(nb), *bmax = pool.get<uint64_t>(nb);
+    EncArgs ea{d_src, d_src, sstc_records{KR.type, KR.kl, KR.vl, KR.tx, KR.ko, KR.vo}, bf, nb_max, Pe, bo, blen, d_dst, 1};
+    ea.nb_dev = dn + 1;
+    uint64_t *bmin = pool.get<uint64_t>(nb_max), *bmax = pool.get<uint64_t>(nb_max);
     // blocks past an LDS slot are encoded by the wave that met them (config 5 319 -> 233 us)
     ea.need = need;
     ea.cap = dst_cap;
-    uint64_t *tmin = pool.get<uint64_t>(nt * kMmSplit), *tmax = pool.get<uint64_t>(nt * kMmSplit);  // per-table partials
+    uint64_t *tmin = pool.get<uint64_t>(nt_max * kMmSplit), *tmax = pool.get<uint64_t>(nt_max * kMmSplit);  // per-table partials
     ea.bmin = bmin; // block min / max txn, reduced by the encode kernels
     ea.bmax = bmax;
     ea.src_end = src_end;
     ea.guard = guard;
     CK(launch_enc_emit(ea, s));
-    ck_meta_kernel<<<static_cast<uint32_t>((nb + 255) / 256), 256, 0, s>>>(bo, nb, btab, BL, MS, blen, tbf, d_table_off,
-                                                                          tdata, d_dst, need, dst_cap, guard);
-    ck_tab_minmax_kernel<<<static_cast<uint32_t>(nt * kMmSplit), 256, 0, s>>>(tbf, bmin, bmax, tmin, tmax);
-    ck_footer_kernel<<<grid(nt), 256, 0, s>>>(nt, tbf, d_table_off, tdata, tmeta, tmin, tmax, d_dst, dst_cap, guard);
+    ck_meta_kernel<<<static_cast<uint32_t>((nb_max + 255) / 256), 256, 0, s>>>(bo, L, btab, BL, MS, blen, tbf,
+                                                                              d_table_off, tdata, d_dst, need,
+                                                                              dst_cap, guard);
+    ck_tab_minmax_kernel<<<static_cast<uint32_t>(nt_max * kMmSplit), 256, 0, s>>>(tbf, L, bmin, bmax, tmin, tmax);
+    ck_footer_kernel<<<grid(nt_max), 256, 0, s>>>(L, tbf, d_table_off, tdata, tmeta, tmin, tmax, d_dst, dst_cap, guard);
     CK(hipGetLastError());
-    fetch(arena, s, {need, reinterpret_cast<const uint64_t *>(guard)}, nullptr, 0, true);
+    fetch(arena, s, {need, reinterpret_cast<const uint64_t *>(guard), dn, dn + 1}, nullptr, 0, true);
     res[4] = arena.host[0];
+    res[2] = arena.host[3];
+    res[3] = arena.host[2];
+    if (arena.host[2] > max_tables) {
+      err = "more output tables than max_tables";
+      return SSTC_E_CAPACITY;
+    }
     if (arena.host[1]) {
       err = "device consistency check failed (guard bits 0x" + [](uint64_t v) {
         char b[24];

@@ -1274,7 +1274,8 @@ __global__ __launch_bounds__(kEncWaves *kWave) void enc_lds_kernel(EncArgs a) {
   const uint32_t lane = lane_id();
   const uint32_t wg = a.xcd ? xcd_logical_block(blockIdx.x, gridDim.x) : blockIdx.x;
   const uint64_t b = static_cast<uint64_t>(wg) * kEncWaves + wave;
-  if (b >= a.nblocks || a.over()) return;
+  const uint64_t nbl = a.nb_dev ? *a.nb_dev : a.nblocks; // compaction: the count on the device, nblocks its bound
+  if (b >= nbl || nbl > a.nblocks || a.over()) return;
   uint8_t *img = lds + wave * kEncSlot;
   const uint64_t bo = uniform64(a.out_blk_off[b]);
   const uint64_t L64 = uniform64(a.out_blk_len[b]);

@@ -85,11 +85,15 @@ struct EncArgs {
   // [5, *src_end); a block that fails is not written and sets *guard
   const uint64_t *src_end = nullptr;
   unsigned long long *guard = nullptr;
+  // optional (compaction): the block count is on the device (nb_dev) and
+  // nblocks is only its host-side upper bound (the grid); a count past the
+  // bound means a corrupt layout: every wave stands down
+  const uint64_t *nb_dev = nullptr;
 };
 
 // consistency-guard bits of the compaction job (sstc_compact.hip)
 constexpr unsigned long long kGuardMergeId = 1, kGuardEntry = 2, kGuardBlockRange = 4, kGuardMeta = 8,
-                             kGuardFooter = 16;
+                             kGuardFooter = 16, kGuardLayout = 32;
 
 // point lookups (sstc_get.hip)
 struct GetArgs {

@@ -234,6 +234,51 @@ def test_compact_capacity_exceeded_writes_nothing(codec):
             assert np.array_equal(d[:need], np.concatenate(want))
 
 
+def test_compact_max_tables_exceeded_writes_nothing(codec):
+    """More output tables than max_tables: SSTC_E_CAPACITY and not one byte of
+    the output buffer written.  The table / block counts stay on the device
+    (the layout runs on host-side bounds clamped to max_tables), so every
+    layout, encode, meta and footer kernel must stand down on its own."""
+    import ctypes
+    import torch
+    from sstcodec._lib import CompactParams, CompactResult
+    g = load_golden("compact_small_base1.npz")
+    ins = [g[f"in{i}"] for i in range(4)]
+    src = torch.from_numpy(np.concatenate(ins)).to(codec.device)
+    idx = codec.open_tables(src, [f.size for f in ins], strict=True)
+    P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    # a 4 KiB table limit splits the ~50 KB of surviving keys + values into many tables
+    prm = CompactParams(4096, 4 << 10, 1, 0)
+    need = int(src.numel()) * 2
+    for max_tables, rc_want in ((3, -5), (4096, 0)):
+        toff = torch.zeros(max_tables + 1, dtype=torch.int64, device=codec.device)
+        tlen = torch.zeros(max_tables, dtype=torch.int64, device=codec.device)
+        dst = torch.full((need,), 0xA5, dtype=torch.uint8, device=codec.device)
+        res = CompactResult()
+        codec._stream()
+        rc = codec.lib.sstc_compact(codec.h, P(src), P(idx["blk_off"]), P(idx["blk_len"]), int(idx["blk_off"].numel()),
+                                    idx["table_first_block"].ctypes.data_as(ctypes.c_void_p), len(ins),
+                                    ctypes.byref(prm), P(dst), need, P(toff), P(tlen), max_tables, ctypes.byref(res))
+        assert rc == rc_want
+        if rc:
+            assert res.tables_out > max_tables
+            assert (dst.cpu().numpy() == 0xA5).all(), "a writer ran although the tables exceed max_tables"
+        else:
+            assert res.tables_out > 3
+
+
+def test_compact_all_deletes_base_level(codec, oracle):
+    """Every input record a DELETE at the base level: ShouldKeepEntry drops
+    them all but the first merged record (compact.cc:324-363 keeps the first
+    record unconditionally), so the job emits one table of one entry."""
+    sets = W.compaction_inputs(3, 2000, 5000, seed=3, vmax=64, p_delete=1.0)
+    ins = [oracle.table_build(r, 4096) for r in sets]
+    want, kept = oracle.compact(ins, 4096, 1 << 20, 1)
+    outs, res = codec.compact(ins, 4096, 1 << 20, 1)
+    assert res.records_kept == kept == 1 and len(outs) == len(want) == 1
+    assert np.array_equal(outs[0], want[0])
+
+
 def test_compact_long_keys_many_windows(codec, oracle):
     """Keys longer than the 16 B sort prefix, all sharing it (every merge
     comparison falls back to the source bytes), over 10 inputs (two merge
