@@ -231,12 +231,14 @@ typedef struct sstc_compact_result {
  * them, and the survivors are written as complete SST images (blocks, meta
  * section, 40 B footer) back to back into d_dst: table t at d_table_off[t]
  * with d_table_len[t] bytes (TableBuilder::GetFileSize() = d_table_len[t] + 1).
- * d_table_off needs max_tables+1 elements.  This call allocates its own
- * workspace and synchronises the stream (output sizes are data dependent).
- * Output larger than dst_cap: SSTC_E_CAPACITY with result->bytes_out = the
- * exact size needed and not one byte of d_dst written (every writer checks
- * the size on the device); more tables than max_tables: SSTC_E_CAPACITY
- * before any write to d_dst. */
+ * d_table_off needs max_tables+1 elements; entries past tables_out may be
+ * overwritten (d_table_len with 0, d_table_off with the total).  This call
+ * allocates its own workspace and synchronises the stream (output sizes are
+ * data dependent).  Output larger than dst_cap: SSTC_E_CAPACITY with
+ * result->bytes_out = the exact size needed and not one byte of d_dst written
+ * (every writer checks the size on the device); more tables than max_tables:
+ * SSTC_E_CAPACITY (result->tables_out = the count) and not one byte of d_dst
+ * written. */
 int sstc_compact(sstc_ctx *ctx, const uint8_t *d_src, const uint64_t *d_blk_off, const uint64_t *d_blk_len,
                  uint64_t nblocks, const uint64_t *h_table_first_block, uint32_t ntables,
                  const sstc_compact_params *params, uint8_t *d_dst, uint64_t dst_cap, uint64_t *d_table_off,
