@@ -743,6 +743,18 @@ struct Lay {
   __device__ __forceinline__ bool ok() const { return dn[0] <= nt_max && dn[1] <= nb_max; }
 };
 
+// Offset of block b in the concatenated data blocks: the blocks partition the
+// survivors in order, so it is the entry bytes before its first record + 16 B
+// per offset entry before it + 16 B per extra before it -- a closed form of
+// the survivors' entry-size prefix sums (no scan of the block lengths)
+struct BlkOff {
+  const uint64_t *Pe, *bf;
+  __device__ __forceinline__ uint64_t operator[](uint64_t b) const {
+    const uint64_t f = bf[b];
+    return Pe[f] + 16 * (f + b);
+  }
+};
+
 // block b: length, meta entry size, table index
 __global__ void ck_block_info_kernel(const uint64_t *bf, Lay L, const uint64_t *Pe, const uint32_t *kl,
                                      const uint64_t *tf, uint64_t *blen, uint64_t *msz, uint32_t *btab,
@@ -772,7 +784,7 @@ __global__ void ck_block_info_kernel(const uint64_t *bf, Lay L, const uint64_t *
 }
 
 // table t: first block index, data / meta bytes, total
-__global__ void ck_table_info_kernel(const uint64_t *tf, Lay L, const uint64_t *bf, const uint64_t *BL,
+__global__ void ck_table_info_kernel(const uint64_t *tf, Lay L, const uint64_t *bf, BlkOff BL,
                                      const uint64_t *MS, uint64_t *tbf, uint64_t *tdata, uint64_t *tmeta,
                                      uint64_t *tlen) {
   const uint64_t t = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
@@ -810,7 +822,7 @@ __global__ void ck_table_info_kernel(const uint64_t *tf, Lay L, const uint64_t *
   tlen[t] = tdata[t] + tmeta[t] + 40;
 }
 
-__global__ void ck_block_off_kernel(const uint32_t *btab, Lay L, const uint64_t *BL, const uint64_t *tbf,
+__global__ void ck_block_off_kernel(const uint32_t *btab, Lay L, BlkOff BL, const uint64_t *tbf,
                                     const uint64_t *toff, uint64_t *bo) {
   const uint64_t b = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (b >= L.nb_max || !L.ok() || b >= L.nb()) return;
@@ -862,7 +874,7 @@ __device__ __forceinline__ bool meta_keys(uint64_t b, const uint64_t *bo, const 
   if (!ok) atomicOr(guard, kGuardMeta);
   return ok;
 }
-__device__ __forceinline__ void meta_entry(uint8_t *p, uint64_t b, const uint32_t *btab, const uint64_t *BL,
+__device__ __forceinline__ void meta_entry(uint8_t *p, uint64_t b, const uint32_t *btab, const BlkOff &BL,
                                            const uint64_t *blen, const uint64_t *tbf, const MKeys &m) {
   const uint32_t t = btab[b];
   put_le(p, m.fk, 4);
@@ -874,7 +886,7 @@ __device__ __forceinline__ void meta_entry(uint8_t *p, uint64_t b, const uint32_
 }
 
 __global__ __launch_bounds__(256) void ck_meta_kernel(const uint64_t *bo, Lay L, const uint32_t *btab,
-                                                      const uint64_t *BL, const uint64_t *MS, const uint64_t *blen,
+                                                      BlkOff BL, const uint64_t *MS, const uint64_t *blen,
                                                       const uint64_t *tbf, const uint64_t *toff,
                                                       const uint64_t *tdata, uint8_t *dst, const uint64_t *need,
                                                       uint64_t cap, unsigned long long *guard) {
@@ -1339,8 +1351,8 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     const uint64_t nzb = scan_status_words(nb_max); // <= nb_max
     uint64_t *ws3 = pool.get<uint64_t>(2 * nzb);
     ck_block_info_kernel<<<grid(nb_max), 256, 0, s>>>(bf, L, Pe, KR.kl, tf, blen, msz, btab, ws3, 2 * nzb, guard);
-    uint64_t *BL = pool.get<uint64_t>(nb_max + 1), *MS = pool.get<uint64_t>(nb_max + 1);
-    CK(launch_scan(blen, nb_max, 0, BL, ws3, s, true));
+    const BlkOff BL{Pe, bf}; // block offsets in closed form (Pe[0] = 0)
+    uint64_t *MS = pool.get<uint64_t>(nb_max + 1);
     CK(launch_scan(msz, nb_max, 0, MS, ws3 + nzb, s, true));
     uint64_t *tbf = pool.get<uint64_t>(nt_max + 1), *tdata = pool.get<uint64_t>(nt_max),
              *tmeta = pool.get<uint64_t>(nt_max);

@@ -1773,7 +1773,18 @@ __global__ __launch_bounds__(kWave) void seg_hops_kernel(const uint64_t *Pw, uin
   uint64_t pos = 0, nseg = 0, glen = 0, wpos = Pw[0];
   bool done = false;
   while (!done) {
-    if (glen == 0) { // no prediction yet: one exact hop
+    if (glen == 0 && pos < m && wm - wpos >= threshold) {
+      // no segment length seen yet: predict one from the mean weight of the
+      // rest (equal-sized records: the first window holds the answer, no
+      // exact search); a
+      // window that misses falls back to the exact hop below
+      const uint64_t rest = wm - wpos, nrec = m - pos;
+      const uint64_t g = rest ? static_cast<uint64_t>(static_cast<double>(threshold) * static_cast<double>(nrec) /
+                                                      static_cast<double>(rest))
+                              : 0;
+      glen = g >= 1 && g <= nrec ? g : 0;
+    }
+    if (glen == 0) { // no prediction: one exact hop
       if (pos >= m) break;
       if (lane == 0) first[nseg] = pos;
       nseg++;
