@@ -91,16 +91,18 @@ template <class T> int grow(sstc_ctx *c, T *&p, uint64_t &cap, uint64_t need, co
 // scan_ws is zeroed when (re)allocated; every scan on it then takes a fresh
 // epoch (sstc::launch_scan), so no memset precedes a scan.  When the 14-bit
 // epoch would wrap, the words are cleared once and the count restarts.
-int ensure_scan(sstc_ctx *c, uint64_t n) {
+int ensure_scan_words(sstc_ctx *c, uint64_t words) {
   const uint64_t old = c->cap_scan;
   const uint64_t *before = c->scan_ws;
-  if (int r = grow(c, c->scan_ws, c->cap_scan, sstc::scan_workspace_elems(n), "scan workspace")) return r;
+  if (int r = grow(c, c->scan_ws, c->cap_scan, words, "scan workspace")) return r;
   if (c->scan_ws != before || c->cap_scan != old) {
     SSTC_HIP(hipMemsetAsync(c->scan_ws, 0, c->cap_scan * sizeof(uint64_t), c->stream), "scan workspace clear");
     c->scan_epoch = 0;
   }
   return SSTC_OK;
 }
+
+int ensure_scan(sstc_ctx *c, uint64_t n) { return ensure_scan_words(c, sstc::scan_workspace_elems(n)); }
 
 int next_epoch(sstc_ctx *c, uint32_t &epoch) {
   if (c->scan_epoch + 1 >= sstc::kScanEpochs) {
@@ -319,7 +321,9 @@ int sstc_encode_blocks(sstc_ctx *c, const uint8_t *d_key_src, const uint8_t *d_v
   if (int r = bind_device(c)) return r;
   if (nblocks >= 0xFFFFFFFFull) return fail(SSTC_E_INVALID_ARG, "too many blocks for one call");
   if (int r = ensure_records(c, nrec)) return r;
-  if (int r = ensure_scan(c, nblocks + 1)) return r; // the block-length scan's workspace
+  if (int r = ensure_scan_words(c, std::max(sstc::scan_workspace_elems(nblocks + 1),
+                                             sstc::enc_offsets_workspace(nblocks))))
+    return r; // the block-offset scan's workspace
   // block lengths (entry sizes summed per block), their scan = block offsets,
   // P (entry-size prefix) per block, then the block images
   uint32_t ep = 0;

@@ -2078,6 +2078,7 @@ hipError_t launch_decode(const DecArgs &a, hipStream_t s) {
 // sized for the smallest tile any scan uses (kScanThreads x 4 items)
 uint64_t scan_workspace_elems(uint64_t n) { return (n + 4 * kScanThreads - 1) / (4 * kScanThreads) + 2; }
 
+
 // u64 array scans (block counts, block lengths, segmentation node counts):
 // kArrItems per thread (16 / 8 / 4: the three block-level scans of config 3
 // took 28.4 / 20.9 / 25.9 us); the entry-size scan keeps kLbItems
@@ -2115,6 +2116,118 @@ hipError_t launch_scan_entry_sizes(const uint32_t *klen, const uint32_t *vlen, u
   return scan_any(EntryIn{klen, vlen, add}, nrec, 0, out, ws, s, false, epoch);
 }
 
+// Block lengths and offsets of a records -> blocks encode in ONE kernel
+// (enc_bsum_kernel + a block scan were two launches, ~13 us of the config-2
+// encode leg): a workgroup per tile of kBoTile blocks sums every block's entry
+// sizes with kBsG lanes per block -- the block bounds of all its passes, then
+// the first kBoUnroll records of every lane, issued before any is used (one
+// dependent round trip each) --, scans the tile's lengths, and takes the
+// tile's offset from a decoupled look-back over the tiles (ticketed,
+// epoch-tagged status words, as scan_lookback_kernel).  ws = [ticket,
+// status[tiles]].
+constexpr uint32_t kBoTile = 256, kBoPasses = kBoTile * kBsG / 256, kBoUnroll = 4;
+__global__ __launch_bounds__(256) void enc_offsets_kernel(const uint32_t *kl, const uint32_t *vl,
+                                                          const uint64_t *blk_first, uint64_t nblocks,
+                                                          uint64_t out_base, uint64_t *blk_off, uint64_t *blk_len,
+                                                          uint64_t *ws, uint32_t epoch) {
+  __shared__ uint64_t s_len[kBoTile];
+  __shared__ uint64_t s_wsum[256 / kWave];
+  __shared__ uint64_t s_tile, s_prefix;
+  const uint32_t tid = threadIdx.x, lane = lane_id(), w = tid / kWave, g = tid % kBsG;
+  if (tid == 0) {
+    const uint64_t t = __hip_atomic_fetch_add(ws, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (t + 1 == gridDim.x) __hip_atomic_store(ws, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_tile = t;
+  }
+  __syncthreads();
+  const uint64_t tile = s_tile, b0 = tile * kBoTile;
+  uint64_t F0[kBoPasses], F1[kBoPasses];
+#pragma unroll
+  for (uint32_t p = 0; p < kBoPasses; p++) {
+    const uint64_t b = b0 + p * (256 / kBsG) + tid / kBsG;
+    const uint64_t bc = b < nblocks ? b : 0;
+    F0[p] = blk_first[bc];
+    F1[p] = b < nblocks ? blk_first[bc + 1] : F0[p];
+  }
+  uint32_t K[kBoPasses][kBoUnroll], V[kBoPasses][kBoUnroll];
+#pragma unroll
+  for (uint32_t p = 0; p < kBoPasses; p++) {
+#pragma unroll
+    for (uint32_t k = 0; k < kBoUnroll; k++) {
+      const uint64_t r = F0[p] + g + k * kBsG;
+      const uint64_t rc = r < F1[p] ? r : 0; // record 0 exists whenever a block is non-empty
+      K[p][k] = kl[rc];
+      V[p][k] = vl[rc];
+    }
+  }
+#pragma unroll
+  for (uint32_t p = 0; p < kBoPasses; p++) {
+    uint64_t sum = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kBoUnroll; k++)
+      if (F0[p] + g + k * kBsG < F1[p]) sum += entry_size(K[p][k], V[p][k]);
+    for (uint64_t r = F0[p] + g + kBoUnroll * kBsG; r < F1[p]; r += kBsG) sum += entry_size(kl[r], vl[r]);
+#pragma unroll
+    for (uint32_t d = kBsG / 2; d > 0; d >>= 1) sum += __shfl_xor(sum, d, kWave); // inside the 8-lane group
+    const uint64_t b = b0 + p * (256 / kBsG) + tid / kBsG;
+    if (g == 0) s_len[p * (256 / kBsG) + tid / kBsG] = b < nblocks ? sum + 16 * (F1[p] - F0[p]) + 16 : 0;
+  }
+  __syncthreads();
+  const uint64_t len = s_len[tid];
+  const uint64_t incl = wave_incl_scan_u64(len);
+  if (lane == kWave - 1) s_wsum[w] = incl;
+  __syncthreads();
+  uint64_t wbase = 0, total = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < 256 / kWave; k++) {
+    const uint64_t x = s_wsum[k];
+    if (k < w) wbase += x;
+    total += x;
+  }
+  if (w == 0) {
+    const uint64_t tag = static_cast<uint64_t>(epoch) << kLbEpochShift;
+    uint64_t *status = ws + 1;
+    uint64_t prefix = 0;
+    if (tile == 0) {
+      if (lane == 0) __hip_atomic_store(&status[0], kLbInc | tag | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      if (lane == 0) __hip_atomic_store(&status[tile], kLbAgg | tag | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      int64_t p = static_cast<int64_t>(tile) - 1; // window [p - 63, p]
+      uint64_t spins = 0;
+      for (;;) {
+        const int64_t q = p - static_cast<int64_t>(lane);
+        uint64_t st = q >= 0 ? __hip_atomic_load(&status[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                             : kLbInc | tag;
+        if (((st >> kLbEpochShift) & 0x3FFFu) != epoch) st = 0; // a stale word: not published yet
+        const uint64_t inc = __ballot((st >> 62) == 2);
+        const uint32_t need = inc ? static_cast<uint32_t>(__ffsll(static_cast<long long>(inc))) : kWave;
+        if (__ballot((st >> 62) == 0 && lane < need)) {
+          if (++spins > kLbSpinLimit) break; // a predecessor never published: give up (wrong sums, no hang)
+          __builtin_amdgcn_s_sleep(1);
+          continue;
+        }
+        prefix += wave_sum_u64(lane < need ? (st & kLbVal) : 0);
+        if (inc) break;
+        p -= kWave;
+      }
+      if (lane == 0)
+        __hip_atomic_store(&status[tile], kLbInc | tag | (prefix + total), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (lane == 0) s_prefix = prefix;
+  }
+  __syncthreads();
+  const uint64_t b = b0 + tid;
+  const uint64_t off = out_base + s_prefix + wbase + incl - len;
+  if (b < nblocks) {
+    blk_off[b] = off;
+    blk_len[b] = len;
+    if (b + 1 == nblocks) blk_off[nblocks] = off + len;
+  }
+}
+
+uint64_t enc_offsets_workspace(uint64_t nblocks) { return (nblocks + kBoTile - 1) / kBoTile + 2; }
+
 hipError_t launch_enc_offsets(const uint32_t *kl, const uint32_t *vl, const uint64_t *blk_first, uint64_t nblocks,
                               uint64_t out_base, uint64_t *blk_off, uint64_t *blk_len, uint64_t *ws, hipStream_t s,
                               uint32_t epoch) {
@@ -2122,8 +2235,14 @@ hipError_t launch_enc_offsets(const uint32_t *kl, const uint32_t *vl, const uint
     enc_none_kernel<<<1, 1, 0, s>>>(out_base, blk_off);
     return hipGetLastError();
   }
-  enc_bsum_kernel<<<grid_for(nblocks * kBsG, 256), 256, 0, s>>>(kl, vl, blk_first, nblocks, blk_len);
-  return scan_any<ArrIn, kArrItems>(ArrIn{blk_len}, nblocks, out_base, blk_off, ws, s, false, epoch);
+  if (nblocks <= kScanTile || epoch == 0) { // one workgroup's scan / no epoch: sum kernel + scan
+    enc_bsum_kernel<<<grid_for(nblocks * kBsG, 256), 256, 0, s>>>(kl, vl, blk_first, nblocks, blk_len);
+    return scan_any<ArrIn, kArrItems>(ArrIn{blk_len}, nblocks, out_base, blk_off, ws, s, false, epoch);
+  }
+  // ws: enc_offsets_workspace(nblocks) words
+  enc_offsets_kernel<<<static_cast<uint32_t>((nblocks + kBoTile - 1) / kBoTile), 256, 0, s>>>(
+      kl, vl, blk_first, nblocks, out_base, blk_off, blk_len, ws, epoch);
+  return hipGetLastError();
 }
 
 hipError_t launch_enc_emit(const EncArgs &a, hipStream_t s) {

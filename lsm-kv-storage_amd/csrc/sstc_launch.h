@@ -137,7 +137,10 @@ hipError_t launch_scan(const uint64_t *in, uint64_t n, uint64_t carry_in, uint64
 hipError_t launch_scan_entry_sizes(const uint32_t *klen, const uint32_t *vlen, uint64_t nrec, uint64_t add,
                                    uint64_t *out, uint64_t *ws, hipStream_t s, uint32_t epoch);
 // block offsets (nblocks + 1) and lengths of a records -> blocks encode: block
-// lengths by reduction over each block's records, then a scan over the blocks
+// lengths by reduction over each block's records and their scan, one kernel
+// (ws: enc_offsets_workspace(nblocks) words, epoch != 0) or, for one
+// workgroup's worth of blocks / epoch 0, a sum kernel + a scan
+uint64_t enc_offsets_workspace(uint64_t nblocks);
 hipError_t launch_enc_offsets(const uint32_t *kl, const uint32_t *vl, const uint64_t *blk_first, uint64_t nblocks,
                               uint64_t out_base, uint64_t *blk_off, uint64_t *blk_len, uint64_t *ws, hipStream_t s,
                               uint32_t epoch);
