@@ -631,16 +631,20 @@ __global__ __launch_bounds__(kFtThreads) void ck_filter_kernel(const SK *s, uint
       ko[j] = rr[g].ko;
     }
   }
-  // per row and wave: kept count and the two byte sums by wave reductions,
-  // exchanged once through LDS for the whole tile (one barrier instead of two
-  // per row of a workgroup scan)
+  // per row and wave: kept count and the two byte sums, exchanged once
+  // through LDS for the whole tile (one barrier instead of two per row of a
+  // workgroup scan); the sums are the last lanes of the rows' inclusive DPP
+  // scans, which the survivor writes below reuse (no separate LDS-swizzle
+  // reductions)
   __shared__ uint64_t s_row[kFfRows][kFtThreads / kWave][3];
+  uint64_t dinc[kFfRows], einc[kFfRows];
 #pragma unroll
   for (uint32_t j = 0; j < kFfRows; j++) {
     const bool k = (km >> j) & 1u;
     const uint64_t c = static_cast<uint64_t>(__popcll(__ballot(k)));
-    const uint64_t d = wave_sum_u64(k ? data_bytes(kl[j], vl[j]) : 0ull);
-    const uint64_t e = wave_sum_u64(k ? entry_size(kl[j], vl[j]) : 0ull);
+    dinc[j] = wave_incl_scan_u64(k ? data_bytes(kl[j], vl[j]) : 0ull);
+    einc[j] = wave_incl_scan_u64(k ? entry_size(kl[j], vl[j]) : 0ull);
+    const uint64_t d = readlane_u64(dinc[j], kWave - 1), e = readlane_u64(einc[j], kWave - 1);
     if (lane == 0) {
       s_row[j][w][0] = c;
       s_row[j][w][1] = d;
@@ -700,7 +704,7 @@ __global__ __launch_bounds__(kFtThreads) void ck_filter_kernel(const SK *s, uint
     const uint32_t rank = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(bal >> 32),
                                                     __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(bal), 0u));
     const uint64_t dv = k ? data_bytes(kl[j], vl[j]) : 0ull, ev = k ? entry_size(kl[j], vl[j]) : 0ull;
-    const uint64_t dincl = wave_incl_scan_u64(dv), eincl = wave_incl_scan_u64(ev);
+    const uint64_t dincl = dinc[j], eincl = einc[j];
     const uint64_t q = off[0] + rank;
     if (k && q < n) { // (q < n holds by construction; the bound guards the stores)
       out.type[q] = static_cast<uint8_t>(ty[j]);

@@ -154,6 +154,11 @@ constexpr uint64_t kLbAgg = 1ull << 62, kLbInc = 2ull << 62, kLbVal = (1ull << 4
 constexpr uint32_t kLbEpochShift = 48;
 constexpr uint64_t kLbSpinLimit = 1ull << 24; // never reached unless a tile died
 
+__device__ __forceinline__ uint64_t readlane_u64(uint64_t v, uint32_t l) {
+  return (static_cast<uint64_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(v >> 32), l)) << 32) |
+         __builtin_amdgcn_readlane(static_cast<uint32_t>(v), l);
+}
+
 __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
 #pragma unroll
   for (uint32_t d = kWave / 2; d > 0; d >>= 1) v += __shfl_xor(v, d, kWave);
