@@ -504,14 +504,16 @@ constexpr uint32_t kDecWaves = 4;
 // Parse one block into the record table (and, when asked, the 32 B sort keys
 // of the compaction merge).  R reads block bytes (LDS image or HBM).
 template <class R>
+// base / base1: rec_base[b], rec_base[b + 1], loaded by the caller before it
+// waits for the block's bytes (one dependent round trip fewer per wave)
 __device__ __forceinline__ uint32_t decode_block(const DecArgs &a, const R &rd, uint64_t b, uint64_t off,
-                                                 uint64_t len) {
+                                                 uint64_t len, uint64_t base, uint64_t base1) {
   const uint32_t lane = lane_id();
-  const uint64_t base = uniform64(a.rec_base[b]);
+  base = uniform64(base);
   const uint64_t n = uniform64(rd.u64(len - 16));
   const uint64_t doff = uniform64(rd.u64(len - 8));
   uint32_t st = check_extra(len, n, doff);
-  if (st == kBlkOk && n != uniform64(a.rec_base[b + 1]) - base) st = kBlkCountMismatch;
+  if (st == kBlkOk && n != uniform64(base1) - base) st = kBlkCountMismatch;
   if (st != kBlkOk) return st;
   // previous record of the block (sortedness check): carried across chunks
   uint64_t c0 = 0, c1 = 0, ctx = 0, cs = 0;
@@ -604,11 +606,12 @@ __global__ __launch_bounds__(kDecWaves *kWave) void decode_kernel(DecArgs a) {
   if (len < 16) {
     st = kBlkTooSmall;
   } else if (pad + len + 16 <= kRtSlot) {
+    const uint64_t base = a.rec_base[b], base1 = a.rec_base[b + 1]; // in flight with the block's DMA
     rt_stage<1>(a.src + (off - pad), img, static_cast<uint32_t>((pad + len + 15) >> 4));
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    st = decode_block(a, LdsReader{img + pad}, b, off, len);
+    st = decode_block(a, LdsReader{img + pad}, b, off, len, base, base1);
   } else {
-    st = decode_block(a, GlobalReader{a.src + off}, b, off, len);
+    st = decode_block(a, GlobalReader{a.src + off}, b, off, len, a.rec_base[b], a.rec_base[b + 1]);
   }
   if (lane_id() == 0) {
     if (a.status) a.status[b] = st;
@@ -1274,11 +1277,30 @@ __global__ __launch_bounds__(kEncWaves *kWave) void enc_lds_kernel(EncArgs a) {
   const uint32_t lane = lane_id();
   const uint32_t wg = a.xcd ? xcd_logical_block(blockIdx.x, gridDim.x) : blockIdx.x;
   const uint64_t b = static_cast<uint64_t>(wg) * kEncWaves + wave;
-  const uint64_t nbl = a.nb_dev ? *a.nb_dev : a.nblocks; // compaction: the count on the device, nblocks its bound
-  if (b >= nbl || nbl > a.nblocks || a.over()) return;
+  if (b >= a.nblocks) return;
   uint8_t *img = lds + wave * kEncSlot;
-  const uint64_t bo = uniform64(a.out_blk_off[b]);
-  const uint64_t L64 = uniform64(a.out_blk_len[b]);
+  uint64_t bo, L64, f0_v, f1_v;
+  if constexpr (kMode == 0) {
+    // every load that depends on b only is issued before any of them is
+    // waited for (the compiler sank the record range behind the large-block
+    // branch: a dependent round trip of its own; config-2 encode leg -1.5 %)
+    const uint64_t bo_v = a.out_blk_off[b], L_v = a.out_blk_len[b];
+    f0_v = a.blk_first[b];
+    f1_v = a.blk_first[b + 1];
+    __builtin_amdgcn_sched_barrier(0); // all issued before the first use waits
+    // the all-ones test is never true for a real block (a 2^64 - 1 byte
+    // length); it keeps the four loads ahead of the branch
+    if ((bo_v & L_v & f0_v & f1_v) == ~0ull) return;
+    bo = uniform64(bo_v);
+    L64 = uniform64(L_v);
+  } else {
+    // (the same hoisting measured 2-3 % slower for the compaction encode,
+    // profiles/r03_ab/encode_prologue.md)
+    const uint64_t nbl = *a.nb_dev; // the count on the device, nblocks its bound
+    if (b >= nbl || nbl > a.nblocks || a.over()) return;
+    bo = uniform64(a.out_blk_off[b]);
+    L64 = uniform64(a.out_blk_len[b]);
+  }
   const uint32_t pad = static_cast<uint32_t>(bo & 15u);
   if (pad + L64 + 16 > kEncSlot) { // large block
     { // this wave writes it straight to HBM
@@ -1310,22 +1332,26 @@ __global__ __launch_bounds__(kEncWaves *kWave) void enc_lds_kernel(EncArgs a) {
     return;
   }
   const uint32_t L = static_cast<uint32_t>(L64);
-  const uint64_t f0 = uniform64(a.blk_first[b]);
-  const uint32_t n = static_cast<uint32_t>(uniform64(a.blk_first[b + 1]) - f0);
-  // mode 0 scans its entry offsets in the wave (P0 unused); L = D + 16 n + 16
-  const uint64_t P0 = kMode == 0 ? 0ull : uniform64(a.P[f0]);
+  if constexpr (kMode == 1) {
+    f0_v = a.blk_first[b];
+    f1_v = a.blk_first[b + 1];
+  }
+  const uint64_t f0 = uniform64(f0_v);
+  const uint32_t n = static_cast<uint32_t>(uniform64(f1_v) - f0);
+  // L = D + 16 n + 16
   const uint32_t D = L - 16u * n - 16u;
   uint8_t *im = img + pad; // image byte 0 == block byte 0
 
   if constexpr (kMode == 1) {
+    const uint64_t P0 = uniform64(a.P[f0]);
     if (!enc1_block_ok(a, bo, L64, n) || (a.guard && uniform64(a.P[f0 + n]) - P0 != D)) {
       if (lane == 0) atomicOr(a.guard, kGuardBlockRange);
       return;
     }
     if (!enc_copy_entries<4>(a, img, pad, f0, n, P0, D, b)) return;
   } else {
-    enc_copy_split<GK, GV, kQ>(a, img, s_dummy + threadIdx.x, pad, f0, n, P0, D,
-                               s_tbl + wave * kWave);
+    // mode 0 scans its entry offsets in the wave
+    enc_copy_split<GK, GV, kQ>(a, img, s_dummy + threadIdx.x, pad, f0, n, 0, D, s_tbl + wave * kWave);
   }
   if (lane == 0) {
     lds_st_u64u(im, D + 16 * n, n);
