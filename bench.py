@@ -491,7 +491,7 @@ def codec_legs(codec, dev, stream, src, off, ln, steps):
         "verified": ok}
     return {"decode": leg(dms, d_alg, "decode_kernel", f"{nb} x {BLOCK_BYTES} B blocks read + {nrec} x 33 B SoA "
                           "records written", ok_dec),
-            "encode": leg(ems, e_alg, "enc_bsum + block-length scan + enc_lds_kernel<0> (entry offsets scanned in the block wave; blocks past an LDS slot by their own wave)",
+            "encode": leg(ems, e_alg, "enc_offsets_kernel (block lengths + offsets, one kernel) + enc_lds_kernel<0> (entry offsets scanned in the block wave; blocks past an LDS slot by their own wave)",
                           f"{nb} x {BLOCK_BYTES} B blocks written + {nrec} x 116 B key/value read + "
                           f"{nrec} x 33 B SoA read", ok_enc)}
 
