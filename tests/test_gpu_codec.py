@@ -437,6 +437,37 @@ def test_encode_span_alignments_vs_oracle(codec, oracle, seed):
     assert np.array_equal(dst.cpu().numpy()[seed * 5:seed * 5 + want.size], want)
 
 
+def test_encode_many_blocks_of_many_records_vs_oracle(codec, oracle):
+    """More than one workgroup's worth of blocks (> 2048: the one-kernel block
+    offsets with the look-back over 256-block tiles) whose blocks hold ~90 tiny
+    records each (past the 32 records whose loads the offsets kernel issues up
+    front), a few blocks past the LDS slot, out_base unaligned."""
+    rng = np.random.default_rng(808)
+    n = 300_000
+    klen = rng.integers(0, 13, n).astype(np.uint32)
+    vlen = rng.integers(0, 13, n).astype(np.uint32)
+    big = rng.random(n) < 0.0005
+    vlen[big] = rng.integers(5000, 9000, int(big.sum()))
+    typ = (rng.random(n) < 0.1).astype(np.uint8)
+    vlen[typ == 1] = W.NO_VALUE
+    key_off = np.cumsum(klen.astype(np.uint64)) - klen.astype(np.uint64)
+    vb = np.where(vlen == W.NO_VALUE, 0, vlen).astype(np.uint64)
+    val_off = np.cumsum(vb) - vb
+    rec = {"type": typ, "key_len": klen, "val_len": vlen, "txn": rng.integers(0, 2 ** 63, n, dtype=np.uint64),
+           "key_off": key_off, "val_off": np.where(typ == 1, 0, val_off).astype(np.uint64),
+           "key_src": rng.integers(0, 256, int(key_off[-1] + klen[-1]) + 16, dtype=np.uint8),
+           "val_src": rng.integers(0, 256, int(val_off[-1] + vb[-1]) + 16, dtype=np.uint8)}
+    first = oracle.segment(rec, 4096)
+    assert first.size - 1 > 2048
+    want, woff, wlen = oracle.encode_blocks(rec, first, base=11)
+    dst, off, ln = codec.encode(records_table(rec), t8(rec["key_src"]), t8(rec["val_src"]), t64(first),
+                                out_base=11)
+    torch.cuda.synchronize()
+    o = cpu_u64(off)
+    assert np.array_equal(o[:-1], woff) and np.array_equal(cpu_u64(ln), wlen) and int(o[-1]) == 11 + want.size
+    assert np.array_equal(dst.cpu().numpy()[11:11 + want.size], want)
+
+
 def test_encode_empty(codec):
     """No blocks: out_blk_off[0] = out_base, nothing written."""
     rec = W.uniform_records(0)
