@@ -2151,13 +2151,14 @@ hipError_t launch_scan_entry_sizes(const uint32_t *klen, const uint32_t *vlen, u
 // tile's offset from a decoupled look-back over the tiles (ticketed,
 // epoch-tagged status words, as scan_lookback_kernel).  ws = [ticket,
 // status[tiles]].
-constexpr uint32_t kBoTile = 256, kBoPasses = kBoTile * kBsG / 256, kBoUnroll = 4;
-__global__ __launch_bounds__(256) void enc_offsets_kernel(const uint32_t *kl, const uint32_t *vl,
-                                                          const uint64_t *blk_first, uint64_t nblocks,
-                                                          uint64_t out_base, uint64_t *blk_off, uint64_t *blk_len,
-                                                          uint64_t *ws, uint32_t epoch) {
+constexpr uint32_t kBoThreads = 1024, kBoTile = 256, kBoPasses = kBoTile * kBsG / kBoThreads, kBoUnroll = 4;
+constexpr uint32_t kBoScanWaves = kBoTile / kWave;
+__global__ __launch_bounds__(kBoThreads) void enc_offsets_kernel(const uint32_t *kl, const uint32_t *vl,
+                                                                 const uint64_t *blk_first, uint64_t nblocks,
+                                                                 uint64_t out_base, uint64_t *blk_off,
+                                                                 uint64_t *blk_len, uint64_t *ws, uint32_t epoch) {
   __shared__ uint64_t s_len[kBoTile];
-  __shared__ uint64_t s_wsum[256 / kWave];
+  __shared__ uint64_t s_wsum[kBoScanWaves];
   __shared__ uint64_t s_tile, s_prefix;
   const uint32_t tid = threadIdx.x, lane = lane_id(), w = tid / kWave, g = tid % kBsG;
   if (tid == 0) {
@@ -2170,7 +2171,7 @@ __global__ __launch_bounds__(256) void enc_offsets_kernel(const uint32_t *kl, co
   uint64_t F0[kBoPasses], F1[kBoPasses];
 #pragma unroll
   for (uint32_t p = 0; p < kBoPasses; p++) {
-    const uint64_t b = b0 + p * (256 / kBsG) + tid / kBsG;
+    const uint64_t b = b0 + p * (kBoThreads / kBsG) + tid / kBsG;
     const uint64_t bc = b < nblocks ? b : 0;
     F0[p] = blk_first[bc];
     F1[p] = b < nblocks ? blk_first[bc + 1] : F0[p];
@@ -2195,17 +2196,18 @@ __global__ __launch_bounds__(256) void enc_offsets_kernel(const uint32_t *kl, co
     for (uint64_t r = F0[p] + g + kBoUnroll * kBsG; r < F1[p]; r += kBsG) sum += entry_size(kl[r], vl[r]);
 #pragma unroll
     for (uint32_t d = kBsG / 2; d > 0; d >>= 1) sum += __shfl_xor(sum, d, kWave); // inside the 8-lane group
-    const uint64_t b = b0 + p * (256 / kBsG) + tid / kBsG;
-    if (g == 0) s_len[p * (256 / kBsG) + tid / kBsG] = b < nblocks ? sum + 16 * (F1[p] - F0[p]) + 16 : 0;
+    const uint32_t lb = p * (kBoThreads / kBsG) + tid / kBsG;
+    if (g == 0) s_len[lb] = b0 + lb < nblocks ? sum + 16 * (F1[p] - F0[p]) + 16 : 0;
   }
   __syncthreads();
-  const uint64_t len = s_len[tid];
+  // the tile scan: thread tid < kBoTile holds block b0 + tid
+  const uint64_t len = tid < kBoTile ? s_len[tid] : 0;
   const uint64_t incl = wave_incl_scan_u64(len);
-  if (lane == kWave - 1) s_wsum[w] = incl;
+  if (w < kBoScanWaves && lane == kWave - 1) s_wsum[w] = incl;
   __syncthreads();
   uint64_t wbase = 0, total = 0;
 #pragma unroll
-  for (uint32_t k = 0; k < 256 / kWave; k++) {
+  for (uint32_t k = 0; k < kBoScanWaves; k++) {
     const uint64_t x = s_wsum[k];
     if (k < w) wbase += x;
     total += x;
@@ -2244,8 +2246,8 @@ __global__ __launch_bounds__(256) void enc_offsets_kernel(const uint32_t *kl, co
   }
   __syncthreads();
   const uint64_t b = b0 + tid;
-  const uint64_t off = out_base + s_prefix + wbase + incl - len;
-  if (b < nblocks) {
+  if (tid < kBoTile && b < nblocks) {
+    const uint64_t off = out_base + s_prefix + wbase + incl - len;
     blk_off[b] = off;
     blk_len[b] = len;
     if (b + 1 == nblocks) blk_off[nblocks] = off + len;
@@ -2266,7 +2268,7 @@ hipError_t launch_enc_offsets(const uint32_t *kl, const uint32_t *vl, const uint
     return scan_any<ArrIn, kArrItems>(ArrIn{blk_len}, nblocks, out_base, blk_off, ws, s, false, epoch);
   }
   // ws: enc_offsets_workspace(nblocks) words
-  enc_offsets_kernel<<<static_cast<uint32_t>((nblocks + kBoTile - 1) / kBoTile), 256, 0, s>>>(
+  enc_offsets_kernel<<<static_cast<uint32_t>((nblocks + kBoTile - 1) / kBoTile), kBoThreads, 0, s>>>(
       kl, vl, blk_first, nblocks, out_base, blk_off, blk_len, ws, epoch);
   return hipGetLastError();
 }
