@@ -1338,6 +1338,10 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     }
     const uint64_t m = arena.host[0];
     res[1] = m;
+    if (max_tables == 0) { // m >= 1 here: at least one output table (the layout below writes table 0)
+      err = "more output tables than max_tables";
+      return SSTC_E_CAPACITY;
+    }
     // 4. the table split (key+value bytes, compact.cc:290) and the block split
     // (entry + offset-entry bytes, table_builder.cc:57-59) clamped at table ends
     uint64_t *tf = pool.get<uint64_t>(m + 1), *dn = pool.get<uint64_t>(2);

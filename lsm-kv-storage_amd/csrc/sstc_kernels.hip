@@ -2275,6 +2275,7 @@ hipError_t launch_enc_offsets(const uint32_t *kl, const uint32_t *vl, const uint
 
 hipError_t launch_enc_emit(const EncArgs &a, hipStream_t s) {
   if (!a.nblocks) return hipSuccess;
+  if (a.entries_in_src && (!a.nb_dev || !a.need)) return hipErrorInvalidValue; // mode 1 reads both on the device
   const uint32_t g = grid_for(a.nblocks, kEncWaves);
   // G = 8 lanes per span, 2 span groups in flight: G = 16 and kQ = 4 / 8 were
   // slower (profiles/r02_ab/encode_ab.md)

@@ -250,9 +250,9 @@ def test_compact_max_tables_exceeded_writes_nothing(codec):
     # a 4 KiB table limit splits the ~50 KB of surviving keys + values into many tables
     prm = CompactParams(4096, 4 << 10, 1, 0)
     need = int(src.numel()) * 2
-    for max_tables, rc_want in ((3, -5), (4096, 0)):
-        toff = torch.zeros(max_tables + 1, dtype=torch.int64, device=codec.device)
-        tlen = torch.zeros(max_tables, dtype=torch.int64, device=codec.device)
+    for max_tables, rc_want in ((0, -5), (3, -5), (4096, 0)):
+        toff = torch.full((max_tables + 1,), -7, dtype=torch.int64, device=codec.device)
+        tlen = torch.full((max(max_tables, 1),), -7, dtype=torch.int64, device=codec.device)
         dst = torch.full((need,), 0xA5, dtype=torch.uint8, device=codec.device)
         res = CompactResult()
         codec._stream()
@@ -261,8 +261,10 @@ def test_compact_max_tables_exceeded_writes_nothing(codec):
                                     ctypes.byref(prm), P(dst), need, P(toff), P(tlen), max_tables, ctypes.byref(res))
         assert rc == rc_want
         if rc:
-            assert res.tables_out > max_tables
+            assert res.tables_out > max_tables or max_tables == 0
             assert (dst.cpu().numpy() == 0xA5).all(), "a writer ran although the tables exceed max_tables"
+            if max_tables == 0:  # not even the table arrays
+                assert int(toff[0]) == -7 and int(tlen[0]) == -7
         else:
             assert res.tables_out > 3
 
