@@ -218,12 +218,16 @@ __device__ __forceinline__ uint32_t kw_interleave(const KGroup &gr, uint32_t v) 
   return v;
 }
 
+// kL lanes per splitter (one per run of its group): 8, or 4 for passes whose
+// groups merge <= 4 runs (config 4's first two passes: half the waves)
+template <uint32_t kL>
 __global__ __launch_bounds__(256) void ck_kw_split_kernel(const SK *in, const SK *smp, const KGroup *groups,
                                                           uint32_t ngroups, uint32_t nids, KeyView kv, uint32_t *C,
                                                           uint64_t *G, Abort stop) {
+  static_assert(kL == 4 || kL == 8, "lanes per splitter");
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t uu = t >> 3, r = t & 7u;
-  if (uu >= nids || stop()) return; // whole 8-lane groups leave together
+  const uint32_t uu = t / kL, r = t % kL;
+  if (uu >= nids || stop()) return; // whole lane groups leave together
   const KGroup &gr = groups[find_group(groups, ngroups, uu, [](const KGroup &x) { return x.base; })];
   const uint32_t local = kw_interleave(gr, uu - gr.base), nsamp = gr.sbase[gr.nruns], S = gr.stride;
   const uint32_t u = gr.base + local;
@@ -262,9 +266,9 @@ __global__ __launch_bounds__(256) void ck_kw_split_kernel(const SK *in, const SK
   }
   uint64_t sr = (c + S - 1) / S, sc = c;
 #pragma unroll
-  for (uint32_t d = 1; d < 8; d <<= 1) {
-    sr += __shfl_xor(sr, d, 8);
-    sc += __shfl_xor(sc, d, 8);
+  for (uint32_t d = 1; d < kL; d <<= 1) {
+    sr += __shfl_xor(sr, d, kL);
+    sc += __shfl_xor(sc, d, kL);
   }
   const uint64_t row = gr.base + sr;
   C[row * kKWay + r] = static_cast<uint32_t>(c);
@@ -1232,7 +1236,7 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     // k-way merge passes; run boundaries of every pass are known on the host,
     // so all group descriptors go up in one upload (lives until the next sync)
     std::vector<KGroup> kg;
-    std::vector<uint32_t> pass_groups, pass_ids, pass_wgs;
+    std::vector<uint32_t> pass_groups, pass_ids, pass_wgs, pass_ways;
     {
       std::vector<uint64_t> cur = run_start;
       // passes: ceil(log8 runs), each pass as narrow as that allows (the
@@ -1281,6 +1285,7 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
         }
         next.push_back(cur.back());
         pass_groups.push_back(ng);
+        pass_ways.push_back(static_cast<uint32_t>(way));
         pass_ids.push_back(ids);
         pass_wgs.push_back(wgs);
         cur = std::move(next);
@@ -1304,7 +1309,12 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
         for (size_t p = 0; p < pass_groups.size(); p++) {
           const uint32_t ng = pass_groups[p];
           ck_kw_sample_kernel<<<grid(pass_ids[p]), 256, 0, s>>>(A, d_kg + at, ng, pass_ids[p], Sm, stop);
-          ck_kw_split_kernel<<<grid(static_cast<uint64_t>(pass_ids[p]) * 8), 256, 0, s>>>(A, Sm, d_kg + at, ng, pass_ids[p], kv, Cm, Gm, stop);
+          if (pass_ways[p] <= 4)
+            ck_kw_split_kernel<4><<<grid(static_cast<uint64_t>(pass_ids[p]) * 4), 256, 0, s>>>(A, Sm, d_kg + at, ng,
+                                                                                               pass_ids[p], kv, Cm, Gm, stop);
+          else
+            ck_kw_split_kernel<8><<<grid(static_cast<uint64_t>(pass_ids[p]) * 8), 256, 0, s>>>(A, Sm, d_kg + at, ng,
+                                                                                               pass_ids[p], kv, Cm, Gm, stop);
           ck_kw_bounds_kernel<<<grid(pass_ids[p]), 256, 0, s>>>(d_kg + at, ng, pass_ids[p], Gm, Jm, stop);
           if (pass_wgs[p]) {
             ck_kw_win_kernel<<<grid(pass_wgs[p]), 256, 0, s>>>(d_kg + at, ng, pass_wgs[p], Cm, Gm, Jm, Wm, stop);
