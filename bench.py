@@ -498,133 +498,292 @@ def codec_legs(codec, dev, stream, src, off, ln, steps):
 
 def read_compact_traffic(workload):
     """HBM bytes per sstc_compact call from the PMC passes of
-    tools/pmc_compact_job.sh (profiles/pmc_compact.json), or None."""
-    try:
-        with open(os.path.join(ROOT, "profiles", "pmc_compact.json")) as f:
-            d = json.load(f)
-        if d.get("workload") == workload:
-            return float(d["hbm_bytes_per_call"])
-    except (OSError, ValueError, KeyError):
-        pass
+    tools/pmc_compact_job.sh (profiles/pmc_compact*.json), or None."""
+    for name in ("pmc_compact.json", "pmc_compact_c4.json"):
+        try:
+            with open(os.path.join(ROOT, "profiles", name)) as f:
+                d = json.load(f)
+            if d.get("workload") == workload:
+                return float(d["hbm_bytes_per_call"])
+        except (OSError, ValueError, KeyError):
+            pass
     return None
 
 
-def compact_leg(codec, dev, stream, steps, cpu_ref=True):
+def _sha(b):
+    import hashlib
+    return hashlib.sha256(b).hexdigest()
+
+
+class GpuCompaction:
+    """One compaction job (db/compact.cc:232-322) on this rank's GPU: the input
+    SSTs are written by the flush-path sstc::TableBuilder into `td` (and must
+    hash to the reference TableBuilder's files, when a fixture covers them),
+    uploaded once, indexed on the device (sstc_open_tables); run() is one
+    device-resident sstc_compact call; outputs() hashes every output SST."""
+
+    def __init__(self, codec, dev, stream, td, record_sets, fixture, block_threshold=4096, table_limit=32 << 20):
+        import ctypes
+        from sstcodec._lib import CompactParams, CompactResult
+        from sstcodec.table import build_table
+        self.codec, self.dev, self.stream = codec, dev, stream
+        files, self.paths = [], []
+        self.inputs_ok = None if fixture is None else True
+        for i, rec in enumerate(record_sets):
+            p = os.path.join(td, f"in{i}.sst")
+            fs, _ = build_table(codec, p, rec, block_threshold)
+            img = np.fromfile(p, np.uint8)
+            if fixture is not None:
+                w = fixture["inputs"][i]
+                self.inputs_ok &= fs == w["file_size"] and _sha(img.tobytes()) == w["sha256"]
+            files.append(img)
+            self.paths.append((p, fs))
+        if self.inputs_ok is False:
+            raise SystemExit("compaction leg: input SSTs differ from the reference TableBuilder's")
+        self.src = torch.from_numpy(np.concatenate(files)).to(dev)
+        sizes = [f.size for f in files]
+        del files
+        idx = codec.open_tables(self.src, sizes, strict=True)
+        self.bo, self.bl, self.h_tfb = idx["blk_off"], idx["blk_len"], idx["table_first_block"]
+        self.cap = int(self.src.numel()) + (1 << 20)
+        self.dst = torch.empty(self.cap, dtype=torch.uint8, device=dev)
+        self.max_t = 1 << 12
+        self.toff = torch.zeros(self.max_t + 1, dtype=torch.int64, device=dev)
+        self.tlen = torch.zeros(self.max_t, dtype=torch.int64, device=dev)
+        self.prm = CompactParams(block_threshold, table_limit, 1, 0)
+        self.res = CompactResult()
+        self.ntables = len(sizes)
+        self.in_bytes = int(self.src.numel())
+        self._ct = ctypes
+
+    def run(self):
+        ct, P = self._ct, lambda t: self._ct.c_void_p(t.data_ptr())  # noqa: E731
+        self.codec._stream()
+        check(self.codec.lib.sstc_compact(self.codec.h, P(self.src), P(self.bo), P(self.bl), int(self.bo.numel()),
+                                          self.h_tfb.ctypes.data_as(ct.c_void_p), self.ntables,
+                                          ct.byref(self.prm), P(self.dst), self.cap, P(self.toff), P(self.tlen),
+                                          self.max_t, ct.byref(self.res)), "sstc_compact")
+
+    def sync(self):
+        torch.cuda.synchronize()
+
+    def outputs(self):
+        """[(sha256, GetFileSize())] of the last call's output SSTs, output bytes."""
+        nt = self.res.tables_out
+        o = self.toff[: nt + 1].cpu().numpy()
+        d = self.dst[: int(o[nt])].cpu().numpy()
+        return [(_sha(d[int(o[t]):int(o[t + 1])].tobytes()), int(o[t + 1] - o[t]) + 1) for t in range(nt)], int(o[nt])
+
+    def free(self):
+        del self.src, self.dst
+        torch.cuda.empty_cache()
+
+
+def time_job(job, steps, ranks=None, warmup=2):
+    """K back-to-back calls bracketed by a barrier + device sync on both sides
+    (max over ranks is taken by the caller); also the median of `steps` single
+    calls (each bracketed by syncs; the job makes host fetches inside)."""
+    for _ in range(warmup):
+        job.run()
+    job.sync()
+    singles = []
+    for _ in range(steps):
+        job.sync()
+        t0 = time.perf_counter()
+        job.run()
+        job.sync()
+        singles.append(time.perf_counter() - t0)
+    if ranks is not None:
+        ranks.barrier()
+    job.sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        job.run()
+    job.sync()
+    if ranks is not None:
+        ranks.barrier()
+    return time.perf_counter() - t0, float(np.median(singles))
+
+
+def ref_compact_baseline(paths, td, in_bytes, block_threshold=4096, table_limit=32 << 20):
+    """The reference's own MergeIterator + TableReaderIterator + TableBuilder
+    under the DoCompactJob loop (oracle/_ref/ref_compact, built from
+    /root/reference by oracle/Makefile), one pinned thread, on the same input
+    files (page-cache-hot), outputs written + fsync'd by the reference's
+    TableBuilder (table_builder.cc:147-177)."""
+    import subprocess
+    ref = os.path.join(ROOT, "oracle", "_ref", "ref_compact")
+    if not os.path.exists(ref):
+        return None
+    od = os.path.join(td, "ref_out")
+    os.makedirs(od, exist_ok=True)
+    cpu = current_cpu()
+    t0 = time.perf_counter()
+    r = subprocess.run([ref, od, str(block_threshold), str(table_limit), "1"] +
+                       [x for p, fs in paths for x in (p, str(fs))],
+                       capture_output=True, text=True, preexec_fn=lambda: os.sched_setaffinity(0, {cpu}))
+    el = time.perf_counter() - t0
+    if r.returncode != 0:
+        return None
+    return {"value": round(in_bytes / el / 2 ** 30, 3), "unit": "GiB/s", "seconds": round(el, 3), "cores": 1,
+            "kind": "reference", "pinned_cpu": cpu,
+            "sample": "the whole job once: the reference's MergeIterator + TableReaderIterator + TableBuilder under "
+                      "the DoCompactJob loop (oracle/_ref/ref_compact), input files page-cache-hot, outputs written + "
+                      "fsync'd like the reference"}
+
+
+def files_leg(codec, paths, td, fixture, in_bytes, reps=3, io_threads=8):
+    """The path north_star names end to end (SST files -> SST files):
+    sstc_compact_files over the input files -- host-side index parse, chunked
+    preads into pinned memory overlapped with H2D, the device job, D2H + one
+    pwrite + fsync per output SST (io/linux_file.cc:138-195,
+    table_builder.cc:147-177) -- fsync ON, like the reference's TableBuilder.
+    Median of `reps` runs; every output verified against the reference's hashes."""
+    od = os.path.join(td, "files_out")
+    os.makedirs(od, exist_ok=True)
+    pipe = sstcodec.FilePipe(codec, io_threads=io_threads)
+    ps, sz = [p for p, _ in paths], [fs for _, fs in paths]
+    runs = []
+    ok = True
+    for _ in range(reps + 1):
+        for f in os.listdir(od):  # fresh outputs each run (the job opens existing files without O_TRUNC)
+            os.unlink(os.path.join(od, f))
+        outs, tm = pipe.compact_files(ps, sz, od + "/", 0, fixture["block_threshold"], fixture["table_limit"], 1,
+                                      fsync=True)
+        runs.append(tm)
+        if fixture is not None:
+            got = []
+            for sid, fsize, _, _ in outs:
+                with open(os.path.join(od, f"{sid}.sst"), "rb") as f:
+                    got.append((_sha(f.read()), fsize))
+            ok &= got == [(w["sha256"], w["file_size"]) for w in fixture["outputs_base1"]]
+    pipe.close()
+    runs = runs[1:]  # the first run warms the pipe's pinned staging
+    k = int(np.argsort([r["total_s"] for r in runs])[len(runs) // 2])
+    t = runs[k]
+    return {"what": f"sstc_compact_files: {len(ps)} SST files -> {len(outs)} SST files, fsync on, {io_threads} I/O "
+                    f"threads, median of {reps}",
+            "s_median": round(t["total_s"], 4), "GiBps_in": round(in_bytes / t["total_s"] / 2 ** 30, 2),
+            "breakdown_s": {k2: round(v, 4) for k2, v in t.items() if k2 != "total_s"},
+            "verified_vs_reference": bool(ok)}
+
+
+def compact_leg(codec, dev, stream, steps, cpu_ref=True, files=True):
     """BASELINE config 3 -- the compaction hot path north_star replaces
     (db/compact.cc:232-322): 8 SSTs x 1 M records (16 B keys, 100 B values,
-    disjoint interleave) resident in HBM -> sstc_compact (decode, k-way merge,
-    keep/drop, 32 MiB table split, 4 KiB block split, encode, meta, footers) ->
-    28 output SSTs in HBM.  Inputs are written by the flush-path
-    sstc::TableBuilder and must hash to the reference TableBuilder's files;
-    every output must hash to the reference's compaction
-    (tests/golden/compaction_configs.json "config3").  Time = median of
-    `steps` calls, each bracketed by device syncs (the job makes host fetches
-    inside), plus the HIP-event span on the codec's stream.  Roofline: the job
-    must read every input byte once and write every output byte once:
-    algorithmic bytes = input + output bytes.  cpu_baseline: the reference's
-    own MergeIterator + TableReaderIterator + TableBuilder under the
-    DoCompactJob loop (oracle/_ref/ref_compact, 1 thread, files incl. fsync)
-    on the same input files, once."""
-    import ctypes
-    import hashlib
+    disjoint interleave) -> sstc_compact (decode, k-way merge, keep/drop,
+    32 MiB table split, 4 KiB block split, encode, meta, footers) -> 28 output
+    SSTs.  Inputs are written by the flush-path sstc::TableBuilder and must
+    hash to the reference TableBuilder's files; every output must hash to the
+    reference's compaction (tests/golden/compaction_configs.json "config3").
+    Device-resident time = median of `steps` calls, each bracketed by device
+    syncs.  Roofline: the job must read every input byte once and write every
+    output byte once: algorithmic bytes = input + output bytes.  `files`: the
+    same job file -> file (sstc_compact_files, fsync on) beside the
+    reference's own loop on the same files (cpu_baseline, like for like)."""
     import shutil
-    import subprocess
     import tempfile
-    from sstcodec._lib import CompactParams, CompactResult
-    from sstcodec.table import build_table
     fx = json.load(open(os.path.join(ROOT, "tests", "golden", "compaction_configs.json")))["config3"]
     td = tempfile.mkdtemp(prefix="sstc_bench_c3_", dir=os.environ.get("TMPDIR", "/tmp"))
     try:
-        files, paths = [], []
-        inputs_ok = True
-        for i, rec in enumerate(W.config_inputs(3)):
-            p = os.path.join(td, f"in{i}.sst")
-            fs, _ = build_table(codec, p, rec, 4096)
-            img = np.fromfile(p, np.uint8)
-            inputs_ok &= (fs == fx["inputs"][i]["file_size"] and
-                          hashlib.sha256(img.tobytes()).hexdigest() == fx["inputs"][i]["sha256"])
-            files.append(img)
-            paths.append((p, fs))
-        if not inputs_ok:
-            raise SystemExit("compact leg: input SSTs differ from the reference TableBuilder's")
-        src = torch.from_numpy(np.concatenate(files)).to(dev)
-        sizes = [f.size for f in files]
-        del files
-        idx = codec.open_tables(src, sizes, strict=True)
-        bo, bl, h_tfb = idx["blk_off"], idx["blk_len"], idx["table_first_block"]
-        cap = int(src.numel()) + (1 << 20)
-        dst = torch.empty(cap, dtype=torch.uint8, device=dev)
-        max_t = 1 << 12
-        toff = torch.zeros(max_t + 1, dtype=torch.int64, device=dev)
-        tlen = torch.zeros(max_t, dtype=torch.int64, device=dev)
-        prm = CompactParams(4096, 32 << 20, 1, 0)
-        res = CompactResult()
-        P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
-
-        def run():
-            codec._stream()
-            check(codec.lib.sstc_compact(codec.h, P(src), P(bo), P(bl), int(bo.numel()),
-                                         h_tfb.ctypes.data_as(ctypes.c_void_p), len(sizes), ctypes.byref(prm),
-                                         P(dst), cap, P(toff), P(tlen), max_t, ctypes.byref(res)), "sstc_compact")
-
-        for _ in range(2):
-            run()
+        job = GpuCompaction(codec, dev, stream, td, W.config_inputs(3), fx)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        _, t = time_job(job, steps)
+        e0.record(stream)
+        job.run()
+        e1.record(stream)
         torch.cuda.synchronize()
-        walls, evs = [], []
-        for _ in range(steps):
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            e0.record(stream)
-            run()
-            e1.record(stream)
-            torch.cuda.synchronize()
-            walls.append(time.perf_counter() - t0)
-            evs.append(e0.elapsed_time(e1) * 1e-3)
-        nt = res.tables_out
-        o = toff[: nt + 1].cpu().numpy()
-        d = dst[: int(o[nt])].cpu().numpy()
-        got = [(hashlib.sha256(d[int(o[t]):int(o[t + 1])].tobytes()).hexdigest(), int(o[t + 1] - o[t]) + 1)
-               for t in range(nt)]
+        got, out_bytes = job.outputs()
         ok = got == [(w["sha256"], w["file_size"]) for w in fx["outputs_base1"]]
-        in_bytes, out_bytes = int(src.numel()), int(o[nt])
-        del src, dst, d
-        torch.cuda.empty_cache()
-        t = float(np.median(walls))
+        in_bytes, res = job.in_bytes, job.res
+        paths = job.paths
+        job.free()
         alg = in_bytes + out_bytes
-        traffic = read_compact_traffic("config3")
         leg = {"workload": "config3: 8 SSTs x 1 M records (16 B keys, 100 B values) -> 28 SSTs, sstc_compact, "
                            "device-resident", "steps": steps, "ms_median": round(t * 1e3, 4),
-               "ms_events_median": round(float(np.median(evs)) * 1e3, 4),
+               "ms_events_one_call": round(e0.elapsed_time(e1), 4),
                "GiBps_in": round(in_bytes / t / 2 ** 30, 1), "records_in": res.records_in,
-               "records_kept": res.records_kept, "tables_out": nt, "input_bytes": in_bytes, "output_bytes": out_bytes,
-               "verified_vs_reference": ok, "inputs_equal_reference": inputs_ok,
+               "records_kept": res.records_kept, "tables_out": res.tables_out, "input_bytes": in_bytes,
+               "output_bytes": out_bytes, "verified_vs_reference": ok, "inputs_equal_reference": job.inputs_ok,
                "roofline": {"bound": "hbm", "achieved": round(alg / t / 1e9, 1), "peak": HBM_PEAK_GBPS,
                             "unit": "GB/s", "frac": round(alg / t / 1e9 / HBM_PEAK_GBPS, 4),
-                            "traffic": traffic, "alg_bytes_per_call": alg,
+                            "traffic": read_compact_traffic("config3"), "alg_bytes_per_call": alg,
                             "alg": "input bytes read once + output bytes written once (a copy's traffic)",
                             "kernel": "sstc_compact (whole job, ~30 kernels; wall time incl. its host syncs)"}}
         if not ok:
             raise SystemExit("compact leg: outputs differ from the reference's compaction: timing invalid")
-        ref = os.path.join(ROOT, "oracle", "_ref", "ref_compact")
-        if cpu_ref and os.path.exists(ref):
-            od = os.path.join(td, "ref_out")
-            os.makedirs(od)
-            cpu = current_cpu()
-            t0 = time.perf_counter()
-            r = subprocess.run([ref, od, "4096", str(32 << 20), "1"] + [x for p, fs in paths for x in (p, str(fs))],
-                               capture_output=True, text=True, preexec_fn=lambda: os.sched_setaffinity(0, {cpu}))
-            el = time.perf_counter() - t0
-            if r.returncode == 0:
-                leg["cpu_baseline"] = {
-                    "value": round(in_bytes / el / 2 ** 30, 3), "unit": "GiB/s", "seconds": round(el, 3),
-                    "cores": 1, "kind": "reference", "pinned_cpu": cpu,
-                    "sample": "the whole config-3 job once: the reference's MergeIterator + TableReaderIterator "
-                              "+ TableBuilder under the DoCompactJob loop (oracle/_ref/ref_compact), input files "
-                              "page-cache-hot, outputs written + fsync'd like the reference"}
+        if files:
+            leg["files"] = files_leg(codec, paths, td, fx, in_bytes)
+        if cpu_ref:
+            base = ref_compact_baseline(paths, td, in_bytes)
+            if base:
+                base["compare_with"] = "legs.compact.files (file -> file, fsync on): the like-for-like GPU number"
+                leg["cpu_baseline"] = base
         return leg
     finally:
         shutil.rmtree(td, ignore_errors=True)
+
+
+class HostPlumbing:
+    """--plumbing stand-in for GpuCompaction (no GPU): the same shard, rank
+    and aggregation path, with a host merge of the shard's key indices as the
+    "job".  Not a measurement."""
+
+    def __init__(self, record_sets):
+        self.keys = [np.asarray(r["key_src"]).reshape(-1, 16) for r in record_sets]
+        self.in_bytes = sum(int(np.asarray(r["key_src"]).size + np.asarray(r["val_src"]).size)
+                            for r in record_sets)
+        self.inputs_ok = None
+        self.out = None
+
+    def run(self):
+        allk = np.concatenate(self.keys)
+        self.out = allk[np.lexsort(allk.T[::-1])]
+
+    def sync(self):
+        pass
+
+    def outputs(self):
+        return [(_sha(self.out.tobytes()), self.out.size)], self.in_bytes
+
+    def key_range(self):
+        return int(bytes(self.out[0]).decode()[1:]), int(bytes(self.out[-1]).decode()[1:])
+
+    def free(self):
+        pass
+
+
+def config4_leg(ranks, make_job, steps, fixture_of):
+    """BASELINE config 4 at N GPUs: 1024 input SSTs sharded 128 per GPU
+    (SURVEY.md §8(e)), rank r compacting its own key-range-disjoint shard
+    (workload.config_inputs(4, r)) with its own job -- exactly 8 independent
+    DoCompactJob runs (db/compact.cc:232-322), no data-path collective.  Each
+    rank verifies its outputs against the reference's
+    (compaction_configs.json "config4_rank{r}"); value = all ranks' input
+    bytes x K / max-over-ranks wall time of K back-to-back calls (barrier +
+    device sync on both sides)."""
+    job, fixture = make_job(ranks.rank), fixture_of(ranks.rank)
+    wall, single = time_job(job, steps, ranks)
+    got, out_bytes = job.outputs()
+    ok = None if fixture is None else got == [(w["sha256"], w["file_size"]) for w in fixture["outputs_base1"]]
+    lo, hi = job.key_range() if hasattr(job, "key_range") else (-1, -1)
+    in_bytes = job.in_bytes
+    job.free()
+    per = ranks.gather([wall, single, in_bytes, out_bytes, -1 if ok is None else int(ok), lo, hi])
+    wall_max = max(p[0] for p in per)
+    total_in = sum(p[2] for p in per)
+    rows = []
+    for r, (w, s1, ib, ob, okr, klo, khi) in enumerate(per):
+        frac = (ib + ob) / s1 / 1e9 / HBM_PEAK_GBPS
+        rows.append({"rank": r, "GiBps": round(ib * steps / w / 2 ** 30, 2), "ms_per_call": round(w / steps * 1e3, 4),
+                     "ms_single_median": round(s1 * 1e3, 4), "input_bytes": int(ib), "output_bytes": int(ob),
+                     "roofline_frac": round(frac, 4), "verified_vs_reference": None if okr < 0 else bool(okr),
+                     "key_index_range": [int(klo), int(khi)] if klo >= 0 else None})
+    return {"workload": "config4: 1024 SSTs x 100 k records sharded 128 per GPU, one sstc_compact job per rank "
+                        "(device-resident, key-range-disjoint shards)",
+            "n_gpus": ranks.world, "steps": steps, "GiBps_aggregate": round(total_in * steps / wall_max / 2 ** 30, 2),
+            "ms_per_call_max": round(wall_max / steps * 1e3, 4), "scaling": "weak", "per_rank": rows,
+            "roofline_note": "per rank: (input + output bytes) / median single-call time / 8 TB/s"}
 
 
 def main():
@@ -640,6 +799,10 @@ def main():
     ap.add_argument("--no-legs", action="store_true", help="skip the decode-only / encode-only legs")
     ap.add_argument("--no-compact", action="store_true", help="skip the config-3 compaction leg")
     ap.add_argument("--compact-steps", type=int, default=10)
+    ap.add_argument("--no-files-leg", action="store_true", help="skip the config-3 file -> file compaction leg")
+    ap.add_argument("--no-compact4", action="store_true", help="skip the config-4 (128 SSTs per GPU) leg")
+    ap.add_argument("--c4-steps", type=int, default=5)
+    ap.add_argument("--c4-keys", type=int, default=100_000, help="records per SST of the config-4 leg")
     ap.add_argument("--plumbing", action="store_true",
                     help="CPU-only launcher check (gloo, host copy as the step): NOT a measurement")
     args = ap.parse_args()
@@ -684,6 +847,7 @@ def main():
     ms_step = wall_max / args.steps * 1e3
     traffic = read_traffic(nb)
 
+    out = None
     if rank == 0:
         out = {
             "metric": METRIC,
@@ -722,7 +886,7 @@ def main():
                 out["legs"] = codec_legs(codec, dev, stream, src, off, ln, max(10, args.steps // 2))
             if not args.no_compact:
                 out.setdefault("legs", {})["compact"] = compact_leg(codec, dev, stream, args.compact_steps,
-                                                                     not args.no_cpu_baseline)
+                                                                     not args.no_cpu_baseline, not args.no_files_leg)
             if not args.no_hbm_variant:
                 out["roofline"]["hbm_1gib"] = hbm_variant(codec, dev, 4 * nb)
             if not args.no_e2e:
@@ -737,8 +901,38 @@ def main():
                 all_cores = cpu_baseline_threads(s, o, l_, nproc(), min(5.0, args.cpu_seconds))
                 if all_cores:
                     out["cpu_baseline_all"] = all_cores
+    if not args.no_compact4:
+        # every rank: its own 128-SST shard of config 4 (collective call: all ranks run it)
+        c4 = compact4(args, ranks, codec, dev, stream)
+        if rank == 0:
+            out.setdefault("legs", {})["compact_config4"] = c4
+    if rank == 0:
         print(json.dumps(out), flush=True)
     ranks.close()
+
+
+def _c4_fixture(rank, keys):
+    if keys != 100_000:
+        return None
+    fx = json.load(open(os.path.join(ROOT, "tests", "golden", "compaction_configs.json")))
+    return fx.get(f"config4_rank{rank}")
+
+
+def compact4(args, ranks, codec, dev, stream):
+    import shutil
+    import tempfile
+    td = tempfile.mkdtemp(prefix=f"sstc_bench_c4_r{ranks.rank}_", dir=os.environ.get("TMPDIR", "/tmp"))
+    try:
+        make = lambda r: GpuCompaction(codec, dev, stream, td, W.config_inputs(4, r, keys=args.c4_keys),  # noqa: E731
+                                       _c4_fixture(r, args.c4_keys))
+        leg = config4_leg(ranks, make, args.c4_steps, lambda r: _c4_fixture(r, args.c4_keys))
+    finally:
+        shutil.rmtree(td, ignore_errors=True)
+    bad = [p["rank"] for p in leg["per_rank"] if p["verified_vs_reference"] is False]
+    if bad:
+        raise SystemExit(f"config-4 leg: ranks {bad} produced outputs that differ from the reference's")
+    leg["traffic_rank0"] = read_compact_traffic("config4")
+    return leg
 
 
 def plumbing(args, ranks):
@@ -756,8 +950,13 @@ def plumbing(args, ranks):
     wall = time.perf_counter() - t0
     per_rank = ranks.gather([wall, float(b[0])])
     wall_max = max(w for w, _ in per_rank)
+    c4 = None
+    if not args.no_compact4:  # the config-4 shard / rank / aggregation path with a host merge as the job
+        keys = min(args.c4_keys, 64)
+        c4 = config4_leg(ranks, lambda r: HostPlumbing(W.config_inputs(4, r, keys=keys)), 2, lambda r: None)
+        c4["data"] = f"plumbing: 128 SSTs x {keys} records per rank, host merge of the key indices: not a measurement"
     if ranks.rank == 0:
-        print(json.dumps({"metric": METRIC, "value": round(nb * BLOCK_BYTES * ranks.world * args.steps / wall_max
+        print(json.dumps({"metric": METRIC, "compact_config4": c4, "value": round(nb * BLOCK_BYTES * ranks.world * args.steps / wall_max
                                                           / 2 ** 30, 3),
                           "unit": "GiB/s", "n_gpus": ranks.world, "steps": args.steps, "warmup": args.warmup,
                           "scaling": "weak", "data": "plumbing check (host copy, gloo): not a measurement",

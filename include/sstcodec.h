@@ -56,7 +56,8 @@ extern "C" {
 #define SSTC_E_NOMEM -3
 #define SSTC_E_NO_DEVICE -4
 #define SSTC_E_CAPACITY -5 /* workspace too small: call sstc_ctx_reserve */
-#define SSTC_E_INTERNAL -6 /* a device-side consistency check of a job failed: nothing was written */
+#define SSTC_E_INTERNAL -6 /* a device-side consistency check of a job failed: no out-of-range access was made,
+                              but d_dst and the output table arrays are undefined (partly written) */
 
 /* per-block status, d_block_status[b] */
 #define SSTC_BLK_OK 0
@@ -344,8 +345,9 @@ int sstc_pipe_destroy(sstc_pipe *pipe);
 /* Compact the SST files in_paths[0..n_in) (iterator order, each with its
  * GetFileSize() value in in_file_sizes = bytes + 1) into out_prefix + id +
  * ".sst", ids first_sst_id, first_sst_id + 1, ... (Compact::DoCompactJob's
- * GetNextSSTId() sequence).  Output files are created or truncated; fsync when
- * do_fsync (TableBuilder::Finish does).  Per output: id, GetFileSize() and the
+ * GetNextSSTId() sequence).  Output files are created, or -- when the path
+ * exists -- opened without truncation as io/linux_file.cc:99-119 does (a longer
+ * stale file keeps its tail); fsync when do_fsync (TableBuilder::Finish does).  Per output: id, GetFileSize() and the
  * smallest / largest key copied into key_arena (what VersionEdit::AddNewFiles
  * records).  timing may be NULL. */
 int sstc_compact_files(sstc_pipe *pipe, const char *const *in_paths, const uint64_t *in_file_sizes,

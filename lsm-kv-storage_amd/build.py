@@ -23,6 +23,7 @@ ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "lib")
 ARCH = os.environ.get("SSTC_OFFLOAD_ARCH", "gfx950")
+REFERENCE = os.environ.get("SSTC_REFERENCE", "/root/reference")  # headers for the drop-in test TU only
 
 HIP_SOURCES = ["sstc_kernels.hip", "sstc_compact.hip", "sstc_get.hip", "sstc_api.hip"]
 HOST_SOURCES = ["host/sst_table.cpp", "host/compact_files.cpp"]
@@ -136,6 +137,23 @@ def build(verbose=False):
     if os.path.exists(tu) and _newer(exe, [tu, so, os.path.join(ROOT, "include", "sstc_table.h")]):
         cmd = [os.environ.get("CXX", "g++"), "-O2", "-std=c++17", "-Wall", "-I" + os.path.join(ROOT, "include"), tu,
                "-o", exe, "-L" + LIB, "-lsstcodec", "-Wl,-rpath,$ORIGIN"]
+        if verbose:
+            print(" ".join(cmd))
+        subprocess.run(cmd, check=True)
+    # the re-entrancy test library (tests/cpp/flush_threads.cc): the engine's
+    # concurrent flushes through kvs::sstable::TableBuilder of the drop-in
+    # header, which includes two of the reference's own headers (common/macros.h,
+    # db/status.h) -- built where the reference is present, shipped prebuilt
+    tu = os.path.join(ROOT, "tests", "cpp", "flush_threads.cc")
+    tso = os.path.join(LIB, "libsstc_threads.so")
+    dropin = os.path.join(ROOT, "include", "dropin", "sstable", "table_builder.h")
+    if os.path.exists(tu) and os.path.exists(os.path.join(REFERENCE, "db", "status.h")) and \
+            _newer(tso, [tu, so, dropin, os.path.join(ROOT, "include", "sstc_table.h")]):
+        rocm = os.path.dirname(os.path.dirname(os.path.realpath(hipcc)))
+        cmd = [os.environ.get("CXX", "g++"), "-O2", "-std=c++20", "-fPIC", "-shared", "-Wall",
+               "-D__HIP_PLATFORM_AMD__", "-I" + os.path.join(ROOT, "include", "dropin"),
+               "-I" + os.path.join(ROOT, "include"), "-I" + REFERENCE, "-I" + os.path.join(rocm, "include"), tu,
+               "-o", tso, "-L" + LIB, "-lsstcodec", "-Wl,-rpath,$ORIGIN", "-lpthread"]
         if verbose:
             print(" ".join(cmd))
         subprocess.run(cmd, check=True)

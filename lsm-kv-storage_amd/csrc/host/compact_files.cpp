@@ -379,7 +379,13 @@ int sstc_compact_files(sstc_pipe *pipe, const char *const *in_paths, const uint6
         const uint8_t *img = pipe->h_out + toff[t];
         const uint64_t bytes = toff[t + 1] - toff[t];
         const std::string path = prefix + std::to_string(first_sst_id + t) + ".sst";
-        const int fd = ::open(path.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
+        // io/linux_file.cc:99-119 (LinuxWriteOnlyFile::Open): an output path
+        // that already exists is opened WITHOUT O_TRUNC, so a longer stale
+        // file keeps its tail past the new table's bytes, as the reference's
+        // compaction leaves it (GetFileSize and the table image are unchanged)
+        ::chmod(path.c_str(), 0644);
+        const bool create = ::access(path.c_str(), F_OK) != 0;
+        const int fd = ::open(path.c_str(), create ? (O_WRONLY | O_CREAT | O_TRUNC) : O_WRONLY, 0644);
         if (fd < 0 || !pwrite_full(fd, img, bytes, 0) || (do_fsync && ::fsync(fd) < 0)) werr = 2;
         if (fd >= 0) ::close(fd);
         table_keys(img, bytes, lo[t], hi[t]);

@@ -78,10 +78,35 @@ struct DevBuf {
   template <class T> T *as() const { return static_cast<T *>(p); }
 };
 
-template <class T> DevBuf upload(const std::vector<T> &v) {
+} // namespace
+} // namespace sstc
+
+extern "C" int sstc__ctx_device(const sstc_ctx *ctx); // sstc_api.hip: the device a context is bound to
+extern "C" void *sstc__ctx_stream(const sstc_ctx *ctx); // sstc_api.hip: the stream a context runs on
+
+namespace sstc {
+namespace {
+
+// Every copy runs on the context's own stream, in order with its kernels: a
+// null-stream hipMemcpy would not be ordered after work on a non-blocking
+// stream, and on a blocking one it would serialise every thread's builder
+// (concurrent flushes, db_impl.cc:354-362, each own a context and a stream).
+hipStream_t stream_of(sstc_ctx *ctx) { return static_cast<hipStream_t>(sstc__ctx_stream(ctx)); }
+
+void h2d(sstc_ctx *ctx, void *d, const void *h, size_t n) {
+  if (n && hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, stream_of(ctx)) != hipSuccess)
+    throw std::runtime_error("hipMemcpyAsync H2D failed");
+}
+
+bool d2h(sstc_ctx *ctx, void *h, const void *d, size_t n) {
+  return !n || hipMemcpyAsync(h, d, n, hipMemcpyDeviceToHost, stream_of(ctx)) == hipSuccess;
+}
+
+bool sync(sstc_ctx *ctx) { return hipStreamSynchronize(stream_of(ctx)) == hipSuccess; }
+
+template <class T> DevBuf upload(sstc_ctx *ctx, const std::vector<T> &v) {
   DevBuf d(v.size() * sizeof(T));
-  if (!v.empty() && hipMemcpy(d.p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice) != hipSuccess)
-    throw std::runtime_error("hipMemcpy H2D failed");
+  h2d(ctx, d.p, v.data(), v.size() * sizeof(T));
   return d;
 }
 
@@ -180,8 +205,6 @@ void TableBuilder::FlushBlock() {
   block_size_ = 0;
 }
 
-extern "C" int sstc__ctx_device(const sstc_ctx *ctx); // sstc_api.hip: the device a context is bound to
-
 namespace {
 // per-host-thread, per-device staging reused across Finish() calls (flush /
 // compaction threads each build many SSTs): one pinned host buffer and one
@@ -273,7 +296,7 @@ void TableBuilder::Finish() {
     std::memcpy(h + o_keys, keys_.data(), keys_.size());
     std::memcpy(h + o_vals, vals_.data(), vals_.size());
     uint8_t *d = stage.Dev(dev_bytes);
-    if (hipMemcpy(d, h, in_bytes, hipMemcpyHostToDevice) != hipSuccess) throw std::runtime_error("hipMemcpy H2D failed");
+    h2d(ctx_, d, h, in_bytes); // pinned: a true async copy, ordered before the encode
     sstc_records rec{d + o_type, reinterpret_cast<uint32_t *>(d + o_kl), reinterpret_cast<uint32_t *>(d + o_vl),
                      reinterpret_cast<uint64_t *>(d + o_txn), reinterpret_cast<uint64_t *>(d + o_ko),
                      reinterpret_cast<uint64_t *>(d + o_vo)};
@@ -283,10 +306,9 @@ void TableBuilder::Finish() {
     uint64_t errs = 0;
     check(sstc_ctx_error_count(ctx_, &errs), "sstc_ctx_error_count"); // synchronises the stream
     // blocks straight into the file image, the block index beside it
-    if (hipMemcpy(h, d + o_dst, data_bytes, hipMemcpyDeviceToHost) != hipSuccess ||
-        hipMemcpy(blk_off.data(), d + o_off, (nb + 1) * 8, hipMemcpyDeviceToHost) != hipSuccess ||
-        hipMemcpy(blk_len.data(), d + o_len, nb * 8, hipMemcpyDeviceToHost) != hipSuccess)
-      throw std::runtime_error("hipMemcpy D2H failed");
+    if (!d2h(ctx_, h, d + o_dst, data_bytes) || !d2h(ctx_, blk_off.data(), d + o_off, (nb + 1) * 8) ||
+        !d2h(ctx_, blk_len.data(), d + o_len, nb * 8) || !sync(ctx_))
+      throw std::runtime_error("hipMemcpyAsync D2H failed");
   }
   // meta section: one entry per block (table_builder.cc:101-145), then the
   // footer (table_builder.cc:179-211), appended to the file image in place
@@ -364,7 +386,7 @@ int decode_host(sstc_ctx *ctx, std::vector<uint8_t> &data, const std::vector<uin
                 const std::vector<uint64_t> &len, uint32_t txn_mode, HostRecords &out) {
   const uint64_t nb = off.size();
   if (data.empty()) data.push_back(0);
-  DevBuf d_src = upload(data), d_off = upload(off), d_len = upload(len), d_base((nb + 1) * 8),
+  DevBuf d_src = upload(ctx, data), d_off = upload(ctx, off), d_len = upload(ctx, len), d_base((nb + 1) * 8),
          d_status(nb * 4 + 4);
   check(sstc_count_records(ctx, d_src.as<uint8_t>(), d_off.as<uint64_t>(), d_len.as<uint64_t>(), nb,
                            d_base.as<uint64_t>()),
@@ -372,7 +394,7 @@ int decode_host(sstc_ctx *ctx, std::vector<uint8_t> &data, const std::vector<uin
   uint64_t errs = 0;
   check(sstc_ctx_error_count(ctx, &errs), "sync");
   out.base.resize(nb + 1);
-  if (hipMemcpy(out.base.data(), d_base.p, (nb + 1) * 8, hipMemcpyDeviceToHost) != hipSuccess) return SSTC_E_HIP;
+  if (!d2h(ctx, out.base.data(), d_base.p, (nb + 1) * 8) || !sync(ctx)) return SSTC_E_HIP;
   const uint64_t n = out.base[nb];
   DevBuf d_type(n + 1), d_kl(4 * n + 4), d_vl(4 * n + 4), d_txn(8 * n + 8), d_ko(8 * n + 8), d_vo(8 * n + 8);
   sstc_records rec{d_type.as<uint8_t>(), d_kl.as<uint32_t>(), d_vl.as<uint32_t>(),
@@ -388,20 +410,20 @@ int decode_host(sstc_ctx *ctx, std::vector<uint8_t> &data, const std::vector<uin
   out.txn.resize(n);
   out.ko.resize(n);
   out.vo.resize(n);
-  bool ok = hipMemcpy(out.status.data(), d_status.p, nb * 4, hipMemcpyDeviceToHost) == hipSuccess;
-  ok = ok && hipMemcpy(out.type.data(), d_type.p, n, hipMemcpyDeviceToHost) == hipSuccess;
-  ok = ok && hipMemcpy(out.kl.data(), d_kl.p, 4 * n, hipMemcpyDeviceToHost) == hipSuccess;
-  ok = ok && hipMemcpy(out.vl.data(), d_vl.p, 4 * n, hipMemcpyDeviceToHost) == hipSuccess;
-  ok = ok && hipMemcpy(out.txn.data(), d_txn.p, 8 * n, hipMemcpyDeviceToHost) == hipSuccess;
-  ok = ok && hipMemcpy(out.ko.data(), d_ko.p, 8 * n, hipMemcpyDeviceToHost) == hipSuccess;
-  ok = ok && hipMemcpy(out.vo.data(), d_vo.p, 8 * n, hipMemcpyDeviceToHost) == hipSuccess;
+  bool ok = d2h(ctx, out.status.data(), d_status.p, nb * 4) && d2h(ctx, out.type.data(), d_type.p, n) &&
+            d2h(ctx, out.kl.data(), d_kl.p, 4 * n) && d2h(ctx, out.vl.data(), d_vl.p, 4 * n) &&
+            d2h(ctx, out.txn.data(), d_txn.p, 8 * n) && d2h(ctx, out.ko.data(), d_ko.p, 8 * n) &&
+            d2h(ctx, out.vo.data(), d_vo.p, 8 * n);
+  ok = sync(ctx) && ok;
   return ok ? SSTC_OK : SSTC_E_HIP;
 }
 
-struct CtxHolder { // one context per host thread, destroyed at thread exit
+struct CtxHolder { // one context + one non-blocking stream per host thread, destroyed at thread exit
   sstc_ctx *ctx = nullptr;
+  hipStream_t stream = nullptr;
   ~CtxHolder() {
-    if (ctx) sstc_ctx_destroy(ctx);
+    if (ctx) sstc_ctx_destroy(ctx); // synchronises the stream
+    if (stream) (void)hipStreamDestroy(stream);
   }
 };
 } // namespace
@@ -411,7 +433,11 @@ sstc_ctx *ThreadContext() {
   if (!h.ctx) {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) dev = 0;
-    check(sstc_ctx_create(dev, nullptr, &h.ctx), "sstc_ctx_create");
+    // its own stream: concurrent builders on pool threads overlap on the GPU
+    // instead of queueing on the null stream
+    if (hipStreamCreateWithFlags(&h.stream, hipStreamNonBlocking) != hipSuccess)
+      throw std::runtime_error("hipStreamCreateWithFlags failed");
+    check(sstc_ctx_create(dev, h.stream, &h.ctx), "sstc_ctx_create");
   }
   return h.ctx;
 }

@@ -113,7 +113,12 @@ int next_epoch(sstc_ctx *c, uint32_t &epoch) {
   return SSTC_OK;
 }
 
-int ensure_blocks(sstc_ctx *c, uint64_t nb) { return ensure_scan(c, nb + 1); }
+// every per-block scan a call may run: the u64 block scans and the encode's
+// one-kernel block offsets (a tile per 256 blocks, finer than the scans'), so
+// that no call after sstc_ctx_reserve grows the workspace
+int ensure_blocks(sstc_ctx *c, uint64_t nb) {
+  return ensure_scan_words(c, std::max(sstc::scan_workspace_elems(nb + 1), sstc::enc_offsets_workspace(nb)));
+}
 
 int ensure_records(sstc_ctx *c, uint64_t nr) {
   if (int r = grow(c, c->P, c->cap_records, nr + 1, "record workspace")) return r;
@@ -135,6 +140,7 @@ uint32_t sstc_version(void) { return SSTC_ABI_VERSION; }
 // through sstc_last_error_string
 int sstc__fail(int code, const char *what) { return fail(code, what); }
 int sstc__ctx_device(const sstc_ctx *c) { return c ? c->device : -1; }
+void *sstc__ctx_stream(const sstc_ctx *c) { return c ? static_cast<void *>(c->stream) : nullptr; }
 
 // test hook (not in the public header): the context's scan epoch, to run scans
 // across the 14-bit wrap of next_epoch without 16 k calls first
@@ -321,9 +327,7 @@ int sstc_encode_blocks(sstc_ctx *c, const uint8_t *d_key_src, const uint8_t *d_v
   if (int r = bind_device(c)) return r;
   if (nblocks >= 0xFFFFFFFFull) return fail(SSTC_E_INVALID_ARG, "too many blocks for one call");
   if (int r = ensure_records(c, nrec)) return r;
-  if (int r = ensure_scan_words(c, std::max(sstc::scan_workspace_elems(nblocks + 1),
-                                             sstc::enc_offsets_workspace(nblocks))))
-    return r; // the block-offset scan's workspace
+  if (int r = ensure_blocks(c, nblocks)) return r; // the block-offset scan's workspace
   // block lengths (entry sizes summed per block), their scan = block offsets,
   // P (entry-size prefix) per block, then the block images
   uint32_t ep = 0;

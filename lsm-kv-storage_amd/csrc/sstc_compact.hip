@@ -555,8 +555,14 @@ constexpr uint32_t kFfRows = 8, kFfTile = kFtThreads * kFfRows;
 __device__ __forceinline__ bool ff_same_key(const SK &a, const SK &b, const KeyView &kv) {
   return key_cmp(a.p0, a.p1, a.kl, a.id, b.p0, b.p1, b.kl, b.id, kv) == 0;
 }
+// a record read back by the gallop / binary search carries an unchecked
+// merged id: one out of range (a broken merge, rejected by the guard) is
+// taken as "not the same key", so no key compare indexes past the inputs
+__device__ __forceinline__ bool ff_same_key_at(const SK &a, const SK &b, const KeyView &kv, uint64_t n) {
+  return a.id < n && ff_same_key(a, b, kv);
+}
 __device__ __forceinline__ uint32_t ff_keep(const SK *s, uint64_t i, const SK &x, const SK &pv, uint32_t ty,
-                                            uint32_t base_level, const KeyView &kv) {
+                                            uint32_t base_level, const KeyView &kv, uint64_t n) {
   if (i == 0) return 1;
   if (!ff_same_key(pv, x, kv)) return ty == kTypePut ? 1u : (base_level ? 0u : 1u);
   if (x.tx != pv.tx) return 0;
@@ -567,7 +573,7 @@ __device__ __forceinline__ uint32_t ff_keep(const SK *s, uint64_t i, const SK &x
   for (uint64_t step = 1;; step <<= 1) {
     if (hi == 0) break;
     const uint64_t p = hi > step ? hi - step : 0;
-    if (ff_same_key(s[p], x, kv)) {
+    if (ff_same_key_at(s[p], x, kv, n)) {
       hi = p;
     } else {
       lo = static_cast<int64_t>(p);
@@ -576,7 +582,7 @@ __device__ __forceinline__ uint32_t ff_keep(const SK *s, uint64_t i, const SK &x
   }
   while (lo + 1 < static_cast<int64_t>(hi)) {
     const uint64_t mid = static_cast<uint64_t>((lo + static_cast<int64_t>(hi)) >> 1);
-    if (ff_same_key(s[mid], x, kv)) hi = mid;
+    if (ff_same_key_at(s[mid], x, kv, n)) hi = mid;
     else lo = static_cast<int64_t>(mid);
   }
   return s[hi].tx == x.tx ? 1u : 0u;
@@ -626,7 +632,7 @@ __global__ __launch_bounds__(kFtThreads) void ck_filter_kernel(const SK *s, uint
     for (uint32_t g = 0; g < kGroup; g++) {
       const uint32_t j = j0 + g;
       const uint64_t i = t0 + static_cast<uint64_t>(j) * kFtThreads + tid;
-      const uint32_t k = i < n ? ff_keep(s, i, x[g], pv[g], rr[g].type, base_level, kv) : 0u;
+      const uint32_t k = i < n ? ff_keep(s, i, x[g], pv[g], rr[g].type, base_level, kv, n) : 0u;
       km |= k << j;
       kl[j] = x[g].kl;
       tx[j] = x[g].tx;
@@ -1413,7 +1419,7 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
         char b[24];
         snprintf(b, sizeof b, "%llx", static_cast<unsigned long long>(v));
         return std::string(b);
-      }(arena.host[1]) + "): the output is incomplete";
+      }(arena.host[1]) + "): d_dst and the table arrays are undefined";
       return SSTC_E_INTERNAL;
     }
     if (res[4] > dst_cap) {

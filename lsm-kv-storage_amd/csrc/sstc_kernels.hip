@@ -2181,10 +2181,16 @@ __global__ __launch_bounds__(kBoThreads) void enc_offsets_kernel(const uint32_t 
   for (uint32_t p = 0; p < kBoPasses; p++) {
 #pragma unroll
     for (uint32_t k = 0; k < kBoUnroll; k++) {
+      // a lane past its block's records re-reads the block's first record; an
+      // empty block reads nothing (nrec may be 0 with NULL record columns)
       const uint64_t r = F0[p] + g + k * kBsG;
-      const uint64_t rc = r < F1[p] ? r : 0; // record 0 exists whenever a block is non-empty
-      K[p][k] = kl[rc];
-      V[p][k] = vl[rc];
+      const uint64_t rc = r < F1[p] ? r : F0[p];
+      K[p][k] = 0;
+      V[p][k] = 0;
+      if (F0[p] < F1[p]) {
+        K[p][k] = kl[rc];
+        V[p][k] = vl[rc];
+      }
     }
   }
 #pragma unroll

@@ -35,6 +35,14 @@ def test_bench_launches_n_ranks(n):
     assert [p["rank"] for p in out["per_rank"]] == list(range(n))
     assert [p["shard_tag"] for p in out["per_rank"]] == list(range(n))  # each rank ran its own shard
     assert out["value"] > 0
+    # the config-4 leg's rank path: rank r merged its own 128-SST shard of
+    # workload.config_inputs(4, r), the shards' key ranges are disjoint and
+    # consecutive, the aggregate is over all ranks
+    c4 = out["compact_config4"]
+    assert c4["n_gpus"] == n and [p["rank"] for p in c4["per_rank"]] == list(range(n))
+    per = 128 * 64
+    assert [p["key_index_range"] for p in c4["per_rank"]] == [[r * per, (r + 1) * per - 1] for r in range(n)]
+    assert c4["GiBps_aggregate"] > 0 and all(p["GiBps"] > 0 for p in c4["per_rank"])
 
 
 def test_bench_refuses_world_mismatch():

@@ -32,18 +32,21 @@ def _worker(rank, world, port, q):
         from sstcodec import workload as W
         mine = shard.sst_shard(1024, world, rank)
         # each rank encodes + round-trips only its own SSTs (4 tiny ones here)
+        import time
         orc = Oracle()
+        dist.barrier()
+        t0 = time.perf_counter()
         lo, hi = shard.record_range(rank, 500)
         rec = W.uniform_records(500, key_index=np.arange(lo, hi, dtype=np.uint64), seed=1 + rank)
         first = W.segment(rec, 4096)
         src, off, ln = orc.encode_blocks(rec, first)
         dst, out_len, status, bad = orc.roundtrip(src, off, ln, 1)
         ok = bad == 0 and np.array_equal(dst, src)
-        t = 1.0 + rank  # pretend per-rank wall time
+        t = time.perf_counter() - t0  # this rank's measured wall time for its shard
         tmax = shard.max_over_ranks(t)
         total = shard.sum_over_ranks(float(src.size))
         gathered = [None] * world
-        dist.all_gather_object(gathered, (mine[0], mine[-1], len(mine), lo, hi))
+        dist.all_gather_object(gathered, (mine[0], mine[-1], len(mine), lo, hi, t))
         q.put((rank, ok, tmax, total, gathered))
     finally:
         dist.destroy_process_group()
@@ -63,8 +66,8 @@ def test_two_rank_sharding():
         assert p.exitcode == 0
     for rank, ok, tmax, total, gathered in res:
         assert ok
-        assert tmax == 2.0  # max over ranks
-        (a0, a1, an, lo0, hi0), (b0, b1, bn, lo1, hi1) = gathered
+        (a0, a1, an, lo0, hi0, ta), (b0, b1, bn, lo1, hi1, tb) = gathered
+        assert ta > 0 and tb > 0 and tmax == max(ta, tb)  # max over the ranks' measured times
         assert a0 == 0 and a1 + 1 == b0 and b1 == 1023 and an == bn == 512  # disjoint + complete
         assert hi0 == lo1  # disjoint key ranges
         assert total > 0

@@ -477,3 +477,33 @@ def test_encode_empty(codec):
                               out_base=7, dst=dst)
     torch.cuda.synchronize()
     assert int(off[0]) == 7 and int(dst.abs().sum()) == 0
+
+
+@pytest.mark.parametrize("nb", [5, 3000])
+def test_encode_empty_blocks_null_columns(codec, oracle, nb):
+    """nrec = 0 with NULL record columns and source pointers, nb empty block
+    ranges (3000 > 2048: the one-kernel block offsets, which must not touch a
+    record column for an empty block): every block is the 16 B image of
+    BlockBuilder::EncodeExtraInfo on no entries (block_builder.cc:95-109)."""
+    import ctypes
+    from sstcodec._lib import Records, check
+    first = torch.zeros(nb + 1, dtype=torch.int64, device=DEV)
+    out_off = torch.empty(nb + 1, dtype=torch.int64, device=DEV)
+    out_len = torch.empty(nb, dtype=torch.int64, device=DEV)
+    base = 5
+    dst = torch.full((base + 16 * nb + 16,), 0xAB, dtype=torch.uint8, device=DEV)
+    codec._stream()
+    null = ctypes.c_void_p(0)
+    check(codec.lib.sstc_encode_blocks(codec.h, null, null, Records(0, 0, 0, 0, 0, 0), 0,
+                                       ctypes.c_void_p(first.data_ptr()), nb, base, ctypes.c_void_p(dst.data_ptr()),
+                                       ctypes.c_void_p(out_off.data_ptr()), ctypes.c_void_p(out_len.data_ptr())),
+          "sstc_encode_blocks")
+    torch.cuda.synchronize()
+    rec = W.uniform_records(0)
+    want, woff, wlen = oracle.encode_blocks(rec, np.zeros(nb + 1, np.uint64), base=base)
+    assert want.size == 16 * nb and not want.any()
+    assert np.array_equal(cpu_u64(out_off), np.append(woff, base + 16 * nb))
+    assert np.array_equal(cpu_u64(out_len), wlen)
+    d = dst.cpu().numpy()
+    assert np.array_equal(d[base:base + 16 * nb], want)
+    assert (d[:base] == 0xAB).all() and (d[base + 16 * nb:] == 0xAB).all()
