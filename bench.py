@@ -35,7 +35,13 @@ reference compacts on one thread.
 legs (N=1): decode alone and encode alone over the same blocks, each with its
 own roofline sub-object; compact = BASELINE config 3 (8 SSTs x 1 M records)
 through the device compaction job sstc_compact, verified against the
-reference's output hashes, with its own roofline and reference CPU baseline.
+reference's output hashes, with its own roofline; compact.files = the same job
+file -> file (sstc_compact_files, fsync on) with the reference's own loop on
+the same files beside it as compact.cpu_baseline (like for like).
+legs.compact_config4 (every N): BASELINE config 4 -- each rank compacts its own
+128-SST shard (workload.config_inputs(4, rank)) with one sstc_compact job,
+verified against the reference's outputs for that shard; per-rank GiB/s and
+roofline fraction, aggregate = all ranks' input bytes / max-over-ranks time.
 
 Input pin: the GPU-built block buffer is hashed and must equal the reference
 BlockBuilder's encoding of the same records (tests/golden/bench_inputs.json).

@@ -854,19 +854,32 @@ __device__ __forceinline__ void put_le(uint8_t *p, uint64_t v, int n) {
 // the workgroup's 256 blocks is written with aligned 16 B stores (byte stores
 // straight to HBM from 256 threads at a 56 B stride cost ~10x more).
 constexpr uint32_t kMetaLds = 24576; // 256 entries of keys up to 32 B (32 KiB: 4 workgroups per CU, 48 -> 45 us at 16 KiB)
-// The entry's keys are read back from the block the encode just wrote (its
-// first entry at the block start, its last found through the block's extra
-// and offset section: three lines per block, vs. gathering both keys and
-// their lengths / offsets from the survivor columns and the input: config 3
-// fetched 324 MB for 16 MB of entries).  MKeys: where the two keys are.
+// The block's first / last key come from the encode, which had both entries
+// in hand: their source key offsets and key lengths (EncArgs::bkey, 24 B per
+// block), so a meta entry costs one dependent read of each key from the input
+// (round 3 read them back from the block just encoded -- extra, then the last
+// offset entry, then the key: three dependent lines per block, 247 MB fetched
+// for 16 MB of meta at config 3).  MKeys: where the two keys are.
 struct MKeys {
   const uint8_t *k0, *k1;
   uint32_t fk, lk;
 };
-// the block's keys inside the block (the encode guard has checked every entry
-// against its block image) and the entry size the layout used (MS)
-__device__ __forceinline__ bool meta_keys(uint64_t b, const uint64_t *bo, const uint64_t *blen, const uint64_t *MS,
-                                          const uint8_t *dst, uint64_t cap, unsigned long long *guard, MKeys &m) {
+// the keys inside the source bytes [0, send) and the entry size the layout
+// used (MS); a failed check sets the guard
+__device__ __forceinline__ bool meta_keys(uint64_t b, const uint64_t *bkey, const uint64_t *MS, const uint8_t *src,
+                                          uint64_t send, unsigned long long *guard, MKeys &m) {
+  const uint64_t k0 = bkey[3 * b], k1 = bkey[3 * b + 1], kk = bkey[3 * b + 2];
+  m.fk = static_cast<uint32_t>(kk);
+  m.lk = static_cast<uint32_t>(kk >> 32);
+  m.k0 = src + k0;
+  m.k1 = src + k1;
+  const bool ok = m.fk <= kMaxKey && m.lk <= kMaxKey && k0 <= send && m.fk <= send - k0 && k1 <= send &&
+                  m.lk <= send - k1 && MS[b + 1] - MS[b] == 24ull + m.fk + m.lk;
+  if (!ok) atomicOr(guard, kGuardMeta);
+  return ok;
+}
+__device__ __forceinline__ bool meta_keys_rb(uint64_t b, const uint64_t *bo, const uint64_t *blen, const uint64_t *MS,
+                                             const uint8_t *dst, uint64_t cap, unsigned long long *guard, MKeys &m) {
   const uint64_t o = bo[b], L = blen[b];
   bool ok = o <= cap && L <= cap - o && L >= 32;
   if (ok) {
@@ -899,11 +912,12 @@ __device__ __forceinline__ void meta_entry(uint8_t *p, uint64_t b, const uint32_
   put_le(p + 16 + m.fk + m.lk, blen[b], 8);
 }
 
-__global__ __launch_bounds__(256) void ck_meta_kernel(const uint64_t *bo, Lay L, const uint32_t *btab,
+__global__ __launch_bounds__(256) void ck_meta_kernel(const uint64_t *bkey, Lay L, const uint32_t *btab,
                                                       BlkOff BL, const uint64_t *MS, const uint64_t *blen,
                                                       const uint64_t *tbf, const uint64_t *toff,
                                                       const uint64_t *tdata, uint8_t *dst, const uint64_t *need,
-                                                      uint64_t cap, unsigned long long *guard) {
+                                                      uint64_t cap, unsigned long long *guard, const uint8_t *src,
+                                                      const uint64_t *src_end, const uint64_t *bo_rb) {
   __shared__ __attribute__((aligned(16))) uint8_t img[kMetaLds + 16];
   if (*need > cap || !L.ok()) return; // output capacity exceeded / corrupt layout: nothing is written
   const uint64_t nb = L.nb();
@@ -912,6 +926,7 @@ __global__ __launch_bounds__(256) void ck_meta_kernel(const uint64_t *bo, Lay L,
   const uint64_t bend = b0 + 256u < nb ? b0 + 256u : nb;
   const uint64_t b = b0 + threadIdx.x;
   const uint64_t m0 = MS[b0];
+  const uint64_t send = *src_end;
   // a table's meta section must end inside the output buffer
   auto in_cap = [&](uint64_t t, uint64_t at, uint64_t len) {
     const uint64_t o = toff[t] + tdata[t] + at;
@@ -921,14 +936,14 @@ __global__ __launch_bounds__(256) void ck_meta_kernel(const uint64_t *bo, Lay L,
   };
   MKeys mk{};
   if (MS[bend] - m0 > kMetaLds) {  // long keys: direct per-thread writes
-    if (b < bend && meta_keys(b, bo, blen, MS, dst, cap, guard, mk)) {
+    if (b < bend && (bkey ? meta_keys(b, bkey, MS, src, send, guard, mk) : meta_keys_rb(b, bo_rb, blen, MS, dst, cap, guard, mk))) {
       const uint32_t t = btab[b];
       if (in_cap(t, MS[b] - MS[tbf[t]], MS[b + 1] - MS[b]))
         meta_entry(dst + toff[t] + tdata[t] + (MS[b] - MS[tbf[t]]), b, btab, BL, blen, tbf, mk);
     }
     return;
   }
-  const bool ok = b >= bend || meta_keys(b, bo, blen, MS, dst, cap, guard, mk);
+  const bool ok = b >= bend || (bkey ? meta_keys(b, bkey, MS, src, send, guard, mk) : meta_keys_rb(b, bo_rb, blen, MS, dst, cap, guard, mk));
   if (b < bend && ok) meta_entry(img + (MS[b] - m0), b, btab, BL, blen, tbf, mk);
   if (__syncthreads_or(!ok)) return; // a bad entry: the workgroup writes nothing
   for (uint64_t bs = b0; bs < bend;) {  // one run per output table touched
@@ -1399,10 +1414,13 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     ea.bmax = bmax;
     ea.src_end = src_end;
     ea.guard = guard;
+    static const bool meta_rb = getenv("SSTC_AB_META_RB") != nullptr; // A/B (temporary)
+    uint64_t *bkey = meta_rb ? nullptr : pool.get<uint64_t>(3 * nb_max); // each block's first / last key for the meta entries
+    ea.bkey = bkey;
     CK(launch_enc_emit(ea, s));
-    ck_meta_kernel<<<static_cast<uint32_t>((nb_max + 255) / 256), 256, 0, s>>>(bo, L, btab, BL, MS, blen, tbf,
+    ck_meta_kernel<<<static_cast<uint32_t>((nb_max + 255) / 256), 256, 0, s>>>(bkey, L, btab, BL, MS, blen, tbf,
                                                                               d_table_off, tdata, d_dst, need,
-                                                                              dst_cap, guard);
+                                                                              dst_cap, guard, d_src, src_end, bo);
     ck_tab_minmax_kernel<<<static_cast<uint32_t>(nt_max * kMmSplit), 256, 0, s>>>(tbf, L, bmin, bmax, tmin, tmax);
     ck_footer_kernel<<<grid(nt_max), 256, 0, s>>>(L, tbf, d_table_off, tdata, tmeta, tmin, tmax, d_dst, dst_cap, guard);
     CK(hipGetLastError());

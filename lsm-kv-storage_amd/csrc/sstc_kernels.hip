@@ -874,6 +874,11 @@ __device__ bool enc_emit_block_entries_wave(const EncArgs &a, uint64_t b) {
     }
   }
   uint8_t *blk = a.dst + a.out_blk_off[b];
+  if (a.bkey && lane == 0 && n) {
+    a.bkey[3 * b] = a.in.key_off[f0];
+    a.bkey[3 * b + 1] = a.in.key_off[f1 - 1];
+    a.bkey[3 * b + 2] = a.in.key_len[f0] | static_cast<uint64_t>(a.in.key_len[f1 - 1]) << 32;
+  }
   for (uint64_t i = 0; i < n; i++) {
     const uint64_t r = f0 + i;
     const uint64_t o = a.P[r] - P0, sz = a.P[r + 1] - a.P[r];
@@ -969,6 +974,7 @@ __device__ __forceinline__ bool enc_copy_entries(const EncArgs &a, uint8_t *img,
   const uint32_t lane = lane_id();
   const uint32_t g = lane & 15u, sub = lane >> 4;
   uint64_t tmin = ~0ull, tmax = 0; // the block's min / max txn (table footer, table_builder.cc:47-49)
+  uint64_t kfirst = 0, klast = 0;  // key offset | key length << 40 of the first / last entry (EncArgs::bkey)
   for (uint32_t c0 = 0; c0 < n; c0 += kWave) {
     const uint32_t nc = n - c0 < kWave ? n - c0 : kWave;
     uint32_t my_o = 0, my_sz = 0, my_kl = 0, my_ty = 0;
@@ -1035,6 +1041,15 @@ __device__ __forceinline__ bool enc_copy_entries(const EncArgs &a, uint8_t *img,
       tmin = my_tx < tmin ? my_tx : tmin;
       tmax = my_tx > tmax ? my_tx : tmax;
     }
+    if (a.bkey) {
+      if (c0 == 0) kfirst = readlane_u64(my_ko, 0) | static_cast<uint64_t>(__shfl(my_kl, 0, kWave)) << 40;
+      klast = readlane_u64(my_ko, nc - 1) | static_cast<uint64_t>(__shfl(my_kl, static_cast<int>(nc - 1), kWave)) << 40;
+    }
+  }
+  if (a.bkey && lane == 0 && n) {
+    a.bkey[3 * b] = kfirst & ((1ull << 40) - 1);
+    a.bkey[3 * b + 1] = klast & ((1ull << 40) - 1);
+    a.bkey[3 * b + 2] = (kfirst >> 40) | (klast >> 40) << 32;
   }
   if (a.bmin) {
     for (uint32_t d = kWave / 2; d > 0; d >>= 1) {

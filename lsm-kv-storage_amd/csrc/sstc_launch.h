@@ -89,6 +89,10 @@ struct EncArgs {
   // nblocks is only its host-side upper bound (the grid); a count past the
   // bound means a corrupt layout: every wave stands down
   const uint64_t *nb_dev = nullptr;
+  // optional (compaction): per block the source key offsets of its first and
+  // last entry and their key lengths ([3 b] first, [3 b + 1] last, [3 b + 2]
+  // = fk | lk << 32) for the meta entries (AddIndexBlockEntry)
+  uint64_t *bkey = nullptr;
 };
 
 // consistency-guard bits of the compaction job (sstc_compact.hip)
