@@ -855,7 +855,7 @@ __device__ __forceinline__ void put_le(uint8_t *p, uint64_t v, int n) {
 // straight to HBM from 256 threads at a 56 B stride cost ~10x more).
 constexpr uint32_t kMetaLds = 24576; // 256 entries of keys up to 32 B (32 KiB: 4 workgroups per CU, 48 -> 45 us at 16 KiB)
 // The block's first / last key come from the encode, which had both entries
-// in hand: their source key offsets and key lengths (EncArgs::bkey, 24 B per
+// in hand: their source key offsets and key lengths (EncArgs::bmeta, 16 B per
 // block), so a meta entry costs one dependent read of each key from the input
 // (round 3 read them back from the block just encoded -- extra, then the last
 // offset entry, then the key: three dependent lines per block, 247 MB fetched
@@ -866,38 +866,16 @@ struct MKeys {
 };
 // the keys inside the source bytes [0, send) and the entry size the layout
 // used (MS); a failed check sets the guard
-__device__ __forceinline__ bool meta_keys(uint64_t b, const uint64_t *bkey, const uint64_t *MS, const uint8_t *src,
+__device__ __forceinline__ bool meta_keys(uint64_t b, const uint64_t *bmeta, const uint64_t *MS, const uint8_t *src,
                                           uint64_t send, unsigned long long *guard, MKeys &m) {
-  const uint64_t k0 = bkey[3 * b], k1 = bkey[3 * b + 1], kk = bkey[3 * b + 2];
-  m.fk = static_cast<uint32_t>(kk);
-  m.lk = static_cast<uint32_t>(kk >> 32);
+  const uint64_t w0 = bmeta[4 * b + 2], w1 = bmeta[4 * b + 3];
+  const uint64_t k0 = w0 & ((1ull << 40) - 1), k1 = w1 & ((1ull << 40) - 1);
+  m.fk = static_cast<uint32_t>(w0 >> 40);
+  m.lk = static_cast<uint32_t>(w1 >> 40);
   m.k0 = src + k0;
   m.k1 = src + k1;
   const bool ok = m.fk <= kMaxKey && m.lk <= kMaxKey && k0 <= send && m.fk <= send - k0 && k1 <= send &&
                   m.lk <= send - k1 && MS[b + 1] - MS[b] == 24ull + m.fk + m.lk;
-  if (!ok) atomicOr(guard, kGuardMeta);
-  return ok;
-}
-__device__ __forceinline__ bool meta_keys_rb(uint64_t b, const uint64_t *bo, const uint64_t *blen, const uint64_t *MS,
-                                             const uint8_t *dst, uint64_t cap, unsigned long long *guard, MKeys &m) {
-  const uint64_t o = bo[b], L = blen[b];
-  bool ok = o <= cap && L <= cap - o && L >= 32;
-  if (ok) {
-    const uint8_t *blk = dst + o;
-    const uint64_t n = g_u64u(blk + L - 16), doff = g_u64u(blk + L - 8);
-    ok = n >= 1 && doff <= L - 16 && n <= (L - 16 - doff) / 16;
-    if (ok) {
-      const uint64_t lo = g_u64u(blk + doff + 16 * (n - 1));
-      m.fk = g_u32u(blk + 1);
-      ok = lo + 5 <= doff && m.fk <= kMaxKey && 5ull + m.fk <= doff;
-      if (ok) {
-        m.lk = g_u32u(blk + lo + 1);
-        m.k0 = blk + 5;
-        m.k1 = blk + lo + 5;
-        ok = m.lk <= kMaxKey && lo + 5 + m.lk <= doff && MS[b + 1] - MS[b] == 24ull + m.fk + m.lk;
-      }
-    }
-  }
   if (!ok) atomicOr(guard, kGuardMeta);
   return ok;
 }
@@ -912,12 +890,12 @@ __device__ __forceinline__ void meta_entry(uint8_t *p, uint64_t b, const uint32_
   put_le(p + 16 + m.fk + m.lk, blen[b], 8);
 }
 
-__global__ __launch_bounds__(256) void ck_meta_kernel(const uint64_t *bkey, Lay L, const uint32_t *btab,
+__global__ __launch_bounds__(256) void ck_meta_kernel(const uint64_t *bmeta, Lay L, const uint32_t *btab,
                                                       BlkOff BL, const uint64_t *MS, const uint64_t *blen,
                                                       const uint64_t *tbf, const uint64_t *toff,
                                                       const uint64_t *tdata, uint8_t *dst, const uint64_t *need,
                                                       uint64_t cap, unsigned long long *guard, const uint8_t *src,
-                                                      const uint64_t *src_end, const uint64_t *bo_rb) {
+                                                      const uint64_t *src_end) {
   __shared__ __attribute__((aligned(16))) uint8_t img[kMetaLds + 16];
   if (*need > cap || !L.ok()) return; // output capacity exceeded / corrupt layout: nothing is written
   const uint64_t nb = L.nb();
@@ -936,14 +914,14 @@ __global__ __launch_bounds__(256) void ck_meta_kernel(const uint64_t *bkey, Lay 
   };
   MKeys mk{};
   if (MS[bend] - m0 > kMetaLds) {  // long keys: direct per-thread writes
-    if (b < bend && (bkey ? meta_keys(b, bkey, MS, src, send, guard, mk) : meta_keys_rb(b, bo_rb, blen, MS, dst, cap, guard, mk))) {
+    if (b < bend && meta_keys(b, bmeta, MS, src, send, guard, mk)) {
       const uint32_t t = btab[b];
       if (in_cap(t, MS[b] - MS[tbf[t]], MS[b + 1] - MS[b]))
         meta_entry(dst + toff[t] + tdata[t] + (MS[b] - MS[tbf[t]]), b, btab, BL, blen, tbf, mk);
     }
     return;
   }
-  const bool ok = b >= bend || (bkey ? meta_keys(b, bkey, MS, src, send, guard, mk) : meta_keys_rb(b, bo_rb, blen, MS, dst, cap, guard, mk));
+  const bool ok = b >= bend || meta_keys(b, bmeta, MS, src, send, guard, mk);
   if (b < bend && ok) meta_entry(img + (MS[b] - m0), b, btab, BL, blen, tbf, mk);
   if (__syncthreads_or(!ok)) return; // a bad entry: the workgroup writes nothing
   for (uint64_t bs = b0; bs < bend;) {  // one run per output table touched
@@ -981,8 +959,8 @@ __global__ __launch_bounds__(256) void ck_meta_kernel(const uint64_t *bkey, Lay 
 // partial; the footer kernel folds a table's kMmSplit partials (no atomics:
 // same-address atomics from every XCD serialise)
 constexpr uint32_t kMmSplit = 16;
-__global__ __launch_bounds__(256) void ck_tab_minmax_kernel(const uint64_t *tbf, Lay L, const uint64_t *bmin,
-                                                            const uint64_t *bmax, uint64_t *pmin, uint64_t *pmax) {
+__global__ __launch_bounds__(256) void ck_tab_minmax_kernel(const uint64_t *tbf, Lay L, const uint64_t *bmeta,
+                                                            uint64_t *pmin, uint64_t *pmax) {
   __shared__ uint64_t smn[256 / kWave], smx[256 / kWave];
   const uint64_t t = blockIdx.x / kMmSplit, g = blockIdx.x % kMmSplit;
   if (!L.ok() || t >= L.nt()) return; // uniform over the workgroup
@@ -990,8 +968,9 @@ __global__ __launch_bounds__(256) void ck_tab_minmax_kernel(const uint64_t *tbf,
   const uint64_t b0 = f + n * g / kMmSplit, b1 = f + n * (g + 1) / kMmSplit;
   uint64_t mn = ~0ull, mx = 0;
   for (uint64_t b = b0 + threadIdx.x; b < b1; b += 256) {
-    mn = bmin[b] < mn ? bmin[b] : mn;
-    mx = bmax[b] > mx ? bmax[b] : mx;
+    const uint64_t x = bmeta[4 * b], y = bmeta[4 * b + 1];
+    mn = x < mn ? x : mn;
+    mx = y > mx ? y : mx;
   }
   for (uint32_t d = kWave / 2; d > 0; d >>= 1) {
     const uint64_t x = __shfl_xor(mn, d, kWave), y = __shfl_xor(mx, d, kWave);
@@ -1405,23 +1384,19 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     // 6. encode blocks, meta entries, footers
     EncArgs ea{d_src, d_src, sstc_records{KR.type, KR.kl, KR.vl, KR.tx, KR.ko, KR.vo}, bf, nb_max, Pe, bo, blen, d_dst, 1};
     ea.nb_dev = dn + 1;
-    uint64_t *bmin = pool.get<uint64_t>(nb_max), *bmax = pool.get<uint64_t>(nb_max);
+    uint64_t *bmeta = pool.get<uint64_t>(4 * nb_max); // per block: min / max txn, first / last key
     // blocks past an LDS slot are encoded by the wave that met them (config 5 319 -> 233 us)
     ea.need = need;
     ea.cap = dst_cap;
     uint64_t *tmin = pool.get<uint64_t>(nt_max * kMmSplit), *tmax = pool.get<uint64_t>(nt_max * kMmSplit);  // per-table partials
-    ea.bmin = bmin; // block min / max txn, reduced by the encode kernels
-    ea.bmax = bmax;
+    ea.bmeta = bmeta; // block min / max txn (reduced by the encode kernels) and first / last key
     ea.src_end = src_end;
     ea.guard = guard;
-    static const bool meta_rb = getenv("SSTC_AB_META_RB") != nullptr; // A/B (temporary)
-    uint64_t *bkey = meta_rb ? nullptr : pool.get<uint64_t>(3 * nb_max); // each block's first / last key for the meta entries
-    ea.bkey = bkey;
     CK(launch_enc_emit(ea, s));
-    ck_meta_kernel<<<static_cast<uint32_t>((nb_max + 255) / 256), 256, 0, s>>>(bkey, L, btab, BL, MS, blen, tbf,
+    ck_meta_kernel<<<static_cast<uint32_t>((nb_max + 255) / 256), 256, 0, s>>>(bmeta, L, btab, BL, MS, blen, tbf,
                                                                               d_table_off, tdata, d_dst, need,
-                                                                              dst_cap, guard, d_src, src_end, bo);
-    ck_tab_minmax_kernel<<<static_cast<uint32_t>(nt_max * kMmSplit), 256, 0, s>>>(tbf, L, bmin, bmax, tmin, tmax);
+                                                                              dst_cap, guard, d_src, src_end);
+    ck_tab_minmax_kernel<<<static_cast<uint32_t>(nt_max * kMmSplit), 256, 0, s>>>(tbf, L, bmeta, tmin, tmax);
     ck_footer_kernel<<<grid(nt_max), 256, 0, s>>>(L, tbf, d_table_off, tdata, tmeta, tmin, tmax, d_dst, dst_cap, guard);
     CK(hipGetLastError());
     fetch(arena, s, {need, reinterpret_cast<const uint64_t *>(guard), dn, dn + 1}, nullptr, 0, true);

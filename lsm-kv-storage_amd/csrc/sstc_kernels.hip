@@ -874,11 +874,6 @@ __device__ bool enc_emit_block_entries_wave(const EncArgs &a, uint64_t b) {
     }
   }
   uint8_t *blk = a.dst + a.out_blk_off[b];
-  if (a.bkey && lane == 0 && n) {
-    a.bkey[3 * b] = a.in.key_off[f0];
-    a.bkey[3 * b + 1] = a.in.key_off[f1 - 1];
-    a.bkey[3 * b + 2] = a.in.key_len[f0] | static_cast<uint64_t>(a.in.key_len[f1 - 1]) << 32;
-  }
   for (uint64_t i = 0; i < n; i++) {
     const uint64_t r = f0 + i;
     const uint64_t o = a.P[r] - P0, sz = a.P[r + 1] - a.P[r];
@@ -974,7 +969,7 @@ __device__ __forceinline__ bool enc_copy_entries(const EncArgs &a, uint8_t *img,
   const uint32_t lane = lane_id();
   const uint32_t g = lane & 15u, sub = lane >> 4;
   uint64_t tmin = ~0ull, tmax = 0; // the block's min / max txn (table footer, table_builder.cc:47-49)
-  uint64_t kfirst = 0, klast = 0;  // key offset | key length << 40 of the first / last entry (EncArgs::bkey)
+  uint64_t kfirst = 0, klast = 0;  // key offset | key length << 40 of the first / last entry (EncArgs::bmeta)
   for (uint32_t c0 = 0; c0 < n; c0 += kWave) {
     const uint32_t nc = n - c0 < kWave ? n - c0 : kWave;
     uint32_t my_o = 0, my_sz = 0, my_kl = 0, my_ty = 0;
@@ -1041,26 +1036,19 @@ __device__ __forceinline__ bool enc_copy_entries(const EncArgs &a, uint8_t *img,
       tmin = my_tx < tmin ? my_tx : tmin;
       tmax = my_tx > tmax ? my_tx : tmax;
     }
-    if (a.bkey) {
+    if (a.bmeta) {
       if (c0 == 0) kfirst = readlane_u64(my_ko, 0) | static_cast<uint64_t>(__shfl(my_kl, 0, kWave)) << 40;
       klast = readlane_u64(my_ko, nc - 1) | static_cast<uint64_t>(__shfl(my_kl, static_cast<int>(nc - 1), kWave)) << 40;
     }
   }
-  if (a.bkey && lane == 0 && n) {
-    a.bkey[3 * b] = kfirst & ((1ull << 40) - 1);
-    a.bkey[3 * b + 1] = klast & ((1ull << 40) - 1);
-    a.bkey[3 * b + 2] = (kfirst >> 40) | (klast >> 40) << 32;
-  }
-  if (a.bmin) {
+  if (a.bmeta) {
     for (uint32_t d = kWave / 2; d > 0; d >>= 1) {
       const uint64_t x = __shfl_xor(tmin, d, kWave), y = __shfl_xor(tmax, d, kWave);
       tmin = x < tmin ? x : tmin;
       tmax = y > tmax ? y : tmax;
     }
-    if (lane == 0) {
-      a.bmin[b] = tmin;
-      a.bmax[b] = tmax;
-    }
+    if (lane < 4) // min, max, first / last key (offset | length << 40): one store
+      a.bmeta[4 * b + lane] = lane == 0 ? tmin : (lane == 1 ? tmax : (lane == 2 ? kfirst : klast));
   }
   return true;
 }
@@ -1324,7 +1312,7 @@ __global__ __launch_bounds__(kEncWaves *kWave) void enc_lds_kernel(EncArgs a) {
         enc_emit_block<kWave>(a, b, img, lane); // its LDS image holds the lanes' chunk slots
       } else {
         if (!enc_emit_block_entries_wave(a, b)) return;
-        if (a.bmin) { // the block's min / max txn (table footer), reduced by the wave
+        if (a.bmeta) { // the block's min / max txn (table footer), reduced by the wave
           const uint64_t f0 = a.blk_first[b], f1 = a.blk_first[b + 1];
           uint64_t mn = ~0ull, mx = 0;
           for (uint64_t r = f0 + lane; r < f1; r += kWave) {
@@ -1337,9 +1325,10 @@ __global__ __launch_bounds__(kEncWaves *kWave) void enc_lds_kernel(EncArgs a) {
             mn = x < mn ? x : mn;
             mx = y > mx ? y : mx;
           }
-          if (lane == 0) {
-            a.bmin[b] = mn;
-            a.bmax[b] = mx;
+          if (lane < 4) { // min, max, first / last key (offset | length << 40): one store
+            const uint64_t r = lane < 2 ? 0 : (lane == 2 ? f0 : f1 - 1);
+            const uint64_t k = lane < 2 ? 0 : a.in.key_off[r] | static_cast<uint64_t>(a.in.key_len[r]) << 40;
+            a.bmeta[4 * b + lane] = lane == 0 ? mn : (lane == 1 ? mx : k);
           }
         }
       }

@@ -73,8 +73,11 @@ struct EncArgs {
   uint8_t *dst;
   uint32_t entries_in_src = 0; // records decoded from blocks in key_src (== val_src)
   uint32_t xcd = 0;
-  // optional (compaction, entries_in_src): per-block min / max txn
-  uint64_t *bmin = nullptr, *bmax = nullptr;
+  // optional (compaction, entries_in_src): per block 4 words -- min txn, max
+  // txn (table footer, table_builder.cc:47-49), and the first / last entry's
+  // key offset | key length << 40 (meta entries, AddIndexBlockEntry): one
+  // 4-lane store per block
+  uint64_t *bmeta = nullptr;
   // optional capacity guard (compaction): nothing is written when *need > cap
   const uint64_t *need = nullptr;
   uint64_t cap = 0;
@@ -89,10 +92,6 @@ struct EncArgs {
   // nblocks is only its host-side upper bound (the grid); a count past the
   // bound means a corrupt layout: every wave stands down
   const uint64_t *nb_dev = nullptr;
-  // optional (compaction): per block the source key offsets of its first and
-  // last entry and their key lengths ([3 b] first, [3 b + 1] last, [3 b + 2]
-  // = fk | lk << 32) for the meta entries (AddIndexBlockEntry)
-  uint64_t *bkey = nullptr;
 };
 
 // consistency-guard bits of the compaction job (sstc_compact.hip)
