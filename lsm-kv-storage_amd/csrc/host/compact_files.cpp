@@ -331,7 +331,12 @@ int sstc_compact_files(sstc_pipe *pipe, const char *const *in_paths, const uint6
   uint64_t cap = total + total / 2 + (1u << 20);
   int rc = SSTC_E_CAPACITY;
   for (int attempt = 0; attempt < 2 && rc == SSTC_E_CAPACITY; attempt++) {
-    if (grow_dev(pipe->d_dst, pipe->cap_d_dst, cap)) return bail(SSTC_E_NOMEM, "sstc_compact_files: output");
+    if (grow_dev(pipe->d_dst, pipe->cap_d_dst, cap)) {
+      const std::string what = "sstc_compact_files: output buffer of " + std::to_string(cap) + " bytes (" +
+                               std::to_string(res.tables_out) + " tables, " + std::to_string(res.blocks_out) +
+                               " blocks, " + std::to_string(res.records_kept) + " records)";
+      return bail(SSTC_E_NOMEM, what.c_str());
+    }
     rc = sstc_compact(pipe->ctx, pipe->d_src, d_off, d_len, nblocks, tfb.data(), n_in, params, pipe->d_dst,
                       pipe->cap_d_dst, d_toff, d_tlen, max_tables, &res);
     cap = res.bytes_out; // exact size known after a capacity miss

@@ -432,6 +432,9 @@ sstc_ctx *ThreadContext() {
   thread_local CtxHolder h;
   if (!h.ctx) {
     int dev = 0;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+      throw std::runtime_error("no HIP device: libsstcodec has no CPU path");
     if (hipGetDevice(&dev) != hipSuccess) dev = 0;
     // its own stream: concurrent builders on pool threads overlap on the GPU
     // instead of queueing on the null stream

@@ -593,7 +593,13 @@ __global__ __launch_bounds__(kFtThreads) void ck_filter_kernel(const SK *s, uint
                                                                uint64_t *Pe, uint64_t *ws, uint64_t *totals,
                                                                Abort stop, unsigned long long *guard) {
   __shared__ uint64_t s_tile, s_pre[3];
-  if (stop()) return; // uniform over the grid: no ticket drawn, the host rejects the job
+  if (stop()) { // uniform over the grid: no ticket drawn, the host rejects the job
+    if (blockIdx.x == 0 && threadIdx.x == 0) { // no survivor: the layout below splits nothing, writes nothing
+      totals[0] = totals[1] = totals[2] = 0;
+      Pd[0] = Pe[0] = 0;
+    }
+    return;
+  }
   const uint32_t tid = threadIdx.x, lane = lane_id(), w = tid / kWave;
   if (tid == 0) {
     const uint64_t t = __hip_atomic_fetch_add(ws, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -822,7 +828,14 @@ __global__ void ck_table_info_kernel(const uint64_t *tf, Lay L, const uint64_t *
     else hi = mid;
   }
   tbf[t] = lo;
-  if (t == nt) return;
+  if (t == nt) { // the sentinel: a zero length when nt < nt_max (the table scan runs over nt_max)
+    if (t < L.nt_max) {
+      tlen[t] = 0;
+      tdata[t] = 0;
+      tmeta[t] = 0;
+    }
+    return;
+  }
   // tbf[t+1] computed by its own thread; recompute here for the sizes
   uint64_t lo2 = 0, hi2 = nb + 1;
   const uint64_t r2 = tf[t + 1];
@@ -1062,10 +1075,12 @@ struct Pool {
 // greedy segmentation of [0, m) by weights whose prefix sums are
 // Pw[i] + add * i (>= threshold closes), optionally clamped at ends[0..*nends];
 // the count lands in *dn on the device.
-void segment(Pool &pool, const uint64_t *Pw, uint64_t add, uint64_t m, uint64_t threshold, const uint64_t *ends,
-             const uint64_t *nends, uint64_t *first, uint64_t *dn, hipStream_t s, bool long_segments) {
-  uint32_t *J = pool.get<uint32_t>(segment_workspace_u32(m));
-  CK(launch_segment(Pw, m, threshold, J, dn, first, s, ends, nends, add, long_segments));
+// m: the device record count, n its host bound
+void segment(Pool &pool, const uint64_t *Pw, uint64_t add, uint64_t n, const uint64_t *m, uint64_t threshold,
+             const uint64_t *ends, const uint64_t *nends, uint64_t *first, uint64_t *dn, hipStream_t s,
+             bool long_segments) {
+  uint32_t *J = pool.get<uint32_t>(segment_workspace_u32(n));
+  CK(launch_segment(Pw, n, threshold, J, dn, first, s, ends, nends, add, long_segments, m));
 }
 
 struct Words {
@@ -1086,11 +1101,23 @@ __global__ __launch_bounds__(256) void ck_pack_kernel(Words w, const uint64_t *a
 
 // run starts (record index of every input table's first block) to the device
 // (fetched to the host by the pack kernel); thread 0 also snapshots the context's decode
-// error counter and clears the unsorted count for this job
-__global__ void ck_run_starts_kernel(const uint64_t *rec_base, const uint64_t *tfb, uint64_t n, uint64_t *out,
-                                     const unsigned long long *err_count, uint64_t *errs,
-                                     unsigned long long *bad, unsigned long long *guard) {
+// error counter and clears the unsorted count for this job; workgroup 0 sums
+// the count kernel's per-workgroup block byte sums into *in_bytes
+__global__ __launch_bounds__(256) void ck_run_starts_kernel(const uint64_t *rec_base, const uint64_t *tfb, uint64_t n,
+                                                            uint64_t *out, const unsigned long long *err_count,
+                                                            uint64_t *errs, unsigned long long *bad,
+                                                            unsigned long long *guard, const uint64_t *len_part,
+                                                            uint64_t nparts, uint64_t *in_bytes) {
   const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (blockIdx.x == 0) {
+    __shared__ uint64_t s_part[256 / kWave];
+    uint64_t v = 0;
+    for (uint64_t p = threadIdx.x; p < nparts; p += 256) v += len_part[p];
+    v = wave_sum_u64(v);
+    if (lane_id() == 0) s_part[threadIdx.x / kWave] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) *in_bytes = s_part[0] + s_part[1] + s_part[2] + s_part[3];
+  }
   if (i == 0) {
     *errs = *err_count;
     *bad = 0;
@@ -1162,17 +1189,21 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
   try {
     Pool pool(arena);
     const uint64_t nws = scan_workspace_elems(nblocks + 1) + 64;
-    // Host syncs: (1) per-block record counts (they size every array), (2) the
-    // kept count with the sortedness / decode error flags, (3) the table and
-    // block counts, (4) completion with the output size (the capacity check is
-    // on the device: no writer touches d_dst when the output exceeds dst_cap).
-    // Everything else stays on the stream.
+    // Host syncs: (1) the run starts and the input block bytes (they size
+    // every array and bound the output counts), (2) completion with the
+    // output size, the table / block counts and the error flags (the
+    // capacity check is on the device: no writer touches d_dst when the
+    // output exceeds dst_cap).  Everything else stays on the stream: the
+    // kept count stays on the device (the segmentation reads it there), so
+    // the host enqueues the whole tail while the merge runs.
     // 1. decode every block
     uint64_t *rb_all = pool.get<uint64_t>(nblocks + 1);
     uint64_t *ws = pool.get<uint64_t>(nws);
     uint64_t *errs = pool.get<uint64_t>(2);
     uint64_t *d_tfb = pool.get<uint64_t>(ntables + 1), *d_rs = pool.get<uint64_t>(ntables + 1);
-    CK(launch_count(d_src, d_blk_off, d_blk_len, nblocks, rb_all, s, ws));
+    const uint64_t nparts = (nblocks + 255) / 256;
+    uint64_t *len_part = pool.get<uint64_t>(nparts + 1), *in_bytes_d = pool.get<uint64_t>(1);
+    CK(launch_count(d_src, d_blk_off, d_blk_len, nblocks, rb_all, s, ws, len_part));
     CK(launch_scan(rb_all, nblocks, 0, rb_all, ws, s, true));
     unsigned long long *bad = reinterpret_cast<unsigned long long *>(pool.get<uint64_t>(1));
     // consistency guard: [0] bits set by any check of the job, [1] the end of
@@ -1182,9 +1213,10 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     // record index of every input table's first record (its run start)
     CK(hipMemcpyAsync(d_tfb, h_tfb, (ntables + 1) * 8, hipMemcpyHostToDevice, s));
     ck_run_starts_kernel<<<grid(ntables + 1), 256, 0, s>>>(rb_all, d_tfb, ntables + 1, d_rs, err_count, errs, bad,
-                                                           guard);
-    fetch(arena, s, {}, d_rs, ntables + 1);
-    std::vector<uint64_t> run_start(arena.host, arena.host + ntables + 1);
+                                                           guard, len_part, nparts, in_bytes_d);
+    fetch(arena, s, {in_bytes_d}, d_rs, ntables + 1);
+    const uint64_t in_bytes = arena.host[0]; // every survivor's entry lies in these bytes
+    std::vector<uint64_t> run_start(arena.host + 1, arena.host + 2 + ntables);
     const uint64_t n = run_start[ntables];
     res[0] = n;
     if (n >= 0xFFFFFFFFull) {
@@ -1331,38 +1363,45 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
                                                                         totals, stop, guard);
     if (arena.fault == 1) CK(hipMemsetAsync(KR.ko, 0xFF, n * sizeof(uint64_t), s)); // test: bad key offsets
     if (arena.fault == 2) CK(hipMemsetAsync(Pe, 0x5A, (n + 1) * sizeof(uint64_t), s)); // test: bad prefix sums
-    fetch(arena, s, {totals, reinterpret_cast<const uint64_t *>(bad),
-                           reinterpret_cast<const uint64_t *>(err_count), errs,
-                           reinterpret_cast<const uint64_t *>(guard), totals + 1, totals + 2});
-    if (arena.host[2] != arena.host[3]) {
-      err = "an input block failed to decode";
-      return SSTC_E_INVALID_ARG;
-    }
-    if (arena.host[1]) {
-      err = "input SST records are not sorted (key asc, txn desc)";
-      return SSTC_E_INVALID_ARG;
-    }
-    if (arena.host[4]) {
-      err = "device consistency check failed after the merge (merged record ids out of range)";
-      return SSTC_E_INTERNAL;
-    }
-    const uint64_t m = arena.host[0];
-    res[1] = m;
-    if (max_tables == 0) { // m >= 1 here: at least one output table (the layout below writes table 0)
+    // the job's error words (decode errors, unsorted inputs, guard bits) are
+    // read after the last kernel: a rejected job writes nothing (the filter
+    // of a stopped job reports no survivor)
+    const std::initializer_list<const uint64_t *> err_words = {
+        reinterpret_cast<const uint64_t *>(err_count), errs, reinterpret_cast<const uint64_t *>(bad),
+        reinterpret_cast<const uint64_t *>(guard)};
+    auto job_error = [&](const uint64_t *h) -> int { // h: the err_words as fetched
+      if (h[0] != h[1]) {
+        err = "an input block failed to decode";
+        return SSTC_E_INVALID_ARG;
+      }
+      if (h[2]) {
+        err = "input SST records are not sorted (key asc, txn desc)";
+        return SSTC_E_INVALID_ARG;
+      }
+      if (h[3] & kGuardMergeId) {
+        err = "device consistency check failed after the merge (merged record ids out of range)";
+        return SSTC_E_INTERNAL;
+      }
+      return SSTC_OK;
+    };
+    if (max_tables == 0) { // no room for the first table (m >= 1 unless the job is rejected)
+      fetch(arena, s, err_words, nullptr, 0, true);
+      if (const int r = job_error(arena.host)) return r;
       err = "more output tables than max_tables";
       return SSTC_E_CAPACITY;
     }
     // 4. the table split (key+value bytes, compact.cc:290) and the block split
-    // (entry + offset-entry bytes, table_builder.cc:57-59) clamped at table ends
-    uint64_t *tf = pool.get<uint64_t>(m + 1), *dn = pool.get<uint64_t>(2);
-    segment(pool, Pd, 0, m, table_limit, nullptr, nullptr, tf, dn, s, true);
-    uint64_t *bf = pool.get<uint64_t>(m + 1);
-    segment(pool, Pe, 16, m, block_threshold, tf, dn, bf, dn + 1, s, false); // blocks end at table ends
-    // 5. layout over the count bounds (no host fetch: see Lay)
+    // (entry + offset-entry bytes, table_builder.cc:57-59) clamped at table
+    // ends, over the device kept count (totals[0]; n bounds it)
+    uint64_t *tf = pool.get<uint64_t>(n + 1), *dn = pool.get<uint64_t>(2);
+    segment(pool, Pd, 0, n, totals, table_limit, nullptr, nullptr, tf, dn, s, true);
+    uint64_t *bf = pool.get<uint64_t>(n + 1);
+    segment(pool, Pe, 16, n, totals, block_threshold, tf, dn, bf, dn + 1, s, false); // blocks end at table ends
+    // 5. layout over count bounds (no host fetch: see Lay): the survivors'
+    // key+value and entry + offset-entry bytes are at most the input block bytes
     const uint64_t tl = table_limit ? table_limit : 1, bt = block_threshold ? block_threshold : 1;
-    const uint64_t kv_bytes = arena.host[5], entry_bytes = arena.host[6];
-    const uint64_t nt_max = std::max<uint64_t>(1, std::min<uint64_t>({m, kv_bytes / tl + 1, max_tables}));
-    const uint64_t nb_max = std::max<uint64_t>(1, std::min<uint64_t>(m, (entry_bytes + 16 * m) / bt + nt_max));
+    const uint64_t nt_max = std::max<uint64_t>(1, std::min<uint64_t>({n, in_bytes / tl + 1, max_tables}));
+    const uint64_t nb_max = std::max<uint64_t>(1, std::min<uint64_t>(n, in_bytes / bt + nt_max));
     const Lay L{dn, nt_max, nb_max};
     uint64_t *blen = pool.get<uint64_t>(nb_max), *msz = pool.get<uint64_t>(nb_max);
     uint32_t *btab = pool.get<uint32_t>(nb_max);
@@ -1399,20 +1438,25 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     ck_tab_minmax_kernel<<<static_cast<uint32_t>(nt_max * kMmSplit), 256, 0, s>>>(tbf, L, bmeta, tmin, tmax);
     ck_footer_kernel<<<grid(nt_max), 256, 0, s>>>(L, tbf, d_table_off, tdata, tmeta, tmin, tmax, d_dst, dst_cap, guard);
     CK(hipGetLastError());
-    fetch(arena, s, {need, reinterpret_cast<const uint64_t *>(guard), dn, dn + 1}, nullptr, 0, true);
-    res[4] = arena.host[0];
-    res[2] = arena.host[3];
-    res[3] = arena.host[2];
-    if (arena.host[2] > max_tables) {
+    fetch(arena, s,
+          {reinterpret_cast<const uint64_t *>(err_count), errs, reinterpret_cast<const uint64_t *>(bad),
+           reinterpret_cast<const uint64_t *>(guard), need, dn, dn + 1, totals},
+          nullptr, 0, true);
+    if (const int r = job_error(arena.host)) return r;
+    res[1] = arena.host[7];
+    res[4] = arena.host[4];
+    res[2] = arena.host[6];
+    res[3] = arena.host[5];
+    if (arena.host[5] > max_tables) {
       err = "more output tables than max_tables";
       return SSTC_E_CAPACITY;
     }
-    if (arena.host[1]) {
+    if (arena.host[3]) {
       err = "device consistency check failed (guard bits 0x" + [](uint64_t v) {
         char b[24];
         snprintf(b, sizeof b, "%llx", static_cast<unsigned long long>(v));
         return std::string(b);
-      }(arena.host[1]) + "): d_dst and the table arrays are undefined";
+      }(arena.host[3]) + "): d_dst and the table arrays are undefined";
       return SSTC_E_INTERNAL;
     }
     if (res[4] > dst_cap) {

@@ -485,11 +485,18 @@ __device__ __forceinline__ void zero_words(uint64_t *w, uint64_t nz) {
 }
 
 __global__ void count_kernel(const uint8_t *src, const uint64_t *blk_off, const uint64_t *blk_len,
-                             uint64_t nblocks, uint64_t *counts, uint64_t *zws, uint64_t nz) {
+                             uint64_t nblocks, uint64_t *counts, uint64_t *zws, uint64_t nz, uint64_t *len_part) {
   const uint64_t b = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   zero_words(zws, nz); // the look-back status words of the scan that follows
+  const uint64_t len = b < nblocks ? blk_len[b] : 0;
+  if (len_part) { // uniform: the workgroup's byte sum (bounds the compaction's output counts)
+    __shared__ uint64_t s_part[4];
+    const uint64_t v = wave_sum_u64(len);
+    if (lane_id() == 0) s_part[threadIdx.x / kWave] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) len_part[blockIdx.x] = s_part[0] + s_part[1] + s_part[2] + s_part[3];
+  }
   if (b >= nblocks) return;
-  const uint64_t len = blk_len[b];
   uint64_t c = 0;
   if (len >= 16) {
     const uint8_t *blk = src + blk_off[b];
@@ -1436,6 +1443,7 @@ struct SegArgs {
   uint64_t *zws;          // cleared here: the win scan's look-back status words
   uint64_t nz;
   uint32_t *tentry;       // cleared here: tiles + 1 entry counters
+  const uint64_t *mp;     // optional: the record count on the device (m is then its bound)
 };
 
 // index of the first end > i (ends sorted, ends[ne] = m > i)
@@ -1455,17 +1463,22 @@ __global__ __launch_bounds__(kChThreads) void seg_walk_kernel(SegArgs a) {
   __shared__ uint32_t jn[kChTile], jc[kChTile];
   __shared__ uint64_t s_wend, s_t0;
   const uint32_t tid = threadIdx.x;
+  const uint64_t m = a.mp ? *a.mp : a.m;
   const uint64_t c0 = static_cast<uint64_t>(blockIdx.x) * kChTile;
-  const uint64_t c1 = c0 + kChTile < a.m ? c0 + kChTile : a.m;
-  const uint32_t len = static_cast<uint32_t>(c1 - c0);
-  const uint64_t nl = a.m + 1 - c0 < kLw ? a.m + 1 - c0 : kLw;
-  const uint64_t ne = a.ends ? *a.nends : 0;
-  if (tid == 0) { // first table end past the tile start (its search overlaps the window fill)
-    s_t0 = a.ends ? seg_end_index(a.ends, ne, c0) : 0;
+  if (tid == 0) {
     a.tentry[blockIdx.x] = 0;
     if (blockIdx.x == 0) a.tentry[gridDim.x] = 0;
     for (uint64_t z = blockIdx.x; z < a.nz; z += gridDim.x) a.zws[z] = 0;
   }
+  if (c0 >= m) { // a tile past the device count (uniform): no window, no node
+    if (tid == 0) a.win[blockIdx.x] = 0;
+    return;
+  }
+  const uint64_t c1 = c0 + kChTile < m ? c0 + kChTile : m;
+  const uint32_t len = static_cast<uint32_t>(c1 - c0);
+  const uint64_t nl = m + 1 - c0 < kLw ? m + 1 - c0 : kLw;
+  const uint64_t ne = a.ends ? *a.nends : 0;
+  if (tid == 0) s_t0 = a.ends ? seg_end_index(a.ends, ne, c0) : 0; // first table end past the tile start
   { // all loads of the window in flight before the LDS stores
     constexpr uint32_t kFill = kLw / kChThreads;
     uint64_t v[kFill];
@@ -1484,7 +1497,7 @@ __global__ __launch_bounds__(kChThreads) void seg_walk_kernel(SegArgs a) {
   const SegW W{a.Pw, lw, a.add, c0, nl};
   if (tid == kChThreads - 1) { // entry window end: J0 of the record before the tile
     const uint64_t i = c0 - 1;
-    uint64_t lim = a.m;
+    uint64_t lim = m;
     if (a.ends) { // first end > c0 - 1: s_t0, or the one before it when it equals c0
       const uint64_t t = s_t0;
       lim = t > 0 && a.ends[t - 1] == c0 ? c0 : a.ends[t];
@@ -1498,11 +1511,11 @@ __global__ __launch_bounds__(kChThreads) void seg_walk_kernel(SegArgs a) {
   {
     const uint64_t i0 = c0 + tid * kPer;
     uint64_t t = s_t0;
-    uint64_t end = a.ends ? a.ends[t] : a.m; // ends[ne] = m: the walks below stop at ne
+    uint64_t end = a.ends ? a.ends[t] : m; // ends[ne] = m: the walks below stop at ne
 #pragma unroll
     for (uint32_t r = 0; r < kPer; r++) {
       const uint64_t i = i0 + r;
-      if (a.ends && i < a.m)
+      if (a.ends && i < m)
         while (end <= i) end = a.ends[++t]; // ends[ne] = m > i
       lim[r] = i < c1 ? end : 0;
     }
@@ -1566,15 +1579,17 @@ struct NodeArgs {
   const uint64_t *base; // node base of every tile (exclusive scan of win), tiles + 1
   uint64_t m, tiles;
   uint32_t *Nx, *Nc, *Nt; // level 0: next node, segments, tile
+  const uint64_t *mp;     // optional device record count
 };
 
 __global__ void seg_node_kernel(NodeArgs a) {
   const uint64_t k = blockIdx.x;
   const uint64_t b0 = a.base[k], nw = a.base[k + 1] - b0, c0 = k * kChTile;
+  const uint64_t m = a.mp ? *a.mp : a.m;
   for (uint64_t o = threadIdx.x; o < nw; o += blockDim.x) {
     const uint64_t x = a.Fx[c0 + o];
     uint32_t nx = kNoNode;
-    if (x < a.m) {
+    if (x < m) {
       const uint64_t t = x / kChTile;
       nx = static_cast<uint32_t>(a.base[t] + (x - t * kChTile));
     }
@@ -1604,8 +1619,16 @@ __global__ void seg_npow_kernel(const uint32_t *Nx, const uint32_t *Nc, uint32_t
 
 // visits of the node chain from node 0, total segments, first[total] = m
 __global__ void seg_ndepth_kernel(const uint32_t *Nx, const uint32_t *Nc, uint32_t levels, uint64_t stride,
-                                  uint64_t m, uint64_t *d_visits, uint64_t *first, uint64_t *d_count) {
+                                  uint64_t m, const uint64_t *mp, uint64_t *d_visits, uint64_t *first,
+                                  uint64_t *d_count) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  if (mp) m = *mp;
+  if (m == 0) { // no records (an aborted compaction): no node, no segment
+    *d_visits = 0;
+    *d_count = 0;
+    first[0] = 0;
+    return;
+  }
   uint64_t pos = 0, hops = 0, tot = 0, w = 1;
   for (uint32_t k = 1; k < levels; k++) w *= kSegRadix;
   for (int k = static_cast<int>(levels) - 1; k >= 0; k--, w /= kSegRadix) {
@@ -1650,8 +1673,9 @@ __global__ void seg_nentry_kernel(const uint32_t *Nx, const uint32_t *Nc, const 
 // count of the marks: O(log chain) barriers instead of a serial walk (a tile
 // of 64 KiB values is a 2048-step chain).  Chains estimated at <= 128 steps
 // (e.g. 4 KiB blocks of small records: ~73 per tile) are walked by one thread.
-__global__ __launch_bounds__(kChThreads) void seg_emit_kernel(const uint32_t *J0, uint64_t m, const uint32_t *tentry,
-                                                              const uint32_t *tbefore, uint64_t *first) {
+__global__ __launch_bounds__(kChThreads) void seg_emit_kernel(const uint32_t *J0, uint64_t m, const uint64_t *mp,
+                                                              const uint32_t *tentry, const uint32_t *tbefore,
+                                                              uint64_t *first) {
   constexpr uint32_t kPer = kChTile / kChThreads;
   constexpr uint16_t kOut = 0xFFFF; // successor outside the tile
   constexpr uint32_t kSerialChain = 128;
@@ -1660,7 +1684,8 @@ __global__ __launch_bounds__(kChThreads) void seg_emit_kernel(const uint32_t *J0
   __shared__ uint32_t s_wsum[kChThreads / kWave];
   const uint64_t k = blockIdx.x;
   const uint32_t e = tentry[k];
-  if (!e) return; // a segment spans the whole tile
+  if (!e) return; // a segment spans the whole tile (or the tile is past the device count)
+  if (mp) m = *mp;
   const uint64_t c0 = k * kChTile, c1 = c0 + kChTile < m ? c0 + kChTile : m;
   const uint32_t len = static_cast<uint32_t>(c1 - c0), tid = threadIdx.x;
   {
@@ -1797,8 +1822,10 @@ __device__ uint64_t hop_exact(const uint64_t *Pw, uint64_t add, uint64_t m, uint
 constexpr uint32_t kHopAhead = 8;
 
 __global__ __launch_bounds__(kWave) void seg_hops_kernel(const uint64_t *Pw, uint64_t add, uint64_t m,
-                                                         uint64_t threshold, uint64_t *first, uint64_t *d_count) {
+                                                         const uint64_t *mp, uint64_t threshold, uint64_t *first,
+                                                         uint64_t *d_count) {
   const uint32_t lane = lane_id();
+  if (mp) m = *mp; // m = 0: no segment, first[0] = 0
   const uint64_t wm = Pw[m] + add * m;
   uint64_t pos = 0, nseg = 0, glen = 0, wpos = Pw[0];
   bool done = false;
@@ -2092,9 +2119,10 @@ hipError_t launch_roundtrip(const RtArgs &a, hipStream_t s) {
 }
 
 hipError_t launch_count(const uint8_t *src, const uint64_t *blk_off, const uint64_t *blk_len,
-                        uint64_t nblocks, uint64_t *counts, hipStream_t s, uint64_t *scan_ws) {
+                        uint64_t nblocks, uint64_t *counts, hipStream_t s, uint64_t *scan_ws, uint64_t *len_part) {
   const uint64_t nz = scan_ws ? scan_status_words(nblocks) : 0;
-  if (nblocks) count_kernel<<<grid_for(nblocks, 256), 256, 0, s>>>(src, blk_off, blk_len, nblocks, counts, scan_ws, nz);
+  if (nblocks)
+    count_kernel<<<grid_for(nblocks, 256), 256, 0, s>>>(src, blk_off, blk_len, nblocks, counts, scan_ws, nz, len_part);
   return hipGetLastError();
 }
 
@@ -2333,14 +2361,14 @@ uint64_t segment_workspace_u32(uint64_t nrec) { return SegLayout(nrec).total + 2
 
 hipError_t launch_segment(const uint64_t *Pw, uint64_t nrec, uint64_t threshold, uint32_t *J,
                           uint64_t *d_nblocks, uint64_t *blk_first, hipStream_t s, const uint64_t *ends,
-                          const uint64_t *d_nends, uint64_t add, bool long_segments) {
+                          const uint64_t *d_nends, uint64_t add, bool long_segments, const uint64_t *d_nrec) {
   if (nrec == 0) { // no records: no segment, first[0] = 0
     hipError_t e = hipMemsetAsync(d_nblocks, 0, sizeof(uint64_t), s);
     if (e == hipSuccess) e = hipMemsetAsync(blk_first, 0, sizeof(uint64_t), s);
     return e;
   }
   if (long_segments && !ends) {
-    seg_hops_kernel<<<1, kWave, 0, s>>>(Pw, add, nrec, threshold, blk_first, d_nblocks);
+    seg_hops_kernel<<<1, kWave, 0, s>>>(Pw, add, nrec, d_nrec, threshold, blk_first, d_nblocks);
     return hipGetLastError();
   }
   const SegLayout L(nrec);
@@ -2350,23 +2378,24 @@ hipError_t launch_segment(const uint64_t *Pw, uint64_t nrec, uint64_t threshold,
   uint32_t *tentry = J + L.tentry, *tbefore = J + L.tbefore;
   const uint64_t stride = nrec + 1;
   SegArgs a{Pw, add, nrec, threshold, ends, d_nends, J + L.J0, J + L.Fx, J + L.Fc, win, blk_first, d_nblocks,
-            sws, scan_status_words(L.tiles), tentry};
+            sws, scan_status_words(L.tiles), tentry, d_nrec};
   seg_walk_kernel<<<static_cast<uint32_t>(L.tiles), kChThreads, 0, s>>>(a);
   hipError_t e = launch_scan(win, L.tiles, 0, base, sws, s, true); // base[tiles] = node count
   if (e != hipSuccess) return e;
   const uint64_t *nn = base + L.tiles;
-  NodeArgs na{J + L.Fx, J + L.Fc, base, nrec, L.tiles, J + L.Nx, J + L.Nc, J + L.Nt};
+  NodeArgs na{J + L.Fx, J + L.Fc, base, nrec, L.tiles, J + L.Nx, J + L.Nc, J + L.Nt, d_nrec};
   seg_node_kernel<<<static_cast<uint32_t>(L.tiles), 256, 0, s>>>(na);
   const uint32_t pg = static_cast<uint32_t>(std::min<uint64_t>(grid_for(nrec + 1, 256), 2048));
   for (uint64_t k = 0; k + 1 < L.levels; k++)
     seg_npow_kernel<<<pg, 256, 0, s>>>(J + L.Nx + k * stride, J + L.Nc + k * stride, J + L.Nx + (k + 1) * stride,
                                        J + L.Nc + (k + 1) * stride, nn);
-  seg_ndepth_kernel<<<1, 64, 0, s>>>(J + L.Nx, J + L.Nc, static_cast<uint32_t>(L.levels), stride, nrec, visits,
-                                     blk_first, d_nblocks);
+  seg_ndepth_kernel<<<1, 64, 0, s>>>(J + L.Nx, J + L.Nc, static_cast<uint32_t>(L.levels), stride, nrec, d_nrec,
+                                     visits, blk_first, d_nblocks);
   seg_nentry_kernel<<<grid_for(L.tiles, 256), 256, 0, s>>>(J + L.Nx, J + L.Nc, J + L.Nt, base,
                                                            static_cast<uint32_t>(L.levels), stride, visits,
                                                            tentry, tbefore);
-  seg_emit_kernel<<<static_cast<uint32_t>(L.tiles), kChThreads, 0, s>>>(J + L.J0, nrec, tentry, tbefore, blk_first);
+  seg_emit_kernel<<<static_cast<uint32_t>(L.tiles), kChThreads, 0, s>>>(J + L.J0, nrec, d_nrec, tentry, tbefore,
+                                                                        blk_first);
   return hipGetLastError();
 }
 

@@ -123,7 +123,8 @@ hipError_t launch_get(const GetArgs &a, hipStream_t s);
 hipError_t launch_roundtrip(const RtArgs &a, hipStream_t s);
 hipError_t launch_copy_probe(const uint8_t *src, uint8_t *dst, uint64_t n16, hipStream_t s);
 hipError_t launch_count(const uint8_t *src, const uint64_t *blk_off, const uint64_t *blk_len,
-                        uint64_t nblocks, uint64_t *counts, hipStream_t s, uint64_t *scan_ws = nullptr);
+                        uint64_t nblocks, uint64_t *counts, hipStream_t s, uint64_t *scan_ws = nullptr,
+                        uint64_t *len_part = nullptr); // len_part: per-workgroup sums of blk_len (256 blocks each)
 hipError_t launch_decode(const DecArgs &a, hipStream_t s);
 uint64_t scan_workspace_elems(uint64_t n);
 // look-back status words a scan of n items needs cleared (0: single-workgroup scan)
@@ -155,7 +156,9 @@ uint64_t segment_workspace_u32(uint64_t nrec);
 hipError_t launch_segment(const uint64_t *Pw, uint64_t nrec, uint64_t threshold, uint32_t *J,
                           uint64_t *d_nblocks, uint64_t *blk_first, hipStream_t s,
                           const uint64_t *ends = nullptr, const uint64_t *d_nends = nullptr, uint64_t add = 0,
-                          bool long_segments = false);
+                          bool long_segments = false, const uint64_t *d_nrec = nullptr);
+// d_nrec: the record count on the device (nrec is then only its upper bound:
+// grids and workspace are sized by nrec, the kernels segment *d_nrec records)
 
 // persistent device workspace of one context (compaction)
 struct Arena {

@@ -99,3 +99,14 @@ def same_up_to_tie_order(a, b, inputs):
         elif not all(r in pool[p] for r in x + y):
             return False
     return True
+
+
+@pytest.fixture(autouse=True)
+def _gpu_memlog(request):
+    """SSTC_MEMLOG=1: free device memory after every GPU test (finds a test
+    that leaves workspace behind)."""
+    yield
+    if os.environ.get("SSTC_MEMLOG") and request.node.get_closest_marker("gpu"):
+        import torch
+        free, total = torch.cuda.mem_get_info()
+        print(f"\n[memlog] {request.node.name}: free {free / 2**30:.1f} of {total / 2**30:.1f} GiB", flush=True)
