@@ -775,10 +775,10 @@ struct BlkOff {
   }
 };
 
-// block b: length, meta entry size, table index, encode pieces (EncArgs::pieces)
+// block b: length, meta entry size, table index
 __global__ void ck_block_info_kernel(const uint64_t *bf, Lay L, const uint64_t *Pe, const uint32_t *kl,
                                      const uint64_t *tf, uint64_t *blen, uint64_t *msz, uint32_t *btab,
-                                     uint64_t *pc, uint64_t *zws, uint64_t nz, unsigned long long *guard) {
+                                     uint64_t *zws, uint64_t nz, unsigned long long *guard) {
   const uint64_t b = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (b < nz) zws[b] = 0; // look-back status words of the two block scans that follow
   if (b >= L.nb_max) return;
@@ -788,15 +788,12 @@ __global__ void ck_block_info_kernel(const uint64_t *bf, Lay L, const uint64_t *
     blen[b] = 0;
     msz[b] = 0;
     btab[b] = 0;
-    pc[b] = 0;
     if (!ok && b == 0) atomicOr(guard, kGuardLayout);
     return;
   }
   const uint64_t f0 = bf[b], f1 = bf[b + 1];
-  const uint64_t len = (Pe[f1] - Pe[f0]) + 16 * (f1 - f0) + 16;
-  blen[b] = len;
+  blen[b] = (Pe[f1] - Pe[f0]) + 16 * (f1 - f0) + 16;
   msz[b] = 24ull + kl[f0] + kl[f1 - 1]; // AddIndexBlockEntry, table_builder.cc:101-145
-  pc[b] = enc_pieces(len);
   uint64_t lo = 0, hi = nt;
   while (lo + 1 < hi) {
     const uint64_t mid = (lo + hi) >> 1;
@@ -1410,13 +1407,10 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     uint32_t *btab = pool.get<uint32_t>(nb_max);
     const uint64_t nzb = scan_status_words(nb_max); // <= nb_max
     uint64_t *ws3 = pool.get<uint64_t>(2 * nzb);
-    uint64_t *pc = pool.get<uint64_t>(nb_max), *PC = pool.get<uint64_t>(nb_max + 1);
-    ck_block_info_kernel<<<grid(nb_max), 256, 0, s>>>(bf, L, Pe, KR.kl, tf, blen, msz, btab, pc, ws3, 2 * nzb,
-                                                      guard);
+    ck_block_info_kernel<<<grid(nb_max), 256, 0, s>>>(bf, L, Pe, KR.kl, tf, blen, msz, btab, ws3, 2 * nzb, guard);
     const BlkOff BL{Pe, bf}; // block offsets in closed form (Pe[0] = 0)
     uint64_t *MS = pool.get<uint64_t>(nb_max + 1);
     CK(launch_scan(msz, nb_max, 0, MS, ws3 + nzb, s, true));
-    CK(launch_scan(pc, nb_max, 0, PC, ws3, s, true)); // the encode's large-block pieces
     uint64_t *tbf = pool.get<uint64_t>(nt_max + 1), *tdata = pool.get<uint64_t>(nt_max),
              *tmeta = pool.get<uint64_t>(nt_max);
     ck_table_info_kernel<<<grid(nt_max + 1), 256, 0, s>>>(tf, L, bf, BL, MS, tbf, tdata, tmeta, d_table_len);
@@ -1437,7 +1431,6 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     ea.bmeta = bmeta; // block min / max txn (reduced by the encode kernels) and first / last key
     ea.src_end = src_end;
     ea.guard = guard;
-    ea.pieces = PC; // large blocks in pieces (enc_piece_kernel)
     CK(launch_enc_emit(ea, s));
     ck_meta_kernel<<<static_cast<uint32_t>((nb_max + 255) / 256), 256, 0, s>>>(bmeta, L, btab, BL, MS, blen, tbf,
                                                                               d_table_off, tdata, d_dst, need,

@@ -666,6 +666,7 @@ __global__ __launch_bounds__(256) void enc_bsum_kernel(const uint32_t *kl, const
 // by byte through a per-thread LDS slot.
 constexpr uint32_t kEncThreads = 256;
 constexpr uint32_t kEncWaves = 4;
+constexpr uint32_t kEncSlot = 4608;       // LDS image bytes per wave (enc_lds_kernel)
 
 __device__ __forceinline__ u32x4 load16_unaligned(const uint8_t *p) {
   uint32_t sh;
@@ -813,7 +814,7 @@ __device__ __forceinline__ u32x4 funnel16(const u32x4 &v0, const u32x4 &v1, uint
 // faster on config 5 (210 us) but its 98 VGPRs cost enc_lds_kernel<1> a wave
 // per SIMD: config 3 encode 500 -> 624 us (profiles/r02_ab/encode_ab.md)
 constexpr uint32_t kWaveSpanUnroll = 4;
-template <uint32_t kU, bool kNt = false>
+template <uint32_t kU>
 __device__ __forceinline__ void copy_span_wave(uint8_t *dp, const uint8_t *sp, uint64_t len) {
   const uint32_t lane = lane_id();
   const uintptr_t d0 = reinterpret_cast<uintptr_t>(dp), d1 = d0 + len;
@@ -832,10 +833,10 @@ __device__ __forceinline__ void copy_span_wave(uint8_t *dp, const uint8_t *sp, u
 #pragma unroll
     for (uint32_t u = 0; u < kU; u++) { // clamped at nch: sa[nch] is inside the read allowance
       const uint64_t k = k0 + static_cast<uint64_t>(u) * kWave + lane;
-      v[u] = kNt ? __builtin_nontemporal_load(sa + (k < nch ? k : nch)) : sa[k < nch ? k : nch];
+      v[u] = sa[k < nch ? k : nch];
     }
     const uint64_t kn = k0 + static_cast<uint64_t>(kU) * kWave;
-    v[kU] = kNt ? __builtin_nontemporal_load(sa + (kn < nch ? kn : nch)) : sa[kn < nch ? kn : nch];
+    v[kU] = sa[kn < nch ? kn : nch];
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (uint32_t u = 0; u < kU; u++) {
@@ -860,133 +861,6 @@ __device__ __forceinline__ void copy_span_wave(uint8_t *dp, const uint8_t *sp, u
   }
   for (uintptr_t x = d0 + lane; x < cb; x += kWave) dp[x - d0] = sp[x - d0];
   for (uintptr_t x = ce + lane; x < d1; x += kWave) dp[x - d0] = sp[x - d0];
-}
-
-// copy_span_wave without the funnel: every lane loads its 16 source bytes with
-// one byte-misaligned global_load_dwordx4 (the target runs in unaligned-access
-// mode; a wave's 64 loads still cover contiguous lines) and stores them to an
-// aligned destination chunk; kU chunks per lane in flight.  Reads exactly
-// [sp, sp + len).
-template <uint32_t kU, bool kNt = false>
-__device__ __forceinline__ void copy_span_wave_ua(uint8_t *dp, const uint8_t *sp, uint64_t len) {
-  const uint32_t lane = lane_id();
-  const uintptr_t d0 = reinterpret_cast<uintptr_t>(dp), d1 = d0 + len;
-  const uintptr_t cb = (d0 + 15) & ~static_cast<uintptr_t>(15), ce = d1 & ~static_cast<uintptr_t>(15);
-  if (cb >= ce) {
-    for (uint64_t x = lane; x < len; x += kWave) dp[x] = sp[x];
-    return;
-  }
-  const uint64_t nch = (ce - cb) >> 4;
-  const uint8_t *s0 = sp + (cb - d0);
-  u32x4 *da = reinterpret_cast<u32x4 *>(cb);
-  for (uint64_t k0 = 0; k0 < nch; k0 += static_cast<uint64_t>(kWave) * kU) {
-    u32x4 v[kU];
-#pragma unroll
-    for (uint32_t u = 0; u < kU; u++) { // clamped: every load unconditional, in flight together
-      const uint64_t k = k0 + static_cast<uint64_t>(u) * kWave + lane;
-      const uint8_t *q = s0 + 16 * (k < nch ? k : nch - 1);
-      if (kNt) v[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(q)); // unaligned-access mode
-      else __builtin_memcpy(&v[u], q, 16);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (uint32_t u = 0; u < kU; u++) {
-      const uint64_t k = k0 + static_cast<uint64_t>(u) * kWave + lane;
-      if (k < nch) __builtin_nontemporal_store(v[u], da + k);
-    }
-  }
-  for (uintptr_t x = d0 + lane; x < cb; x += kWave) dp[x - d0] = sp[x - d0];
-  for (uintptr_t x = ce + lane; x < d1; x += kWave) dp[x - d0] = sp[x - d0];
-}
-
-// copy_span_wave_ua software-pipelined: round i+1's loads are issued before
-// round i's stores, so a load's wait never covers the stores before it (gfx9's
-// vmcnt retires loads and stores in issue order: in the plain loop every
-// round's first load waits for the previous round's stores to be acknowledged)
-template <uint32_t kU>
-__device__ __forceinline__ void copy_span_wave_pipe(uint8_t *dp, const uint8_t *sp, uint64_t len) {
-  const uint32_t lane = lane_id();
-  const uint64_t head = (16 - (reinterpret_cast<uintptr_t>(dp) & 15)) & 15; // bytes before the first aligned chunk
-  if (head + 16 > len) {
-    for (uint64_t x = lane; x < len; x += kWave) dp[x] = sp[x];
-    return;
-  }
-  const uint64_t nch = (len - head) >> 4, R = static_cast<uint64_t>(kWave) * kU, nfull = nch / R;
-  const uint8_t *s0 = sp + head;
-  u32x4 *da = reinterpret_cast<u32x4 *>(dp + head); // pointer arithmetic keeps the global address space
-  auto ld = [&](u32x4 (&v)[kU], uint64_t r) { // round r, clamped, unconditional
-#pragma unroll
-    for (uint32_t u = 0; u < kU; u++) {
-      const uint64_t k = r * R + static_cast<uint64_t>(u) * kWave + lane;
-      __builtin_memcpy(&v[u], s0 + 16 * (k < nch ? k : nch - 1), 16);
-    }
-  };
-  auto st = [&](const u32x4 (&v)[kU], uint64_t r) { // a full round
-#pragma unroll
-    for (uint32_t u = 0; u < kU; u++) __builtin_nontemporal_store(v[u], da + r * R + static_cast<uint64_t>(u) * kWave + lane);
-  };
-  // two register sets, no copies between them: round r + 1's loads go out
-  // before round r's stores
-  u32x4 A[kU], B[kU];
-  ld(A, 0);
-  uint64_t r = 0;
-  for (; r + 2 <= nfull; r += 2) {
-    ld(B, r + 1);
-    st(A, r);
-    ld(A, r + 2);
-    st(B, r + 1);
-  }
-  if (r < nfull) { // one full round left, then the partial one from B
-    ld(B, r + 1);
-    st(A, r);
-    r++;
-#pragma unroll
-    for (uint32_t u = 0; u < kU; u++) A[u] = B[u];
-  }
-#pragma unroll
-  for (uint32_t u = 0; u < kU; u++) { // the partial last round (in A)
-    const uint64_t k = r * R + static_cast<uint64_t>(u) * kWave + lane;
-    if (k < nch) __builtin_nontemporal_store(A[u], da + k);
-  }
-  for (uint64_t x = lane; x < head; x += kWave) dp[x] = sp[x];
-  for (uint64_t x = head + 16 * nch + lane; x < len; x += kWave) dp[x] = sp[x];
-}
-
-// copy_span_wave_ua by nw waves together (wave wv of them): chunk k goes to
-// thread k mod (64 nw), so the group's loads of one round are one contiguous
-// run; the edge bytes are wave 0's.
-template <uint32_t kU>
-__device__ __forceinline__ void copy_span_group_ua(uint8_t *dp, const uint8_t *sp, uint64_t len, uint32_t wv,
-                                                   uint32_t nw) {
-  const uint32_t lane = lane_id();
-  const uintptr_t d0 = reinterpret_cast<uintptr_t>(dp), d1 = d0 + len;
-  const uintptr_t cb = (d0 + 15) & ~static_cast<uintptr_t>(15), ce = d1 & ~static_cast<uintptr_t>(15);
-  if (cb >= ce) {
-    if (wv == 0)
-      for (uint64_t x = lane; x < len; x += kWave) dp[x] = sp[x];
-    return;
-  }
-  const uint64_t nch = (ce - cb) >> 4, nt = static_cast<uint64_t>(nw) * kWave, tid = wv * kWave + lane;
-  const uint8_t *s0 = sp + (cb - d0);
-  u32x4 *da = reinterpret_cast<u32x4 *>(cb);
-  for (uint64_t k0 = 0; k0 < nch; k0 += nt * kU) {
-    u32x4 v[kU];
-#pragma unroll
-    for (uint32_t u = 0; u < kU; u++) {
-      const uint64_t k = k0 + u * nt + tid;
-      __builtin_memcpy(&v[u], s0 + 16 * (k < nch ? k : nch - 1), 16);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (uint32_t u = 0; u < kU; u++) {
-      const uint64_t k = k0 + u * nt + tid;
-      if (k < nch) __builtin_nontemporal_store(v[u], da + k);
-    }
-  }
-  if (wv == 0) {
-    for (uintptr_t x = d0 + lane; x < cb; x += kWave) dp[x - d0] = sp[x - d0];
-    for (uintptr_t x = ce + lane; x < d1; x += kWave) dp[x - d0] = sp[x - d0];
-  }
 }
 
 // A compaction block past the LDS slot of the enc_lds_kernel<1> wave that met
@@ -1031,178 +905,6 @@ __device__ bool enc_emit_block_entries_wave(const EncArgs &a, uint64_t b) {
   return true;
 }
 
-
-// Pieces of the compaction's large blocks (EncArgs::pieces).  Piece k of block
-// b covers the block bytes [16-aligned block start + k kPieceBytes, + kPieceBytes)
-// clipped to the block: its entries' spans (one copy_span_wave per entry
-// met), their txns, and the parts of the offset section and the extra that fall
-// inside.  Every wave of the grid takes a contiguous run of the pieces (one
-// search for its first block, then a walk), so a large block is spread over
-// as many waves as it has pieces and the grid's waves carry equal bytes.
-
-// first x in [lo, hi] with end(x) > key (end nondecreasing, end(hi) > key), by
-// 64-ary probing across the wave (one batch of loads per round)
-template <class F>
-__device__ __forceinline__ uint64_t wave_first_gt(uint64_t lo, uint64_t hi, uint64_t key, F end) {
-  const uint32_t lane = lane_id();
-  while (lo < hi) {
-    const uint64_t step = (hi - lo + kWave) / kWave; // ceil((hi - lo + 1) / 64)
-    const uint64_t x = lo + lane * step;
-    const bool le = x <= hi && end(x) <= key; // a prefix of the lanes
-    const uint64_t c = static_cast<uint64_t>(__popcll(__ballot(le)));
-    if (c == 0) return lo;
-    const uint64_t last = lo + (c - 1) * step; // end(last) <= key
-    hi = last + step < hi ? last + step : hi;
-    lo = last + 1;
-  }
-  return lo;
-}
-
-constexpr uint32_t kLaneSpan = 256; // entry spans up to this many bytes are copied by one lane
-#ifndef SSTC_PIECE_UNROLL
-#define SSTC_PIECE_UNROLL 4
-#endif
-#ifndef SSTC_PIECE_GRID
-#define SSTC_PIECE_GRID 1536
-#endif
-#ifndef SSTC_PIECE_WPE
-#define SSTC_PIECE_WPE 0
-#endif
-#ifndef SSTC_PIECE_UA
-#define SSTC_PIECE_UA 0
-#endif
-#ifndef SSTC_PIECE_RR
-#define SSTC_PIECE_RR 0
-#endif
-#ifndef SSTC_PIECE_NT
-#define SSTC_PIECE_NT 0
-#endif
-#ifndef SSTC_PIECE_WG
-#define SSTC_PIECE_WG 0
-#endif
-#ifndef SSTC_PIECE_PIPE
-#define SSTC_PIECE_PIPE 0
-#endif
-__device__ __forceinline__ void lane_copy(uint8_t *dst, const uint8_t *src, uint32_t len); // below
-
-// wv / nw: this wave among the nw waves that copy the piece together (the
-// entry walk is repeated by each; the small writes are wave 0's)
-__device__ void enc_piece(const EncArgs &a, uint64_t b, uint64_t k, uint32_t wv = 0, uint32_t nw = 1) {
-  const uint32_t lane = lane_id();
-  const bool w0 = wv == 0;
-  const uint64_t f0 = a.blk_first[b], f1 = a.blk_first[b + 1], n = f1 - f0;
-  const uint64_t bo = a.out_blk_off[b], L = a.out_blk_len[b];
-  const uint64_t P0 = a.P[f0], D = a.P[f1] - P0;
-  if (!enc1_block_ok(a, bo, L, n) || L != D + 16 * n + 16 || n == 0) {
-    if (w0 && lane == 0 && a.guard) atomicOr(a.guard, kGuardBlockRange);
-    return;
-  }
-  const uint64_t A = bo & ~15ull;
-  const uint64_t s0 = A + k * kPieceBytes, s1 = s0 + kPieceBytes;
-  const uint64_t lo = s0 > bo ? s0 - bo : 0, hi = s1 - bo < L ? s1 - bo : L; // block bytes [lo, hi)
-  if (lo >= hi) return;
-  uint8_t *blk = a.dst + bo;
-  if (lo < D) { // entries: the one holding byte lo, then on while they start before hi, 64 at a time
-    uint64_t r = wave_first_gt(f0, f1 - 1, lo, [&](uint64_t x) { return a.P[x + 1] - P0; });
-    for (;; r += kWave) {
-      const uint64_t ri = r + lane;
-      uint64_t o = ~0ull, sz = 0, ko = 0, tx = 0;
-      uint32_t kl = 0;
-      if (ri < f1) {
-        o = a.P[ri] - P0;
-        sz = a.P[ri + 1] - P0 - o;
-        ko = a.in.key_off[ri];
-        kl = a.in.key_len[ri];
-        tx = a.in.txn[ri];
-      }
-      const bool on = o < hi; // a prefix of the lanes (offsets ascend)
-      const uint64_t live = __ballot(on);
-      if (!live) break;
-      if (__any(on && !enc1_entry_ok(a, o, sz, kl, ko, D))) {
-        if (w0 && lane == 0) atomicOr(a.guard, kGuardEntry);
-        return;
-      }
-      const uint64_t e = o + sz - 8; // the span [o, e) is the source bytes, [e, o + sz) the txn
-      const uint64_t c0 = o > lo ? o : lo, c1 = e < hi ? e : hi;
-      const bool has = on && c0 < c1, small = has && c1 - c0 <= kLaneSpan && w0;
-      // short spans: a lane each (a block of small entries would otherwise
-      // cost the wave one round trip per entry); long ones: the whole wave
-      if (small) lane_copy(blk + c0, a.key_src + ko - 5 + (c0 - o), static_cast<uint32_t>(c1 - c0));
-      for (uint64_t big = __ballot(has && c1 - c0 > kLaneSpan); big; big &= big - 1) {
-        const int j = __ffsll(static_cast<long long>(big)) - 1;
-        const uint64_t jc0 = readlane_u64(c0, j), jc1 = readlane_u64(c1, j);
-        const uint64_t src = readlane_u64(ko, j) - 5 + (jc0 - readlane_u64(o, j));
-#if SSTC_PIECE_WG
-        copy_span_group_ua<SSTC_PIECE_UNROLL>(blk + jc0, a.key_src + src, jc1 - jc0, wv, nw);
-#elif SSTC_PIECE_PIPE
-        copy_span_wave_pipe<SSTC_PIECE_UNROLL>(blk + jc0, a.key_src + src, jc1 - jc0);
-#elif SSTC_PIECE_UA
-        copy_span_wave_ua<SSTC_PIECE_UNROLL, SSTC_PIECE_NT>(blk + jc0, a.key_src + src, jc1 - jc0);
-#else
-        copy_span_wave<SSTC_PIECE_UNROLL, SSTC_PIECE_NT>(blk + jc0, a.key_src + src, jc1 - jc0);
-#endif
-      }
-      if (on && w0)
-        for (uint32_t t = 0; t < 8; t++)
-          if (e + t >= lo && e + t < hi) blk[e + t] = static_cast<uint8_t>(tx >> (8 * t));
-      if (~live) break; // an entry past the piece, or past the block
-    }
-  }
-  const uint64_t t0 = lo > D ? lo : D, t1 = w0 ? hi : t0; // offset section + extra inside the piece
-  for (uint64_t x = t0 + lane; x < t1; x += kWave) {
-    uint64_t v;
-    if (x < D + 16 * n) {
-      const uint64_t i = (x - D) >> 4, j = (x - D) & 15;
-      const uint64_t st = a.P[f0 + i] - P0;
-      v = j < 8 ? st : a.P[f0 + i + 1] - P0 - st;
-    } else {
-      v = x - D - 16 * n < 8 ? n : D;
-    }
-    blk[x] = static_cast<uint8_t>(v >> (8 * ((x - D) & 7)));
-  }
-}
-
-constexpr uint32_t kPieceWaves = 4, kPieceGrid = SSTC_PIECE_GRID; // 6 waves per SIMD (79 VGPRs) x 4 SIMDs x 256 CUs: one resident round
-
-__global__ __launch_bounds__(kPieceWaves *kWave)
-#if SSTC_PIECE_WPE
-__attribute__((amdgpu_waves_per_eu(SSTC_PIECE_WPE)))
-#endif
-void enc_piece_kernel(EncArgs a) {
-  const uint64_t nb = *a.nb_dev;
-  if (nb > a.nblocks || a.over()) return;
-  const uint64_t T = a.pieces[nb];
-#if SSTC_PIECE_WG // the workgroup's waves copy each piece together
-  const uint64_t W = gridDim.x, w = blockIdx.x;
-  const uint32_t wv = uniform(threadIdx.x / kWave), nw = kPieceWaves;
-#else
-  const uint64_t W = static_cast<uint64_t>(gridDim.x) * kPieceWaves;
-  const uint64_t w = static_cast<uint64_t>(blockIdx.x) * kPieceWaves + uniform(threadIdx.x / kWave);
-  const uint32_t wv = 0, nw = 1;
-#endif
-  auto before = [&](uint64_t x) { return a.pieces[x]; };
-#if SSTC_PIECE_RR
-  // round robin: at any time the grid's waves copy neighbouring pieces (the
-  // in-flight reads and writes sweep the buffers like the block kernels')
-  for (uint64_t p = w; p < T; p += W) {
-    const uint64_t b = wave_first_gt(0, nb - 1, p, [&](uint64_t x) { return before(x + 1); });
-    enc_piece(a, uniform64(b), p - before(b), wv, nw);
-  }
-  return;
-#endif
-  const uint64_t p0 = T * w / W, p1 = T * (w + 1) / W;
-  if (p0 >= p1) return;
-  uint64_t b = wave_first_gt(0, nb - 1, p0, [&](uint64_t x) { return before(x + 1); });
-  uint64_t pb = before(b), pe = before(b + 1);
-  for (uint64_t p = p0; p < p1; p++) {
-    while (pe <= p) { // the next block with pieces (uniform)
-      b++;
-      pb = pe;
-      pe = before(b + 1);
-    }
-    enc_piece(a, uniform64(b), p - pb, wv, nw);
-  }
-}
 
 // One lane copies len bytes from global src to LDS dst, both at arbitrary
 // alignment: head bytes until dst is 4-aligned, then one aligned source dword
@@ -1610,13 +1312,13 @@ __global__ __launch_bounds__(kEncWaves *kWave) void enc_lds_kernel(EncArgs a) {
     L64 = uniform64(a.out_blk_len[b]);
   }
   const uint32_t pad = static_cast<uint32_t>(bo & 15u);
-  if (kMode == 1 && a.pieces ? enc_big_block(L64) : pad + L64 + 16 > kEncSlot) { // large block
-    { // this wave writes it straight to HBM (or enc_piece_kernel does, in pieces)
+  if (pad + L64 + 16 > kEncSlot) { // large block
+    { // this wave writes it straight to HBM
       if constexpr (kMode == 0) {
         enc_wave_offsets(a, b);
         enc_emit_block<kWave>(a, b, img, lane); // its LDS image holds the lanes' chunk slots
       } else {
-        if (!a.pieces && !enc_emit_block_entries_wave(a, b)) return;
+        if (!enc_emit_block_entries_wave(a, b)) return;
         if (a.bmeta) { // the block's min / max txn (table footer), reduced by the wave
           const uint64_t f0 = a.blk_first[b], f1 = a.blk_first[b + 1];
           uint64_t mn = ~0ull, mx = 0;
@@ -2620,7 +2322,6 @@ hipError_t launch_enc_emit(const EncArgs &a, hipStream_t s) {
   // (key, value) span pairs were slower (profiles/r02_ab/encode_ab.md)
   if (!a.entries_in_src) enc_lds_kernel<0><<<g, kEncWaves * kWave, 0, s>>>(a);
   else enc_lds_kernel<1><<<g, kEncWaves * kWave, 0, s>>>(a);
-  if (a.entries_in_src && a.pieces && a.nb_dev) enc_piece_kernel<<<kPieceGrid, kPieceWaves * kWave, 0, s>>>(a);
   // blocks past an LDS slot are encoded by the wave that met them (a listed
   // pass by a workgroup per block was slower: Zipf set 329 -> 236 us, config 5
   // 319 -> 233 us; profiles/r02_ab/)

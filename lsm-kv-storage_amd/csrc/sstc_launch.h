@@ -92,26 +92,7 @@ struct EncArgs {
   // nblocks is only its host-side upper bound (the grid); a count past the
   // bound means a corrupt layout: every wave stands down
   const uint64_t *nb_dev = nullptr;
-  // optional (compaction, mode 1): blocks past the LDS slot by the
-  // pad-independent test enc_big_block are not copied by the wave that meets
-  // them but in pieces of kPieceBytes by enc_piece_kernel, every wave of a
-  // full grid taking a contiguous run of pieces (a 128 KiB block no longer
-  // rides on one wave).  pieces[b] = the pieces before block b (an exclusive
-  // scan of enc_pieces over the blocks, nblocks + 1 words)
-  const uint64_t *pieces = nullptr;
 };
-
-// the compaction encode's LDS image per wave, and its piece split (EncArgs::pieces)
-constexpr uint32_t kEncSlot = 4608;
-#ifndef SSTC_PIECE_BYTES
-#define SSTC_PIECE_BYTES 16384
-#endif
-constexpr uint64_t kPieceBytes = SSTC_PIECE_BYTES;
-__host__ __device__ inline bool enc_big_block(uint64_t L) { return L + 32 > kEncSlot; }
-// pieces of a block of L bytes: its 16 B-aligned span (up to 15 B of lead) in kPieceBytes
-__host__ __device__ inline uint64_t enc_pieces(uint64_t L) {
-  return enc_big_block(L) ? (L + 15 + kPieceBytes - 1) / kPieceBytes : 0;
-}
 
 // consistency-guard bits of the compaction job (sstc_compact.hip)
 constexpr unsigned long long kGuardMergeId = 1, kGuardEntry = 2, kGuardBlockRange = 4, kGuardMeta = 8,
