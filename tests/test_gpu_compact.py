@@ -269,6 +269,41 @@ def test_compact_max_tables_exceeded_writes_nothing(codec):
             assert res.tables_out > 3
 
 
+@pytest.mark.parametrize("bad", ["unsorted", "corrupt"])
+def test_compact_rejected_job_writes_nothing(codec, oracle, bad):
+    """The host reads the decode / sortedness verdicts only after the last
+    kernel (the whole job is enqueued after the first fetch): a rejected job's
+    filter reports no survivor, so the split finds no table and not one byte
+    of the output buffer is written."""
+    import ctypes
+    import torch
+    from sstcodec._lib import CompactParams, CompactResult
+    sets = W.compaction_inputs(3, 20_000, 50_000, seed=9, vmax=64, p_delete=0.1)
+    if bad == "unsorted":
+        sets[1] = {key: v[::-1].copy() for key, v in sets[1].items()}  # keys descending
+    ins = [oracle.table_build(r, 4096) for r in sets]
+    if bad == "corrupt":
+        ins[2] = ins[2].copy()
+        ins[2][1:5] = np.frombuffer(np.uint32(0xFFFF0000).tobytes(), np.uint8)  # entry 0 of block 0
+    src = torch.from_numpy(np.concatenate(ins)).to(codec.device)
+    idx = codec.open_tables(src, [f.size for f in ins], strict=True)
+    P = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    need = int(src.numel()) * 2
+    dst = torch.full((need,), 0xA5, dtype=torch.uint8, device=codec.device)
+    toff = torch.zeros(4097, dtype=torch.int64, device=codec.device)
+    tlen = torch.zeros(4096, dtype=torch.int64, device=codec.device)
+    res = CompactResult()
+    codec._stream()
+    rc = codec.lib.sstc_compact(codec.h, P(src), P(idx["blk_off"]), P(idx["blk_len"]), int(idx["blk_off"].numel()),
+                                idx["table_first_block"].ctypes.data_as(ctypes.c_void_p), len(ins),
+                                ctypes.byref(CompactParams(4096, 32 << 20, 1, 0)), P(dst), need, P(toff), P(tlen),
+                                4096, ctypes.byref(res))
+    assert rc == -1  # SSTC_E_INVALID_ARG
+    msg = codec.lib.sstc_last_error_string().decode()
+    assert ("not sorted" if bad == "unsorted" else "decode") in msg
+    assert (dst.cpu().numpy() == 0xA5).all(), "a writer ran for a rejected job"
+
+
 def test_compact_all_deletes_base_level(codec, oracle):
     """Every input record a DELETE at the base level: ShouldKeepEntry drops
     them all but the first merged record (compact.cc:324-363 keeps the first

@@ -4,6 +4,7 @@
 #   tests    pytest -m gpu (one process)
 #   smoke    __graft_entry__.smoke()
 #   bench    python bench.py --steps 30
+#   profile  tools/profile.sh: rocprofv3 kernel trace + stats and FETCH / WRITE passes of the bench
 #   trace    rocprofv3 kernel traces of the compaction job, configs 3 4 5 (tools/trace_compact.py tables)
 #   pmc      FETCH_SIZE / WRITE_SIZE of one config-3 and one config-4 compaction call
 #   configs  tools/bench_compact.py configs 3, 3-overlap, 4, 5 with the reference driver beside them
@@ -12,7 +13,7 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 2
 export TMPDIR=/tmp
 out=gpurun_out/${1:-val}; shift
-stages=${*:-tests smoke bench trace pmc configs}
+stages=${*:-tests smoke bench profile trace pmc configs}
 mkdir -p $out
 has() { [[ " $stages " == *" $1 "* ]]; }
 if has tests; then
@@ -27,6 +28,10 @@ fi
 if has bench; then
   timeout -k 10 500 python bench.py --steps 30 > $out/bench.log 2>&1 || { tail -20 $out/bench.log; exit 5; }
   tail -1 $out/bench.log | cut -c1-1500
+fi
+if has profile; then
+  bash tools/profile.sh $(basename $out) > $out/profile.log 2>&1 || { tail -5 $out/profile.log; exit 9; }
+  echo profile ok
 fi
 if has trace; then
   for c in ${CONFIGS:-3 4 5}; do
