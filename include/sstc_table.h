@@ -43,7 +43,9 @@
 
 #ifdef __cplusplus
 #include <cstdint>
+#include <cstring>
 #include <memory>
+#include <new>
 #include <string>
 #include <string_view>
 #include <type_traits>
@@ -62,6 +64,60 @@ using BlockSize = uint64_t;
  * first use and destroyed at thread exit (the reference builds / reads SSTs
  * from pool threads, one TableBuilder per thread: db/db_impl.cc:354-362). */
 sstc_ctx *ThreadContext();
+
+/* Growable host array for the builder's pending records: storage from
+ * sstc_host_alloc (pinned, so Finish() copies it to the GPU without a pack
+ * copy; pageable when pinning fails).  A TableBuilder takes its arrays from a
+ * per-thread pool and returns them with their capacity, so a thread that
+ * builds many SSTs appends into memory that is already pinned and faulted in. */
+template <class T> class HostVec {
+public:
+  HostVec() = default;
+  HostVec(const HostVec &) = delete;
+  HostVec &operator=(const HostVec &) = delete;
+  ~HostVec() {
+    if (p_) sstc_host_free(p_, pinned_);
+  }
+  size_t size() const { return n_; }
+  bool empty() const { return n_ == 0; }
+  T *data() { return p_; }
+  const T *data() const { return p_; }
+  T &operator[](size_t i) { return p_[i]; }
+  const T &operator[](size_t i) const { return p_[i]; }
+  T &back() { return p_[n_ - 1]; }
+  const T &back() const { return p_[n_ - 1]; }
+  void clear() { n_ = 0; }
+  void reserve(size_t c) {
+    if (c > cap_) grow(c);
+  }
+  void push_back(T v) {
+    if (n_ == cap_) grow(cap_ ? 2 * cap_ : 4096);
+    p_[n_++] = v;
+  }
+  void append(const T *src, size_t k) {
+    if (n_ + k > cap_) grow(n_ + k > 2 * cap_ ? n_ + k : 2 * cap_);
+    if (k) std::memcpy(p_ + n_, src, k * sizeof(T));
+    n_ += k;
+  }
+
+private:
+  void grow(size_t c) {
+    int pinned = 0;
+    T *q = static_cast<T *>(sstc_host_alloc(c * sizeof(T), &pinned));
+    if (!q) throw std::bad_alloc();
+    if (n_) std::memcpy(q, p_, n_ * sizeof(T));
+    if (p_) sstc_host_free(p_, pinned_);
+    p_ = q;
+    cap_ = c;
+    pinned_ = pinned;
+  }
+  T *p_ = nullptr;
+  size_t n_ = 0, cap_ = 0;
+  int pinned_ = 0;
+};
+
+/* one TableBuilder's pending records (sst_table.cpp keeps a per-thread pool) */
+struct BuilderArena;
 
 /* One meta entry (reference sstable/block_index.h:22-57). */
 struct BlockIndex {
@@ -116,12 +172,13 @@ private:
   uint64_t threshold_;
   sstc_ctx *ctx_;
   int fd_ = -1;
-  // pending records (host SoA + arenas)
-  std::vector<uint8_t> type_;
-  std::vector<uint32_t> key_len_, val_len_;
-  std::vector<uint64_t> txn_, key_off_, val_off_;
-  std::vector<uint8_t> keys_, vals_;
-  std::vector<uint64_t> blk_first_{0};
+  // pending records (host SoA + arenas), borrowed from the thread's pool
+  BuilderArena *arena_;
+  HostVec<uint8_t> &type_;
+  HostVec<uint32_t> &key_len_, &val_len_;
+  HostVec<uint64_t> &txn_, &key_off_, &val_off_;
+  HostVec<uint8_t> &keys_, &vals_;
+  HostVec<uint64_t> &blk_first_;
   uint64_t block_size_ = 0; /* sum(entry_size + 16) of the open block */
   std::string table_smallest_key_;
   uint64_t min_txn_ = UINT64_MAX, max_txn_ = 0;

@@ -219,6 +219,15 @@ typedef struct sstc_compact_result {
   uint64_t records_in, records_kept, blocks_out, tables_out, bytes_out;
 } sstc_compact_result;
 
+/* Host staging for the C++ mirror's TableBuilder (include/sstc_table.h
+ * HostVec): `bytes` of page-locked memory when the HIP runtime can pin it
+ * (*pinned = 1; a later H2D copy from it is a true async DMA), else ordinary
+ * memory (*pinned = 0); NULL when neither is available.  Free it with
+ * sstc_host_free and the same `pinned`.  (The builder keeps its arrays in a
+ * per-thread pool, so a thread that builds SST after SST pins once.) */
+void *sstc_host_alloc(uint64_t bytes, int *pinned);
+void sstc_host_free(void *p, int pinned);
+
 /* Compact `ntables` input SSTs given in iterator order (compact.cc:186-230).
  * Their data blocks are listed table by table in d_blk_off/d_blk_len (block
  * index order); table t owns blocks [h_table_first_block[t],

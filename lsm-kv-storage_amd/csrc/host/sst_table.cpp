@@ -14,6 +14,7 @@
 #include <unistd.h>
 
 #include <cerrno>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -110,6 +111,27 @@ template <class T> DevBuf upload(sstc_ctx *ctx, const std::vector<T> &v) {
   return d;
 }
 
+} // namespace
+
+extern "C" void *sstc_host_alloc(uint64_t bytes, int *pinned) {
+  void *p = nullptr;
+  if (bytes && hipHostMalloc(&p, bytes, hipHostMallocPortable) == hipSuccess) {
+    if (pinned) *pinned = 1;
+    return p;
+  }
+  (void)hipGetLastError(); // no device / no pinning: ordinary memory
+  if (pinned) *pinned = 0;
+  return std::malloc(bytes ? bytes : 1);
+}
+
+extern "C" void sstc_host_free(void *p, int pinned) {
+  if (!p) return;
+  if (pinned) (void)hipHostFree(p);
+  else std::free(p);
+}
+
+namespace {
+
 void check(int rc, const char *what) {
   if (rc != SSTC_OK) throw std::runtime_error(std::string(what) + ": " + sstc_last_error_string());
 }
@@ -117,11 +139,49 @@ void check(int rc, const char *what) {
 } // namespace
 
 // ---------------------------------------------------------------- TableBuilder
+struct BuilderArena {
+  HostVec<uint8_t> type, keys, vals;
+  HostVec<uint32_t> kl, vl;
+  HostVec<uint64_t> txn, ko, vo, first;
+  void clear() {
+    for (auto *v : {&type, &keys, &vals}) v->clear();
+    kl.clear();
+    vl.clear();
+    for (auto *v : {&txn, &ko, &vo, &first}) v->clear();
+  }
+};
+
+namespace {
+// per-thread pool of builder arenas: a finished builder's pinned, faulted-in
+// arrays are the next builder's (the flush / compaction threads build SST
+// after SST; round 2 spent most of AddEntries in first-touch page faults)
+constexpr size_t kArenaPool = 4;
+thread_local std::vector<std::unique_ptr<BuilderArena>> g_arenas;
+
+BuilderArena *take_arena() {
+  if (g_arenas.empty()) return new BuilderArena();
+  BuilderArena *a = g_arenas.back().release();
+  g_arenas.pop_back();
+  return a;
+}
+
+void give_arena(BuilderArena *a) {
+  a->clear();
+  if (g_arenas.size() < kArenaPool) g_arenas.emplace_back(a);
+  else delete a;
+}
+} // namespace
+
 TableBuilder::TableBuilder(std::string filename, uint64_t block_threshold, sstc_ctx *ctx)
-    : filename_(std::move(filename)), threshold_(block_threshold), ctx_(ctx) {}
+    : filename_(std::move(filename)), threshold_(block_threshold), ctx_(ctx), arena_(take_arena()),
+      type_(arena_->type), key_len_(arena_->kl), val_len_(arena_->vl), txn_(arena_->txn), key_off_(arena_->ko),
+      val_off_(arena_->vo), keys_(arena_->keys), vals_(arena_->vals), blk_first_(arena_->first) {
+  blk_first_.push_back(0);
+}
 
 TableBuilder::~TableBuilder() {
   if (fd_ >= 0) ::close(fd_);
+  give_arena(arena_);
 }
 
 bool TableBuilder::Open() {
@@ -141,11 +201,11 @@ void TableBuilder::AddEntry(std::string_view key, std::string_view value, uint64
   type_.push_back(value_type);
   key_len_.push_back(static_cast<uint32_t>(key.size()));
   key_off_.push_back(keys_.size());
-  keys_.insert(keys_.end(), key.begin(), key.end());
+  keys_.append(reinterpret_cast<const uint8_t *>(key.data()), key.size());
   if (value.data()) {
     val_len_.push_back(static_cast<uint32_t>(value.size()));
     val_off_.push_back(vals_.size());
-    vals_.insert(vals_.end(), value.begin(), value.end());
+    vals_.append(reinterpret_cast<const uint8_t *>(value.data()), value.size());
   } else {
     val_len_.push_back(SSTC_NO_VALUE);
     val_off_.push_back(0);
@@ -182,10 +242,10 @@ void TableBuilder::AddEntries(uint64_t n, const uint8_t *type, const uint32_t *k
     type_.push_back(type[i]);
     key_len_.push_back(kl);
     key_off_.push_back(keys_.size());
-    keys_.insert(keys_.end(), key_src + key_off[i], key_src + key_off[i] + kl);
+    keys_.append(key_src + key_off[i], kl);
     if (vl != SSTC_NO_VALUE) {
       val_off_.push_back(vals_.size());
-      vals_.insert(vals_.end(), val_src + val_off[i], val_src + val_off[i] + vl);
+      vals_.append(val_src + val_off[i], vl);
     } else {
       val_off_.push_back(0);
     }
@@ -283,20 +343,21 @@ void TableBuilder::Finish() {
   const int dev = sstc__ctx_device(ctx_);
   DeviceScope on_ctx_device(dev);
   Staging &stage = g_stage[dev];
-  uint8_t *h = stage.Host(std::max(in_bytes, file_bytes) + 16 * nb + 16);
+  uint8_t *h = stage.Host(file_bytes + 16 * nb + 16); // the file image (blocks D2H'd straight into it)
   std::vector<uint64_t> blk_off(nb + 1), blk_len(nb);
   if (nb) {
-    std::memcpy(h + o_type, type_.data(), n);
-    std::memcpy(h + o_kl, key_len_.data(), 4 * n);
-    std::memcpy(h + o_vl, val_len_.data(), 4 * n);
-    std::memcpy(h + o_txn, txn_.data(), 8 * n);
-    std::memcpy(h + o_ko, key_off_.data(), 8 * n);
-    std::memcpy(h + o_vo, val_off_.data(), 8 * n);
-    std::memcpy(h + o_first, blk_first_.data(), 8 * (nb + 1));
-    std::memcpy(h + o_keys, keys_.data(), keys_.size());
-    std::memcpy(h + o_vals, vals_.data(), vals_.size());
     uint8_t *d = stage.Dev(dev_bytes);
-    h2d(ctx_, d, h, in_bytes); // pinned: a true async copy, ordered before the encode
+    // the arrays are pinned (HostVec): each goes up as a true async copy,
+    // ordered before the encode, with no pack copy on the host
+    h2d(ctx_, d + o_type, type_.data(), n);
+    h2d(ctx_, d + o_kl, key_len_.data(), 4 * n);
+    h2d(ctx_, d + o_vl, val_len_.data(), 4 * n);
+    h2d(ctx_, d + o_txn, txn_.data(), 8 * n);
+    h2d(ctx_, d + o_ko, key_off_.data(), 8 * n);
+    h2d(ctx_, d + o_vo, val_off_.data(), 8 * n);
+    h2d(ctx_, d + o_first, blk_first_.data(), 8 * (nb + 1));
+    h2d(ctx_, d + o_keys, keys_.data(), keys_.size());
+    h2d(ctx_, d + o_vals, vals_.data(), vals_.size());
     sstc_records rec{d + o_type, reinterpret_cast<uint32_t *>(d + o_kl), reinterpret_cast<uint32_t *>(d + o_vl),
                      reinterpret_cast<uint64_t *>(d + o_txn), reinterpret_cast<uint64_t *>(d + o_ko),
                      reinterpret_cast<uint64_t *>(d + o_vo)};
