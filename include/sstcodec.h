@@ -232,9 +232,14 @@ void sstc_host_free(void *p, int pinned);
  * Their data blocks are listed table by table in d_blk_off/d_blk_len (block
  * index order); table t owns blocks [h_table_first_block[t],
  * h_table_first_block[t+1]) (HOST array, ntables+1 elements).  Every input
- * table must be sorted (key ascending, equal keys txn descending), as
- * TableBuilder requires.  Records merge in MergeIterator order (key asc, txn
- * desc; equal (key, txn): lower input table first -- the reference's
+ * table must hold its keys in ascending order (SSTC_E_INVALID_ARG otherwise).
+ * The versions of a key may be in any txn order as read (the compat reader
+ * turns an empty-value PUT's txn t into (t & 0xffffffff) << 32,
+ * block_reader.cc:109-111): they merge as the reference's heap pops them, each
+ * input in file order under the smallest txn before it, for groups of up to
+ * 64 blocks (longer out-of-order groups: SSTC_E_INVALID_ARG).  Records merge
+ * in MergeIterator order (key asc, txn desc; equal (key, txn): lower input
+ * table first -- the reference's
  * std::priority_queue orders such ties by heap history, so inputs holding the
  * same (key, txn) with different contents may differ in order; identical
  * copies, the only kind the engine writes, give the same bytes), ShouldKeepEntry filters

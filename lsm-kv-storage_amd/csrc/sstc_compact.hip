@@ -58,6 +58,8 @@ struct Abort {
 // the prefixes tie) the remaining bytes, then the length (std::string_view <)
 __device__ __forceinline__ int key_cmp(uint64_t a0, uint64_t a1, uint32_t al, uint32_t aid, uint64_t b0,
                                        uint64_t b1, uint32_t bl, uint32_t bid, const KeyView &kv) {
+  al &= ~kSkRead; // SortKey::kl carries the read flag
+  bl &= ~kSkRead;
   if (a0 != b0) return a0 < b0 ? -1 : 1;
   if (a1 != b1) return a1 < b1 ? -1 : 1;
   if (al > 16 && bl > 16) {
@@ -86,11 +88,52 @@ __device__ __forceinline__ bool sk_less(const SK &a, const SK &b, const KeyView 
 // same-address atomic per workgroup (per wave with one block per thread, the
 // serialized atomics took config 3 18 -> 64 us, config 4 -> 104 us).
 constexpr uint32_t kCheckGrid = 512;
-__global__ __launch_bounds__(256) void ck_check_blocks_kernel(const SK *s, const uint64_t *rec_base, uint64_t nblocks,
+
+// A key group continuing from block b - 1 into block b (r = its first record
+// in b): the merge txns of block b's leading part take the running minimum of
+// the group's part before it (the decode computed it per block).  That
+// minimum is the smallest merge txn at the ends of the group's parts in the
+// earlier blocks (each part's last merge txn is its own running minimum), so
+// the walk goes back block end by block end, up to kGroupCarryBlocks blocks.
+// Other threads may lower those ends meanwhile; the minimum is the same.
+__device__ void carry_group(SK *s, const uint64_t *rec_base, uint64_t b, uint64_t r, uint64_t run0, const KeyView &kv,
+                            unsigned long long *bad, unsigned long long *guard) {
+  const SK k = s[r];
+  uint64_t carry = s[r - 1].tx, end = r - 1, bb = b;
+  for (uint32_t hop = 0;; hop++) {
+    // the block holding `end`, then the first record of the group's part in it
+    uint64_t q = bb - 1;
+    while (rec_base[q] > end) q--;
+    const uint64_t f = rec_base[q];
+    const SK y = s[f];
+    if (f == run0 || key_cmp(y.p0, y.p1, y.kl, y.id, k.p0, k.p1, k.kl, k.id, kv) != 0) break; // starts in q
+    const SK z = s[f - 1];
+    if (key_cmp(z.p0, z.p1, z.kl, z.id, k.p0, k.p1, k.kl, k.id, kv) != 0) break;
+    if (hop + 1 >= kGroupCarryBlocks) { // a key's versions over too many blocks: rejected
+      atomicOr(guard, kGuardLongGroup);
+      atomicAdd(bad, 1ull);
+      return;
+    }
+    end = f - 1;
+    bb = q;
+    carry = s[end].tx < carry ? s[end].tx : carry;
+  }
+  const uint64_t e = rec_base[b + 1];
+  for (uint64_t i = r; i < e; i++) {
+    SK x = s[i];
+    if (key_cmp(x.p0, x.p1, x.kl, x.id, k.p0, k.p1, k.kl, k.id, kv) != 0) break;
+    if (carry < x.tx) {
+      x.tx = carry;
+      x.kl |= kSkRead;
+      s[i] = x;
+    }
+  }
+}
+__global__ __launch_bounds__(256) void ck_check_blocks_kernel(SK *s, const uint64_t *rec_base, uint64_t nblocks,
                                        const uint64_t *run_start, uint64_t nruns, KeyView kv,
                                        unsigned long long *bad, Abort stop, uint64_t *zws, uint64_t nz,
                                        const uint64_t *blk_off, const uint64_t *blk_len,
-                                       unsigned long long *src_end) {
+                                       unsigned long long *src_end, unsigned long long *inv) {
   __shared__ uint64_t s_end[256 / kWave];
   const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
   const uint64_t t0 = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
@@ -110,7 +153,10 @@ __global__ __launch_bounds__(256) void ck_check_blocks_kernel(const SK *s, const
       else hi = mid;
     }
     if (run_start[lo] == r) continue; // first record of its run
-    if (sk_less(s[r], s[r - 1], kv)) atomicAdd(bad, 1ull);
+    const SK cur = s[r], pv = s[r - 1];
+    const int c = key_cmp(cur.p0, cur.p1, cur.kl, cur.id, pv.p0, pv.p1, pv.kl, pv.id, kv);
+    if (c < 0) atomicAdd(bad, 1ull);
+    if (c == 0 && cur.tx > pv.tx) atomicOr(inv, 1ull); // a group out of txn order across the boundary
   }
   for (uint32_t d = kWave / 2; d > 0; d >>= 1) {
     const uint64_t y = __shfl_xor(e, d, kWave);
@@ -121,6 +167,32 @@ __global__ __launch_bounds__(256) void ck_check_blocks_kernel(const SK *s, const
   if (threadIdx.x == 0) {
     for (uint32_t w = 1; w < 256 / kWave; w++) e = s_end[w] > e ? s_end[w] : e;
     if (e) atomicMax(src_end, static_cast<unsigned long long>(e));
+  }
+}
+
+// The cross-block carry of the merge txns (carry_group), run only when some
+// record's merge txn differs from its txn as read or a group is out of txn
+// order across a block boundary (inv): every continuing block boundary of
+// such a job takes its group's running minimum from the blocks before it.
+__global__ __launch_bounds__(256) void ck_carry_kernel(SK *s, const uint64_t *rec_base, uint64_t nblocks,
+                                                       const uint64_t *run_start, uint64_t nruns, KeyView kv,
+                                                       unsigned long long *bad, Abort stop,
+                                                       const unsigned long long *inv, unsigned long long *guard) {
+  if (!*inv || stop()) return;
+  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+  for (uint64_t b = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; b < nblocks; b += stride) {
+    const uint64_t r = rec_base[b];
+    if (r == 0 || rec_base[b + 1] == r) continue;
+    uint64_t lo = 0, hi = nruns;
+    while (lo + 1 < hi) {
+      const uint64_t mid = (lo + hi) >> 1;
+      if (run_start[mid] <= r) lo = mid;
+      else hi = mid;
+    }
+    if (run_start[lo] == r) continue;
+    const SK cur = s[r], pv = s[r - 1];
+    if (key_cmp(cur.p0, cur.p1, cur.kl, cur.id, pv.p0, pv.p1, pv.kl, pv.id, kv) == 0)
+      carry_group(s, rec_base, b, r, run_start[lo], kv, bad, guard);
   }
 }
 
@@ -561,11 +633,19 @@ __device__ __forceinline__ bool ff_same_key(const SK &a, const SK &b, const KeyV
 __device__ __forceinline__ bool ff_same_key_at(const SK &a, const SK &b, const KeyView &kv, uint64_t n) {
   return a.id < n && ff_same_key(a, b, kv);
 }
+// ShouldKeepEntry keeps a non-head record iff its txn (as read) is not below
+// its group head's (compact.cc:357-362, `!(last_txn > txn)`).  The head of a
+// merged group is an input's first version of the key, whose merge txn is its
+// txn as read; a record whose merge txn is its txn as read sits at or below
+// the head (merge txns descend through the group), so it needs an equal txn
+// all the way back (quick reject on its predecessor's merge txn).  Only a
+// lowered record (kSkRead; tread = its txn as read) can lie above the head.
 __device__ __forceinline__ uint32_t ff_keep(const SK *s, uint64_t i, const SK &x, const SK &pv, uint32_t ty,
-                                            uint32_t base_level, const KeyView &kv, uint64_t n) {
+                                            uint32_t base_level, const KeyView &kv, uint64_t n, uint64_t tread) {
   if (i == 0) return 1;
   if (!ff_same_key(pv, x, kv)) return ty == kTypePut ? 1u : (base_level ? 0u : 1u);
-  if (x.tx != pv.tx) return 0;
+  const bool lowered = (x.kl & kSkRead) != 0;
+  if (!lowered && x.tx != pv.tx) return 0;
   // group head = first record of x's key group: s[hi] has x's key, s[lo] not
   // (or lo = -1 past the start)
   uint64_t hi = i - 1;
@@ -585,13 +665,22 @@ __device__ __forceinline__ uint32_t ff_keep(const SK *s, uint64_t i, const SK &x
     if (ff_same_key_at(s[mid], x, kv, n)) hi = mid;
     else lo = static_cast<int64_t>(mid);
   }
-  return s[hi].tx == x.tx ? 1u : 0u;
+  return lowered ? (tread >= s[hi].tx ? 1u : 0u) : (s[hi].tx == x.tx ? 1u : 0u);
+}
+
+// the txn of record x as the reference's iterator reads it (parse_entry,
+// block_reader.cc:109-111): for a record whose merge txn was lowered
+// (kSkRead), re-read from its entry in the source
+__device__ __forceinline__ uint64_t read_txn(const KeyView &kv, const RecX &rx, uint32_t kl, uint32_t txn_mode) {
+  const bool after_value = rx.type != kTypeDeleted && !(txn_mode == 0u && rx.vl == 0u);
+  return g_u64u(kv.src + rx.ko + kl + (after_value ? 4ull + rx.vl : 0ull));
 }
 
 __global__ __launch_bounds__(kFtThreads) void ck_filter_kernel(const SK *s, uint64_t n, KeyView kv,
                                                                uint32_t base_level, Rec out, uint64_t *Pd,
                                                                uint64_t *Pe, uint64_t *ws, uint64_t *totals,
-                                                               Abort stop, unsigned long long *guard) {
+                                                               Abort stop, unsigned long long *guard,
+                                                               uint32_t txn_mode) {
   __shared__ uint64_t s_tile, s_pre[3];
   if (stop()) { // uniform over the grid: no ticket drawn, the host rejects the job
     if (blockIdx.x == 0 && threadIdx.x == 0) { // no survivor: the layout below splits nothing, writes nothing
@@ -631,17 +720,24 @@ __global__ __launch_bounds__(kFtThreads) void ck_filter_kernel(const SK *s, uint
     }
     if (__any(bad_id)) { // no key compare may follow such an id: the job is rejected
       if (lane == 0) atomicOr(guard, kGuardMergeId);
-      for (uint32_t g = 0; g < kGroup; g++) x[g].id = pv[g].id = 0;
+      for (uint32_t g = 0; g < kGroup; g++) {
+        x[g].id = pv[g].id = 0;
+        x[g].kl &= ~kSkRead; // and no source read for them
+      }
     }
+    uint64_t tread[kGroup]; // txns as read (a merge txn lowered by its group: re-read, rare)
+#pragma unroll
+    for (uint32_t g = 0; g < kGroup; g++)
+      tread[g] = x[g].kl & kSkRead ? read_txn(kv, rr[g], x[g].kl & ~kSkRead, txn_mode) : x[g].tx;
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (uint32_t g = 0; g < kGroup; g++) {
       const uint32_t j = j0 + g;
       const uint64_t i = t0 + static_cast<uint64_t>(j) * kFtThreads + tid;
-      const uint32_t k = i < n ? ff_keep(s, i, x[g], pv[g], rr[g].type, base_level, kv, n) : 0u;
+      const uint32_t k = i < n ? ff_keep(s, i, x[g], pv[g], rr[g].type, base_level, kv, n, tread[g]) : 0u;
       km |= k << j;
-      kl[j] = x[g].kl;
-      tx[j] = x[g].tx;
+      kl[j] = x[g].kl & ~kSkRead;
+      tx[j] = tread[g];
       vl[j] = rr[g].vl;
       ty[j] = rr[g].type;
       ko[j] = rr[g].ko;
@@ -1123,6 +1219,7 @@ __global__ __launch_bounds__(256) void ck_run_starts_kernel(const uint64_t *rec_
     *bad = 0;
     guard[0] = 0; // consistency-guard bits
     guard[1] = 0; // source end (ck_check_blocks_kernel)
+    guard[2] = 0; // merge txns out of txn order (decode_kernel, ck_check_blocks_kernel)
   }
   if (i < n) out[i] = rec_base[tfb[i]];
 }
@@ -1208,7 +1305,8 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     unsigned long long *bad = reinterpret_cast<unsigned long long *>(pool.get<uint64_t>(1));
     // consistency guard: [0] bits set by any check of the job, [1] the end of
     // the source bytes its blocks span (both cleared by ck_run_starts_kernel)
-    unsigned long long *guard = reinterpret_cast<unsigned long long *>(pool.get<uint64_t>(2));
+    unsigned long long *guard = reinterpret_cast<unsigned long long *>(pool.get<uint64_t>(3));
+    unsigned long long *inv = guard + 2; // merge txns need the cross-block carry (ck_carry_kernel)
     const uint64_t *src_end = reinterpret_cast<const uint64_t *>(guard + 1);
     // record index of every input table's first record (its run start)
     CK(hipMemcpyAsync(d_tfb, h_tfb, (ntables + 1) * 8, hipMemcpyHostToDevice, s));
@@ -1231,6 +1329,7 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     DecArgs da{d_src, d_blk_off, d_blk_len, nblocks, rb_all,
                sstc_records{}, txn_mode, status, err_count, A, bad};
     da.rx = RX;
+    da.inv = inv;
     CK(launch_decode(da, s));
     if (n == 0) { // DoCompactJob still finishes its first (empty) output table
       fetch(arena, s, {reinterpret_cast<const uint64_t *>(err_count), errs});
@@ -1325,7 +1424,9 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
       // the filter's look-back status words, cleared by the check kernel
       ffws = pool.get<uint64_t>(1 + 3 * fftiles);
       ck_check_blocks_kernel<<<std::min<uint32_t>(std::max<uint32_t>(grid(std::max<uint64_t>(nblocks, 1ull + 3 * fftiles)), 1u), kCheckGrid), 256, 0, s>>>(A, rb_all, nblocks, rb, nruns, kv, bad, dec_fail, ffws,
-                                                           1 + 3 * fftiles, d_blk_off, d_blk_len, guard + 1);
+                                                           1 + 3 * fftiles, d_blk_off, d_blk_len, guard + 1, inv);
+      ck_carry_kernel<<<std::min<uint32_t>(std::max<uint32_t>(grid(nblocks), 1u), kCheckGrid), 256, 0, s>>>(
+          A, rb_all, nblocks, rb, nruns, kv, bad, stop, inv, guard);
       if (!kg.empty()) {
         KGroup *d_kg = pool.get<KGroup>(kg.size());
         CK(hipMemcpyAsync(d_kg, kg.data(), kg.size() * sizeof(KGroup), hipMemcpyHostToDevice, s));
@@ -1360,7 +1461,7 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     // 3. keep / drop and the survivors gathered in merge order with their
     // prefix sums (sized by n: the kept count is known after the pass)
     ck_filter_kernel<<<static_cast<uint32_t>(fftiles), kFtThreads, 0, s>>>(A, n, kv, base_level, KR, Pd, Pe, ffws,
-                                                                        totals, stop, guard);
+                                                                        totals, stop, guard, txn_mode);
     if (arena.fault == 1) CK(hipMemsetAsync(KR.ko, 0xFF, n * sizeof(uint64_t), s)); // test: bad key offsets
     if (arena.fault == 2) CK(hipMemsetAsync(Pe, 0x5A, (n + 1) * sizeof(uint64_t), s)); // test: bad prefix sums
     // the job's error words (decode errors, unsorted inputs, guard bits) are
@@ -1374,8 +1475,13 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
         err = "an input block failed to decode";
         return SSTC_E_INVALID_ARG;
       }
+      if (h[3] & kGuardLongGroup) {
+        err = "an input holds versions of one key out of txn order as read over more than " +
+              std::to_string(kGroupCarryBlocks) + " blocks (unsupported)";
+        return SSTC_E_INVALID_ARG;
+      }
       if (h[2]) {
-        err = "input SST records are not sorted (key asc, txn desc)";
+        err = "input SST records are not sorted (key asc)";
         return SSTC_E_INVALID_ARG;
       }
       if (h[3] & kGuardMergeId) {

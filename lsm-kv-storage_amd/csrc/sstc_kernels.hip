@@ -510,7 +510,9 @@ constexpr uint32_t kDecWaves = 4;
 
 // Parse one block into the record table (and, when asked, the 32 B sort keys
 // of the compaction merge).  R reads block bytes (LDS image or HBM).
-template <class R>
+// kSk: the compaction's variant (merge keys with their running-minimum merge
+// txns; its registers stay out of the plain decode)
+template <bool kSk, class R>
 // base / base1: rec_base[b], rec_base[b + 1], loaded by the caller before it
 // waits for the block's bytes (one dependent round trip fewer per wave)
 __device__ __forceinline__ uint32_t decode_block(const DecArgs &a, const R &rd, uint64_t b, uint64_t off,
@@ -522,8 +524,9 @@ __device__ __forceinline__ uint32_t decode_block(const DecArgs &a, const R &rd, 
   uint32_t st = check_extra(len, n, doff);
   if (st == kBlkOk && n != uniform64(base1) - base) st = kBlkCountMismatch;
   if (st != kBlkOk) return st;
-  // previous record of the block (sortedness check): carried across chunks
-  uint64_t c0 = 0, c1 = 0, ctx = 0, cs = 0;
+  // previous record of the block (sortedness check): carried across chunks,
+  // with its merge txn (SortKey)
+  uint64_t c0 = 0, c1 = 0, ctx = 0, cs = 0, ceff = 0;
   uint32_t ckl = 0;
   for (uint64_t i0 = 0; i0 < n; i0 += kWave) {
     const uint64_t i = i0 + lane;
@@ -535,9 +538,12 @@ __device__ __forceinline__ uint32_t decode_block(const DecArgs &a, const R &rd, 
     }
     const uint64_t bad = __ballot(e.code != kBlkOk);
     if (bad) return __shfl(e.code, __ffsll(static_cast<long long>(bad)) - 1, kWave);
+    bool same = false; // same key as the block's previous record
     if (a.unsorted) {
       // TableBuilder requires sorted input (table_builder.h:77): a record may
-      // not sort before its predecessor (key asc, then txn desc)
+      // not sort before its predecessor (key asc, then txn desc).  The
+      // compaction (a.sk) checks the key order only: its merge txns absorb
+      // versions of a key that are out of txn order as read
       const uint64_t k0 = i < n && e.klen ? key_prefix8(__builtin_bswap64(rd.u64(s + 5)), e.klen) : 0;
       const uint64_t k1 = i < n && e.klen > 8 ? key_prefix8(__builtin_bswap64(rd.u64(s + 13)), e.klen - 8) : 0;
       uint64_t q0 = __shfl_up(k0, 1u, kWave), q1 = __shfl_up(k1, 1u, kWave);
@@ -557,13 +563,33 @@ __device__ __forceinline__ uint32_t decode_block(const DecArgs &a, const R &rd, 
           }
         }
         if (c == 0) c = e.klen < ql ? -1 : (e.klen > ql ? 1 : 0);
-        viol = c < 0 || (c == 0 && e.txn > qt);
+        viol = c < 0 || (c == 0 && !kSk && e.txn > qt);
+        same = c == 0;
       }
       const uint64_t v = __ballot(viol);
       if (v && lane == 0) atomicAdd(a.unsorted, static_cast<unsigned long long>(__popcll(v)));
       c0 = __shfl(k0, kWave - 1, kWave), c1 = __shfl(k1, kWave - 1, kWave);
       ctx = __shfl(e.txn, kWave - 1, kWave), cs = __shfl(s, kWave - 1, kWave);
       ckl = __shfl(e.klen, kWave - 1, kWave);
+    }
+    // merge txn: segmented running minimum of the txns as read over the key
+    // groups of the block (Hillis-Steele over (value, segment-start) pairs;
+    // lanes still open after it continue the previous chunk's last group)
+    uint64_t eff = e.txn;
+    if (kSk && a.unsorted) {
+      bool f = !same;
+#pragma unroll
+      for (uint32_t d = 1; d < kWave; d <<= 1) {
+        const uint64_t uv = __shfl_up(eff, d, kWave);
+        const bool uf = __shfl_up(static_cast<int>(f), d, kWave) != 0;
+        if (lane >= d && !f) {
+          eff = uv < eff ? uv : eff;
+          f = uf;
+        }
+      }
+      if (!f && i0 > 0) eff = ceff < eff ? ceff : eff;
+      ceff = __shfl(eff, kWave - 1, kWave);
+      if (a.inv && __any(i < n && eff != e.txn) && lane == 0) atomicOr(a.inv, 1ull);
     }
     if (i < n) {
       const uint64_t r = base + i;
@@ -581,13 +607,13 @@ __device__ __forceinline__ uint32_t decode_block(const DecArgs &a, const R &rd, 
         a.out.key_off[r] = off + s + 5;
         a.out.val_off[r] = e.type != kTypeDeleted ? off + s + 9 + e.klen : 0;
       }
-      if (a.sk) {
+      if (kSk) {
         // 16 B big-endian key prefix (a key is followed by >= 40 B of block)
         SortKey k;
         k.p0 = e.klen ? key_prefix8(__builtin_bswap64(rd.u64(s + 5)), e.klen) : 0;
         k.p1 = e.klen > 8 ? key_prefix8(__builtin_bswap64(rd.u64(s + 13)), e.klen - 8) : 0;
-        k.tx = e.txn;
-        k.kl = e.klen;
+        k.tx = eff;
+        k.kl = e.klen | (eff != e.txn ? kSkRead : 0u);
         k.id = static_cast<uint32_t>(r);
         a.sk[r] = k;
       }
@@ -599,6 +625,7 @@ __device__ __forceinline__ uint32_t decode_block(const DecArgs &a, const R &rd, 
 // One wave per block; a block that fits the LDS slot is staged by LDS-DMA and
 // parsed from LDS (the lane-per-entry header reads would otherwise be
 // dependent HBM round trips), a larger one is parsed from HBM.
+template <bool kSk>
 __global__ __launch_bounds__(kDecWaves *kWave) void decode_kernel(DecArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kDecWaves * kRtSlot];
   const uint32_t wave = uniform(threadIdx.x / kWave);
@@ -616,9 +643,9 @@ __global__ __launch_bounds__(kDecWaves *kWave) void decode_kernel(DecArgs a) {
     const uint64_t base = a.rec_base[b], base1 = a.rec_base[b + 1]; // in flight with the block's DMA
     rt_stage<1>(a.src + (off - pad), img, static_cast<uint32_t>((pad + len + 15) >> 4));
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    st = decode_block(a, LdsReader{img + pad}, b, off, len, base, base1);
+    st = decode_block<kSk>(a, LdsReader{img + pad}, b, off, len, base, base1);
   } else {
-    st = decode_block(a, GlobalReader{a.src + off}, b, off, len, a.rec_base[b], a.rec_base[b + 1]);
+    st = decode_block<kSk>(a, GlobalReader{a.src + off}, b, off, len, a.rec_base[b], a.rec_base[b + 1]);
   }
   if (lane_id() == 0) {
     if (a.status) a.status[b] = st;
@@ -2129,7 +2156,8 @@ hipError_t launch_count(const uint8_t *src, const uint64_t *blk_off, const uint6
 hipError_t launch_decode(const DecArgs &a, hipStream_t s) {
   DecArgs b = a;
   b.xcd = 1; // XCD-grouped block order: neighbouring blocks share L2 lines (-5 % time, config 3)
-  if (a.nblocks) decode_kernel<<<grid_for(a.nblocks, kDecWaves), kDecWaves * kWave, 0, s>>>(b);
+  if (a.nblocks && a.sk) decode_kernel<true><<<grid_for(a.nblocks, kDecWaves), kDecWaves * kWave, 0, s>>>(b);
+  else if (a.nblocks) decode_kernel<false><<<grid_for(a.nblocks, kDecWaves), kDecWaves * kWave, 0, s>>>(b);
   return hipGetLastError();
 }
 

@@ -27,10 +27,19 @@ struct RtArgs {
 };
 
 // 32 B merge key of one record (compaction): 16 B big-endian key prefix (zero
-// padded), txn, key length, record id.
+// padded), merge txn, key length, record id.  The merge txn is the txn as read
+// (compat or correct) run through a running minimum over the record's key
+// group in its input run, so an input whose versions of a key are not in
+// descending txn order as read (the compat empty-value quirk turns txn t into
+// (t & 0xffffffff) << 32, block_reader.cc:109-111) merges the way the
+// reference's MergeIterator heap pops it: a run's records leave in file order
+// and each competes with the others' heads under the smallest txn before it.
+// kSkRead in kl marks a record whose merge txn differs from its txn as read:
+// the filter re-reads that one from the source.
+constexpr uint32_t kSkRead = 1u << 31;
 struct __attribute__((aligned(16))) SortKey {
   uint64_t p0, p1, tx;
-  uint32_t kl, id;
+  uint32_t kl, id; // kl: key length | kSkRead
 };
 
 // per-record fields of the compaction job beside its SortKey (key length and
@@ -56,6 +65,9 @@ struct DecArgs {
   unsigned long long *unsorted = nullptr;
   RecX *rx = nullptr; // compaction: written instead of the `out` columns
   uint32_t xcd = 0;
+  // compaction: set when a record's merge txn differs from its txn as read
+  // (SortKey, kSkRead): the job then runs the cross-block carry
+  unsigned long long *inv = nullptr;
 };
 
 struct EncArgs {
@@ -96,7 +108,9 @@ struct EncArgs {
 
 // consistency-guard bits of the compaction job (sstc_compact.hip)
 constexpr unsigned long long kGuardMergeId = 1, kGuardEntry = 2, kGuardBlockRange = 4, kGuardMeta = 8,
-                             kGuardFooter = 16, kGuardLayout = 32;
+                             kGuardFooter = 16, kGuardLayout = 32, kGuardLongGroup = 64;
+// blocks a key group whose merge txns need a carry may span (ck_check_blocks_kernel)
+constexpr uint32_t kGroupCarryBlocks = 64;
 
 // point lookups (sstc_get.hip)
 struct GetArgs {

@@ -1,0 +1,109 @@
+"""Compaction job (sstc_compact) over randomised shapes against the oracle
+(oracle/ref_compact.cc restating Compact::DoCompactJob, compact.cc:232-363,
+pinned by the reference's own outputs in test_oracle_compact.py): block
+thresholds from 64 B to 64 KiB, table limits from one record per table to
+one table, key widths 6-20 B (past the 16 B merge prefix, sharing it), values up to
+96 KiB (blocks far past the encode's LDS slot), DELETE ratios, overlapping
+and disjoint key sets, 1-13 inputs.  Bit-exact at base levels 1 and 0.
+
+The job reads its kept count, table and block counts on the device only
+(round 4), so every shape here also exercises the count bounds the layout
+runs on (a table / block count past its bound would surface as
+SSTC_E_INTERNAL)."""
+import numpy as np
+import pytest
+from sstcodec import workload as W
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def codec():
+    import sstcodec
+    return sstcodec.Codec(0)
+
+
+def shapes():
+    rng = np.random.default_rng(2024)
+    out = []
+    for seed in range(14):
+        k = int(rng.integers(1, 14))
+        n_per = int(rng.integers(50, 2500))
+        vmax = int(rng.choice([16, 300, 4000, 98304]))
+        if vmax >= 4000:  # keep the inputs within tens of MB
+            k, n_per = min(k, 5), min(n_per, 200 if vmax > 4000 else 1200)
+        out.append(dict(
+            seed=seed, k=k, n_per=n_per,
+            space=int(n_per * rng.choice([1.2, 2.0, 8.0])),
+            key_width=int(rng.choice([6, 8, 16, 18, 20])),  # "k%0{w-1}d": distinct and sorted up to w = 20
+            vmin=int(rng.choice([0, 1, 8])),
+            vmax=vmax,
+            zipf=float(rng.choice([0.0, 1.1, 1.5])),
+            p_delete=float(rng.choice([0.0, 0.1, 0.5, 0.9])),
+            distinct=bool(rng.random() < 0.8),
+            threshold=int(rng.choice([64, 512, 4096, 16384, 65536])),
+            limit_frac=float(rng.choice([0.0, 0.05, 0.3, 2.0])),
+        ))
+    return out
+
+
+SHAPES = shapes()
+
+
+@pytest.mark.timeout(240)
+@pytest.mark.parametrize("shape", SHAPES, ids=[f"s{s['seed']}" for s in SHAPES])
+def test_compact_fuzz_vs_oracle(codec, oracle, shape):
+    s = shape
+    sets = W.compaction_inputs(s["k"], s["n_per"], s["space"], seed=1000 + s["seed"], p_delete=s["p_delete"],
+                               vmin=max(s["vmin"], 1) if s["zipf"] else s["vmin"], vmax=s["vmax"],
+                               key_width=s["key_width"], distinct=s["distinct"], zipf=s["zipf"] or None)
+    ins = [oracle.table_build(r, s["threshold"]) for r in sets]
+    total = sum(int(f.size) for f in ins)
+    limit = max(1, int(total * s["limit_frac"]))  # 0.0 -> 1 B: every record its own table
+    for base in (1, 0):
+        want, kept = oracle.compact(ins, s["threshold"], limit, base)
+        outs, res = codec.compact(ins, s["threshold"], limit, base)
+        assert res.records_kept == kept
+        assert res.tables_out == len(want) == len(outs)
+        for t, (o, w) in enumerate(zip(outs, want)):
+            assert np.array_equal(o, w), f"output table {t} of {len(want)} differs (base {base})"
+
+
+@pytest.mark.parametrize("threshold", [256, 4096])
+@pytest.mark.parametrize("seed", range(3))
+def test_compact_versions_out_of_txn_order(codec, oracle, seed, threshold):
+    """Several versions of a key in one input, some of them empty-value PUTs:
+    the reference's reader returns (txn & 0xffffffff) << 32 for those
+    (block_reader.cc:109-111), so a key's versions are out of txn order as
+    read, and its MergeIterator heap pops each input in file order under the
+    smallest txn so far.  The job merges on that running minimum (per block
+    in the decode, carried across block boundaries: with 256 B blocks a key's
+    ~30 versions span several blocks) and writes the txns as read."""
+    sets = W.compaction_inputs(3, 1500, 50, seed=70 + seed, p_delete=0.1, vmin=0, vmax=3, key_width=16,
+                               distinct=False)
+    ins = [oracle.table_build(r, threshold) for r in sets]
+    for base in (1, 0):
+        want, kept = oracle.compact(ins, threshold, 1 << 20, base)
+        outs, res = codec.compact(ins, threshold, 1 << 20, base)
+        assert res.records_kept == kept and len(outs) == len(want)
+        for o, w in zip(outs, want):
+            assert np.array_equal(o, w)
+
+
+def test_compact_long_version_groups(codec, oracle):
+    """One key's versions over more than kGroupCarryBlocks (64) blocks of an
+    input: in txn order they compact like any other input; out of txn order
+    as read (an empty-value version) the running minimum would have to be
+    carried over more than 64 blocks, which the job rejects with
+    SSTC_E_INVALID_ARG rather than merge wrongly."""
+    import sstcodec
+    sets = W.compaction_inputs(1, 1200, 2, seed=5, p_delete=0.0, vmin=4, vmax=8, key_width=16, distinct=False)
+    ins = [oracle.table_build(r, 128) for r in sets]  # ~3 records per block: ~200 blocks per key
+    want, _ = oracle.compact(ins, 128, 1 << 20, 1)
+    outs, _ = codec.compact(ins, 128, 1 << 20, 1)
+    assert len(outs) == len(want) and all(np.array_equal(o, w) for o, w in zip(outs, want))
+    rec = {key: v.copy() for key, v in sets[0].items()}
+    rec["val_len"][len(rec["val_len"]) // 2] = 0  # one empty-value PUT mid-group: its txn as read jumps
+    bad = [oracle.table_build(rec, 128)]
+    with pytest.raises(sstcodec.SstcError, match="unsupported"):
+        codec.compact(bad, 128, 1 << 20, 1)
