@@ -107,3 +107,75 @@ def test_compact_long_version_groups(codec, oracle):
     bad = [oracle.table_build(rec, 128)]
     with pytest.raises(sstcodec.SstcError, match="unsupported"):
         codec.compact(bad, 128, 1 << 20, 1)
+
+
+def wide_shapes():
+    """Many inputs (multi-pass merges: 8 / 4-way splitter lanes, 2-3 passes),
+    tiny key spaces (long version groups, 2 B keys)."""
+    rng = np.random.default_rng(77)
+    out = []
+    for seed, k in enumerate([20, 64, 130, 9, 33]):
+        tiny = seed >= 3
+        out.append(dict(seed=100 + seed, k=k, n_per=int(rng.integers(30, 300)),
+                        space=8 if tiny else int(rng.integers(200, 5000)),
+                        key_width=2 if tiny else int(rng.choice([8, 16, 20])),
+                        vmax=int(rng.choice([0, 40, 500])), p_delete=float(rng.choice([0.0, 0.3])),
+                        threshold=int(rng.choice([128, 4096])), distinct=not tiny))
+    return out
+
+
+WIDE = wide_shapes()
+
+
+@pytest.mark.timeout(240)
+@pytest.mark.parametrize("shape", WIDE, ids=[f"w{s['seed']}" for s in WIDE])
+def test_compact_fuzz_wide_vs_oracle(codec, oracle, shape):
+    s = shape
+    sets = W.compaction_inputs(s["k"], s["n_per"], s["space"], seed=s["seed"], p_delete=s["p_delete"], vmin=0,
+                               vmax=s["vmax"], key_width=s["key_width"], distinct=s["distinct"])
+    ins = [oracle.table_build(r, s["threshold"]) for r in sets]
+    for base in (1, 0):
+        for limit in (1 << 30, 20_000):
+            want, kept = oracle.compact(ins, s["threshold"], limit, base)
+            outs, res = codec.compact(ins, s["threshold"], limit, base)
+            assert res.records_kept == kept and len(outs) == len(want)
+            for o, w in zip(outs, want):
+                assert np.array_equal(o, w)
+
+
+@pytest.mark.timeout(240)
+@pytest.mark.parametrize("shape", SHAPES[:6] + WIDE[3:], ids=[f"s{s['seed']}" for s in SHAPES[:6] + WIDE[3:]])
+def test_compact_files_fuzz_vs_oracle(codec, oracle, shape, tmp_path):
+    """The same shapes through sstc_compact_files (footer / meta parse on the
+    host, preads, the device job, pwrite + fsync): every output file equals
+    the oracle's table, with the key range VersionEdit::AddNewFiles records."""
+    import sstcodec
+    s = shape
+    zipf = s.get("zipf") or None
+    sets = W.compaction_inputs(s["k"], s["n_per"], s["space"], seed=(1000 if "limit_frac" in s else 0) + s["seed"],
+                               p_delete=s["p_delete"], vmin=(max(s["vmin"], 1) if zipf else s["vmin"]) if "vmin" in s else 0,
+                               vmax=s["vmax"], key_width=s["key_width"], distinct=s["distinct"], zipf=zipf)
+    ins = [oracle.table_build(r, s["threshold"]) for r in sets]
+    limit = max(1, int(sum(int(f.size) for f in ins) * s.get("limit_frac", 0.3)))
+    paths, sizes = [], []
+    for i, img in enumerate(ins):
+        p = tmp_path / f"in{i}.sst"
+        img.tofile(p)
+        paths.append(str(p))
+        sizes.append(img.size + 1)  # GetFileSize
+    want, _ = oracle.compact(ins, s["threshold"], limit, 1)
+    (tmp_path / "out").mkdir()
+    pipe = sstcodec.FilePipe(codec, io_threads=4)
+    try:
+        outs, _ = pipe.compact_files(paths, sizes, str(tmp_path / "out") + "/", 1, s["threshold"], limit, 1)
+    finally:
+        pipe.close()
+    assert len(outs) == len(want)
+    for (sid, fsize, lo, hi), w in zip(outs, want):
+        got = np.fromfile(tmp_path / "out" / f"{sid}.sst", np.uint8)
+        assert fsize == w.size + 1 and np.array_equal(got, w)
+        ix = oracle.table_index(w)  # the table's first / last key from its own meta section
+        if ix["nblocks"]:
+            f0, l0 = int(ix["first_key_off"][0]), int(ix["first_key_len"][0])
+            f1, l1 = int(ix["last_key_off"][-1]), int(ix["last_key_len"][-1])
+            assert lo == bytes(w[f0:f0 + l0]) and hi == bytes(w[f1:f1 + l1])
