@@ -69,17 +69,21 @@ def test_compact_fuzz_vs_oracle(codec, oracle, shape):
             assert np.array_equal(o, w), f"output table {t} of {len(want)} differs (base {base})"
 
 
+@pytest.mark.parametrize("space", [50, 12])
 @pytest.mark.parametrize("threshold", [256, 4096])
 @pytest.mark.parametrize("seed", range(3))
-def test_compact_versions_out_of_txn_order(codec, oracle, seed, threshold):
+def test_compact_versions_out_of_txn_order(codec, oracle, seed, threshold, space):
     """Several versions of a key in one input, some of them empty-value PUTs:
     the reference's reader returns (txn & 0xffffffff) << 32 for those
     (block_reader.cc:109-111), so a key's versions are out of txn order as
     read, and its MergeIterator heap pops each input in file order under the
     smallest txn so far.  The job merges on that running minimum (per block
     in the decode, carried across block boundaries: with 256 B blocks a key's
-    ~30 versions span several blocks) and writes the txns as read."""
-    sets = W.compaction_inputs(3, 1500, 50, seed=70 + seed, p_delete=0.1, vmin=0, vmax=3, key_width=16,
+    ~30 versions span several blocks) and writes the txns as read.  The
+    oracle is pinned for these inputs by the reference's own MergeIterator
+    (tests/test_oracle_compact.py::test_live_ref_compact_versions_out_of_txn_order:
+    seed 71, 4 KiB blocks)."""
+    sets = W.compaction_inputs(3, 1500, space, seed=70 + seed, p_delete=0.1, vmin=0, vmax=3, key_width=16,
                                distinct=False)
     ins = [oracle.table_build(r, threshold) for r in sets]
     for base in (1, 0):

@@ -153,3 +153,36 @@ def test_fixture_exercises_base_level_tombstone_drop(oracle, name):
     outs0, _ = oracle.compact(files, case["block_threshold"], case["table_limit"], 0)
     kept0 = {k for o in outs0 for k, _, _, _ in sst_records(oracle, o)}
     assert heads_deleted <= kept0  # base_level 0 keeps them (framework-defined mode)
+
+
+@pytest.mark.parametrize("space", [50, 12])
+def test_live_ref_compact_versions_out_of_txn_order(oracle, space):
+    """Several versions of a key per input with empty-value PUTs among them:
+    the reference's reader returns their txns as (t & 0xffffffff) << 32, so a
+    key's versions are out of txn order as read.  The oracle's merge (each
+    input in file order, best head first) and keep rule (`!(last_txn > txn)`)
+    equal the reference's own MergeIterator + DoCompactJob loop here -- the
+    pin for tests/test_gpu_compact_fuzz.py's out-of-order cases.  (4 KiB
+    blocks: the reference driver aborts below its default block size; with
+    12 keys a key's ~125 versions per input cross block boundaries.)"""
+    threshold = 4096
+    from oracle import REF_COMPACT, ref_compact
+    if not os.path.exists(REF_COMPACT):
+        pytest.skip("reference compaction driver not built")
+    sets = W.compaction_inputs(3, 1500, space, seed=71, p_delete=0.1, vmin=0, vmax=3, key_width=16, distinct=False)
+    with tempfile.TemporaryDirectory() as td:
+        ins, files = [], []
+        for i, rec in enumerate(sets):
+            f = oracle.table_build(rec, threshold)
+            p = os.path.join(td, f"i{i}.sst")
+            f.tofile(p)
+            ins.append((p, f.size + 1))
+            files.append(f)
+        od = os.path.join(td, "o")
+        os.makedirs(od)
+        outs = ref_compact(ins, od, threshold, 1 << 20, 1)
+        mine, kept = oracle.compact(files, threshold, 1 << 20, 1)
+        assert kept > 50  # versions above their group head survive (compact.cc:357-362)
+        assert len(outs) == len(mine)
+        for (p, fs), m in zip(outs, mine):
+            assert np.array_equal(np.fromfile(p, np.uint8), m) and fs == m.size + 1
