@@ -5,7 +5,7 @@ import sys
 
 rows = list(csv.DictReader(open(sys.argv[1])))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-idx = [i for i, r in enumerate(rows) if r["Kernel_Name"].startswith("sstc::decode_kernel")]
+idx = [i for i, r in enumerate(rows) if "sstc::decode_kernel" in r["Kernel_Name"]]
 start = idx[-1] - 2
 t0 = int(rows[start]["Start_Timestamp"])
 last = t0
