@@ -183,3 +183,46 @@ def test_compact_files_fuzz_vs_oracle(codec, oracle, shape, tmp_path):
             f0, l0 = int(ix["first_key_off"][0]), int(ix["first_key_len"][0])
             f1, l1 = int(ix["last_key_off"][-1]), int(ix["last_key_len"][-1])
             assert lo == bytes(w[f0:f0 + l0]) and hi == bytes(w[f1:f1 + l1])
+
+
+@pytest.mark.parametrize("k", [3, 9, 20])
+def test_compact_with_empty_inputs_among_others(codec, oracle, k):
+    """Empty input SSTs (40 B: footer only) between non-empty ones: zero-length
+    runs in every merge pass (9 and 20 inputs: multi-pass groups with empty
+    runs), at both base levels."""
+    sets = W.compaction_inputs(k, 400, 3000, seed=500 + k, p_delete=0.2, vmax=50)
+    empty = W.compaction_inputs(1, 0, 10)[0]
+    ins = []
+    for i, r in enumerate(sets):
+        if i % 3 == 1:
+            ins.append(oracle.table_build(empty, 4096))
+        ins.append(oracle.table_build(r, 4096))
+    ins.append(oracle.table_build(empty, 4096))
+    for base in (1, 0):
+        want, kept = oracle.compact(ins, 4096, 30_000, base)
+        outs, res = codec.compact(ins, 4096, 30_000, base)
+        assert res.records_kept == kept and len(outs) == len(want)
+        for o, w in zip(outs, want):
+            assert np.array_equal(o, w)
+
+
+def ragged_sorted(n, seed):
+    """mixed_records sorted by key bytes (std::string_view order): ragged keys
+    0-48 B (the empty key repeats, with random txns: out of txn order),
+    empty values (the txn quirk), DELETEs."""
+    r = W.mixed_records(n, seed=seed, max_key=48, max_val=120, p_delete=0.15, p_empty_val=0.1, p_empty_key=0.05)
+    keys = [r["key_src"][int(o):int(o) + int(l)].tobytes() for o, l in zip(r["key_off"], r["key_len"])]
+    order = sorted(range(n), key=lambda i: keys[i])
+    return {k: (v[order] if k not in ("key_src", "val_src") else v) for k, v in r.items()}
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_compact_ragged_keys_vs_oracle(codec, oracle, seed):
+    sets = [ragged_sorted(int(900 + 300 * t), 600 + 10 * seed + t) for t in range(2 + 2 * seed)]
+    ins = [oracle.table_build(r, 4096) for r in sets]
+    for base in (1, 0):
+        want, kept = oracle.compact(ins, 4096, 50_000, base)
+        outs, res = codec.compact(ins, 4096, 50_000, base)
+        assert res.records_kept == kept and len(outs) == len(want)
+        for o, w in zip(outs, want):
+            assert np.array_equal(o, w)
