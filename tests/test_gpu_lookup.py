@@ -89,3 +89,24 @@ def test_lookup_malformed_block(codec, oracle):
     ot, _, _, oblk = oracle.table_get(img, keys)
     assert np.array_equal(typ, ot) and (typ[blk == b] == 4).all() and (typ == 4).any()
     assert codec.error_count() == int((typ == 4).sum())
+
+
+@pytest.mark.parametrize("seed", range(2))
+def test_lookup_ragged_keys_vs_oracle(codec, oracle, seed):
+    """Ragged 0-48 B keys (the empty key repeated with random txns, so a block
+    holds several versions of it out of txn order), empty values, DELETEs:
+    every probe -- present keys, their prefixes and extensions, the empty key
+    -- answers as the reference's GetValue (oracle, pinned by lookup.npz)."""
+    import sstcodec
+    from test_gpu_compact_fuzz import ragged_sorted
+    rec = ragged_sorted(6000, 800 + seed)
+    img = oracle.table_build(rec, [4096, 512][seed])
+    present = [rec["key_src"][int(o):int(o) + int(l)].tobytes() for o, l in zip(rec["key_off"], rec["key_len"])]
+    rng = np.random.default_rng(seed)
+    keys = present[::3] + [k[:-1] for k in present[1::7]] + [k + b"\x00" for k in present[2::11]] + [b"", b"~~~~"]
+    keys = [keys[i] for i in rng.permutation(len(keys))]
+    typ, vo, vl, blk = sstcodec.Lookup(codec, [img]).get(np.zeros(len(keys), np.uint32), keys)
+    ot, ovo, ovl, oblk = oracle.table_get(img, keys)
+    assert np.array_equal(typ, ot) and np.array_equal(blk, oblk)
+    put = typ == 0
+    assert np.array_equal(vo[put], ovo[put]) and np.array_equal(vl[put], ovl[put])
