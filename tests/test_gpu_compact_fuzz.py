@@ -226,3 +226,16 @@ def test_compact_ragged_keys_vs_oracle(codec, oracle, seed):
         assert res.records_kept == kept and len(outs) == len(want)
         for o, w in zip(outs, want):
             assert np.array_equal(o, w)
+
+
+def test_compact_inputs_of_mixed_block_sizes(codec, oracle):
+    """Inputs written with different block thresholds (512 B .. 64 KiB, some
+    blocks past the decode's LDS slot) compacted into 16 KiB blocks."""
+    sets = W.compaction_inputs(5, 1500, 4000, seed=808, p_delete=0.2, vmin=0, vmax=900)
+    ins = [oracle.table_build(r, t) for r, t in zip(sets, (512, 4096, 65536, 1024, 16384))]
+    for base in (1, 0):
+        want, kept = oracle.compact(ins, 16384, 200_000, base)
+        outs, res = codec.compact(ins, 16384, 200_000, base)
+        assert res.records_kept == kept and len(outs) == len(want)
+        for o, w in zip(outs, want):
+            assert np.array_equal(o, w)
