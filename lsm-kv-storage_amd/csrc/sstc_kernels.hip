@@ -1417,8 +1417,11 @@ __global__ __launch_bounds__(kEncWaves *kWave) void enc_lds_kernel(EncArgs a) {
 //    jumping over nodes (log8 tiles levels) with segment counts.
 //  C every visited tile learns its entry and the segments before it, then
 //    seg_emit_kernel re-walks its part of the chain and writes the starts.
-// Few long segments (output tables): seg_hops_kernel, one workgroup hopping
-// along the chain with a 4096-ary search of W per hop.
+// Few long segments (output tables): seg_spec_kernel takes the hop from every
+// predicted segment start in parallel (one wave per start), then
+// seg_hops_kernel, one wave, follows the chain through those answers and hops
+// on its own (windows around the predicted ends, a 512-ary search of W) from
+// the first start that was not predicted.
 // ---------------------------------------------------------------------------
 constexpr uint32_t kChTile = 1024, kChThreads = 256, kChMargin = 256;
 constexpr uint32_t kSegRadix = 8;
@@ -1473,25 +1476,27 @@ struct SegArgs {
   const uint64_t *mp;     // optional: the record count on the device (m is then its bound)
 };
 
-// index of the first end > i (ends sorted, ends[ne] = m > i)
-__device__ __forceinline__ uint64_t seg_end_index(const uint64_t *ends, uint64_t ne, uint64_t i) {
-  uint64_t lo = 0, hi = ne; // first t in [0, ne] with ends[t] > i
-  while (lo < hi) {
-    const uint64_t mid = (lo + hi) >> 1;
-    if (ends[mid] > i) hi = mid;
-    else lo = mid + 1;
-  }
-  return lo;
-}
+// table ends cached in LDS by seg_walk_kernel: ends[t0 - 1 + j], j < kEndCache
+constexpr uint32_t kEndCache = 16;
 
 __global__ __launch_bounds__(kChThreads) void seg_walk_kernel(SegArgs a) {
   constexpr uint32_t kLw = kChTile + kChMargin;
   __shared__ uint64_t lw[kLw + kLw / 8];
   __shared__ uint32_t jn[kChTile], jc[kChTile];
-  __shared__ uint64_t s_wend, s_t0;
+  __shared__ uint64_t s_wend, s_t0, s_e[kEndCache], s_ec;
   const uint32_t tid = threadIdx.x;
-  const uint64_t m = a.mp ? *a.mp : a.m;
   const uint64_t c0 = static_cast<uint64_t>(blockIdx.x) * kChTile;
+  // the window's loads go out on the host bound a.m (Pw holds a.m + 1 words),
+  // together with the device count's: one round trip instead of two
+  constexpr uint32_t kFill = kLw / kChThreads;
+  const uint64_t nlh = a.m + 1 - c0 < kLw ? a.m + 1 - c0 : kLw;
+  uint64_t v[kFill];
+#pragma unroll
+  for (uint32_t r = 0; r < kFill; r++) {
+    const uint32_t x = tid + r * kChThreads;
+    v[r] = x < nlh ? a.Pw[c0 + x] : 0;
+  }
+  const uint64_t m = a.mp ? *a.mp : a.m;
   if (tid == 0) {
     a.tentry[blockIdx.x] = 0;
     if (blockIdx.x == 0) a.tentry[gridDim.x] = 0;
@@ -1504,31 +1509,59 @@ __global__ __launch_bounds__(kChThreads) void seg_walk_kernel(SegArgs a) {
   const uint64_t c1 = c0 + kChTile < m ? c0 + kChTile : m;
   const uint32_t len = static_cast<uint32_t>(c1 - c0);
   const uint64_t nl = m + 1 - c0 < kLw ? m + 1 - c0 : kLw;
-  const uint64_t ne = a.ends ? *a.nends : 0;
-  if (tid == 0) s_t0 = a.ends ? seg_end_index(a.ends, ne, c0) : 0; // first table end past the tile start
-  { // all loads of the window in flight before the LDS stores
-    constexpr uint32_t kFill = kLw / kChThreads;
-    uint64_t v[kFill];
-#pragma unroll
-    for (uint32_t r = 0; r < kFill; r++) {
-      const uint32_t x = tid + r * kChThreads;
-      v[r] = x < nl ? a.Pw[c0 + x] : 0;
+  if (a.ends && tid < kWave) {
+    // t0 = the first table end past the tile start (ends[0..ne] sorted, ends[ne]
+    // = m > c0): a 64-ary search by wave 0, one round trip while ne < 64 (a
+    // thread's binary search was log2(ne) dependent loads on every
+    // workgroup's critical path); its last round leaves ends[t0 - 1 ..] in
+    // the lanes, cached in LDS for the clamps below
+    const uint32_t lane = tid;
+    const uint64_t ne = *a.nends;
+    uint64_t lo = 0, n = ne + 1, below = 0, e = 0; // answer in [lo, lo + n); ends[lo - 1] = below
+    uint32_t f = 0;
+    for (;;) {
+      const uint64_t step = (n + kWave - 1) / kWave;
+      const uint64_t off = static_cast<uint64_t>(lane) * step;
+      const uint64_t x = step == 1 ? (lo + lane < ne ? lo + lane : ne) : lo + (off < n - 1 ? off : n - 1);
+      e = a.ends[x];
+      const uint64_t gt = __ballot(e > c0); // a suffix of the lanes, lane min(n - 1, 63) at least
+      f = static_cast<uint32_t>(__ffsll(static_cast<long long>(gt))) - 1u;
+      if (step == 1) break;
+      if (f) below = readlane_u64(e, f - 1);
+      const uint64_t nlo = f ? lo + static_cast<uint64_t>(f - 1) * step + 1 : lo;
+      const uint64_t xf = lo + (static_cast<uint64_t>(f) * step < n - 1 ? static_cast<uint64_t>(f) * step : n - 1);
+      n = xf - nlo + 1;
+      lo = nlo;
     }
-#pragma unroll
-    for (uint32_t r = 0; r < kFill; r++) {
-      const uint32_t x = tid + r * kChThreads;
-      if (x < nl) lw[lw_slot(x)] = v[r] + a.add * (c0 + x);
+    const uint64_t t0 = lo + f;
+    if (f) below = readlane_u64(e, f - 1);
+    const int64_t j = static_cast<int64_t>(lo + lane) - static_cast<int64_t>(t0) + 1; // slot of ends[lo + lane]
+    if (j >= 1 && j < static_cast<int64_t>(kEndCache) && lo + lane <= ne) s_e[j] = e;
+    if (lane == 0) {
+      s_e[0] = below; // ends[t0 - 1] (unused when t0 = 0)
+      const uint64_t last = lo + kWave - 1 < ne ? lo + kWave - 1 : ne; // ends[t0 - 1 .. last] are cached
+      const uint64_t nc = last + 2 - t0;
+      s_ec = nc < kEndCache ? nc : kEndCache;
+      s_t0 = t0;
     }
   }
+#pragma unroll
+  for (uint32_t r = 0; r < kFill; r++) {
+    const uint32_t x = tid + r * kChThreads;
+    if (x < nl) lw[lw_slot(x)] = v[r] + a.add * (c0 + x);
+  }
   __syncthreads();
+  const uint64_t t0 = a.ends ? s_t0 : 0, ec = a.ends ? s_ec : 0;
+  auto end_at = [&](uint64_t t) -> uint64_t { // ends[t], t >= t0 - 1
+    const uint64_t j = t + 1 - t0;
+    return j < ec ? s_e[j] : a.ends[t];
+  };
   const SegW W{a.Pw, lw, a.add, c0, nl};
   if (tid == kChThreads - 1) { // entry window end: J0 of the record before the tile
     const uint64_t i = c0 - 1;
     uint64_t lim = m;
-    if (a.ends) { // first end > c0 - 1: s_t0, or the one before it when it equals c0
-      const uint64_t t = s_t0;
-      lim = t > 0 && a.ends[t - 1] == c0 ? c0 : a.ends[t];
-    }
+    if (a.ends) // first end > c0 - 1: t0, or the one before it when it equals c0
+      lim = t0 > 0 && end_at(t0 - 1) == c0 ? c0 : end_at(t0);
     s_wend = blockIdx.x ? seg_next_at(W, i, lim, a.threshold, i) : c0;
   }
   // J0 of kPer consecutive records per thread: gallop for the first, then from
@@ -1537,13 +1570,13 @@ __global__ __launch_bounds__(kChThreads) void seg_walk_kernel(SegArgs a) {
   uint64_t lim[kPer];
   {
     const uint64_t i0 = c0 + tid * kPer;
-    uint64_t t = s_t0;
-    uint64_t end = a.ends ? a.ends[t] : m; // ends[ne] = m: the walks below stop at ne
+    uint64_t t = t0;
+    uint64_t end = a.ends ? end_at(t) : m; // ends[ne] = m: the walks below stop at ne
 #pragma unroll
     for (uint32_t r = 0; r < kPer; r++) {
       const uint64_t i = i0 + r;
       if (a.ends && i < m)
-        while (end <= i) end = a.ends[++t]; // ends[ne] = m > i
+        while (end <= i) end = end_at(++t); // ends[ne] = m > i
       lim[r] = i < c1 ? end : 0;
     }
   }
@@ -1846,27 +1879,82 @@ __device__ uint64_t hop_exact(const uint64_t *Pw, uint64_t add, uint64_t m, uint
 // is not inside its window falls back to hop_exact and starts a new round.
 // Equal-sized tables: ~2 load round trips per kHopAhead tables instead of 2
 // per table.
-constexpr uint32_t kHopAhead = 8;
+constexpr uint32_t kHopAhead = 8, kSpecProbe = kHopProbe;
+constexpr uint64_t kSpecSpan = kHopSpan;
+
+// predicted segment length from the mean weight of nrec records of total
+// weight rest (equal-sized records: the exact length); 0: none
+__device__ __forceinline__ uint64_t hop_predict(uint64_t threshold, uint64_t nrec, uint64_t rest) {
+  const uint64_t g = rest ? static_cast<uint64_t>(ceil(static_cast<double>(threshold) * static_cast<double>(nrec) /
+                                                       static_cast<double>(rest)))
+                          : 0;
+  return g >= 1 && g <= nrec ? g : 0;
+}
+
+// Hops in parallel: a lone wave pays an address-translation walk for every
+// page its probes touch, one after another (measured: ~0.9 us per output
+// table, whether a round speculates 8 or 32 hops; touching the pages first
+// just moves the cost), so seg_spec_kernel runs one wave per predicted
+// segment start h * g on as many CUs, each taking the exact hop from there
+// (spec[h]); seg_hops_kernel follows the chain through these answers while
+// every hop starts where predicted (equal-sized tables: all of them) and hops
+// on its own from the first one that does not.
+constexpr uint32_t kSpecHops = 256;
+
+__global__ __launch_bounds__(kWave) void seg_spec_kernel(const uint64_t *Pw, uint64_t add, uint64_t m,
+                                                         const uint64_t *mp, uint64_t threshold, uint64_t *spec) {
+  if (mp) m = *mp;
+  if (m == 0) return;
+  const uint64_t w0 = Pw[0], wm = Pw[m] + add * m;
+  if (wm - w0 < threshold) return;
+  const uint64_t g = hop_predict(threshold, m, wm - w0);
+  const uint64_t p = static_cast<uint64_t>(blockIdx.x) * g;
+  if (g == 0 || p >= m) return;
+  const uint64_t target = Pw[p] + add * p + threshold;
+  const uint64_t nx = wm < target ? m : hop_exact(Pw, add, m, p, g, target); // m: the last segment
+  if (lane_id() == 0) spec[blockIdx.x] = nx;
+}
 
 __global__ __launch_bounds__(kWave) void seg_hops_kernel(const uint64_t *Pw, uint64_t add, uint64_t m,
                                                          const uint64_t *mp, uint64_t threshold, uint64_t *first,
-                                                         uint64_t *d_count) {
+                                                         uint64_t *d_count, const uint64_t *spec) {
   const uint32_t lane = lane_id();
   if (mp) m = *mp; // m = 0: no segment, first[0] = 0
   const uint64_t wm = Pw[m] + add * m;
   uint64_t pos = 0, nseg = 0, glen = 0, wpos = Pw[0];
   bool done = false;
+  if (spec && m > 0 && wm - wpos >= threshold) { // the same prediction as seg_spec_kernel's
+    const uint64_t g = hop_predict(threshold, m, wm - wpos);
+    const uint64_t H = g ? ((m + g - 1) / g < kSpecHops ? (m + g - 1) / g : kSpecHops) : 0; // starts h g < m
+    bool follow = true;
+    for (uint64_t c = 0; c < H && follow; c += kWave) {
+      const uint64_t nv = c + lane < H ? spec[c + lane] : 0;
+      for (uint32_t j = 0; j < kWave && c + j < H; j++) {
+        if (pos != (c + j) * g) { // the chain left the predicted starts
+          follow = false;
+          break;
+        }
+        const uint64_t nx = readlane_u64(nv, j);
+        if (lane == 0) first[nseg] = pos;
+        nseg++;
+        glen = nx - pos;
+        pos = nx;
+        if (pos >= m) {
+          follow = false;
+          done = true;
+          break;
+        }
+      }
+    }
+    if (!done && pos) wpos = Pw[pos] + add * pos;
+  }
   while (!done) {
     if (glen == 0 && pos < m && wm - wpos >= threshold) {
       // no segment length seen yet: predict one from the mean weight of the
       // rest (equal-sized records: the first window holds the answer, no
       // exact search); a
       // window that misses falls back to the exact hop below
-      const uint64_t rest = wm - wpos, nrec = m - pos;
-      const uint64_t g = rest ? static_cast<uint64_t>(static_cast<double>(threshold) * static_cast<double>(nrec) /
-                                                      static_cast<double>(rest))
-                              : 0;
-      glen = g >= 1 && g <= nrec ? g : 0;
+      glen = hop_predict(threshold, m - pos, wm - wpos);
     }
     if (glen == 0) { // no prediction: one exact hop
       if (pos >= m) break;
@@ -1881,13 +1969,13 @@ __global__ __launch_bounds__(kWave) void seg_hops_kernel(const uint64_t *Pw, uin
       wpos = Pw[pos] + add * pos;
       continue;
     }
-    uint64_t v[kHopAhead][kHopProbe], g0s[kHopAhead];
+    uint64_t v[kHopAhead][kSpecProbe], g0s[kHopAhead];
 #pragma unroll
     for (uint32_t h = 0; h < kHopAhead; h++) {
       const uint64_t e = pos + (h + 1) * glen;
-      g0s[h] = e > kHopSpan / 2 ? e - kHopSpan / 2 : 0;
+      g0s[h] = e > kSpecSpan / 2 ? e - kSpecSpan / 2 : 0;
 #pragma unroll
-      for (uint32_t r = 0; r < kHopProbe; r++) {
+      for (uint32_t r = 0; r < kSpecProbe; r++) {
         const uint64_t x = g0s[h] + static_cast<uint64_t>(r) * kWave + lane;
         v[h][r] = Pw[x <= m ? x : m];
       }
@@ -1896,7 +1984,7 @@ __global__ __launch_bounds__(kWave) void seg_hops_kernel(const uint64_t *Pw, uin
 #pragma unroll
     for (uint32_t h = 0; h < kHopAhead; h++) {
 #pragma unroll
-      for (uint32_t r = 0; r < kHopProbe; r++) {
+      for (uint32_t r = 0; r < kSpecProbe; r++) {
         const uint64_t x = g0s[h] + static_cast<uint64_t>(r) * kWave + lane;
         // past m: >= any target (W(m) >= target)
         v[h][r] = x <= m ? v[h][r] + add * x : ~0ull;
@@ -1913,18 +2001,18 @@ __global__ __launch_bounds__(kWave) void seg_hops_kernel(const uint64_t *Pw, uin
       }
       uint64_t nb = 0;
 #pragma unroll
-      for (uint32_t r = 0; r < kHopProbe; r++) nb += __popcll(__ballot(v[h][r] < target));
+      for (uint32_t r = 0; r < kSpecProbe; r++) nb += __popcll(__ballot(v[h][r] < target));
       // records of the window at or before pos are below target too, so the
       // answer is g0 + nb whenever it lies inside the window and nothing
       // before the window can be the answer
       const uint64_t g0 = g0s[h];
       uint64_t nx, wnx;
-      const bool hit = nb < kHopSpan && (nb > 0 || g0 <= pos + 1);
+      const bool hit = nb < kSpecSpan && (nb > 0 || g0 <= pos + 1);
       if (hit) {
         nx = g0 + nb;
         uint64_t t = 0;
 #pragma unroll
-        for (uint32_t r = 0; r < kHopProbe; r++)
+        for (uint32_t r = 0; r < kSpecProbe; r++)
           if (r == (nb >> 6)) t = v[h][r];
         wnx = __shfl(t, static_cast<int>(nb & (kWave - 1)), kWave);
       } else {
@@ -2385,7 +2473,9 @@ struct SegLayout { // u32 offsets into the segmentation workspace
 };
 } // namespace
 
-uint64_t segment_workspace_u32(uint64_t nrec) { return SegLayout(nrec).total + 2; }
+uint64_t segment_workspace_u32(uint64_t nrec) {
+  return std::max<uint64_t>(SegLayout(nrec).total + 2, 2 * kSpecHops); // (the long-segment path: spec words)
+}
 
 hipError_t launch_segment(const uint64_t *Pw, uint64_t nrec, uint64_t threshold, uint32_t *J,
                           uint64_t *d_nblocks, uint64_t *blk_first, hipStream_t s, const uint64_t *ends,
@@ -2396,7 +2486,9 @@ hipError_t launch_segment(const uint64_t *Pw, uint64_t nrec, uint64_t threshold,
     return e;
   }
   if (long_segments && !ends) {
-    seg_hops_kernel<<<1, kWave, 0, s>>>(Pw, add, nrec, d_nrec, threshold, blk_first, d_nblocks);
+    uint64_t *spec = reinterpret_cast<uint64_t *>(J); // kSpecHops words (segment_workspace_u32)
+    if (spec) seg_spec_kernel<<<kSpecHops, kWave, 0, s>>>(Pw, add, nrec, d_nrec, threshold, spec);
+    seg_hops_kernel<<<1, kWave, 0, s>>>(Pw, add, nrec, d_nrec, threshold, blk_first, d_nblocks, spec);
     return hipGetLastError();
   }
   const SegLayout L(nrec);
