@@ -201,6 +201,7 @@ int sstc_ctx_destroy(sstc_ctx *c) {
   bind_device(c);
   (void)hipStreamSynchronize(c->stream);
   if (c->arena.host) (void)hipHostFree(c->arena.host);
+  if (c->arena.up) (void)hipHostFree(c->arena.up);
   if (HostPipe *hp = c->pipe) {
     for (hipStream_t st : {hp->up, hp->down})
       if (st) {

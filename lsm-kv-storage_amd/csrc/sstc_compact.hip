@@ -49,8 +49,10 @@ struct Abort {
   const unsigned long long *err;  // context decode-error counter
   const uint64_t *err0;           // its value before this job's decode
   const unsigned long long *bad;  // unsorted records (null: not checked)
+  const unsigned long long *guard = nullptr; // a long group out of txn order (null: not checked)
   __device__ __forceinline__ bool operator()() const {
-    return *err != *err0 || (bad && *bad);
+    constexpr unsigned long long kLongInv = kGuardLongGroup | kGuardInv;
+    return *err != *err0 || (bad && *bad) || (guard && (*guard & kLongInv) == kLongInv);
   }
 };
 
@@ -79,6 +81,34 @@ __device__ __forceinline__ bool sk_less(const SK &a, const SK &b, const KeyView 
   const int c = key_cmp(a.p0, a.p1, a.kl, a.id, b.p0, b.p1, b.kl, b.id, kv);
   return c < 0 || (c == 0 && a.tx > b.tx);
 }
+
+// k-way merge pass: every group of up to kKWay consecutive sorted runs is
+// merged in ONE pass (ceil(log8 k) passes instead of log2 k pairwise rounds).
+//  1. splitters: every S-th record of every run (S = kKWin / runs).  A wave
+//     lane per (splitter, run) binary-searches the splitter's co-rank in that
+//     run (records of the run that precede it in merge order); 8 lanes reduce
+//     them to the splitter's rank among splitters (sum of ceil(c / S)) and
+//     among records (sum of c), and write the co-rank row in sorted order.
+//     Between two consecutive splitter rows a run contributes <= S records.
+//  2. windows: window w holds the records between the first splitter rows at
+//     or after output ranks w * kKWin and (w + 1) * kKWin (< 2 kKWin records);
+//     a thread per window resolves its output position and sub-runs.
+//  3. merge: a workgroup per window stages the <= kKWay sub-runs in LDS and
+//     merges them by a pairwise merge-path tree (ck_mg_merge_kernel).  Order =
+//     key asc, txn desc, then lower run first, i.e. the stable pairwise merge
+//     of MergeIterator (merge_iterator.cc:34-46).
+constexpr uint32_t kKWay = 8;
+constexpr uint32_t kKWin = 512;
+constexpr uint32_t kKRegion = 2 * kKWin;
+
+struct KGroup {
+  uint64_t start[kKWay + 1]; // absolute run starts; start[nruns] = group end
+  uint32_t sbase[kKWay + 1]; // prefix of the runs' splitter counts
+  uint32_t nruns, stride;    // runs, splitter stride S
+  uint32_t base;             // first splitter id == first row (nsamp + 1 of each, the last a sentinel)
+  uint32_t wg0;              // first merge workgroup
+};
+
 
 // Sortedness of every input run (TableBuilder requires sorted input,
 // table_builder.h:77): decode_kernel checks each record against its
@@ -109,9 +139,8 @@ __device__ void carry_group(SK *s, const uint64_t *rec_base, uint64_t b, uint64_
     if (f == run0 || key_cmp(y.p0, y.p1, y.kl, y.id, k.p0, k.p1, k.kl, k.id, kv) != 0) break; // starts in q
     const SK z = s[f - 1];
     if (key_cmp(z.p0, z.p1, z.kl, z.id, k.p0, k.p1, k.kl, k.id, kv) != 0) break;
-    if (hop + 1 >= kGroupCarryBlocks) { // a key's versions over too many blocks: rejected
+    if (hop + 1 >= kGroupCarryBlocks) { // a key's versions over too many blocks: rejected if out of txn order
       atomicOr(guard, kGuardLongGroup);
-      atomicAdd(bad, 1ull);
       return;
     }
     end = f - 1;
@@ -133,8 +162,14 @@ __global__ __launch_bounds__(256) void ck_check_blocks_kernel(SK *s, const uint6
                                        const uint64_t *run_start, uint64_t nruns, KeyView kv,
                                        unsigned long long *bad, Abort stop, uint64_t *zws, uint64_t nz,
                                        const uint64_t *blk_off, const uint64_t *blk_len,
-                                       unsigned long long *src_end, unsigned long long *inv) {
+                                       unsigned long long *src_end, unsigned long long *guard,
+                                       const uint64_t *kg_host, uint64_t *kg, uint64_t kg_words) {
   __shared__ uint64_t s_end[256 / kWave];
+  // the merge passes' group descriptors, written by the host into pinned
+  // mapped memory before the launch: copied here by workgroup 0 (a copy
+  // command between the decode and the merge cost ~5 us)
+  if (blockIdx.x == 0)
+    for (uint64_t i = threadIdx.x; i < kg_words; i += blockDim.x) kg[i] = kg_host[i];
   const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
   const uint64_t t0 = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   for (uint64_t z = t0; z < nz; z += stride) zws[z] = 0; // filter look-back
@@ -156,7 +191,13 @@ __global__ __launch_bounds__(256) void ck_check_blocks_kernel(SK *s, const uint6
     const SK cur = s[r], pv = s[r - 1];
     const int c = key_cmp(cur.p0, cur.p1, cur.kl, cur.id, pv.p0, pv.p1, pv.kl, pv.id, kv);
     if (c < 0) atomicAdd(bad, 1ull);
-    if (c == 0 && cur.tx > pv.tx) atomicOr(inv, 1ull); // a group out of txn order across the boundary
+    // a key group continuing across the boundary takes its running minimum
+    // from the blocks before it (a no-op unless some version of it is out of
+    // txn order: the minimum of older versions is then >= every txn here)
+    if (c == 0) {
+      if (cur.tx > pv.tx) atomicOr(guard, kGuardInv); // a group out of txn order across the boundary
+      carry_group(s, rec_base, b, r, run_start[lo], kv, bad, guard);
+    }
   }
   for (uint32_t d = kWave / 2; d > 0; d >>= 1) {
     const uint64_t y = __shfl_xor(e, d, kWave);
@@ -170,58 +211,6 @@ __global__ __launch_bounds__(256) void ck_check_blocks_kernel(SK *s, const uint6
   }
 }
 
-// The cross-block carry of the merge txns (carry_group), run only when some
-// record's merge txn differs from its txn as read or a group is out of txn
-// order across a block boundary (inv): every continuing block boundary of
-// such a job takes its group's running minimum from the blocks before it.
-__global__ __launch_bounds__(256) void ck_carry_kernel(SK *s, const uint64_t *rec_base, uint64_t nblocks,
-                                                       const uint64_t *run_start, uint64_t nruns, KeyView kv,
-                                                       unsigned long long *bad, Abort stop,
-                                                       const unsigned long long *inv, unsigned long long *guard) {
-  if (!*inv || stop()) return;
-  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
-  for (uint64_t b = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; b < nblocks; b += stride) {
-    const uint64_t r = rec_base[b];
-    if (r == 0 || rec_base[b + 1] == r) continue;
-    uint64_t lo = 0, hi = nruns;
-    while (lo + 1 < hi) {
-      const uint64_t mid = (lo + hi) >> 1;
-      if (run_start[mid] <= r) lo = mid;
-      else hi = mid;
-    }
-    if (run_start[lo] == r) continue;
-    const SK cur = s[r], pv = s[r - 1];
-    if (key_cmp(cur.p0, cur.p1, cur.kl, cur.id, pv.p0, pv.p1, pv.kl, pv.id, kv) == 0)
-      carry_group(s, rec_base, b, r, run_start[lo], kv, bad, guard);
-  }
-}
-
-// k-way merge pass: every group of up to kKWay consecutive sorted runs is
-// merged in ONE pass (ceil(log8 k) passes instead of log2 k pairwise rounds).
-//  1. splitters: every S-th record of every run (S = kKWin / runs).  A wave
-//     lane per (splitter, run) binary-searches the splitter's co-rank in that
-//     run (records of the run that precede it in merge order); 8 lanes reduce
-//     them to the splitter's rank among splitters (sum of ceil(c / S)) and
-//     among records (sum of c), and write the co-rank row in sorted order.
-//     Between two consecutive splitter rows a run contributes <= S records.
-//  2. windows: window w holds the records between the first splitter rows at
-//     or after output ranks w * kKWin and (w + 1) * kKWin (< 2 kKWin records);
-//     a thread per window resolves its output position and sub-runs.
-//  3. merge: a workgroup per window stages the <= kKWay sub-runs in LDS and
-//     merges them by a pairwise merge-path tree (ck_mg_merge_kernel).  Order =
-//     key asc, txn desc, then lower run first, i.e. the stable pairwise merge
-//     of MergeIterator (merge_iterator.cc:34-46).
-constexpr uint32_t kKWay = 8;
-constexpr uint32_t kKWin = 512;
-constexpr uint32_t kKRegion = 2 * kKWin;
-
-struct KGroup {
-  uint64_t start[kKWay + 1]; // absolute run starts; start[nruns] = group end
-  uint32_t sbase[kKWay + 1]; // prefix of the runs' splitter counts
-  uint32_t nruns, stride;    // runs, splitter stride S
-  uint32_t base;             // first splitter id == first row (nsamp + 1 of each, the last a sentinel)
-  uint32_t wg0;              // first merge workgroup
-};
 
 // y precedes x in merge order, y from run ry, x from run rx != ry
 __device__ __forceinline__ bool kw_before(const SK &y, uint32_t ry, const SK &x, uint32_t rx, const KeyView &kv) {
@@ -899,50 +888,69 @@ __global__ void ck_block_info_kernel(const uint64_t *bf, Lay L, const uint64_t *
   btab[b] = static_cast<uint32_t>(lo);
 }
 
-// table t: first block index, data / meta bytes, total
-__global__ void ck_table_info_kernel(const uint64_t *tf, Lay L, const uint64_t *bf, BlkOff BL,
-                                     const uint64_t *MS, uint64_t *tbf, uint64_t *tdata, uint64_t *tmeta,
-                                     uint64_t *tlen) {
+// table t: first block index, data / meta bytes, total.  kScan: one
+// workgroup holds every table slot (nt_max + 1 <= kTiThreads) and also writes
+// the tables' offsets (the exclusive scan of the totals; one launch fewer)
+constexpr uint32_t kTiThreads = 1024;
+template <bool kScan>
+__global__ __launch_bounds__(kTiThreads) void ck_table_info_kernel(const uint64_t *tf, Lay L, const uint64_t *bf,
+                                                                   BlkOff BL, const uint64_t *MS, uint64_t *tbf,
+                                                                   uint64_t *tdata, uint64_t *tmeta, uint64_t *tlen,
+                                                                   uint64_t *toff) {
   const uint64_t t = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (t > L.nt_max) return;
   const uint64_t nt = L.nt(), nb = L.nb();
-  if (!L.ok() || t > nt) { // past the real tables: zero lengths (the table scan over nt_max stays exact)
-    if (t < L.nt_max) {
-      tlen[t] = 0;
-      tdata[t] = 0;
-      tmeta[t] = 0;
+  uint64_t len = 0; // this slot's total (0 past the real tables: the table scan over nt_max stays exact)
+  if (t <= L.nt_max) {
+    if (!L.ok() || t > nt) {
+      if (t < L.nt_max) {
+        tlen[t] = 0;
+        tdata[t] = 0;
+        tmeta[t] = 0;
+      }
+      tbf[t] = L.ok() ? nb : 0;
+    } else {
+      // block starting at record tf[t] (every table start is a block start)
+      uint64_t lo = 0, hi = nb + 1;
+      const uint64_t r = tf[t];
+      while (lo + 1 < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (bf[mid] <= r) lo = mid;
+        else hi = mid;
+      }
+      tbf[t] = lo;
+      if (t == nt) { // the sentinel: a zero length when nt < nt_max
+        if (t < L.nt_max) {
+          tlen[t] = 0;
+          tdata[t] = 0;
+          tmeta[t] = 0;
+        }
+      } else {
+        // tbf[t+1] computed by its own thread; recompute here for the sizes
+        uint64_t lo2 = 0, hi2 = nb + 1;
+        const uint64_t r2 = tf[t + 1];
+        while (lo2 + 1 < hi2) {
+          const uint64_t mid = (lo2 + hi2) >> 1;
+          if (bf[mid] <= r2) lo2 = mid;
+          else hi2 = mid;
+        }
+        const uint64_t d = BL[lo2] - BL[lo], m = MS[lo2] - MS[lo];
+        tdata[t] = d;
+        tmeta[t] = m;
+        len = d + m + 40;
+        tlen[t] = len;
+      }
     }
-    tbf[t] = L.ok() ? nb : 0;
-    return;
   }
-  // block starting at record tf[t] (every table start is a block start)
-  uint64_t lo = 0, hi = nb + 1;
-  const uint64_t r = tf[t];
-  while (lo + 1 < hi) {
-    const uint64_t mid = (lo + hi) >> 1;
-    if (bf[mid] <= r) lo = mid;
-    else hi = mid;
+  if constexpr (kScan) {
+    __shared__ uint64_t s_w[kTiThreads / kWave];
+    const uint32_t w = threadIdx.x / kWave;
+    const uint64_t inc = wave_incl_scan_u64(len);
+    if (lane_id() == kWave - 1) s_w[w] = inc;
+    __syncthreads();
+    uint64_t before = 0;
+    for (uint32_t x = 0; x < w; x++) before += s_w[x];
+    if (t <= L.nt_max) toff[t] = before + inc - len; // toff[nt_max] = the total
   }
-  tbf[t] = lo;
-  if (t == nt) { // the sentinel: a zero length when nt < nt_max (the table scan runs over nt_max)
-    if (t < L.nt_max) {
-      tlen[t] = 0;
-      tdata[t] = 0;
-      tmeta[t] = 0;
-    }
-    return;
-  }
-  // tbf[t+1] computed by its own thread; recompute here for the sizes
-  uint64_t lo2 = 0, hi2 = nb + 1;
-  const uint64_t r2 = tf[t + 1];
-  while (lo2 + 1 < hi2) {
-    const uint64_t mid = (lo2 + hi2) >> 1;
-    if (bf[mid] <= r2) lo2 = mid;
-    else hi2 = mid;
-  }
-  tdata[t] = BL[lo2] - BL[lo];
-  tmeta[t] = MS[lo2] - MS[lo];
-  tlen[t] = tdata[t] + tmeta[t] + 40;
 }
 
 __global__ void ck_block_off_kernel(const uint32_t *btab, Lay L, BlkOff BL, const uint64_t *tbf,
@@ -1061,23 +1069,28 @@ __global__ __launch_bounds__(256) void ck_meta_kernel(const uint64_t *bmeta, Lay
   }
 }
 
-// min / max txn of every output table (table_builder.cc:47-49): the encode
-// kernels reduce every block, then one workgroup per table reduces its blocks
-// table min / max txn from the blocks' (footer, table_builder.cc:179-211):
-// kMmSplit workgroups per table each reduce a slice of its blocks to a
-// partial; the footer kernel folds a table's kMmSplit partials (no atomics:
-// same-address atomics from every XCD serialise)
-constexpr uint32_t kMmSplit = 16;
-__global__ __launch_bounds__(256) void ck_tab_minmax_kernel(const uint64_t *tbf, Lay L, const uint64_t *bmeta,
-                                                            uint64_t *pmin, uint64_t *pmax) {
-  __shared__ uint64_t smn[256 / kWave], smx[256 / kWave];
-  const uint64_t t = blockIdx.x / kMmSplit, g = blockIdx.x % kMmSplit;
-  if (!L.ok() || t >= L.nt()) return; // uniform over the workgroup
-  const uint64_t f = tbf[t], n = tbf[t + 1] - f;
-  const uint64_t b0 = f + n * g / kMmSplit, b1 = f + n * (g + 1) / kMmSplit;
+// footer of table t (table_builder.cc:179-211), one workgroup per table: its
+// min / max txn (table_builder.cc:47-49) reduced from the blocks' (the encode
+// wrote every block's), then the 40 B footer.  (Round 4: folded the separate
+// 16-workgroups-per-table reduction kernel in -- one launch fewer.)
+constexpr uint32_t kFootThreads = 1024;
+__global__ __launch_bounds__(kFootThreads) void ck_footer_kernel(Lay L, const uint64_t *tbf, const uint64_t *toff,
+                                                                 const uint64_t *tdata, const uint64_t *tmeta,
+                                                                 const uint64_t *bmeta, uint8_t *dst, uint64_t cap,
+                                                                 unsigned long long *guard) {
+  __shared__ uint64_t smn[kFootThreads / kWave], smx[kFootThreads / kWave];
+  const uint64_t t = blockIdx.x;
+  if (!L.ok()) return;
+  const uint64_t nt = L.nt();
+  if (t >= nt || toff[nt] > cap) return; // uniform over the workgroup
+  const uint64_t f = tbf[t], e = tbf[t + 1];
+  const uint64_t o = toff[t], dbytes = tdata[t], mbytes = tmeta[t]; // in flight with the reduction's loads
   uint64_t mn = ~0ull, mx = 0;
-  for (uint64_t b = b0 + threadIdx.x; b < b1; b += 256) {
-    const uint64_t x = bmeta[4 * b], y = bmeta[4 * b + 1];
+#pragma unroll 4
+  for (uint64_t b = f + threadIdx.x; b < e; b += kFootThreads) {
+    const u32x4 v = *reinterpret_cast<const u32x4 *>(bmeta + 4 * b); // min, max
+    const uint64_t x = static_cast<uint64_t>(v.x) | static_cast<uint64_t>(v.y) << 32;
+    const uint64_t y = static_cast<uint64_t>(v.z) | static_cast<uint64_t>(v.w) << 32;
     mn = x < mn ? x : mn;
     mx = y > mx ? y : mx;
   }
@@ -1091,38 +1104,20 @@ __global__ __launch_bounds__(256) void ck_tab_minmax_kernel(const uint64_t *tbf,
     smx[threadIdx.x / kWave] = mx;
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    for (uint32_t w = 1; w < 256 / kWave; w++) {
-      mn = smn[w] < mn ? smn[w] : mn;
-      mx = smx[w] > mx ? smx[w] : mx;
-    }
-    pmin[blockIdx.x] = mn;
-    pmax[blockIdx.x] = mx;
+  if (threadIdx.x != 0) return;
+  for (uint32_t w = 1; w < kFootThreads / kWave; w++) {
+    mn = smn[w] < mn ? smn[w] : mn;
+    mx = smx[w] > mx ? smx[w] : mx;
   }
-}
-
-// footer of table t (table_builder.cc:179-211)
-__global__ void ck_footer_kernel(Lay L, const uint64_t *tbf, const uint64_t *toff, const uint64_t *tdata,
-                                 const uint64_t *tmeta, const uint64_t *tmin, const uint64_t *tmax, uint8_t *dst,
-                                 uint64_t cap, unsigned long long *guard) {
-  const uint64_t t = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (!L.ok()) return;
-  const uint64_t nt = L.nt();
-  if (t >= nt || toff[nt] > cap) return;
-  const uint64_t at = toff[t] + tdata[t] + tmeta[t];
-  if (at < toff[t] || at > cap || cap - at < 40) { // the footer must end inside the output buffer
+  const uint64_t at = o + dbytes + mbytes;
+  if (at < o || at > cap || cap - at < 40) { // the footer must end inside the output buffer
     atomicOr(guard, kGuardFooter);
     return;
   }
-  uint64_t mn = ~0ull, mx = 0;
-  for (uint32_t g = 0; g < kMmSplit; g++) {
-    mn = tmin[t * kMmSplit + g] < mn ? tmin[t * kMmSplit + g] : mn;
-    mx = tmax[t * kMmSplit + g] > mx ? tmax[t * kMmSplit + g] : mx;
-  }
-  uint8_t *p = dst + toff[t] + tdata[t] + tmeta[t];
-  put_le(p, tbf[t + 1] - tbf[t], 8);
-  put_le(p + 8, tdata[t], 8);
-  put_le(p + 16, tmeta[t], 8);
+  uint8_t *p = dst + at;
+  put_le(p, e - f, 8);
+  put_le(p + 8, dbytes, 8);
+  put_le(p + 16, mbytes, 8);
   put_le(p + 24, mn, 8);
   put_le(p + 32, mx, 8);
 }
@@ -1219,7 +1214,6 @@ __global__ __launch_bounds__(256) void ck_run_starts_kernel(const uint64_t *rec_
     *bad = 0;
     guard[0] = 0; // consistency-guard bits
     guard[1] = 0; // source end (ck_check_blocks_kernel)
-    guard[2] = 0; // merge txns out of txn order (decode_kernel, ck_check_blocks_kernel)
   }
   if (i < n) out[i] = rec_base[tfb[i]];
 }
@@ -1243,6 +1237,26 @@ void ensure_host(Arena &arena, uint64_t words) {
   }
   memset(arena.host, 0, cap * sizeof(uint64_t)); // no stale word can equal a sequence number
   arena.host_cap = cap;
+}
+
+// pinned, device-mapped upload bytes (Arena::up); the caller's last job is
+// complete when it returns, so the bytes are free to overwrite
+void ensure_up(Arena &arena, uint64_t bytes) {
+  if (arena.up && arena.up_cap >= bytes) return;
+  if (arena.up) (void)hipHostFree(arena.up);
+  arena.up = nullptr;
+  arena.up_dev = nullptr;
+  arena.up_cap = 0;
+  const uint64_t cap = bytes < 4096 ? 4096 : bytes;
+  if (hipHostMalloc(reinterpret_cast<void **>(&arena.up), cap, hipHostMallocMapped | hipHostMallocCoherent) !=
+          hipSuccess ||
+      hipHostGetDevicePointer(reinterpret_cast<void **>(&arena.up_dev), arena.up, 0) != hipSuccess) {
+    if (arena.up) (void)hipHostFree(arena.up);
+    arena.up = nullptr;
+    arena.up_dev = nullptr;
+    throw std::runtime_error("pinned upload bytes");
+  }
+  arena.up_cap = cap;
 }
 
 // device words (+ an optional array after them) -> pinned host words: one
@@ -1305,8 +1319,7 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     unsigned long long *bad = reinterpret_cast<unsigned long long *>(pool.get<uint64_t>(1));
     // consistency guard: [0] bits set by any check of the job, [1] the end of
     // the source bytes its blocks span (both cleared by ck_run_starts_kernel)
-    unsigned long long *guard = reinterpret_cast<unsigned long long *>(pool.get<uint64_t>(3));
-    unsigned long long *inv = guard + 2; // merge txns need the cross-block carry (ck_carry_kernel)
+    unsigned long long *guard = reinterpret_cast<unsigned long long *>(pool.get<uint64_t>(2));
     const uint64_t *src_end = reinterpret_cast<const uint64_t *>(guard + 1);
     // record index of every input table's first record (its run start)
     CK(hipMemcpyAsync(d_tfb, h_tfb, (ntables + 1) * 8, hipMemcpyHostToDevice, s));
@@ -1329,7 +1342,7 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     DecArgs da{d_src, d_blk_off, d_blk_len, nblocks, rb_all,
                sstc_records{}, txn_mode, status, err_count, A, bad};
     da.rx = RX;
-    da.inv = inv;
+    da.inv = guard;
     CK(launch_decode(da, s));
     if (n == 0) { // DoCompactJob still finishes its first (empty) output table
       fetch(arena, s, {reinterpret_cast<const uint64_t *>(err_count), errs});
@@ -1356,7 +1369,7 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     const KeyView kv{d_src, RX};
     uint64_t nruns = ntables;
     const uint64_t *rb = d_rs; // run starts, nruns + 1
-    const Abort dec_fail{err_count, errs, nullptr}, stop{err_count, errs, bad};
+    const Abort dec_fail{err_count, errs, nullptr}, stop{err_count, errs, bad, guard};
     const uint64_t fftiles = (n + kFfTile - 1) / kFfTile;
     uint64_t *ffws = nullptr; // look-back words of the filter
     // survivors of the keep / drop filter (sized by n: the kept count is known after it)
@@ -1365,7 +1378,8 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
            nullptr}; // vl / vo: not needed by the whole-entry encode
     uint64_t *Pd = pool.get<uint64_t>(n + 1), *Pe = pool.get<uint64_t>(n + 1);
     // k-way merge passes; run boundaries of every pass are known on the host,
-    // so all group descriptors go up in one upload (lives until the next sync)
+    // which builds every pass's group descriptors into pinned mapped memory;
+    // the check kernel copies them to the device
     std::vector<KGroup> kg;
     std::vector<uint32_t> pass_groups, pass_ids, pass_wgs, pass_ways;
     {
@@ -1423,13 +1437,16 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
       }
       // the filter's look-back status words, cleared by the check kernel
       ffws = pool.get<uint64_t>(1 + 3 * fftiles);
+      KGroup *d_kg = kg.empty() ? nullptr : pool.get<KGroup>(kg.size());
+      const uint64_t kg_bytes = kg.size() * sizeof(KGroup);
+      static_assert(sizeof(KGroup) % 8 == 0, "KGroup copied as words");
+      ensure_up(arena, kg_bytes);
+      if (kg_bytes) memcpy(arena.up, kg.data(), kg_bytes);
       ck_check_blocks_kernel<<<std::min<uint32_t>(std::max<uint32_t>(grid(std::max<uint64_t>(nblocks, 1ull + 3 * fftiles)), 1u), kCheckGrid), 256, 0, s>>>(A, rb_all, nblocks, rb, nruns, kv, bad, dec_fail, ffws,
-                                                           1 + 3 * fftiles, d_blk_off, d_blk_len, guard + 1, inv);
-      ck_carry_kernel<<<std::min<uint32_t>(std::max<uint32_t>(grid(nblocks), 1u), kCheckGrid), 256, 0, s>>>(
-          A, rb_all, nblocks, rb, nruns, kv, bad, stop, inv, guard);
+                                                           1 + 3 * fftiles, d_blk_off, d_blk_len, guard + 1, guard,
+                                                           reinterpret_cast<const uint64_t *>(arena.up_dev),
+                                                           reinterpret_cast<uint64_t *>(d_kg), kg_bytes / 8);
       if (!kg.empty()) {
-        KGroup *d_kg = pool.get<KGroup>(kg.size());
-        CK(hipMemcpyAsync(d_kg, kg.data(), kg.size() * sizeof(KGroup), hipMemcpyHostToDevice, s));
         const uint32_t max_ids = *std::max_element(pass_ids.begin(), pass_ids.end());
         uint32_t *Cm = pool.get<uint32_t>(static_cast<uint64_t>(max_ids) * kKWay);
         uint64_t *Gm = pool.get<uint64_t>(max_ids);
@@ -1475,7 +1492,7 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
         err = "an input block failed to decode";
         return SSTC_E_INVALID_ARG;
       }
-      if (h[3] & kGuardLongGroup) {
+      if ((h[3] & kGuardLongGroup) && (h[3] & kGuardInv)) {
         err = "an input holds versions of one key out of txn order as read over more than " +
               std::to_string(kGroupCarryBlocks) + " blocks (unsupported)";
         return SSTC_E_INVALID_ARG;
@@ -1519,8 +1536,14 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     CK(launch_scan(msz, nb_max, 0, MS, ws3 + nzb, s, true));
     uint64_t *tbf = pool.get<uint64_t>(nt_max + 1), *tdata = pool.get<uint64_t>(nt_max),
              *tmeta = pool.get<uint64_t>(nt_max);
-    ck_table_info_kernel<<<grid(nt_max + 1), 256, 0, s>>>(tf, L, bf, BL, MS, tbf, tdata, tmeta, d_table_len);
-    CK(launch_scan(d_table_len, nt_max, 0, d_table_off, ws2, s)); // nt_max + 1 <= max_tables + 1 elements
+    if (nt_max + 1 <= kTiThreads) {
+      ck_table_info_kernel<true><<<1, kTiThreads, 0, s>>>(tf, L, bf, BL, MS, tbf, tdata, tmeta, d_table_len,
+                                                          d_table_off);
+    } else {
+      ck_table_info_kernel<false><<<grid(nt_max + 1), 256, 0, s>>>(tf, L, bf, BL, MS, tbf, tdata, tmeta, d_table_len,
+                                                                   nullptr);
+      CK(launch_scan(d_table_len, nt_max, 0, d_table_off, ws2, s)); // nt_max + 1 <= max_tables + 1 elements
+    }
     // the output size is checked on the device (every writer below stands down
     // when it exceeds dst_cap) and by the host after the last sync
     const uint64_t *need = d_table_off + nt_max; // = d_table_off[nt]: the lengths past nt are zero
@@ -1533,7 +1556,6 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     // blocks past an LDS slot are encoded by the wave that met them (config 5 319 -> 233 us)
     ea.need = need;
     ea.cap = dst_cap;
-    uint64_t *tmin = pool.get<uint64_t>(nt_max * kMmSplit), *tmax = pool.get<uint64_t>(nt_max * kMmSplit);  // per-table partials
     ea.bmeta = bmeta; // block min / max txn (reduced by the encode kernels) and first / last key
     ea.src_end = src_end;
     ea.guard = guard;
@@ -1541,8 +1563,8 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     ck_meta_kernel<<<static_cast<uint32_t>((nb_max + 255) / 256), 256, 0, s>>>(bmeta, L, btab, BL, MS, blen, tbf,
                                                                               d_table_off, tdata, d_dst, need,
                                                                               dst_cap, guard, d_src, src_end);
-    ck_tab_minmax_kernel<<<static_cast<uint32_t>(nt_max * kMmSplit), 256, 0, s>>>(tbf, L, bmeta, tmin, tmax);
-    ck_footer_kernel<<<grid(nt_max), 256, 0, s>>>(L, tbf, d_table_off, tdata, tmeta, tmin, tmax, d_dst, dst_cap, guard);
+    ck_footer_kernel<<<static_cast<uint32_t>(nt_max), kFootThreads, 0, s>>>(L, tbf, d_table_off, tdata, tmeta, bmeta,
+                                                                           d_dst, dst_cap, guard);
     CK(hipGetLastError());
     fetch(arena, s,
           {reinterpret_cast<const uint64_t *>(err_count), errs, reinterpret_cast<const uint64_t *>(bad),
@@ -1557,7 +1579,7 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
       err = "more output tables than max_tables";
       return SSTC_E_CAPACITY;
     }
-    if (arena.host[3]) {
+    if (arena.host[3] & ~(kGuardLongGroup | kGuardInv)) {
       err = "device consistency check failed (guard bits 0x" + [](uint64_t v) {
         char b[24];
         snprintf(b, sizeof b, "%llx", static_cast<unsigned long long>(v));

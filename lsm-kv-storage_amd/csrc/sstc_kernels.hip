@@ -589,7 +589,7 @@ __device__ __forceinline__ uint32_t decode_block(const DecArgs &a, const R &rd, 
       }
       if (!f && i0 > 0) eff = ceff < eff ? ceff : eff;
       ceff = __shfl(eff, kWave - 1, kWave);
-      if (a.inv && __any(i < n && eff != e.txn) && lane == 0) atomicOr(a.inv, 1ull);
+      if (a.inv && __any(i < n && eff != e.txn) && lane == 0) atomicOr(a.inv, kGuardInv);
     }
     if (i < n) {
       const uint64_t r = base + i;

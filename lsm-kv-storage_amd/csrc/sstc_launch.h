@@ -65,8 +65,8 @@ struct DecArgs {
   unsigned long long *unsorted = nullptr;
   RecX *rx = nullptr; // compaction: written instead of the `out` columns
   uint32_t xcd = 0;
-  // compaction: set when a record's merge txn differs from its txn as read
-  // (SortKey, kSkRead): the job then runs the cross-block carry
+  // compaction: the guard word; kGuardInv is set when a record's merge txn
+  // differs from its txn as read (SortKey, kSkRead)
   unsigned long long *inv = nullptr;
 };
 
@@ -108,7 +108,11 @@ struct EncArgs {
 
 // consistency-guard bits of the compaction job (sstc_compact.hip)
 constexpr unsigned long long kGuardMergeId = 1, kGuardEntry = 2, kGuardBlockRange = 4, kGuardMeta = 8,
-                             kGuardFooter = 16, kGuardLayout = 32, kGuardLongGroup = 64;
+                             kGuardFooter = 16, kGuardLayout = 32, kGuardLongGroup = 64,
+                             kGuardInv = 128;
+// kGuardLongGroup / kGuardInv are notes, not faults: a key's versions continue
+// over more than kGroupCarryBlocks blocks / some group is out of txn order as
+// read.  Both together reject the job (the carry would be needed that far).
 // blocks a key group whose merge txns need a carry may span (ck_check_blocks_kernel)
 constexpr uint32_t kGroupCarryBlocks = 64;
 
@@ -182,6 +186,11 @@ struct Arena {
   uint64_t *host_dev = nullptr; // the same words as mapped into the device
   uint64_t host_cap = 0;
   uint64_t seq = 0; // sequence word of the last host fetch (sstc_compact.hip fetch)
+  // pinned, device-mapped bytes the host fills before a launch that copies
+  // them to the device (the merge passes' group descriptors)
+  uint8_t *up = nullptr;
+  uint8_t *up_dev = nullptr;
+  uint64_t up_cap = 0;
   // fault injection for tests (sstc__ctx_set_fault): corrupts the compaction
   // job's filter output on the device so its consistency guard can be tested
   // (1: survivor key offsets, 2: entry prefix sums); 0 in production
