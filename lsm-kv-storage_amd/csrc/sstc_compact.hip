@@ -118,6 +118,7 @@ struct KGroup {
 // same-address atomic per workgroup (per wave with one block per thread, the
 // serialized atomics took config 3 18 -> 64 us, config 4 -> 104 us).
 constexpr uint32_t kCheckGrid = 512;
+constexpr uint32_t kRsLds = 1024; // run starts / table starts searched in LDS up to this many
 
 // A key group continuing from block b - 1 into block b (r = its first record
 // in b): the merge txns of block b's leading part take the running minimum of
@@ -170,6 +171,14 @@ __global__ __launch_bounds__(256) void ck_check_blocks_kernel(SK *s, const uint6
   // command between the decode and the merge cost ~5 us)
   if (blockIdx.x == 0)
     for (uint64_t i = threadIdx.x; i < kg_words; i += blockDim.x) kg[i] = kg_host[i];
+  // the run starts in LDS for the per-block binary search (log2 runs dependent
+  // L2 round trips per block otherwise: config 4's 128 runs, 7 of them)
+  __shared__ uint64_t s_rs[kRsLds];
+  const bool rs_lds = nruns + 1 <= kRsLds;
+  if (rs_lds)
+    for (uint64_t i = threadIdx.x; i <= nruns; i += blockDim.x) s_rs[i] = run_start[i];
+  __syncthreads();
+  const uint64_t *rs = rs_lds ? s_rs : run_start;
   const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
   const uint64_t t0 = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   for (uint64_t z = t0; z < nz; z += stride) zws[z] = 0; // filter look-back
@@ -184,10 +193,10 @@ __global__ __launch_bounds__(256) void ck_check_blocks_kernel(SK *s, const uint6
     uint64_t lo = 0, hi = nruns; // run containing r: last run_start <= r
     while (lo + 1 < hi) {
       const uint64_t mid = (lo + hi) >> 1;
-      if (run_start[mid] <= r) lo = mid;
+      if (rs[mid] <= r) lo = mid;
       else hi = mid;
     }
-    if (run_start[lo] == r) continue; // first record of its run
+    if (rs[lo] == r) continue; // first record of its run
     const SK cur = s[r], pv = s[r - 1];
     const int c = key_cmp(cur.p0, cur.p1, cur.kl, cur.id, pv.p0, pv.p1, pv.kl, pv.id, kv);
     if (c < 0) atomicAdd(bad, 1ull);
@@ -196,7 +205,7 @@ __global__ __launch_bounds__(256) void ck_check_blocks_kernel(SK *s, const uint6
     // txn order: the minimum of older versions is then >= every txn here)
     if (c == 0) {
       if (cur.tx > pv.tx) atomicOr(guard, kGuardInv); // a group out of txn order across the boundary
-      carry_group(s, rec_base, b, r, run_start[lo], kv, bad, guard);
+      carry_group(s, rec_base, b, r, rs[lo], kv, bad, guard);
     }
   }
   for (uint32_t d = kWave / 2; d > 0; d >>= 1) {
@@ -861,14 +870,22 @@ struct BlkOff {
 };
 
 // block b: length, meta entry size, table index
-__global__ void ck_block_info_kernel(const uint64_t *bf, Lay L, const uint64_t *Pe, const uint32_t *kl,
-                                     const uint64_t *tf, uint64_t *blen, uint64_t *msz, uint32_t *btab,
-                                     uint64_t *zws, uint64_t nz, unsigned long long *guard) {
+__global__ __launch_bounds__(256) void ck_block_info_kernel(const uint64_t *bf, Lay L, const uint64_t *Pe,
+                                                            const uint32_t *kl, const uint64_t *tf, uint64_t *blen,
+                                                            uint64_t *msz, uint32_t *btab, uint64_t *tbf,
+                                                            uint64_t *zws, uint64_t nz, unsigned long long *guard) {
   const uint64_t b = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (b < nz) zws[b] = 0; // look-back status words of the two block scans that follow
-  if (b >= L.nb_max) return;
   const bool ok = L.ok();
   const uint64_t nb = L.nb(), nt = L.nt();
+  // the table starts in LDS for the binary search below
+  __shared__ uint64_t s_tf[kRsLds];
+  const bool tf_lds = ok && nt + 1 <= kRsLds;
+  if (tf_lds)
+    for (uint64_t i = threadIdx.x; i <= nt; i += blockDim.x) s_tf[i] = tf[i];
+  __syncthreads();
+  const uint64_t *T = tf_lds ? s_tf : tf;
+  if (b >= L.nb_max) return;
   if (!ok || b >= nb) { // past the real blocks: zero (the scans over nb_max stay exact)
     blen[b] = 0;
     msz[b] = 0;
@@ -882,10 +899,11 @@ __global__ void ck_block_info_kernel(const uint64_t *bf, Lay L, const uint64_t *
   uint64_t lo = 0, hi = nt;
   while (lo + 1 < hi) {
     const uint64_t mid = (lo + hi) >> 1;
-    if (tf[mid] <= f0) lo = mid;
+    if (T[mid] <= f0) lo = mid;
     else hi = mid;
   }
   btab[b] = static_cast<uint32_t>(lo);
+  if (T[lo] == f0) tbf[lo] = b; // a table's first block (ck_table_info_kernel checks it)
 }
 
 // table t: first block index, data / meta bytes, total.  kScan: one
@@ -909,14 +927,21 @@ __global__ __launch_bounds__(kTiThreads) void ck_table_info_kernel(const uint64_
       }
       tbf[t] = L.ok() ? nb : 0;
     } else {
-      // block starting at record tf[t] (every table start is a block start)
-      uint64_t lo = 0, hi = nb + 1;
+      // block starting at record tf[t] (every table start is a block start):
+      // block_info scattered it into tbf[t] for t < nt; checked, and searched
+      // for when it does not hold (a corrupt split: the guards reject the job)
       const uint64_t r = tf[t];
-      while (lo + 1 < hi) {
-        const uint64_t mid = (lo + hi) >> 1;
-        if (bf[mid] <= r) lo = mid;
-        else hi = mid;
-      }
+      auto first_block = [&](uint64_t rr, uint64_t guess) {
+        if (guess <= nb && bf[guess] == rr) return guess;
+        uint64_t lo = 0, hi = nb + 1;
+        while (lo + 1 < hi) {
+          const uint64_t mid = (lo + hi) >> 1;
+          if (bf[mid] <= rr) lo = mid;
+          else hi = mid;
+        }
+        return lo;
+      };
+      const uint64_t lo = first_block(r, t < nt ? tbf[t] : nb), lo2g = t + 1 < nt ? tbf[t + 1] : nb;
       tbf[t] = lo;
       if (t == nt) { // the sentinel: a zero length when nt < nt_max
         if (t < L.nt_max) {
@@ -925,14 +950,8 @@ __global__ __launch_bounds__(kTiThreads) void ck_table_info_kernel(const uint64_
           tmeta[t] = 0;
         }
       } else {
-        // tbf[t+1] computed by its own thread; recompute here for the sizes
-        uint64_t lo2 = 0, hi2 = nb + 1;
-        const uint64_t r2 = tf[t + 1];
-        while (lo2 + 1 < hi2) {
-          const uint64_t mid = (lo2 + hi2) >> 1;
-          if (bf[mid] <= r2) lo2 = mid;
-          else hi2 = mid;
-        }
+        // tbf[t+1]: thread t + 1 writes it; found here the same way for the sizes
+        const uint64_t lo2 = first_block(tf[t + 1], lo2g);
         const uint64_t d = BL[lo2] - BL[lo], m = MS[lo2] - MS[lo];
         tdata[t] = d;
         tmeta[t] = m;
@@ -1530,11 +1549,13 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     uint32_t *btab = pool.get<uint32_t>(nb_max);
     const uint64_t nzb = scan_status_words(nb_max); // <= nb_max
     uint64_t *ws3 = pool.get<uint64_t>(2 * nzb);
-    ck_block_info_kernel<<<grid(nb_max), 256, 0, s>>>(bf, L, Pe, KR.kl, tf, blen, msz, btab, ws3, 2 * nzb, guard);
+    uint64_t *tbf = pool.get<uint64_t>(nt_max + 1);
+    ck_block_info_kernel<<<grid(nb_max), 256, 0, s>>>(bf, L, Pe, KR.kl, tf, blen, msz, btab, tbf, ws3, 2 * nzb,
+                                                      guard);
     const BlkOff BL{Pe, bf}; // block offsets in closed form (Pe[0] = 0)
     uint64_t *MS = pool.get<uint64_t>(nb_max + 1);
     CK(launch_scan(msz, nb_max, 0, MS, ws3 + nzb, s, true));
-    uint64_t *tbf = pool.get<uint64_t>(nt_max + 1), *tdata = pool.get<uint64_t>(nt_max),
+    uint64_t *tdata = pool.get<uint64_t>(nt_max),
              *tmeta = pool.get<uint64_t>(nt_max);
     if (nt_max + 1 <= kTiThreads) {
       ck_table_info_kernel<true><<<1, kTiThreads, 0, s>>>(tf, L, bf, BL, MS, tbf, tdata, tmeta, d_table_len,
