@@ -114,10 +114,8 @@ struct KGroup {
 // table_builder.h:77): decode_kernel checks each record against its
 // predecessor in the same block; this kernel checks the first record of every
 // non-empty block against the last record before it, unless it starts a run.
-// Grid-stride over the blocks with a capped grid: the source-end bound is one
-// same-address atomic per workgroup (per wave with one block per thread, the
-// serialized atomics took config 3 18 -> 64 us, config 4 -> 104 us).
-constexpr uint32_t kCheckGrid = 512;
+// (Until round 4 it also reduced the source-end bound with one same-address
+// atomic per workgroup, which capped its grid; the count kernel reduces it now.)
 constexpr uint32_t kRsLds = 1024; // run starts / table starts searched in LDS up to this many
 
 // A key group continuing from block b - 1 into block b (r = its first record
@@ -162,10 +160,8 @@ __device__ void carry_group(SK *s, const uint64_t *rec_base, uint64_t b, uint64_
 __global__ __launch_bounds__(256) void ck_check_blocks_kernel(SK *s, const uint64_t *rec_base, uint64_t nblocks,
                                        const uint64_t *run_start, uint64_t nruns, KeyView kv,
                                        unsigned long long *bad, Abort stop, uint64_t *zws, uint64_t nz,
-                                       const uint64_t *blk_off, const uint64_t *blk_len,
-                                       unsigned long long *src_end, unsigned long long *guard,
-                                       const uint64_t *kg_host, uint64_t *kg, uint64_t kg_words) {
-  __shared__ uint64_t s_end[256 / kWave];
+                                       unsigned long long *guard, const uint64_t *kg_host, uint64_t *kg,
+                                       uint64_t kg_words) {
   // the merge passes' group descriptors, written by the host into pinned
   // mapped memory before the launch: copied here by workgroup 0 (a copy
   // command between the decode and the merge cost ~5 us)
@@ -182,12 +178,8 @@ __global__ __launch_bounds__(256) void ck_check_blocks_kernel(SK *s, const uint6
   const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
   const uint64_t t0 = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   for (uint64_t z = t0; z < nz; z += stride) zws[z] = 0; // filter look-back
-  const bool go = !stop();
-  uint64_t e = 0; // end of the source bytes the blocks span: the bound of every entry the encode copies
+  if (stop()) return;
   for (uint64_t b = t0; b < nblocks; b += stride) {
-    const uint64_t x = blk_off[b] + blk_len[b];
-    e = x > e ? x : e;
-    if (!go) continue;
     const uint64_t r = rec_base[b];
     if (r == 0 || rec_base[b + 1] == r) continue;
     uint64_t lo = 0, hi = nruns; // run containing r: last run_start <= r
@@ -207,16 +199,6 @@ __global__ __launch_bounds__(256) void ck_check_blocks_kernel(SK *s, const uint6
       if (cur.tx > pv.tx) atomicOr(guard, kGuardInv); // a group out of txn order across the boundary
       carry_group(s, rec_base, b, r, rs[lo], kv, bad, guard);
     }
-  }
-  for (uint32_t d = kWave / 2; d > 0; d >>= 1) {
-    const uint64_t y = __shfl_xor(e, d, kWave);
-    e = y > e ? y : e;
-  }
-  if (lane_id() == 0) s_end[threadIdx.x / kWave] = e;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    for (uint32_t w = 1; w < 256 / kWave; w++) e = s_end[w] > e ? s_end[w] : e;
-    if (e) atomicMax(src_end, static_cast<unsigned long long>(e));
   }
 }
 
@@ -1219,20 +1201,31 @@ __global__ __launch_bounds__(256) void ck_run_starts_kernel(const uint64_t *rec_
                                                             unsigned long long *guard, const uint64_t *len_part,
                                                             uint64_t nparts, uint64_t *in_bytes) {
   const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (blockIdx.x == 0) {
-    __shared__ uint64_t s_part[256 / kWave];
-    uint64_t v = 0;
-    for (uint64_t p = threadIdx.x; p < nparts; p += 256) v += len_part[p];
+  if (blockIdx.x == 0) { // the count kernel's per-workgroup {byte sum, source end} pairs
+    __shared__ uint64_t s_part[256 / kWave], s_end[256 / kWave];
+    uint64_t v = 0, e = 0;
+    for (uint64_t p = threadIdx.x; p < nparts; p += 256) {
+      v += len_part[2 * p];
+      e = len_part[2 * p + 1] > e ? len_part[2 * p + 1] : e;
+    }
     v = wave_sum_u64(v);
-    if (lane_id() == 0) s_part[threadIdx.x / kWave] = v;
+    for (uint32_t d = kWave / 2; d > 0; d >>= 1) {
+      const uint64_t y = __shfl_xor(e, d, kWave);
+      e = y > e ? y : e;
+    }
+    if (lane_id() == 0) {
+      s_part[threadIdx.x / kWave] = v;
+      s_end[threadIdx.x / kWave] = e;
+    }
     __syncthreads();
-    if (threadIdx.x == 0) *in_bytes = s_part[0] + s_part[1] + s_part[2] + s_part[3];
-  }
-  if (i == 0) {
-    *errs = *err_count;
-    *bad = 0;
-    guard[0] = 0; // consistency-guard bits
-    guard[1] = 0; // source end (ck_check_blocks_kernel)
+    if (threadIdx.x == 0) {
+      *in_bytes = s_part[0] + s_part[1] + s_part[2] + s_part[3];
+      for (uint32_t w = 1; w < 256 / kWave; w++) e = s_end[w] > e ? s_end[w] : e;
+      *errs = *err_count;
+      *bad = 0;
+      guard[0] = 0; // consistency-guard bits
+      guard[1] = e; // the end of the source bytes the input blocks span
+    }
   }
   if (i < n) out[i] = rec_base[tfb[i]];
 }
@@ -1332,7 +1325,7 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     uint64_t *errs = pool.get<uint64_t>(2);
     uint64_t *d_tfb = pool.get<uint64_t>(ntables + 1), *d_rs = pool.get<uint64_t>(ntables + 1);
     const uint64_t nparts = (nblocks + 255) / 256;
-    uint64_t *len_part = pool.get<uint64_t>(nparts + 1), *in_bytes_d = pool.get<uint64_t>(1);
+    uint64_t *len_part = pool.get<uint64_t>(2 * nparts + 2), *in_bytes_d = pool.get<uint64_t>(1);
     CK(launch_count(d_src, d_blk_off, d_blk_len, nblocks, rb_all, s, ws, len_part));
     CK(launch_scan(rb_all, nblocks, 0, rb_all, ws, s, true));
     unsigned long long *bad = reinterpret_cast<unsigned long long *>(pool.get<uint64_t>(1));
@@ -1461,8 +1454,10 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
       static_assert(sizeof(KGroup) % 8 == 0, "KGroup copied as words");
       ensure_up(arena, kg_bytes);
       if (kg_bytes) memcpy(arena.up, kg.data(), kg_bytes);
-      ck_check_blocks_kernel<<<std::min<uint32_t>(std::max<uint32_t>(grid(std::max<uint64_t>(nblocks, 1ull + 3 * fftiles)), 1u), kCheckGrid), 256, 0, s>>>(A, rb_all, nblocks, rb, nruns, kv, bad, dec_fail, ffws,
-                                                           1 + 3 * fftiles, d_blk_off, d_blk_len, guard + 1, guard,
+      // a thread per block boundary (the source-end bound, once a same-address
+      // atomic per workgroup that capped this grid, comes from the count kernel)
+      ck_check_blocks_kernel<<<std::max<uint32_t>(grid(std::max<uint64_t>(nblocks, 1ull + 3 * fftiles)), 1u), 256, 0,
+                               s>>>(A, rb_all, nblocks, rb, nruns, kv, bad, dec_fail, ffws, 1 + 3 * fftiles, guard,
                                                            reinterpret_cast<const uint64_t *>(arena.up_dev),
                                                            reinterpret_cast<uint64_t *>(d_kg), kg_bytes / 8);
       if (!kg.empty()) {

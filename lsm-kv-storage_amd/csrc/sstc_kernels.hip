@@ -489,12 +489,25 @@ __global__ void count_kernel(const uint8_t *src, const uint64_t *blk_off, const 
   const uint64_t b = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   zero_words(zws, nz); // the look-back status words of the scan that follows
   const uint64_t len = b < nblocks ? blk_len[b] : 0;
-  if (len_part) { // uniform: the workgroup's byte sum (bounds the compaction's output counts)
-    __shared__ uint64_t s_part[4];
+  if (len_part) { // uniform: the workgroup's byte sum (bounds the compaction's output counts) and the
+                  // end of the source bytes its blocks span (bounds every entry the compaction copies)
+    __shared__ uint64_t s_part[4], s_end[4];
     const uint64_t v = wave_sum_u64(len);
-    if (lane_id() == 0) s_part[threadIdx.x / kWave] = v;
+    uint64_t e = b < nblocks ? blk_off[b] + len : 0;
+    for (uint32_t d = kWave / 2; d > 0; d >>= 1) {
+      const uint64_t y = __shfl_xor(e, d, kWave);
+      e = y > e ? y : e;
+    }
+    if (lane_id() == 0) {
+      s_part[threadIdx.x / kWave] = v;
+      s_end[threadIdx.x / kWave] = e;
+    }
     __syncthreads();
-    if (threadIdx.x == 0) len_part[blockIdx.x] = s_part[0] + s_part[1] + s_part[2] + s_part[3];
+    if (threadIdx.x == 0) {
+      len_part[2 * blockIdx.x] = s_part[0] + s_part[1] + s_part[2] + s_part[3];
+      const uint64_t e01 = s_end[0] > s_end[1] ? s_end[0] : s_end[1], e23 = s_end[2] > s_end[3] ? s_end[2] : s_end[3];
+      len_part[2 * blockIdx.x + 1] = e01 > e23 ? e01 : e23;
+    }
   }
   if (b >= nblocks) return;
   uint64_t c = 0;

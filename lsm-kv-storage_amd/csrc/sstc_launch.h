@@ -142,7 +142,7 @@ hipError_t launch_roundtrip(const RtArgs &a, hipStream_t s);
 hipError_t launch_copy_probe(const uint8_t *src, uint8_t *dst, uint64_t n16, hipStream_t s);
 hipError_t launch_count(const uint8_t *src, const uint64_t *blk_off, const uint64_t *blk_len,
                         uint64_t nblocks, uint64_t *counts, hipStream_t s, uint64_t *scan_ws = nullptr,
-                        uint64_t *len_part = nullptr); // len_part: per-workgroup sums of blk_len (256 blocks each)
+                        uint64_t *len_part = nullptr); // len_part: per workgroup of 256 blocks, {sum of blk_len, max blk_off + blk_len}
 hipError_t launch_decode(const DecArgs &a, hipStream_t s);
 uint64_t scan_workspace_elems(uint64_t n);
 // look-back status words a scan of n items needs cleared (0: single-workgroup scan)
