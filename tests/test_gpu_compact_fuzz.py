@@ -113,6 +113,25 @@ def test_compact_long_version_groups(codec, oracle):
         codec.compact(bad, 128, 1 << 20, 1)
 
 
+@pytest.mark.timeout(240)
+@pytest.mark.parametrize("per_table", [1, 7, 40])
+def test_compact_many_output_tables(codec, oracle, per_table):
+    """Thousands of output tables: equal-sized records with a table limit of
+    per_table records' key + value bytes -- every hop of the table split
+    starts where predicted (the parallel start hops cover the first 256
+    tables, the wave hops on past them), more table slots than one workgroup
+    holds (the table offsets by a separate scan), many table ends per
+    1024-record tile of the block split (its LDS cache of ends overflows) --
+    and per_table = 40 with 4 KiB blocks, tables of several blocks."""
+    sets = W.compaction_inputs(3, 1500, 6000, seed=77, p_delete=0.0, vmin=24, vmax=24, key_width=16)
+    ins = [oracle.table_build(r, 4096) for r in sets]
+    limit = per_table * (16 + 24)
+    want, _ = oracle.compact(ins, 4096 if per_table == 40 else 256, limit, 1)
+    outs, res = codec.compact(ins, 4096 if per_table == 40 else 256, limit, 1)
+    assert len(outs) == len(want) > (256 if per_table < 40 else 50)
+    assert all(np.array_equal(o, w) for o, w in zip(outs, want))
+
+
 def wide_shapes():
     """Many inputs (multi-pass merges: 8 / 4-way splitter lanes, 2-3 passes),
     tiny key spaces (long version groups, 2 B keys)."""
