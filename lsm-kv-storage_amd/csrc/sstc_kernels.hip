@@ -1690,48 +1690,46 @@ __global__ void seg_npow_kernel(const uint32_t *Nx, const uint32_t *Nc, uint32_t
   }
 }
 
-// visits of the node chain from node 0, total segments, first[total] = m
-__global__ void seg_ndepth_kernel(const uint32_t *Nx, const uint32_t *Nc, uint32_t levels, uint64_t stride,
-                                  uint64_t m, const uint64_t *mp, uint64_t *d_visits, uint64_t *first,
+// Visit h of the node chain from node 0: its node (tile, entry) and the
+// segments before it; a visit past the chain's end meets kNoNode on its walk
+// and leaves.  Thread 0 of workgroup 0 also walks the whole chain down the
+// levels: the total segment count and first[total] = m.  (Round 4: one kernel
+// with the depth walk instead of a one-thread launch before this one.)
+__global__ void seg_nentry_kernel(const uint32_t *Nx, const uint32_t *Nc, const uint32_t *Nt, const uint64_t *base,
+                                  uint32_t levels, uint64_t stride, uint64_t m, const uint64_t *mp,
+                                  uint64_t tiles, uint32_t *tentry, uint32_t *tbefore, uint64_t *first,
                                   uint64_t *d_count) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
   if (mp) m = *mp;
-  if (m == 0) { // no records (an aborted compaction): no node, no segment
-    *d_visits = 0;
-    *d_count = 0;
-    first[0] = 0;
-    return;
-  }
-  uint64_t pos = 0, hops = 0, tot = 0, w = 1;
-  for (uint32_t k = 1; k < levels; k++) w *= kSegRadix;
-  for (int k = static_cast<int>(levels) - 1; k >= 0; k--, w /= kSegRadix) {
-    const uint32_t *X = Nx + static_cast<uint64_t>(k) * stride, *C = Nc + static_cast<uint64_t>(k) * stride;
-    for (uint32_t d = 1; d < kSegRadix; d++) {
-      const uint32_t nx = X[pos];
-      if (nx == kNoNode) break;
-      tot += C[pos];
-      pos = nx;
-      hops += w;
+  const uint64_t h = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (h == 0) {
+    if (m == 0) { // no records (an aborted compaction): no node, no segment
+      *d_count = 0;
+      first[0] = 0;
+    } else {
+      uint64_t pos = 0, tot = 0;
+      for (int k = static_cast<int>(levels) - 1; k >= 0; k--) {
+        const uint32_t *X = Nx + static_cast<uint64_t>(k) * stride, *C = Nc + static_cast<uint64_t>(k) * stride;
+        for (uint32_t d = 1; d < kSegRadix; d++) {
+          const uint32_t nx = X[pos];
+          if (nx == kNoNode) break;
+          tot += C[pos];
+          pos = nx;
+        }
+      }
+      tot += Nc[pos];
+      *d_count = tot;
+      first[tot] = m;
     }
   }
-  tot += Nc[pos];
-  *d_visits = hops + 1;
-  *d_count = tot;
-  first[tot] = m;
-}
-
-// visit h: its node (tile, entry) and the segments before it
-__global__ void seg_nentry_kernel(const uint32_t *Nx, const uint32_t *Nc, const uint32_t *Nt, const uint64_t *base,
-                                  uint32_t levels, uint64_t stride, const uint64_t *d_visits, uint32_t *tentry,
-                                  uint32_t *tbefore) {
-  const uint64_t h = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (h >= *d_visits) return;
+  if (m == 0 || h >= tiles) return; // (a tile is visited at most once)
   uint64_t pos = 0, before = 0, q = h;
   for (uint32_t k = 0; k < levels && q; k++, q /= kSegRadix) {
     const uint32_t *X = Nx + static_cast<uint64_t>(k) * stride, *C = Nc + static_cast<uint64_t>(k) * stride;
     for (uint32_t d = static_cast<uint32_t>(q % kSegRadix); d; d--) {
+      const uint32_t nx = X[pos];
+      if (nx == kNoNode) return; // past the chain's last visit
       before += C[pos];
-      pos = X[pos];
+      pos = nx;
     }
   }
   const uint32_t t = Nt[pos];
@@ -2507,7 +2505,7 @@ hipError_t launch_segment(const uint64_t *Pw, uint64_t nrec, uint64_t threshold,
   const SegLayout L(nrec);
   // u64 region 8-aligned relative to J (J itself is 256-aligned by the callers' allocators)
   uint64_t *U = reinterpret_cast<uint64_t *>(J + L.u64);
-  uint64_t *win = U + L.win, *base = U + L.base, *visits = U + L.visits, *sws = U + L.sws;
+  uint64_t *win = U + L.win, *base = U + L.base, *sws = U + L.sws;
   uint32_t *tentry = J + L.tentry, *tbefore = J + L.tbefore;
   const uint64_t stride = nrec + 1;
   SegArgs a{Pw, add, nrec, threshold, ends, d_nends, J + L.J0, J + L.Fx, J + L.Fc, win, blk_first, d_nblocks,
@@ -2522,11 +2520,9 @@ hipError_t launch_segment(const uint64_t *Pw, uint64_t nrec, uint64_t threshold,
   for (uint64_t k = 0; k + 1 < L.levels; k++)
     seg_npow_kernel<<<pg, 256, 0, s>>>(J + L.Nx + k * stride, J + L.Nc + k * stride, J + L.Nx + (k + 1) * stride,
                                        J + L.Nc + (k + 1) * stride, nn);
-  seg_ndepth_kernel<<<1, 64, 0, s>>>(J + L.Nx, J + L.Nc, static_cast<uint32_t>(L.levels), stride, nrec, d_nrec,
-                                     visits, blk_first, d_nblocks);
   seg_nentry_kernel<<<grid_for(L.tiles, 256), 256, 0, s>>>(J + L.Nx, J + L.Nc, J + L.Nt, base,
-                                                           static_cast<uint32_t>(L.levels), stride, visits,
-                                                           tentry, tbefore);
+                                                           static_cast<uint32_t>(L.levels), stride, nrec, d_nrec,
+                                                           L.tiles, tentry, tbefore, blk_first, d_nblocks);
   seg_emit_kernel<<<static_cast<uint32_t>(L.tiles), kChThreads, 0, s>>>(J + L.J0, nrec, d_nrec, tentry, tbefore,
                                                                         blk_first);
   return hipGetLastError();
