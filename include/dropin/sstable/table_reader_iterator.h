@@ -1,0 +1,132 @@
+/*
+ * include/dropin/sstable/table_reader_iterator.h — the drop-in for the
+ * reference's sstable/table_reader_iterator.h
+ * (/root/reference/sstable/table_reader_iterator.h:21-75).
+ *
+ * With include/dropin/ first on the include path and
+ * lsm-kv-storage_amd/csrc/dropin/table_reader_iterator.cc compiled in place of
+ * the reference's sstable/table_reader_iterator.cc, db/compact.cc and
+ * db/merge_iterator.cc build UNCHANGED: every iterator
+ * Compact::CreateMergeIterator makes (compact.cc:201-203,223-225) and
+ * MergeIterator walks (merge_iterator.cc:34-46,79-92) decodes its table on the
+ * GPU.  Same class, same base (kvs::BaseIterator), same constructor, same
+ * include guard as the reference header, so the reference header is never
+ * seen twice.
+ *
+ * Behaviour (table_reader_iterator.cc:14-149): on the first
+ * SeekToFirst / SeekToLast / Seek the whole data section of the table is read
+ * through the TableReader's own file object (a friend of TableReader,
+ * table_reader.h:105) and every block of its BlockIndex vector is decoded in
+ * ONE GPU call (sstc::DecodeBlocks on the calling thread's context, txn in the
+ * reference's compat mode: an empty-value PUT reads (txn & 0xffffffff) << 32,
+ * block_reader.cc:109-111).  Then the iterator walks the decoded records with
+ * the reference's block / entry cursor semantics, including IsValid() being
+ * the block cursor's range check, Seek() not moving the block cursor, and the
+ * out-of-range accessors (empty view, NOT_FOUND, INVALID_TXN_ID,
+ * block_reader_iterator.cc:30-71).  Views stay valid for the iterator's
+ * lifetime (the decoded table is owned by it), so MergeIterator's heap keys
+ * and compact.cc:250's last_current_key never dangle.
+ *
+ * Errors: the reference dereferences a null block iterator when a block
+ * cannot be read (table_reader_iterator.cc:140-142,101) and reads out of
+ * bounds on a corrupt block; this iterator throws std::runtime_error from the
+ * Seek that loads the table instead (read failure, corrupt block, or no HIP
+ * device -- there is no CPU decode path).
+ */
+#ifndef SSTABLE_TABLE_READER_ITERATOR_H
+#define SSTABLE_TABLE_READER_ITERATOR_H
+
+#include "common/base_iterator.h"
+#include "common/macros.h"
+
+// libC++
+#include <cassert>
+#include <cstdint>
+#include <memory>
+#include <string_view>
+#include <vector>
+
+namespace sstc {
+struct DecodedBlocks;
+}
+
+namespace kvs {
+
+namespace sstable {
+
+class BlockReaderCache;
+class BlockReaderIterator;
+class LRUBlockItem;
+class LRUTableItem;
+class TableReader;
+
+class TableReaderIterator : public kvs::BaseIterator {
+public:
+  TableReaderIterator(
+      const std::vector<std::unique_ptr<BlockReaderCache>> &block_reader_cache,
+      std::shared_ptr<LRUTableItem> lru_table_item);
+
+  ~TableReaderIterator();
+
+  // No copy allowed
+  TableReaderIterator(const TableReaderIterator &) = delete;
+  TableReaderIterator &operator=(TableReaderIterator &) = delete;
+
+  // No move allowed
+  TableReaderIterator(TableReaderIterator &&other) = delete;
+  TableReaderIterator &operator=(TableReaderIterator &&other) = delete;
+
+  std::string_view GetKey() override;
+
+  std::string_view GetValue() override;
+
+  db::ValueType GetType() override;
+
+  TxnId GetTransactionId() override;
+
+  bool IsValid() override;
+
+  void Next() override;
+
+  void Prev() override;
+
+  void Seek(std::string_view key) override;
+
+  void SeekToFirst() override;
+
+  void SeekToLast() override;
+
+private:
+  // decodes the table on first use (one GPU call)
+  void Load();
+  // the block the entry cursor runs over (CreateNewBlockReaderIterator)
+  void ShowBlock(uint64_t block);
+  uint64_t EntriesInShownBlock() const;
+  bool EntryValid() const;
+  uint64_t Record() const;
+
+  // block cursor: current_block_offset_index_ of table_reader_iterator.h:64
+  uint64_t current_block_offset_index_;
+  // the block an entry cursor exists for (block_reader_iterator_ != nullptr)
+  // and that cursor (BlockReaderIterator::current_offset_index_)
+  bool has_block_ = false;
+  uint64_t shown_block_ = 0;
+  uint64_t entry_ = 0;
+
+  const std::vector<std::unique_ptr<BlockReaderCache>> &block_reader_cache_;
+
+  std::shared_ptr<LRUTableItem> lru_table_item_;
+
+  const TableReader *table_reader_;
+
+  bool loaded_ = false;
+  uint64_t data_begin_ = 0;
+  std::vector<uint8_t> data_;
+  std::unique_ptr<sstc::DecodedBlocks> rec_;
+};
+
+} // namespace sstable
+
+} // namespace kvs
+
+#endif // SSTABLE_TABLE_READER_ITERATOR_H

@@ -255,6 +255,25 @@ private:
   std::vector<BlockIndex> index_;
 };
 
+/* The records of many blocks decoded in ONE GPU call (sstc_count_records +
+ * sstc_decode_blocks through `ctx`): block b's records are
+ * [base[b], base[b+1]), offsets point into the host bytes that were decoded,
+ * val_len == SSTC_NO_VALUE marks a record without value fields (a DELETE),
+ * status[b] is the block's SSTC_BLK_* code.  What the drop-in
+ * kvs::sstable::TableReaderIterator (include/dropin/sstable/
+ * table_reader_iterator.h) decodes a whole table with. */
+struct DecodedBlocks {
+  std::vector<uint64_t> base;
+  std::vector<uint32_t> status;
+  std::vector<uint8_t> type;
+  std::vector<uint32_t> key_len, val_len;
+  std::vector<uint64_t> txn, key_off, val_off;
+};
+/* blocks (off[b], len[b]) inside data[0, bytes); SSTC_OK or a negative
+ * SSTC_E_* code (bad arguments, HIP failure) */
+int DecodeBlocks(sstc_ctx *ctx, const uint8_t *data, uint64_t bytes, const uint64_t *off, const uint64_t *len,
+                 uint64_t nb, uint32_t txn_mode, DecodedBlocks &out);
+
 /* table_reader_iterator.cc:46-149 over a table decoded whole on the GPU at the
  * first Seek (one sstc_count_records + sstc_decode_blocks call instead of a
  * pread and a BlockReader per block). */

@@ -130,10 +130,15 @@ def build(verbose=False):
         if verbose:
             print(" ".join(cmd))
         subprocess.run(cmd, check=True)
-    # a C++ caller compiled against include/sstc_table.h (the drop-in surface):
-    # the DoCompactJob loop over sstc::TableBuilder / TableReaderIterator
-    tu = os.path.join(ROOT, "tests", "cpp", "compact_loop.cc")
-    exe = os.path.join(LIB, "sstc_compact_loop")
+    # a C++ caller compiled against include/sstc_table.h: the codec's own
+    # reader surface (block readers vs the table iterator, record by record)
+    stale = os.path.join(LIB, "sstc_compact_loop")
+    if os.path.exists(stale):
+        os.remove(stale)
+        _info.pop(os.path.relpath(stale, ROOT), None)
+        _state["changed"] = True
+    tu = os.path.join(ROOT, "tests", "cpp", "readers_check.cc")
+    exe = os.path.join(LIB, "sstc_readers_check")
     if os.path.exists(tu) and _newer(exe, [tu, so, os.path.join(ROOT, "include", "sstc_table.h")]):
         cmd = [os.environ.get("CXX", "g++"), "-O2", "-std=c++17", "-Wall", "-I" + os.path.join(ROOT, "include"), tu,
                "-o", exe, "-L" + LIB, "-lsstcodec", "-Wl,-rpath,$ORIGIN"]

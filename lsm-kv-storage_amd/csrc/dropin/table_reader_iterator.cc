@@ -1,0 +1,200 @@
+// table_reader_iterator.cc — the drop-in kvs::sstable::TableReaderIterator
+// (include/dropin/sstable/table_reader_iterator.h), compiled by the ENGINE's
+// build in place of /root/reference/sstable/table_reader_iterator.cc, with
+// include/dropin/ first and the reference's own headers after it on the
+// include path (oracle/Makefile target `dropin`).  It is not part of
+// libsstcodec.so, which never sees a reference type: this TU is the thin
+// adapter between the engine's TableReader (friend access, table_reader.h:105)
+// and the codec's host API (sstc::DecodeBlocks, include/sstc_table.h).
+//
+// Cursor semantics follow the reference line by line:
+//   table_reader_iterator.cc:41-44   IsValid = block cursor in range
+//   table_reader_iterator.cc:46-67   Next (entry++, else next block's first)
+//   table_reader_iterator.cc:69-90   Prev (entry--, else previous block's last)
+//   table_reader_iterator.cc:92-95   Seek (block by largest key, entry 0, the
+//                                    block cursor is NOT moved)
+//   table_reader_iterator.cc:97-109  SeekToFirst / SeekToLast
+//   block_reader_iterator.cc:20-81   entry cursor (uint64_t, wraps) and the
+//                                    out-of-range accessor values
+// The block caches (table_reader_iterator.cc:125-134) are not consulted:
+// compaction never inserts into them (:144-146) and a cached block holds the
+// file's bytes, which this iterator decodes whole.
+#include "sstable/table_reader_iterator.h"
+
+#include "io/linux_file.h"
+#include "sstable/block_index.h"
+#include "sstable/lru_table_item.h"
+#include "sstable/table_reader.h"
+#include "sstc_table.h"
+
+#include <span>
+#include <stdexcept>
+#include <string>
+
+namespace kvs {
+
+namespace sstable {
+
+TableReaderIterator::TableReaderIterator(
+    const std::vector<std::unique_ptr<BlockReaderCache>> &block_reader_cache,
+    std::shared_ptr<LRUTableItem> lru_table_item)
+    : current_block_offset_index_(0), block_reader_cache_(block_reader_cache),
+      lru_table_item_(lru_table_item), rec_(std::make_unique<sstc::DecodedBlocks>()) {
+  table_reader_ = lru_table_item_->GetTableReader();
+  assert(table_reader_);
+}
+
+// table_reader_iterator.cc:23
+TableReaderIterator::~TableReaderIterator() { lru_table_item_->Unref(); }
+
+void TableReaderIterator::Load() {
+  if (loaded_) return;
+  const std::vector<BlockIndex> &index = table_reader_->block_index_;
+  const uint64_t nb = index.size();
+  // the data section: every block the meta section lists, read with the
+  // TableReader's own file object (table_reader.cc:220-221 reads them one by one)
+  uint64_t lo = UINT64_MAX, hi = 0;
+  for (const BlockIndex &bi : index) {
+    lo = std::min<uint64_t>(lo, bi.GetBlockStartOffset());
+    hi = std::max<uint64_t>(hi, bi.GetBlockStartOffset() + bi.GetBlockSize());
+  }
+  if (nb == 0) lo = hi = 0;
+  data_begin_ = lo;
+  data_.resize(hi - lo);
+  for (uint64_t done = 0; done < data_.size();) {
+    const uint64_t chunk = std::min<uint64_t>(data_.size() - done, 1ull << 30);
+    const ssize_t r = table_reader_->read_file_object_->RandomRead(
+        std::span<Byte>(data_.data() + done, chunk), lo + done);
+    if (r <= 0)
+      throw std::runtime_error("TableReaderIterator: cannot read the data section of " + table_reader_->filename_);
+    done += static_cast<uint64_t>(r);
+  }
+  std::vector<uint64_t> off(nb), len(nb);
+  for (uint64_t b = 0; b < nb; b++) {
+    off[b] = index[b].GetBlockStartOffset() - lo;
+    len[b] = index[b].GetBlockSize();
+  }
+  // every block of the table in ONE GPU decode, txn as the reference reads it
+  const int rc = sstc::DecodeBlocks(sstc::ThreadContext(), data_.data(), data_.size(), off.data(), len.data(), nb,
+                                    SSTC_TXN_COMPAT, *rec_);
+  if (rc != SSTC_OK)
+    throw std::runtime_error("TableReaderIterator: GPU decode of " + table_reader_->filename_ +
+                             " failed: " + sstc_last_error_string());
+  for (uint64_t b = 0; b < nb; b++)
+    if (rec_->status[b] != SSTC_BLK_OK)
+      throw std::runtime_error("TableReaderIterator: corrupt block " + std::to_string(b) + " in " +
+                               table_reader_->filename_ + " (SSTC_BLK code " + std::to_string(rec_->status[b]) +
+                               ")");
+  loaded_ = true;
+}
+
+void TableReaderIterator::ShowBlock(uint64_t block) {
+  has_block_ = true;
+  shown_block_ = block;
+}
+
+uint64_t TableReaderIterator::EntriesInShownBlock() const {
+  return rec_->base[shown_block_ + 1] - rec_->base[shown_block_];
+}
+
+bool TableReaderIterator::EntryValid() const {
+  return has_block_ && shown_block_ + 1 < rec_->base.size() && entry_ < EntriesInShownBlock();
+}
+
+uint64_t TableReaderIterator::Record() const { return rec_->base[shown_block_] + entry_; }
+
+// block_reader_iterator.cc:30-40
+std::string_view TableReaderIterator::GetKey() {
+  if (!EntryValid()) return std::string_view{};
+  const uint64_t r = Record();
+  return {reinterpret_cast<const char *>(data_.data()) + rec_->key_off[r], rec_->key_len[r]};
+}
+
+// block_reader_iterator.cc:42-52 + block_reader.cc:84-102: a DELETE has no
+// value (null view), a PUT a view into the block even when empty
+std::string_view TableReaderIterator::GetValue() {
+  if (!EntryValid()) return std::string_view{};
+  const uint64_t r = Record();
+  if (rec_->type[r] == static_cast<uint8_t>(db::ValueType::DELETED) || rec_->val_len[r] == SSTC_NO_VALUE)
+    return std::string_view{};
+  return {reinterpret_cast<const char *>(data_.data()) + rec_->val_off[r], rec_->val_len[r]};
+}
+
+// block_reader_iterator.cc:54-61
+db::ValueType TableReaderIterator::GetType() {
+  if (!EntryValid()) return db::ValueType::NOT_FOUND;
+  return static_cast<db::ValueType>(rec_->type[Record()]);
+}
+
+// block_reader_iterator.cc:63-71 (compat txn: block_reader.cc:104-114)
+TxnId TableReaderIterator::GetTransactionId() {
+  if (!EntryValid()) return INVALID_TXN_ID;
+  return rec_->txn[Record()];
+}
+
+// table_reader_iterator.cc:41-44
+bool TableReaderIterator::IsValid() {
+  return current_block_offset_index_ < table_reader_->block_index_.size();
+}
+
+// table_reader_iterator.cc:46-67
+void TableReaderIterator::Next() {
+  if (!has_block_) return;
+  entry_++;
+  if (EntryValid()) return;
+  current_block_offset_index_++;
+  if (!IsValid()) return;
+  ShowBlock(current_block_offset_index_);
+  entry_ = 0;
+}
+
+// table_reader_iterator.cc:69-90
+void TableReaderIterator::Prev() {
+  if (!has_block_) return;
+  entry_--;
+  if (EntryValid()) return;
+  current_block_offset_index_--;
+  if (!IsValid()) return;
+  ShowBlock(current_block_offset_index_);
+  entry_ = EntriesInShownBlock() - 1;
+}
+
+// table_reader_iterator.cc:92-95 with TableReader::GetBlockOffsetAndSize
+// (table_reader.cc:191-210): the block with the smallest largest key >= key
+// (the last block when none is), entry cursor at 0; the block cursor stays
+void TableReaderIterator::Seek(std::string_view key) {
+  Load();
+  const std::vector<BlockIndex> &index = table_reader_->block_index_;
+  int64_t left = 0;
+  int64_t right = static_cast<int64_t>(index.size()) - 1;
+  while (left < right) {
+    const int64_t mid = left + (right - left) / 2;
+    if (index[mid].GetLargestKey() >= key) right = mid;
+    else left = mid + 1;
+  }
+  if (right < 0) return; // no block (the reference indexes block_index_[-1])
+  ShowBlock(static_cast<uint64_t>(right));
+  entry_ = 0;
+}
+
+// table_reader_iterator.cc:97-102
+void TableReaderIterator::SeekToFirst() {
+  Load();
+  current_block_offset_index_ = 0;
+  if (!IsValid()) return; // empty table (the reference indexes block_index_[0])
+  ShowBlock(current_block_offset_index_);
+  entry_ = 0;
+}
+
+// table_reader_iterator.cc:104-109
+void TableReaderIterator::SeekToLast() {
+  Load();
+  current_block_offset_index_ = table_reader_->block_index_.size() - 1;
+  if (!IsValid()) return;
+  ShowBlock(current_block_offset_index_);
+  entry_ = EntriesInShownBlock() - 1;
+}
+
+} // namespace sstable
+
+} // namespace kvs

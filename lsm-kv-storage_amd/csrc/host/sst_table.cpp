@@ -105,11 +105,6 @@ bool d2h(sstc_ctx *ctx, void *h, const void *d, size_t n) {
 
 bool sync(sstc_ctx *ctx) { return hipStreamSynchronize(stream_of(ctx)) == hipSuccess; }
 
-template <class T> DevBuf upload(sstc_ctx *ctx, const std::vector<T> &v) {
-  DevBuf d(v.size() * sizeof(T));
-  h2d(ctx, d.p, v.data(), v.size() * sizeof(T));
-  return d;
-}
 
 } // namespace
 
@@ -437,46 +432,59 @@ TableReader::~TableReader() {
 namespace {
 // Batched GPU decode of blocks (off[b], len[b]) inside the host bytes `data`:
 // per-block record counts and status, record fields with offsets into data.
-struct HostRecords {
-  std::vector<uint8_t> type;
-  std::vector<uint32_t> kl, vl, status;
-  std::vector<uint64_t> txn, ko, vo, base;
-};
+using HostRecords = DecodedBlocks;
 
+DevBuf upload_raw(sstc_ctx *ctx, const void *h, size_t n) {
+  DevBuf d(n);
+  h2d(ctx, d.p, h, n);
+  return d;
+}
+} // namespace
+
+int DecodeBlocks(sstc_ctx *ctx, const uint8_t *data, uint64_t bytes, const uint64_t *off, const uint64_t *len,
+                 uint64_t nb, uint32_t txn_mode, DecodedBlocks &out) {
+  if (!ctx || (bytes && !data) || (nb && (!off || !len))) return SSTC_E_INVALID_ARG;
+  for (uint64_t b = 0; b < nb; b++)
+    if (off[b] > bytes || len[b] > bytes - off[b]) return SSTC_E_INVALID_ARG;
+  static const uint8_t kZero[16] = {};
+  try {
+    DeviceScope on_ctx_device(sstc__ctx_device(ctx));
+    DevBuf d_src = upload_raw(ctx, bytes ? data : kZero, bytes ? bytes : 1), d_off = upload_raw(ctx, off, nb * 8),
+           d_len = upload_raw(ctx, len, nb * 8), d_base((nb + 1) * 8), d_status(nb * 4 + 4);
+    check(sstc_count_records(ctx, d_src.as<uint8_t>(), d_off.as<uint64_t>(), d_len.as<uint64_t>(), nb,
+                             d_base.as<uint64_t>()),
+          "sstc_count_records");
+    out.base.resize(nb + 1);
+    if (!d2h(ctx, out.base.data(), d_base.p, (nb + 1) * 8) || !sync(ctx)) return SSTC_E_HIP;
+    const uint64_t n = out.base[nb];
+    DevBuf d_type(n + 1), d_kl(4 * n + 4), d_vl(4 * n + 4), d_txn(8 * n + 8), d_ko(8 * n + 8), d_vo(8 * n + 8);
+    sstc_records rec{d_type.as<uint8_t>(), d_kl.as<uint32_t>(), d_vl.as<uint32_t>(),
+                     d_txn.as<uint64_t>(), d_ko.as<uint64_t>(), d_vo.as<uint64_t>()};
+    check(sstc_decode_blocks(ctx, d_src.as<uint8_t>(), d_off.as<uint64_t>(), d_len.as<uint64_t>(), nb,
+                             d_base.as<uint64_t>(), rec, txn_mode, d_status.as<uint32_t>()),
+          "sstc_decode_blocks");
+    out.status.resize(nb);
+    out.type.resize(n);
+    out.key_len.resize(n);
+    out.val_len.resize(n);
+    out.txn.resize(n);
+    out.key_off.resize(n);
+    out.val_off.resize(n);
+    bool ok = d2h(ctx, out.status.data(), d_status.p, nb * 4) && d2h(ctx, out.type.data(), d_type.p, n) &&
+              d2h(ctx, out.key_len.data(), d_kl.p, 4 * n) && d2h(ctx, out.val_len.data(), d_vl.p, 4 * n) &&
+              d2h(ctx, out.txn.data(), d_txn.p, 8 * n) && d2h(ctx, out.key_off.data(), d_ko.p, 8 * n) &&
+              d2h(ctx, out.val_off.data(), d_vo.p, 8 * n);
+    ok = sync(ctx) && ok;
+    return ok ? SSTC_OK : SSTC_E_HIP;
+  } catch (const std::exception &) {
+    return SSTC_E_HIP;
+  }
+}
+
+namespace {
 int decode_host(sstc_ctx *ctx, std::vector<uint8_t> &data, const std::vector<uint64_t> &off,
                 const std::vector<uint64_t> &len, uint32_t txn_mode, HostRecords &out) {
-  const uint64_t nb = off.size();
-  if (data.empty()) data.push_back(0);
-  DevBuf d_src = upload(ctx, data), d_off = upload(ctx, off), d_len = upload(ctx, len), d_base((nb + 1) * 8),
-         d_status(nb * 4 + 4);
-  check(sstc_count_records(ctx, d_src.as<uint8_t>(), d_off.as<uint64_t>(), d_len.as<uint64_t>(), nb,
-                           d_base.as<uint64_t>()),
-        "sstc_count_records");
-  uint64_t errs = 0;
-  check(sstc_ctx_error_count(ctx, &errs), "sync");
-  out.base.resize(nb + 1);
-  if (!d2h(ctx, out.base.data(), d_base.p, (nb + 1) * 8) || !sync(ctx)) return SSTC_E_HIP;
-  const uint64_t n = out.base[nb];
-  DevBuf d_type(n + 1), d_kl(4 * n + 4), d_vl(4 * n + 4), d_txn(8 * n + 8), d_ko(8 * n + 8), d_vo(8 * n + 8);
-  sstc_records rec{d_type.as<uint8_t>(), d_kl.as<uint32_t>(), d_vl.as<uint32_t>(),
-                   d_txn.as<uint64_t>(), d_ko.as<uint64_t>(), d_vo.as<uint64_t>()};
-  check(sstc_decode_blocks(ctx, d_src.as<uint8_t>(), d_off.as<uint64_t>(), d_len.as<uint64_t>(), nb,
-                           d_base.as<uint64_t>(), rec, txn_mode, d_status.as<uint32_t>()),
-        "sstc_decode_blocks");
-  check(sstc_ctx_error_count(ctx, &errs), "sync");
-  out.status.resize(nb);
-  out.type.resize(n);
-  out.kl.resize(n);
-  out.vl.resize(n);
-  out.txn.resize(n);
-  out.ko.resize(n);
-  out.vo.resize(n);
-  bool ok = d2h(ctx, out.status.data(), d_status.p, nb * 4) && d2h(ctx, out.type.data(), d_type.p, n) &&
-            d2h(ctx, out.kl.data(), d_kl.p, 4 * n) && d2h(ctx, out.vl.data(), d_vl.p, 4 * n) &&
-            d2h(ctx, out.txn.data(), d_txn.p, 8 * n) && d2h(ctx, out.ko.data(), d_ko.p, 8 * n) &&
-            d2h(ctx, out.vo.data(), d_vo.p, 8 * n);
-  ok = sync(ctx) && ok;
-  return ok ? SSTC_OK : SSTC_E_HIP;
+  return DecodeBlocks(ctx, data.data(), data.size(), off.data(), len.data(), off.size(), txn_mode, out);
 }
 
 struct CtxHolder { // one context + one non-blocking stream per host thread, destroyed at thread exit
@@ -522,11 +530,11 @@ int TableReader::DecodeAll(uint32_t txn_mode, std::vector<uint8_t> &data, std::v
   HostRecords r;
   if (int rc = decode_host(ctx_, data, off, len, txn_mode, r)) return rc;
   type = std::move(r.type);
-  key_len = std::move(r.kl);
-  val_len = std::move(r.vl);
+  key_len = std::move(r.key_len);
+  val_len = std::move(r.val_len);
   txn = std::move(r.txn);
-  key_off = std::move(r.ko);
-  val_off = std::move(r.vo);
+  key_off = std::move(r.key_off);
+  val_off = std::move(r.val_off);
   for (uint64_t b = 0; b < nb; b++)
     if (r.status[b] != SSTC_BLK_OK) return static_cast<int>(r.status[b]);
   return SSTC_BLK_OK;
@@ -561,11 +569,11 @@ std::vector<std::unique_ptr<BlockReader>> TableReader::CreateAndSetupDataForBloc
     br->status_ = static_cast<int>(r.status[k]);
     for (uint64_t i = r.base[k]; i < r.base[k + 1]; i++) {
       br->type_.push_back(r.type[i]);
-      br->key_len_.push_back(r.kl[i]);
-      br->val_len_.push_back(r.vl[i]);
+      br->key_len_.push_back(r.key_len[i]);
+      br->val_len_.push_back(r.val_len[i]);
       br->txn_.push_back(r.txn[i]);
-      br->key_off_.push_back(r.ko[i] - off[k]);
-      br->val_off_.push_back(r.vl[i] == SSTC_NO_VALUE ? 0 : r.vo[i] - off[k]);
+      br->key_off_.push_back(r.key_off[i] - off[k]);
+      br->val_off_.push_back(r.val_len[i] == SSTC_NO_VALUE ? 0 : r.val_off[i] - off[k]);
     }
     out[which[k]] = std::move(br);
   }

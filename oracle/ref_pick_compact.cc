@@ -25,8 +25,33 @@
 //   outputs "<id>.sst" (ids k+1, ...).  Prints one line per input the job
 //   picked ("in <table_id>") and one per output ("out <path> <GetFileSize()>
 //   <smallest_hex> <largest_hex>"), in VersionEdit order.
+//
+// usage: <exe> --loop <db_dir> <block_size> <table_limit> <base_level> [<file> <file_size>]...
+//   The DoCompactJob loop (compact.cc:232-322) with the output split at ANY
+//   table_limit (db::Config refuses limits below 4 MiB, db/config.cc:66-70)
+//   and IsBaseLevelForKey() == base_level, over the REAL readers and merge:
+//   TableReaderIterators made as Compact::CreateMergeIterator makes them
+//   (compact.cc:207-225, through the TableReaderCache) and the reference's own
+//   db::MergeIterator.  Prints the "out" lines.  Only the ~40-line loop body
+//   is restated (ShouldKeepEntry is a private member of Compact).
+//
+// usage: <exe> --iter <dump> [<file> <file_size>]...
+//   A scripted walk of every table through sstable::TableReaderIterator
+//   (SeekToFirst + Next to the end and past it, SeekToLast + Prev to the
+//   start and past it, Seek to every block's first / last key and to keys
+//   outside the table, each followed by Nexts), every step's IsValid / key /
+//   value / type / txn written to <dump>: linked against the reference's
+//   table_reader_iterator.cc this is the reference's trace, linked as the
+//   drop-in it is the GPU-decoding iterator's, and the two must be equal.
 #include "common/base_iterator.h"
 #include "common/thread_pool.h"
+#include "db/merge_iterator.h"
+#include "sstable/block_builder.h"
+#include "sstable/block_index.h"
+#include "sstable/lru_table_item.h"
+#include "sstable/table_builder.h"
+#include "sstable/table_reader.h"
+#include "sstable/table_reader_iterator.h"
 #include "db/base_memtable.h"
 #include "db/compact.h"
 #include "db/config.h"
@@ -139,7 +164,149 @@ const sstable::TableReaderCache *DBImpl::GetTableReaderCache() const { return ta
 } // namespace db
 } // namespace kvs
 
+namespace {
+using namespace kvs;
+
+// compact.cc:207-225: a TableReader opened and inserted into the table cache,
+// then an iterator over the cached item
+std::unique_ptr<sstable::TableReaderIterator> OpenIterator(db::DBImpl *db, SSTId id, const char *path,
+                                                           uint64_t file_size) {
+  auto reader = sstable::CreateAndSetupDataForTableReader(std::string(path), id, file_size);
+  if (!reader) return nullptr;
+  auto item = std::make_shared<sstable::LRUTableItem>(id, std::move(reader), db->GetTableReaderCache());
+  auto inserted = db->GetTableReaderCache()->AddNewTableReaderThenGet(id, item, true /*add_then_get*/);
+  return std::make_unique<sstable::TableReaderIterator>(db->GetBlockReaderCache(), inserted);
+}
+
+int RunLoop(int argc, char **argv) {
+  // argv: --loop db_dir block_size table_limit base_level [file size]...
+  g_db_path = std::string(argv[2]);
+  if (g_db_path.back() != '/') g_db_path += '/';
+  g_block_size = std::strtoull(argv[3], nullptr, 10);
+  const uint64_t table_limit = std::strtoull(argv[4], nullptr, 10);
+  const bool base_level = std::atoi(argv[5]) != 0;
+  const int k = (argc - 6) / 2;
+  g_first_id = static_cast<uint64_t>(k) + 1;
+  g_table_limit = 32ull << 20; // what db::Config accepts; the loop splits at table_limit
+  auto *db = new db::DBImpl(true);
+  std::vector<std::unique_ptr<sstable::TableReaderIterator>> its;
+  for (int i = 0; i < k; i++) {
+    its.push_back(OpenIterator(db, static_cast<SSTId>(i + 1), argv[6 + 2 * i],
+                               std::strtoull(argv[7 + 2 * i], nullptr, 10)));
+    if (!its.back()) return 4;
+  }
+  auto iterator = std::make_unique<db::MergeIterator>(std::move(its));
+  auto report = [](uint64_t id, sstable::TableBuilder &t) {
+    std::printf("out %s%llu.sst %llu %s %s\n", g_db_path.c_str(), (unsigned long long)id,
+                (unsigned long long)t.GetFileSize(), Hex(t.GetSmallestKey()).c_str(), Hex(t.GetLargestKey()).c_str());
+  };
+  // ---- compact.cc:235-311 (the loop as written, minus the version edits)
+  uint64_t new_sst_id = db->GetNextSSTId();
+  std::string filename = db->GetDBPath() + std::to_string(new_sst_id) + ".sst";
+  auto new_sst = std::make_unique<sstable::TableBuilder>(std::move(filename), db->GetConfig());
+  if (!new_sst->Open()) return 5;
+  std::string last_current_key; // an owned copy: the intended semantics of compact.cc:250
+  bool have_last = false;
+  TxnId last_txn_id = INVALID_TXN_ID;
+  for (iterator->SeekToFirst(); iterator->IsValid(); iterator->Next()) {
+    std::string_view key = iterator->GetKey();
+    std::string_view value = iterator->GetValue();
+    db::ValueType type = iterator->GetType();
+    TxnId txn_id = iterator->GetTransactionId();
+    // ShouldKeepEntry (compact.cc:324-363) with IsBaseLevelForKey() == base_level
+    bool should_keep_entry;
+    if (!have_last) should_keep_entry = true;
+    else if (last_current_key != key) should_keep_entry = type == db::ValueType::PUT ? true : !base_level;
+    else should_keep_entry = !(last_txn_id > txn_id);
+    if (!have_last || last_current_key != key) {
+      last_current_key.assign(key.data(), key.size());
+      last_txn_id = txn_id;
+      have_last = true;
+    }
+    if (!should_keep_entry) continue;
+    if (!new_sst) {
+      new_sst_id = db->GetNextSSTId();
+      filename = db->GetDBPath() + std::to_string(new_sst_id) + ".sst";
+      new_sst = std::make_unique<sstable::TableBuilder>(std::move(filename), db->GetConfig());
+      if (!new_sst->Open()) return 5;
+    }
+    new_sst->AddEntry(key, value, txn_id, type);
+    if (new_sst->GetDataSize() >= table_limit) {
+      new_sst->Finish();
+      report(new_sst_id, *new_sst);
+      new_sst.reset();
+    }
+  }
+  if (new_sst) {
+    new_sst->Finish();
+    report(new_sst_id, *new_sst);
+  }
+  std::fflush(stdout);
+  _exit(0);
+}
+
+int RunIter(int argc, char **argv) {
+  // argv: --iter dump [file size]...
+  std::FILE *dump = std::fopen(argv[2], "wb");
+  if (!dump) return 4;
+  char tmpl[] = "/tmp/sstref_iterXXXXXX";
+  if (!mkdtemp(tmpl)) return 3;
+  g_db_path = std::string(tmpl) + "/";
+  auto *db = new db::DBImpl(true);
+  auto put = [&](const void *p, size_t n) { std::fwrite(p, 1, n, dump); };
+  auto view = [&](std::string_view v) {
+    const uint8_t has = v.data() != nullptr;
+    const uint32_t n = static_cast<uint32_t>(v.size());
+    put(&has, 1), put(&n, 4);
+    if (n) put(v.data(), n);
+  };
+  uint64_t steps = 0;
+  for (int i = 3; i + 1 < argc; i += 2) {
+    const uint64_t fs = std::strtoull(argv[i + 1], nullptr, 10);
+    auto it = OpenIterator(db, static_cast<SSTId>(i), argv[i], fs);
+    if (!it) return 4;
+    auto step = [&](char op) {
+      const uint8_t valid = it->IsValid();
+      const uint8_t type = static_cast<uint8_t>(it->GetType());
+      const TxnId txn = it->GetTransactionId();
+      put(&op, 1), put(&valid, 1), put(&type, 1), put(&txn, 8);
+      view(it->GetKey());
+      view(it->GetValue());
+      steps++;
+    };
+    // the block index, through a second reader (the iterator's is private)
+    auto reader = sstable::CreateAndSetupDataForTableReader(std::string(argv[i]), 0, fs);
+    if (!reader) return 4;
+    std::vector<std::string> keys;
+    for (const auto &bi : reader->GetBlockIndex()) {
+      keys.emplace_back(bi.GetSmallestKey());
+      keys.emplace_back(bi.GetLargestKey());
+    }
+    it->SeekToFirst();
+    for (step('F'); it->IsValid(); step('N')) it->Next();
+    it->Next(), step('N');
+    it->SeekToLast();
+    for (step('L'); it->IsValid(); step('P')) it->Prev();
+    it->Next(), step('N'); // the entry cursor wraps back to entry 0 of the shown block
+    keys.emplace_back("");
+    keys.emplace_back(std::string(1, '\0'));
+    keys.emplace_back(std::string(64, '\xff'));
+    for (const std::string &k : keys) {
+      it->Seek(k), step('S');
+      for (int j = 0; j < 3; j++) it->Next(), step('N');
+      it->Prev(), step('P');
+    }
+  }
+  std::fclose(dump);
+  std::printf("iter ok %llu\n", (unsigned long long)steps);
+  std::fflush(stdout);
+  _exit(0);
+}
+} // namespace
+
 int main(int argc, char **argv) {
+  if (argc >= 6 && std::string(argv[1]) == "--loop" && (argc - 6) % 2 == 0) return RunLoop(argc, argv);
+  if (argc >= 3 && std::string(argv[1]) == "--iter" && (argc - 3) % 2 == 0) return RunIter(argc, argv);
   if (argc < 4 || (argc - 4) % 4) {
     std::fprintf(stderr, "usage: %s db_dir block_size table_limit [file size smallest_hex largest_hex]...\n",
                  argv[0]);

@@ -59,15 +59,16 @@ def test_no_gpu_fails_loudly():
 
 def test_cpp_caller_compiles_and_fails_loudly_without_gpu():
     """A C++ translation unit compiled against include/sstc_table.h (the
-    DoCompactJob loop, tests/cpp/compact_loop.cc) is built by build.py and
+    reader surface check, tests/cpp/readers_check.cc) is built by build.py and
     links the library; with no GPU it exits non-zero saying so."""
     import subprocess
     import torch
-    exe = os.path.join(ROOT, "lsm-kv-storage_amd", "lib", "sstc_compact_loop")
+    exe = os.path.join(ROOT, "lsm-kv-storage_amd", "lib", "sstc_readers_check")
     assert os.path.exists(exe), "run lsm-kv-storage_amd/build.py"
     if torch.cuda.is_available():
         pytest.skip("GPU present")
-    r = subprocess.run([exe, "/tmp", "4096", "100", "1"], capture_output=True, text=True, timeout=60)
+    r = subprocess.run([exe, "--readers", "/tmp/sstc_readers_nogpu.dump", "/nonexistent.sst", "100"],
+                       capture_output=True, text=True, timeout=60)
     assert r.returncode != 0 and "no HIP device" in r.stderr
 
 

@@ -1,12 +1,9 @@
-"""A C++ caller compiled against include/sstc_table.h (tests/cpp/compact_loop.cc,
-built by lsm-kv-storage_amd/build.py): the DoCompactJob loop of
-/root/reference/db/compact.cc:232-322 written with the reference's own
-spellings over the drop-in types (kvs::sstable::TableBuilder = sstc::TableBuilder
-constructed from (std::string&&, const db::Config*), AddEntry with
-db::ValueType, inputs through sstc::TableReaderIterator, the reference
-MergeIterator's std::priority_queue).  Its output files must be the
-reference's bytes -- including the equal-(key, txn) tie order, which the host
-heap reproduces."""
+"""A C++ caller compiled against include/sstc_table.h (tests/cpp/readers_check.cc,
+built by lsm-kv-storage_amd/build.py): the codec's own C++ reader surface
+(sstc::TableReader block readers, one block per call and batched, against the
+sstc::TableReaderIterator stream) must yield the reference's decode of the
+same files.  The compaction loop under the reference's own MergeIterator, fed
+by the drop-in kvs::sstable::TableReaderIterator, is tests/test_gpu_dropin.py."""
 import hashlib
 import json
 import os
@@ -14,13 +11,10 @@ import subprocess
 
 import numpy as np
 import pytest
-from conftest import GOLDEN, ROOT, load_golden, tie_case
-from test_gpu_files import first_last_key
-from sstcodec import workload as W
+from conftest import GOLDEN, ROOT
 
 pytestmark = pytest.mark.gpu
-EXE = os.path.join(ROOT, "lsm-kv-storage_amd", "lib", "sstc_compact_loop")
-CASES = json.load(open(os.path.join(GOLDEN, "compaction.json")))
+EXE = os.path.join(ROOT, "lsm-kv-storage_amd", "lib", "sstc_readers_check")
 
 
 def write(tmp_path, files):
@@ -30,52 +24,6 @@ def write(tmp_path, files):
         f.tofile(p)
         args += [p, str(f.size + 1)]
     return args
-
-
-def run_loop(tmp_path, files, limit, base, block_size=4096):
-    od = tmp_path / f"out{base}"
-    od.mkdir(exist_ok=True)
-    r = subprocess.run([EXE, str(od), str(block_size), str(limit), str(base)] + write(tmp_path, files), capture_output=True,
-                       text=True, timeout=120)
-    assert r.returncode == 0, r.stderr
-    outs = []
-    for ln in r.stdout.strip().splitlines():
-        p, lo, hi, s = ln.split(" ")
-        img = np.fromfile(p, np.uint8)
-        # GetSmallestKey / GetLargestKey (what AddNewFiles records) = first / last key of the file
-        want_lo, want_hi = first_last_key(img)
-        assert (bytes.fromhex(lo) if lo != "-" else b"") == want_lo
-        assert (bytes.fromhex(hi) if hi != "-" else b"") == want_hi
-        outs.append((img, int(s)))
-    return outs
-
-
-@pytest.mark.parametrize("name", sorted(CASES))
-@pytest.mark.parametrize("base", [1, 0])
-def test_cpp_compact_loop_matches_reference(oracle, tmp_path, name, base):
-    case = CASES[name]
-    sets = W.compaction_inputs(case["k"], case["n_per"], case["key_space"], vmax=case["vmax"],
-                               distinct=case["distinct"], **case.get("gen", {}))
-    files = [oracle.table_build(r, case["block_threshold"]) for r in sets]
-    outs = run_loop(tmp_path, files, case["table_limit"], base, case["block_threshold"])
-    want = case[f"outputs_base{base}"]
-    assert len(outs) == len(want)
-    for (img, fs), w in zip(outs, want):
-        assert fs == w["file_size"] == img.size + 1
-        assert hashlib.sha256(img.tobytes()).hexdigest() == w["sha256"]
-
-
-@pytest.mark.parametrize("name", ["same", "diff"])
-@pytest.mark.parametrize("base", [1, 0])
-def test_cpp_compact_loop_ties_match_reference(tmp_path, name, base):
-    """Equal (key, txn) across inputs, identical AND differing copies: the host
-    std::priority_queue pops ties in the reference's order, so even the
-    'diff' case is the reference's bytes on this path."""
-    ins, want = tie_case(load_golden("compact_ties.npz"), name, base)
-    outs = run_loop(tmp_path, ins, 6000, base)
-    assert len(outs) == len(want)
-    for (img, fs), w in zip(outs, want):
-        assert np.array_equal(img, w) and fs == w.size + 1
 
 
 def test_cpp_block_readers_and_iterator(oracle, tmp_path):

@@ -1,15 +1,27 @@
 """The drop-in of INTEGRATION.md, run: oracle/_ref/compact_dropin is
-/root/reference/db/compact.cc (Compact::PickCompact -> DoCompactJob) compiled
-UNCHANGED with include/dropin/sstable/table_builder.h first on the include
-path, so every output SST it builds goes through sstc::TableBuilder (blocks
-encoded on this GPU at Finish()).  Its outputs must be the reference's own
-bytes.  (The binary is built in the container by `make -C oracle dropin`,
+/root/reference/db/compact.cc (Compact::PickCompact -> DoCompactJob) AND
+/root/reference/db/merge_iterator.cc compiled UNCHANGED with include/dropin/
+first on the include path, so
+  * every input table is read through the drop-in
+    kvs::sstable::TableReaderIterator (include/dropin/sstable/
+    table_reader_iterator.h): the whole table decoded in one GPU call
+    (sstc_count_records + sstc_decode_blocks), and
+  * every output SST is built by sstc::TableBuilder (blocks encoded on this
+    GPU at Finish()).
+Its outputs must be the reference's own bytes.  (The binaries are built in the
+container by `make -C oracle dropin`, see
 tests/test_oracle_aswritten.py::test_dropin_builds_unmodified_compact_cc, and
-travels with the tree like libsstcodec.so.)
+travel with the tree like libsstcodec.so.)
 
-Cases: those whose as-written output equals the fixed semantics under both
-allocator settings (tests/golden/aswritten.json), since this binary runs the
-reference's dangling `last_current_key` as written (compact.cc:250)."""
+Expected bytes: the fixed-semantics outputs of tests/golden/aswritten.json
+(the reference's MergeIterator + TableReaderIterator + TableBuilder under the
+DoCompactJob loop with an owned last key).  The as-written reference's
+`last_current_key` view dangles once its block is freed (compact.cc:250,
+table_reader_iterator.cc:148); the drop-in iterator owns its decoded table
+for its whole life, so the unchanged compact.cc runs the intended semantics on
+every case, including the ones where the reference as written keeps stale
+duplicates or crashes (config 5, probe5000, config3_overlap, cj_zipf).
+"""
 import hashlib
 import json
 import os
@@ -18,49 +30,178 @@ import sys
 
 import numpy as np
 import pytest
-from conftest import GOLDEN, ROOT
+from conftest import GOLDEN, ROOT, load_golden, tie_case
 
 sys.path.insert(0, GOLDEN)
 import make_golden_aswritten as G  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 MANIFEST = json.load(open(os.path.join(GOLDEN, "aswritten.json")))
+CJ = json.load(open(os.path.join(GOLDEN, "compaction.json")))
 EXE = os.path.join(ROOT, "oracle", "_ref", "compact_dropin")
+REF_EXE = os.path.join(ROOT, "oracle", "_ref", "ref_pick_compact")
+RUNNABLE = [n for n, c in MANIFEST.items() if isinstance(c, dict) and "fixed_outputs" in c]
 
 
 def sha(a):
     return hashlib.sha256(np.ascontiguousarray(a, np.uint8).tobytes()).hexdigest()
 
 
-@pytest.mark.timeout(300)
-@pytest.mark.parametrize("name", ["probe100", "config3"])
-def test_reference_compaction_with_dropin_table_builder(tmp_path, name):
-    if not os.path.exists(EXE):
-        pytest.skip("oracle/_ref/compact_dropin not built (needs /root/reference at build time)")
+def need(exe):
+    if not os.path.exists(exe):
+        pytest.skip(f"{os.path.relpath(exe, ROOT)} not built (needs /root/reference at build time)")
+
+
+def first_last_key(img):
+    from oracle import Oracle
+    orc = Oracle()
+    idx = orc.table_index(img)
+    keys = []
+    for o, ln in ((int(idx["blk_off"][0]), int(idx["blk_len"][0])), (int(idx["blk_off"][-1]), int(idx["blk_len"][-1]))):
+        st, d = orc.decode_block(img[o:o + ln], 1)
+        assert st == 0
+        j = 0 if not keys else len(d["type"]) - 1
+        ko, kl = int(d["key_off"][j]), int(d["key_len"][j])
+        keys.append(img[o + ko:o + ko + kl].tobytes())
+    return keys[0], keys[1]
+
+
+def build_inputs(tmp_path, sets, T):
     import sstcodec
-    from oracle import table_key_range
     from sstcodec.table import build_table
-    case = MANIFEST[name]
-    assert case["no_trim_equals_fixed"] and case["default_equals_fixed"]
-    fac, T, limit, _ = G.CASES[name]
     codec = sstcodec.Codec(0)
+    out = []
+    try:
+        for i, rec in enumerate(sets):
+            p = str(tmp_path / f"in{i}.sst")
+            fs, _ = build_table(codec, p, rec, T)
+            out.append((p, fs, rec))
+    finally:
+        codec.close()
+    return out
+
+
+def case_inputs(name):
+    fac, T, limit, _ = G.CASES[name]
+    if fac is None:
+        return G.compaction_json_inputs(name[3:])
+    return fac(), T, limit
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("name", RUNNABLE)
+def test_unmodified_compact_cc_gpu_decode_and_encode(tmp_path, name):
+    """Compact::PickCompact as written, with GPU decode (drop-in
+    TableReaderIterator) and GPU encode (drop-in TableBuilder): every output
+    file, GetFileSize() and VersionEdit key range equal to the reference's."""
+    need(EXE)
+    from oracle import table_key_range
+    case = MANIFEST[name]
+    sets, T, limit = case_inputs(name)
+    ins = build_inputs(tmp_path, sets, T)
+    del sets
     args = [EXE, str(tmp_path / "db"), str(T), str(limit)]
     (tmp_path / "db").mkdir()
-    for i, rec in enumerate(fac()):
-        p = str(tmp_path / f"in{i}.sst")
-        fs, _ = build_table(codec, p, rec, T)
-        assert fs == case["inputs"][i]["file_size"] and sha(np.fromfile(p, np.uint8)) == case["inputs"][i]["sha256"]
+    for (p, fs, rec), want in zip(ins, case["inputs"]):
+        assert fs == want["file_size"] and sha(np.fromfile(p, np.uint8)) == want["sha256"]
         lo, hi = table_key_range(rec)
-        args += [p, str(fs), lo.hex(), hi.hex()]
-    codec.close()
-    r = subprocess.run(args, capture_output=True, text=True, timeout=240)
+        args += [p, str(fs), lo.hex() or "-", hi.hex() or "-"]
+    ins = None
+    r = subprocess.run(args, capture_output=True, text=True, timeout=540)
     assert r.returncode == 0, r.stderr[-2000:]
     picked, outs = G.parse_pick_output(r.stdout)
     assert picked == list(range(1, len(case["inputs"]) + 1))
-    got = [(sha(np.fromfile(p, np.uint8)), fs) for p, fs, _, _ in outs]
+    got = []
+    for p, fs, lo, hi in outs:
+        img = np.fromfile(p, np.uint8)
+        got.append((sha(img), fs))
+        assert (lo, hi) == first_last_key(img)  # what VersionEdit::AddNewFiles recorded
     assert got == [(o["sha256"], o["file_size"]) for o in case["fixed_outputs"]]
-    # and VersionEdit::AddNewFiles got the reference's key ranges
-    assert [(lo.hex(), hi.hex()) for _, _, lo, hi in outs] == \
-        [(o["smallest"], o["largest"]) for o in case["no_trim"]["outputs"]]
-    print(f"{name}: db/compact.cc unchanged + sstc::TableBuilder -> {len(outs)} outputs equal to the reference's",
-          flush=True)
+    print(f"{name}: db/compact.cc + db/merge_iterator.cc unchanged, GPU decode + GPU encode -> "
+          f"{len(outs)} outputs equal to the reference's", flush=True)
+
+
+def run_loop(exe, tmp_path, files, T, limit, base, tag):
+    od = tmp_path / f"out_{tag}_{base}"
+    od.mkdir()
+    args = [exe, "--loop", str(od), str(T), str(limit), str(base)]
+    for i, f in enumerate(files):
+        p = str(tmp_path / f"{tag}_in{i}.sst")
+        f.tofile(p)
+        args += [p, str(f.size + 1)]
+    r = subprocess.run(args, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    _, outs = G.parse_pick_output(r.stdout)
+    res = []
+    for p, fs, lo, hi in outs:
+        img = np.fromfile(p, np.uint8)
+        assert (lo, hi) == first_last_key(img)
+        res.append((img, fs))
+    return res
+
+
+@pytest.mark.parametrize("name", sorted(CJ))
+@pytest.mark.parametrize("base", [1, 0])
+def test_merge_iterator_over_dropin_readers(oracle, tmp_path, name, base):
+    """The reference's own db::MergeIterator over drop-in TableReaderIterators
+    (made as Compact::CreateMergeIterator makes them, through the
+    TableReaderCache), the DoCompactJob loop at any table limit and both
+    IsBaseLevelForKey answers: every compaction.json case, bit-exact."""
+    need(EXE)
+    from sstcodec import workload as W
+    case = CJ[name]
+    sets = W.compaction_inputs(case["k"], case["n_per"], case["key_space"], vmax=case["vmax"],
+                               distinct=case["distinct"], **case.get("gen", {}))
+    files = [oracle.table_build(r, case["block_threshold"]) for r in sets]
+    outs = run_loop(EXE, tmp_path, files, case["block_threshold"], case["table_limit"], base, name)
+    want = case[f"outputs_base{base}"]
+    assert [(sha(i), fs) for i, fs in outs] == [(w["sha256"], w["file_size"]) for w in want]
+
+
+@pytest.mark.parametrize("name", ["same", "diff"])
+@pytest.mark.parametrize("base", [1, 0])
+def test_merge_iterator_ties_over_dropin_readers(tmp_path, name, base):
+    """Equal (key, txn) across inputs, identical AND differing copies: the
+    reference's own heap pops the ties, fed by drop-in iterators, so even the
+    'diff' case is the reference's bytes."""
+    need(EXE)
+    ins, want = tie_case(load_golden("compact_ties.npz"), name, base)
+    outs = run_loop(EXE, tmp_path, ins, 4096, 6000, base, name)
+    assert len(outs) == len(want)
+    for (img, fs), w in zip(outs, want):
+        assert np.array_equal(img, w) and fs == w.size + 1
+
+
+def trace_tables(oracle, tmp_path):
+    from readers_util import reader_records
+    from sstcodec import workload as W
+    rec = reader_records()
+    big = W.mixed_records(400, seed=11, max_val=9000)  # values past a block: 1-entry blocks
+    files = [oracle.table_build(rec, 4096), oracle.table_build(rec, 32768), oracle.table_build(big, 4096)]
+    args = []
+    for i, f in enumerate(files):
+        p = str(tmp_path / f"t{i}.sst")
+        f.tofile(p)
+        args += [p, str(f.size + 1)]
+    return args
+
+
+def test_iterator_trace_equals_reference(oracle, tmp_path):
+    """The same scripted walk (SeekToFirst + Next past the end, SeekToLast +
+    Prev past the start and the entry cursor's wrap back, Seek to every
+    block's first / last key and to keys outside the table, each followed by
+    Next / Prev) through the reference's TableReaderIterator and through the
+    drop-in: IsValid, key, value (incl. null vs empty views), type and txn
+    (compat quirk of block_reader.cc:109-111) equal at every step."""
+    need(EXE)
+    need(REF_EXE)
+    args = trace_tables(oracle, tmp_path)
+    dumps = []
+    for exe, tag in ((REF_EXE, "ref"), (EXE, "dropin")):
+        d = str(tmp_path / f"{tag}.dump")
+        r = subprocess.run([exe, "--iter", d] + args, capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, (tag, r.stderr[-2000:])
+        dumps.append((r.stdout.strip(), open(d, "rb").read()))
+    assert dumps[0][0] == dumps[1][0] and dumps[0][0].startswith("iter ok ")
+    assert len(dumps[0][1]) > 1_000_000
+    assert dumps[0][1] == dumps[1][1]

@@ -120,7 +120,72 @@ def test_dropin_builds_unmodified_compact_cc():
     defined = subprocess.run(["nm", "-C", "--defined-only", exe], capture_output=True, text=True, check=True).stdout
     assert "kvs::sstable::TableBuilder::AddEntry" not in defined
     assert "kvs::db::Compact::DoCompactJob()" in defined
-    # the compiled TU is the reference's own file, byte for byte
-    dep = subprocess.run(["make", "-C", os.path.join(ROOT, "oracle"), "-n", "-B", obj], capture_output=True,
-                         text=True).stdout
+    # the decode side: compact.cc constructs sstable::TableReaderIterator with
+    # the reference's signature (compact.cc:201-203,223-225), and the one in the
+    # binary is the drop-in (its Load() decodes through sstc::DecodeBlocks), not
+    # the reference's (whose CreateNewBlockReaderIterator reads block by block)
+    assert ("kvs::sstable::TableReaderIterator::TableReaderIterator(std::vector<std::unique_ptr<"
+            "kvs::sstable::BlockReaderCache") in undef
+    assert "kvs::sstable::TableReaderIterator::Load()" in defined
+    assert "kvs::db::MergeIterator::Next()" in defined
+    assert "TableReaderIterator::CreateNewBlockReaderIterator" not in defined
+    tri = os.path.join(ROOT, "oracle", "_ref", "dropin_obj", "sstc", "table_reader_iterator.o")
+    tri_undef = subprocess.run(["nm", "-C", "-u", tri], capture_output=True, text=True, check=True).stdout
+    assert "sstc::DecodeBlocks(" in tri_undef
+    # the compiled TUs are the reference's own files, byte for byte
+    mk = ["make", "-C", os.path.join(ROOT, "oracle"), "-n", "-B"]
+    dep = subprocess.run(mk + [obj], capture_output=True, text=True).stdout
     assert f"{REF}/db/compact.cc" in dep
+    mobj = os.path.join(ROOT, "oracle", "_ref", "dropin_obj", "db", "merge_iterator.o")
+    assert f"{REF}/db/merge_iterator.cc" in subprocess.run(mk + [mobj], capture_output=True, text=True).stdout
+    # no CPU decode path: without a GPU the drop-in reader fails loudly
+    import torch
+    if not torch.cuda.is_available():
+        from oracle import Oracle
+        from sstcodec import workload as W
+        img = Oracle().table_build(W.mixed_records(50, seed=1), 4096)
+        p = "/tmp/sstc_dropin_nogpu.sst"
+        img.tofile(p)
+        r = subprocess.run([exe, "--iter", "/tmp/sstc_dropin_nogpu.dump", p, str(img.size + 1)], capture_output=True,
+                           text=True, timeout=60)
+        assert r.returncode != 0 and "no HIP device" in r.stderr, (r.returncode, r.stderr[-500:])
+
+
+@pytest.mark.skipif(not os.path.exists(REF), reason="needs /root/reference")
+def test_loop_harness_over_reference_readers_matches_fixtures(oracle, tmp_path):
+    """oracle/_ref/ref_pick_compact --loop: the DoCompactJob loop over the
+    reference's own TableReaderIterator + MergeIterator reproduces every
+    compaction.json fixture at both base levels and the tie fixtures -- the
+    harness the GPU test runs with the drop-in readers is itself pinned."""
+    exe = os.path.join(ROOT, "oracle", "_ref", "ref_pick_compact")
+    subprocess.run(["make", "-C", os.path.join(ROOT, "oracle"), "-j8"], check=True, capture_output=True)
+    from conftest import load_golden, tie_case
+    from sstcodec import workload as W
+    cj = json.load(open(os.path.join(GOLDEN, "compaction.json")))
+
+    def run(files, T, limit, base, tag):
+        od = tmp_path / f"o_{tag}_{base}"
+        od.mkdir()
+        args = [exe, "--loop", str(od), str(T), str(limit), str(base)]
+        for i, f in enumerate(files):
+            p = str(tmp_path / f"{tag}_{i}.sst")
+            f.tofile(p)
+            args += [p, str(f.size + 1)]
+        r = subprocess.run(args, capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, r.stderr[-2000:]
+        return [(np.fromfile(p, np.uint8), fs) for p, fs, _, _ in G.parse_pick_output(r.stdout)[1]]
+
+    for name, case in sorted(cj.items()):
+        sets = W.compaction_inputs(case["k"], case["n_per"], case["key_space"], vmax=case["vmax"],
+                                   distinct=case["distinct"], **case.get("gen", {}))
+        files = [oracle.table_build(r, case["block_threshold"]) for r in sets]
+        for base in (1, 0):
+            outs = run(files, case["block_threshold"], case["table_limit"], base, name)
+            assert [(sha(i), fs) for i, fs in outs] == \
+                [(w["sha256"], w["file_size"]) for w in case[f"outputs_base{base}"]], (name, base)
+    g = load_golden("compact_ties.npz")
+    for name in ("same", "diff"):
+        for base in (1, 0):
+            ins, want = tie_case(g, name, base)
+            outs = run(ins, 4096, 6000, base, "tie" + name)
+            assert len(outs) == len(want) and all(np.array_equal(i, w) for (i, _), w in zip(outs, want))
