@@ -49,11 +49,7 @@ struct Abort {
   const unsigned long long *err;  // context decode-error counter
   const uint64_t *err0;           // its value before this job's decode
   const unsigned long long *bad;  // unsorted records (null: not checked)
-  const unsigned long long *guard = nullptr; // a long group out of txn order (null: not checked)
-  __device__ __forceinline__ bool operator()() const {
-    constexpr unsigned long long kLongInv = kGuardLongGroup | kGuardInv;
-    return *err != *err0 || (bad && *bad) || (guard && (*guard & kLongInv) == kLongInv);
-  }
+  __device__ __forceinline__ bool operator()() const { return *err != *err0 || (bad && *bad); }
 };
 
 // three-way key compare: prefix, then (only when both are longer than 16 B and
@@ -123,10 +119,12 @@ constexpr uint32_t kRsLds = 1024; // run starts / table starts searched in LDS u
 // the group's part before it (the decode computed it per block).  That
 // minimum is the smallest merge txn at the ends of the group's parts in the
 // earlier blocks (each part's last merge txn is its own running minimum), so
-// the walk goes back block end by block end, up to kGroupCarryBlocks blocks.
+// the walk goes back block end by block end, up to kGroupCarryBlocks blocks;
+// a group reaching further back is left to long_carry_repair (kGuardLongGroup).
 // Other threads may lower those ends meanwhile; the minimum is the same.
-__device__ void carry_group(SK *s, const uint64_t *rec_base, uint64_t b, uint64_t r, uint64_t run0, const KeyView &kv,
-                            unsigned long long *bad, unsigned long long *guard) {
+// Returns true when it lowered a merge txn.
+__device__ bool carry_group(SK *s, const uint64_t *rec_base, uint64_t b, uint64_t r, uint64_t run0, const KeyView &kv,
+                            unsigned long long *guard) {
   const SK k = s[r];
   uint64_t carry = s[r - 1].tx, end = r - 1, bb = b;
   for (uint32_t hop = 0;; hop++) {
@@ -138,14 +136,15 @@ __device__ void carry_group(SK *s, const uint64_t *rec_base, uint64_t b, uint64_
     if (f == run0 || key_cmp(y.p0, y.p1, y.kl, y.id, k.p0, k.p1, k.kl, k.id, kv) != 0) break; // starts in q
     const SK z = s[f - 1];
     if (key_cmp(z.p0, z.p1, z.kl, z.id, k.p0, k.p1, k.kl, k.id, kv) != 0) break;
-    if (hop + 1 >= kGroupCarryBlocks) { // a key's versions over too many blocks: rejected if out of txn order
+    if (hop + 1 >= kGroupCarryBlocks) { // a key's versions over many blocks: the repair pass carries it
       atomicOr(guard, kGuardLongGroup);
-      return;
+      return false;
     }
     end = f - 1;
     bb = q;
     carry = s[end].tx < carry ? s[end].tx : carry;
   }
+  bool wrote = false;
   const uint64_t e = rec_base[b + 1];
   for (uint64_t i = r; i < e; i++) {
     SK x = s[i];
@@ -154,14 +153,105 @@ __device__ void carry_group(SK *s, const uint64_t *rec_base, uint64_t b, uint64_
       x.tx = carry;
       x.kl |= kSkRead;
       s[i] = x;
+      wrote = true;
     }
   }
+  return wrote;
 }
+
+__device__ __forceinline__ bool is_run_start(const uint64_t *rs, uint64_t nruns, uint64_t r) {
+  uint64_t lo = 0, hi = nruns; // last run_start <= r
+  while (lo + 1 < hi) {
+    const uint64_t mid = (lo + hi) >> 1;
+    if (rs[mid] <= r) lo = mid;
+    else hi = mid;
+  }
+  return rs[lo] == r;
+}
+
+// The carries of EVERY block boundary as one segmented min-scan over the
+// blocks, by one workgroup (the last of ck_check_blocks_kernel to finish, and
+// only when some walk gave up at kGroupCarryBlocks AND some group is out of
+// txn order, kGuardInv): block b contributes the merge txn at its end
+// (its trailing group's running minimum) and starts a new segment unless the
+// whole block continues the group of the block before it; the carry into a
+// block whose first record continues that group is the scan up to the block
+// before.  Values already lowered by carry_group are at least as low as the
+// decode's and never below the group's true minimum, so the scan over them is
+// the true one.  O(blocks), whatever a group's length: what MergeIterator's
+// heap does for any number of versions (merge_iterator.cc:34-46 with the
+// compat txn of block_reader.cc:109-111).
+__device__ void long_carry_repair(SK *s, const uint64_t *rec_base, uint64_t nblocks, const uint64_t *rs,
+                                  uint64_t nruns, const KeyView &kv) {
+  __shared__ uint64_t s_v[256];
+  __shared__ uint32_t s_r[256];
+  __shared__ uint64_t s_carry; // scan value at the end of the previous chunk
+  const uint32_t tid = threadIdx.x;
+  if (tid == 0) s_carry = UINT64_MAX;
+  __syncthreads();
+  for (uint64_t c0 = 0; c0 < nblocks; c0 += 256) {
+    const uint64_t b = c0 + tid;
+    uint64_t v = UINT64_MAX, r0 = 0, r1 = 0;
+    uint32_t rst = 0;
+    bool cont = false;
+    if (b < nblocks) {
+      r0 = rec_base[b];
+      r1 = rec_base[b + 1];
+      if (r1 > r0) { // an empty block is transparent (identity element)
+        const SK f = s[r0], l = s[r1 - 1];
+        if (r0 > 0 && !is_run_start(rs, nruns, r0)) {
+          const SK p = s[r0 - 1];
+          cont = key_cmp(f.p0, f.p1, f.kl, f.id, p.p0, p.p1, p.kl, p.id, kv) == 0;
+        }
+        const bool full = cont && key_cmp(l.p0, l.p1, l.kl, l.id, f.p0, f.p1, f.kl, f.id, kv) == 0;
+        v = l.tx;
+        rst = !full;
+      }
+    }
+    s_v[tid] = v;
+    s_r[tid] = rst;
+    __syncthreads();
+    // inclusive segmented min-scan (Hillis-Steele): (a, b) -> b.reset ? b : (a.reset, min)
+    for (uint32_t d = 1; d < 256; d <<= 1) {
+      uint64_t nv = s_v[tid];
+      uint32_t nr = s_r[tid];
+      if (tid >= d && !nr) {
+        nv = s_v[tid - d] < nv ? s_v[tid - d] : nv;
+        nr = s_r[tid - d];
+      }
+      __syncthreads();
+      s_v[tid] = nv;
+      s_r[tid] = nr;
+      __syncthreads();
+    }
+    const uint64_t cin = s_carry;
+    // the scan value before block b (exclusive), the chunk's carry folded in
+    uint64_t before = cin;
+    if (tid > 0) before = s_r[tid - 1] ? s_v[tid - 1] : (s_v[tid - 1] < cin ? s_v[tid - 1] : cin);
+    const uint64_t last = s_r[255] ? s_v[255] : (s_v[255] < cin ? s_v[255] : cin);
+    __syncthreads();
+    if (tid == 0) s_carry = last;
+    if (cont) {
+      const SK k = s[r0];
+      for (uint64_t i = r0; i < r1; i++) {
+        SK x = s[i];
+        if (key_cmp(x.p0, x.p1, x.kl, x.id, k.p0, k.p1, k.kl, k.id, kv) != 0) break;
+        if (before < x.tx) {
+          x.tx = before;
+          x.kl |= kSkRead;
+          s[i] = x;
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
 __global__ __launch_bounds__(256) void ck_check_blocks_kernel(SK *s, const uint64_t *rec_base, uint64_t nblocks,
                                        const uint64_t *run_start, uint64_t nruns, KeyView kv,
                                        unsigned long long *bad, Abort stop, uint64_t *zws, uint64_t nz,
                                        unsigned long long *guard, const uint64_t *kg_host, uint64_t *kg,
-                                       uint64_t kg_words) {
+                                       uint64_t kg_words, unsigned int *ticket) {
   // the merge passes' group descriptors, written by the host into pinned
   // mapped memory before the launch: copied here by workgroup 0 (a copy
   // command between the decode and the merge cost ~5 us)
@@ -178,28 +268,57 @@ __global__ __launch_bounds__(256) void ck_check_blocks_kernel(SK *s, const uint6
   const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
   const uint64_t t0 = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   for (uint64_t z = t0; z < nz; z += stride) zws[z] = 0; // filter look-back
-  if (stop()) return;
-  for (uint64_t b = t0; b < nblocks; b += stride) {
-    const uint64_t r = rec_base[b];
-    if (r == 0 || rec_base[b + 1] == r) continue;
-    uint64_t lo = 0, hi = nruns; // run containing r: last run_start <= r
-    while (lo + 1 < hi) {
-      const uint64_t mid = (lo + hi) >> 1;
-      if (rs[mid] <= r) lo = mid;
-      else hi = mid;
-    }
-    if (rs[lo] == r) continue; // first record of its run
-    const SK cur = s[r], pv = s[r - 1];
-    const int c = key_cmp(cur.p0, cur.p1, cur.kl, cur.id, pv.p0, pv.p1, pv.kl, pv.id, kv);
-    if (c < 0) atomicAdd(bad, 1ull);
-    // a key group continuing across the boundary takes its running minimum
-    // from the blocks before it (a no-op unless some version of it is out of
-    // txn order: the minimum of older versions is then >= every txn here)
-    if (c == 0) {
-      if (cur.tx > pv.tx) atomicOr(guard, kGuardInv); // a group out of txn order across the boundary
-      carry_group(s, rec_base, b, r, rs[lo], kv, bad, guard);
+  const bool stopped = stop(); // uniform
+  bool wrote = false;
+  if (!stopped) {
+    for (uint64_t b = t0; b < nblocks; b += stride) {
+      const uint64_t r = rec_base[b];
+      if (r == 0 || rec_base[b + 1] == r) continue;
+      uint64_t lo = 0, hi = nruns; // run containing r: last run_start <= r
+      while (lo + 1 < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (rs[mid] <= r) lo = mid;
+        else hi = mid;
+      }
+      if (rs[lo] == r) continue; // first record of its run
+      const SK cur = s[r], pv = s[r - 1];
+      const int c = key_cmp(cur.p0, cur.p1, cur.kl, cur.id, pv.p0, pv.p1, pv.kl, pv.id, kv);
+      if (c < 0) atomicAdd(bad, 1ull);
+      // a key group continuing across the boundary takes its running minimum
+      // from the blocks before it (a no-op unless some version of it is out of
+      // txn order: the minimum of older versions is then >= every txn here)
+      if (c == 0) {
+        if (cur.tx > pv.tx) atomicOr(guard, kGuardInv); // a group out of txn order across the boundary
+        wrote |= carry_group(s, rec_base, b, r, rs[lo], kv, guard);
+      }
     }
   }
+  // Long groups: the last workgroup to finish repairs them (an in-launch
+  // hand-off: every workgroup that lowered a merge txn drains its stores and
+  // releases them at agent scope before its ticket; the last arriver acquires
+  // before it reads them).  No workgroup waits on another.
+  __shared__ uint32_t s_last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const bool any = __syncthreads_or(wrote);
+  if (threadIdx.x == 0) {
+    if (any) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    const uint32_t t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t last = 0;
+    if (t == gridDim.x - 1) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const unsigned long long g = __hip_atomic_load(guard, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      constexpr unsigned long long kLongInv = kGuardLongGroup | kGuardInv;
+      last = (g & kLongInv) == kLongInv && !stop(); // the job's verdicts are final here
+      __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    s_last = last;
+  }
+  __syncthreads();
+  if (s_last) long_carry_repair(s, rec_base, nblocks, rs, nruns, kv);
 }
 
 
@@ -1225,6 +1344,7 @@ __global__ __launch_bounds__(256) void ck_run_starts_kernel(const uint64_t *rec_
       *bad = 0;
       guard[0] = 0; // consistency-guard bits
       guard[1] = e; // the end of the source bytes the input blocks span
+      guard[2] = 0; // ck_check_blocks_kernel's ticket
     }
   }
   if (i < n) out[i] = rec_base[tfb[i]];
@@ -1331,7 +1451,8 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     unsigned long long *bad = reinterpret_cast<unsigned long long *>(pool.get<uint64_t>(1));
     // consistency guard: [0] bits set by any check of the job, [1] the end of
     // the source bytes its blocks span (both cleared by ck_run_starts_kernel)
-    unsigned long long *guard = reinterpret_cast<unsigned long long *>(pool.get<uint64_t>(2));
+    // guard[0] bits, guard[1] source end, guard[2] the check kernel's ticket
+    unsigned long long *guard = reinterpret_cast<unsigned long long *>(pool.get<uint64_t>(3));
     const uint64_t *src_end = reinterpret_cast<const uint64_t *>(guard + 1);
     // record index of every input table's first record (its run start)
     CK(hipMemcpyAsync(d_tfb, h_tfb, (ntables + 1) * 8, hipMemcpyHostToDevice, s));
@@ -1381,7 +1502,7 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     const KeyView kv{d_src, RX};
     uint64_t nruns = ntables;
     const uint64_t *rb = d_rs; // run starts, nruns + 1
-    const Abort dec_fail{err_count, errs, nullptr}, stop{err_count, errs, bad, guard};
+    const Abort dec_fail{err_count, errs, nullptr}, stop{err_count, errs, bad};
     const uint64_t fftiles = (n + kFfTile - 1) / kFfTile;
     uint64_t *ffws = nullptr; // look-back words of the filter
     // survivors of the keep / drop filter (sized by n: the kept count is known after it)
@@ -1459,7 +1580,8 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
       ck_check_blocks_kernel<<<std::max<uint32_t>(grid(std::max<uint64_t>(nblocks, 1ull + 3 * fftiles)), 1u), 256, 0,
                                s>>>(A, rb_all, nblocks, rb, nruns, kv, bad, dec_fail, ffws, 1 + 3 * fftiles, guard,
                                                            reinterpret_cast<const uint64_t *>(arena.up_dev),
-                                                           reinterpret_cast<uint64_t *>(d_kg), kg_bytes / 8);
+                                                           reinterpret_cast<uint64_t *>(d_kg), kg_bytes / 8,
+                                                           reinterpret_cast<unsigned int *>(guard + 2));
       if (!kg.empty()) {
         const uint32_t max_ids = *std::max_element(pass_ids.begin(), pass_ids.end());
         uint32_t *Cm = pool.get<uint32_t>(static_cast<uint64_t>(max_ids) * kKWay);
@@ -1504,11 +1626,6 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     auto job_error = [&](const uint64_t *h) -> int { // h: the err_words as fetched
       if (h[0] != h[1]) {
         err = "an input block failed to decode";
-        return SSTC_E_INVALID_ARG;
-      }
-      if ((h[3] & kGuardLongGroup) && (h[3] & kGuardInv)) {
-        err = "an input holds versions of one key out of txn order as read over more than " +
-              std::to_string(kGroupCarryBlocks) + " blocks (unsupported)";
         return SSTC_E_INVALID_ARG;
       }
       if (h[2]) {

@@ -1533,12 +1533,16 @@ __global__ __launch_bounds__(kChThreads) void seg_walk_kernel(SegArgs a) {
     uint64_t lo = 0, n = ne + 1, below = 0, e = 0; // answer in [lo, lo + n); ends[lo - 1] = below
     uint32_t f = 0;
     for (;;) {
-      const uint64_t step = (n + kWave - 1) / kWave;
+      // step = ceil((n - 1) / 63) past one round: lane 63 probes lo + n - 1
+      // (ends[lo + n - 1] > c0 is the invariant), so the ballot is never empty
+      const uint64_t step = n <= kWave ? 1 : (n - 2) / (kWave - 1) + 1;
       const uint64_t off = static_cast<uint64_t>(lane) * step;
       const uint64_t x = step == 1 ? (lo + lane < ne ? lo + lane : ne) : lo + (off < n - 1 ? off : n - 1);
       e = a.ends[x];
       const uint64_t gt = __ballot(e > c0); // a suffix of the lanes, lane min(n - 1, 63) at least
-      f = static_cast<uint32_t>(__ffsll(static_cast<long long>(gt))) - 1u;
+      // (never empty; a corrupt end list must not turn f into ~0 and send the
+      // next round's loads out of range)
+      f = gt ? static_cast<uint32_t>(__ffsll(static_cast<long long>(gt))) - 1u : kWave - 1;
       if (step == 1) break;
       if (f) below = readlane_u64(e, f - 1);
       const uint64_t nlo = f ? lo + static_cast<uint64_t>(f - 1) * step + 1 : lo;

@@ -112,8 +112,9 @@ constexpr unsigned long long kGuardMergeId = 1, kGuardEntry = 2, kGuardBlockRang
                              kGuardInv = 128;
 // kGuardLongGroup / kGuardInv are notes, not faults: a key's versions continue
 // over more than kGroupCarryBlocks blocks / some group is out of txn order as
-// read.  Both together reject the job (the carry would be needed that far).
-// blocks a key group whose merge txns need a carry may span (ck_check_blocks_kernel)
+// read.  Both together send the check kernel's last workgroup through the
+// repair pass (long_carry_repair: the carries as one segmented min-scan).
+// blocks a thread of ck_check_blocks_kernel walks back for a key group's carry
 constexpr uint32_t kGroupCarryBlocks = 64;
 
 // point lookups (sstc_get.hip)

@@ -95,12 +95,11 @@ def test_compact_versions_out_of_txn_order(codec, oracle, seed, threshold, space
 
 
 def test_compact_long_version_groups(codec, oracle):
-    """One key's versions over more than kGroupCarryBlocks (64) blocks of an
-    input: in txn order they compact like any other input; out of txn order
-    as read (an empty-value version) the running minimum would have to be
-    carried over more than 64 blocks, which the job rejects with
-    SSTC_E_INVALID_ARG rather than merge wrongly."""
-    import sstcodec
+    """One key's versions over far more than kGroupCarryBlocks (64) blocks of
+    an input (~200 blocks), in txn order and out of it as read (an
+    empty-value version mid-group: its txn as read jumps): the running minimum
+    is carried over every block (the check kernel's last workgroup repairs
+    what its 64-block walks leave, long_carry_repair), bit-exact."""
     sets = W.compaction_inputs(1, 1200, 2, seed=5, p_delete=0.0, vmin=4, vmax=8, key_width=16, distinct=False)
     ins = [oracle.table_build(r, 128) for r in sets]  # ~3 records per block: ~200 blocks per key
     want, _ = oracle.compact(ins, 128, 1 << 20, 1)
@@ -109,8 +108,87 @@ def test_compact_long_version_groups(codec, oracle):
     rec = {key: v.copy() for key, v in sets[0].items()}
     rec["val_len"][len(rec["val_len"]) // 2] = 0  # one empty-value PUT mid-group: its txn as read jumps
     bad = [oracle.table_build(rec, 128)]
-    with pytest.raises(sstcodec.SstcError, match="unsupported"):
-        codec.compact(bad, 128, 1 << 20, 1)
+    for base in (1, 0):
+        want, kept = oracle.compact(bad, 128, 1 << 20, base)
+        outs, res = codec.compact(bad, 128, 1 << 20, base)
+        assert res.records_kept == kept and len(outs) == len(want)
+        assert all(np.array_equal(o, w) for o, w in zip(outs, want))
+
+
+@pytest.mark.parametrize("seed", range(4))
+@pytest.mark.parametrize("threshold", [128, 512])
+def test_compact_long_groups_out_of_txn_order_fuzz(codec, oracle, seed, threshold):
+    """Three inputs over three keys, hundreds of versions per key per input
+    (each key's group spans 100-500 small blocks), empty-value PUTs among
+    them (out of txn order as read), DELETEs: every group needs carries far
+    past 64 blocks, several groups per input, groups ending and starting
+    inside blocks; bit-exact vs the oracle at both base levels and with
+    output splits."""
+    sets = W.compaction_inputs(3, 1500, 3, seed=200 + seed, p_delete=0.1, vmin=0, vmax=3, key_width=16,
+                               distinct=False)
+    ins = [oracle.table_build(r, threshold) for r in sets]
+    for base in (1, 0):
+        for limit in (1 << 20, 200):
+            want, kept = oracle.compact(ins, threshold, limit, base)
+            outs, res = codec.compact(ins, threshold, limit, base)
+            assert res.records_kept == kept and len(outs) == len(want)
+            assert all(np.array_equal(o, w) for o, w in zip(outs, want))
+
+
+def test_compact_long_in_order_group_beside_short_out_of_order_group(codec, oracle):
+    """a long group in txn order (its walks give up at 64 blocks)
+    and, in another input, a short group out of txn order: the job-wide notes
+    send the job through the repair pass, which must leave the in-order group
+    as it is and carry the short one; bit-exact."""
+    long = W.compaction_inputs(1, 1200, 1, seed=5, p_delete=0.0, vmin=4, vmax=8, key_width=16, distinct=False)[0]
+    short = W.compaction_inputs(1, 300, 40, seed=6, p_delete=0.0, vmin=0, vmax=3, key_width=16, distinct=False)[0]
+    short["val_len"][::7] = 0
+    ins = [oracle.table_build(long, 128), oracle.table_build(short, 128)]
+    want, kept = oracle.compact(ins, 128, 1 << 20, 1)
+    outs, res = codec.compact(ins, 128, 1 << 20, 1)
+    assert res.records_kept == kept and all(np.array_equal(o, w) for o, w in zip(outs, want))
+
+
+def long_hot_key_inputs():
+    """a hot key with 2000 versions in one input (values 150-250 B:
+    ~16 entries per 4 KiB block, so its group spans ~125 blocks) holding an
+    older empty-value PUT, beside two ordinary inputs that hold the same key too."""
+    hot = W.compaction_inputs(1, 2000, 1, seed=31, p_delete=0.0, vmin=150, vmax=250, key_width=16,
+                              distinct=False)[0]
+    hot["val_len"][1500] = 0  # an older version (txns descend in file order) with an empty value
+    hot["val_off"][1500] = 0
+    other = W.compaction_inputs(2, 3000, 5000, seed=32, p_delete=0.1, vmin=0, vmax=200, key_width=16)
+    return [hot] + other
+
+
+def test_compact_hot_key_2000_versions_vs_reference(codec, oracle, tmp_path):
+    """The hot key of long_hot_key_inputs through sstc_compact: bit-exact vs the
+    oracle (pinned for exactly these inputs by the reference's own
+    MergeIterator + DoCompactJob loop, tests/test_oracle_compact.py::
+    test_live_ref_compact_hot_key_2000_versions) and, where the reference
+    driver travelled with the tree, vs a live run of it on this box."""
+    import os
+    from oracle import REF_COMPACT, ref_compact
+    sets = long_hot_key_inputs()
+    ins = [oracle.table_build(r, 4096) for r in sets]
+    idx = oracle.table_index(ins[0])
+    assert len(idx["blk_off"]) > 100  # the group spans > 70 blocks
+    want, kept = oracle.compact(ins, 4096, 1 << 20, 1)
+    outs, res = codec.compact(ins, 4096, 1 << 20, 1)
+    assert res.records_kept == kept and len(outs) == len(want)
+    assert all(np.array_equal(o, w) for o, w in zip(outs, want))
+    if os.path.exists(REF_COMPACT):
+        files = []
+        for i, f in enumerate(ins):
+            p = str(tmp_path / f"h{i}.sst")
+            f.tofile(p)
+            files.append((p, f.size + 1))
+        od = tmp_path / "ref"
+        od.mkdir()
+        ref = ref_compact(files, str(od), 4096, 1 << 20, 1)
+        assert len(ref) == len(outs)
+        for (p, fs), o in zip(ref, outs):
+            assert np.array_equal(np.fromfile(p, np.uint8), o) and fs == o.size + 1
 
 
 @pytest.mark.timeout(240)
@@ -129,6 +207,25 @@ def test_compact_many_output_tables(codec, oracle, per_table):
     want, _ = oracle.compact(ins, 4096 if per_table == 40 else 256, limit, 1)
     outs, res = codec.compact(ins, 4096 if per_table == 40 else 256, limit, 1)
     assert len(outs) == len(want) > (256 if per_table < 40 else 50)
+    assert all(np.array_equal(o, w) for o, w in zip(outs, want))
+
+
+@pytest.mark.parametrize("n_tables", [126, 127, 128, 129, 191, 300])
+def test_compact_tiles_inside_the_last_of_many_tables(codec, oracle, n_tables):
+    """n_tables equal output tables of 1100 records each (more than a 1024-record
+    block-split tile), so tiles start inside the last table: the block split's
+    64-ary search for a tile's first table end must reach the end list's last
+    element (127 tables = 128 ends: two search rounds, its top lane at the
+    range end)."""
+    per = 1100
+    total = n_tables * per
+    # one input holding every key of the space once: exactly n_tables outputs
+    sets = W.compaction_inputs(1, total, total, seed=91, p_delete=0.0, vmin=24, vmax=24, key_width=16)
+    ins = [oracle.table_build(r, 4096) for r in sets]
+    limit = per * (16 + 24)
+    want, _ = oracle.compact(ins, 4096, limit, 1)
+    outs, res = codec.compact(ins, 4096, limit, 1)
+    assert len(want) == n_tables and len(outs) == len(want)
     assert all(np.array_equal(o, w) for o, w in zip(outs, want))
 
 

@@ -4,6 +4,7 @@ compact_small_*.npz, made by oracle/_ref/ref_compact)."""
 import hashlib
 import json
 import os
+import sys
 import tempfile
 
 import numpy as np
@@ -183,6 +184,37 @@ def test_live_ref_compact_versions_out_of_txn_order(oracle, space):
         outs = ref_compact(ins, od, threshold, 1 << 20, 1)
         mine, kept = oracle.compact(files, threshold, 1 << 20, 1)
         assert kept > 50  # versions above their group head survive (compact.cc:357-362)
+        assert len(outs) == len(mine)
+        for (p, fs), m in zip(outs, mine):
+            assert np.array_equal(np.fromfile(p, np.uint8), m) and fs == m.size + 1
+
+
+def test_live_ref_compact_hot_key_2000_versions(oracle):
+    """a hot key with 2000 versions over ~125 blocks of one
+    input, an older empty-value PUT among them (out of txn order as the
+    reference reads it), beside two ordinary inputs: the oracle equals the
+    reference's own MergeIterator + DoCompactJob loop (oracle/_ref/ref_compact)
+    -- the pin for tests/test_gpu_compact_fuzz.py::
+    test_compact_hot_key_2000_versions_vs_reference."""
+    from oracle import REF_COMPACT, ref_compact
+    if not os.path.exists(REF_COMPACT):
+        pytest.skip("reference compaction driver not built")
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from test_gpu_compact_fuzz import long_hot_key_inputs
+    sets = long_hot_key_inputs()
+    with tempfile.TemporaryDirectory() as td:
+        ins, files = [], []
+        for i, rec in enumerate(sets):
+            f = oracle.table_build(rec, 4096)
+            p = os.path.join(td, f"h{i}.sst")
+            f.tofile(p)
+            ins.append((p, f.size + 1))
+            files.append(f)
+        assert len(oracle.table_index(files[0])["blk_off"]) > 100
+        od = os.path.join(td, "o")
+        os.makedirs(od)
+        outs = ref_compact(ins, od, 4096, 1 << 20, 1)
+        mine, kept = oracle.compact(files, 4096, 1 << 20, 1)
         assert len(outs) == len(mine)
         for (p, fs), m in zip(outs, mine):
             assert np.array_equal(np.fromfile(p, np.uint8), m) and fs == m.size + 1
