@@ -370,6 +370,27 @@ int sstc_compact_files(sstc_pipe *pipe, const char *const *in_paths, const uint6
                        uint32_t max_outs, uint32_t *n_out, uint8_t *key_arena, uint64_t key_arena_cap,
                        sstc_files_timing *timing);
 
+/* In-process multi-device compaction (the engine's one
+ * compaction job, db/db_impl.cc:548,553-598, spread over the node's GPUs
+ * without a process per GPU): n_shards key-range-disjoint input groups, shard s
+ * = in_paths[shard_first[s] .. shard_first[s + 1]) (shard_first has
+ * n_shards + 1 entries, shard_first[0] = 0), each compacted independently
+ * exactly as sstc_compact_files would, shard s by pipes[s % n_pipes] (create
+ * one pipe per device, each on a context of its own device) on a host thread
+ * of its own per pipe.  No data crosses devices.  Output ids continue from
+ * shard to shard: shard 0 takes first_sst_id.., shard s the ids after shard
+ * s - 1's last (the GetNextSSTId() sequence of the shards compacted one after
+ * another; a shard writes only once the shards before it know their table
+ * counts).  outs / key_arena receive the outputs in shard order; timing, when
+ * not NULL, has n_shards entries.  A failing shard fails the call with its
+ * error; the shards after it write nothing, the ones before it complete.
+ * The pipes must be distinct (each is used by one thread). */
+int sstc_compact_files_multi(sstc_pipe *const *pipes, uint32_t n_pipes, const char *const *in_paths,
+                             const uint64_t *in_file_sizes, const uint32_t *shard_first, uint32_t n_shards,
+                             const char *out_prefix, uint64_t first_sst_id, const sstc_compact_params *params,
+                             uint32_t do_fsync, sstc_file_out *outs, uint32_t max_outs, uint32_t *n_out,
+                             uint8_t *key_arena, uint64_t key_arena_cap, sstc_files_timing *timing);
+
 #ifdef __cplusplus
 }
 #endif

@@ -26,6 +26,7 @@
 #include <condition_variable>
 #include <cstring>
 #include <deque>
+#include <functional>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -45,7 +46,19 @@ struct sstc_pipe {
   uint8_t *h_in = nullptr, *h_out = nullptr, *d_src = nullptr, *d_dst = nullptr;
   uint64_t *d_idx = nullptr;
   uint64_t cap_h_in = 0, cap_h_out = 0, cap_d_src = 0, cap_d_dst = 0, cap_d_idx = 0;
+  // test hooks (sstc__pipe_set_test_caps): the first attempt's output
+  // capacity and the retry's size bound, 0 = the production values
+  uint64_t test_first_cap = 0, test_bound = 0;
 };
+
+// test hook, not in the header: force the first attempt's output capacity
+// (first_cap) and the retry's size bound (bound); 0 restores the production value
+extern "C" int sstc__pipe_set_test_caps(sstc_pipe *pipe, uint64_t first_cap, uint64_t bound) {
+  if (!pipe) return SSTC_E_INVALID_ARG;
+  pipe->test_first_cap = first_cap;
+  pipe->test_bound = bound;
+  return SSTC_OK;
+}
 
 namespace {
 
@@ -213,16 +226,25 @@ int sstc_pipe_destroy(sstc_pipe *p) {
   return SSTC_OK;
 }
 
-int sstc_compact_files(sstc_pipe *pipe, const char *const *in_paths, const uint64_t *in_file_sizes,
-                       uint32_t n_in, const char *out_prefix, uint64_t first_sst_id,
-                       const sstc_compact_params *params, uint32_t do_fsync, sstc_file_out *outs,
-                       uint32_t max_outs, uint32_t *n_out, uint8_t *key_arena, uint64_t key_arena_cap,
-                       sstc_files_timing *timing) {
-  if (!pipe || (n_in && (!in_paths || !in_file_sizes)) || !out_prefix || !params || !outs || !n_out)
-    return sstc__fail(SSTC_E_INVALID_ARG, "sstc_compact_files: NULL argument");
-  if (params->table_limit == 0 || params->block_threshold == 0)
-    return sstc__fail(SSTC_E_INVALID_ARG, "sstc_compact_files: bad parameters");
-  *n_out = 0;
+} // extern "C"
+
+namespace {
+
+// one compaction's outputs (sstc_file_out with key offsets into keys)
+struct FilesOut {
+  std::vector<sstc_file_out> outs;
+  std::string keys;
+  sstc_files_timing tm{};
+};
+
+// first_id(nt, id): called once the output table count nt is known and before
+// any output is written; sets the first output id or returns an error code
+// (then nothing is written)
+using FirstId = std::function<int(uint64_t, uint64_t &)>;
+
+int compact_files_impl(sstc_pipe *pipe, const char *const *in_paths, const uint64_t *in_file_sizes, uint32_t n_in,
+                       const char *out_prefix, const FirstId &first_id, const sstc_compact_params *params,
+                       uint32_t do_fsync, uint32_t max_outs, FilesOut &result) {
   if (hipSetDevice(pipe->device) != hipSuccess) return sstc__fail(SSTC_E_HIP, "hipSetDevice");
   const auto t0 = clk::now();
   hipStream_t s = pipe->stream;
@@ -327,6 +349,13 @@ int sstc_compact_files(sstc_pipe *pipe, const char *const *in_paths, const uint6
   const auto t2 = clk::now();
 
   // ---- compact on the device
+  // Output size bound from the input alone: every surviving entry is its
+  // input entry's bytes plus, at worst, a block of its own (16 B extra) and a
+  // meta entry (24 B + its key twice: at most twice the entry), each output
+  // table a 40 B footer; an input entry takes >= 29 B with its offset entry.
+  // So output <= 2 * input + 40 B per record (<= 1.4 * input) + 40 B per table.
+  // A device-reported size past it is an internal fault, never an allocation.
+  const uint64_t bound = pipe->test_bound ? pipe->test_bound : 4 * total + 64 * max_tables + (1u << 20);
   sstc_compact_result res{};
   uint64_t cap = total + total / 2 + (1u << 20);
   int rc = SSTC_E_CAPACITY;
@@ -337,9 +366,20 @@ int sstc_compact_files(sstc_pipe *pipe, const char *const *in_paths, const uint6
                                " blocks, " + std::to_string(res.records_kept) + " records)";
       return bail(SSTC_E_NOMEM, what.c_str());
     }
-    rc = sstc_compact(pipe->ctx, pipe->d_src, d_off, d_len, nblocks, tfb.data(), n_in, params, pipe->d_dst,
-                      pipe->cap_d_dst, d_toff, d_tlen, max_tables, &res);
-    cap = res.bytes_out; // exact size known after a capacity miss
+    const uint64_t use = attempt == 0 && pipe->test_first_cap ? std::min(pipe->test_first_cap, pipe->cap_d_dst)
+                                                               : pipe->cap_d_dst;
+    rc = sstc_compact(pipe->ctx, pipe->d_src, d_off, d_len, nblocks, tfb.data(), n_in, params, pipe->d_dst, use,
+                      d_toff, d_tlen, max_tables, &res);
+    if (rc == SSTC_E_CAPACITY) { // the exact size is known after a capacity miss
+      if (res.bytes_out <= use || res.bytes_out > bound) {
+        (void)sstc__ctx_sync(pipe->ctx);
+        const std::string what = "sstc_compact_files: the device reported an output size of " +
+                                 std::to_string(res.bytes_out) + " bytes after a capacity miss at " +
+                                 std::to_string(use) + " (bound from the input: " + std::to_string(bound) + ")";
+        return sstc__fail(SSTC_E_INTERNAL, what.c_str());
+      }
+      cap = res.bytes_out;
+    }
   }
   if (rc != SSTC_OK) { // sstc_compact set the error string
     (void)sstc__ctx_sync(pipe->ctx);
@@ -350,6 +390,8 @@ int sstc_compact_files(sstc_pipe *pipe, const char *const *in_paths, const uint6
   // ---- store: per-table D2H with an event, writer threads pwrite + fsync
   const uint64_t nt = res.tables_out;
   if (nt > max_outs) return sstc__fail(SSTC_E_CAPACITY, "sstc_compact_files: more output tables than max_outs");
+  uint64_t first_sst_id = 0;
+  if (const int r = first_id(nt, first_sst_id)) return r;
   std::vector<uint64_t> toff(nt + 1);
   if (hipMemcpy(toff.data(), d_toff, 8 * (nt + 1), hipMemcpyDeviceToHost) != hipSuccess)
     return sstc__fail(SSTC_E_HIP, "sstc_compact_files: table offsets");
@@ -399,33 +441,151 @@ int sstc_compact_files(sstc_pipe *pipe, const char *const *in_paths, const uint6
   for (auto &t : writers) t.join();
   for (auto &e : ev) (void)hipEventDestroy(e);
   if (werr) return sstc__fail(werr == 1 ? SSTC_E_HIP : SSTC_E_INVALID_ARG, "sstc_compact_files: output write failed");
-  uint64_t kat = 0;
+  result.outs.resize(nt);
+  result.keys.clear();
   for (uint64_t t = 0; t < nt; t++) {
-    sstc_file_out &o = outs[t];
+    sstc_file_out &o = result.outs[t];
     o.sst_id = first_sst_id + t;
     o.file_size = toff[t + 1] - toff[t] + 1;
     o.smallest_key_len = static_cast<uint32_t>(lo[t].size());
     o.largest_key_len = static_cast<uint32_t>(hi[t].size());
-    o.smallest_key_off = kat;
-    o.largest_key_off = kat + lo[t].size();
-    if (key_arena) {
-      if (kat + lo[t].size() + hi[t].size() > key_arena_cap)
-        return sstc__fail(SSTC_E_CAPACITY, "sstc_compact_files: key_arena too small");
-      std::memcpy(key_arena + kat, lo[t].data(), lo[t].size());
-      std::memcpy(key_arena + kat + lo[t].size(), hi[t].data(), hi[t].size());
-    }
-    kat += lo[t].size() + hi[t].size();
+    o.smallest_key_off = result.keys.size();
+    o.largest_key_off = result.keys.size() + lo[t].size();
+    result.keys += lo[t];
+    result.keys += hi[t];
   }
-  *n_out = static_cast<uint32_t>(nt);
   const auto t4 = clk::now();
-  if (timing) {
-    timing->index_s = secs(t0, t1);
-    timing->load_s = secs(t1, t2);
-    timing->compact_s = secs(t2, t3);
-    timing->store_s = secs(t3, t4);
-    timing->total_s = secs(t0, t4);
-  }
+  result.tm.index_s = secs(t0, t1);
+  result.tm.load_s = secs(t1, t2);
+  result.tm.compact_s = secs(t2, t3);
+  result.tm.store_s = secs(t3, t4);
+  result.tm.total_s = secs(t0, t4);
   return SSTC_OK;
+}
+
+// copies outputs (shard after shard) into the caller's arrays
+int copy_outs(const std::vector<const FilesOut *> &parts, sstc_file_out *outs, uint32_t max_outs, uint32_t *n_out,
+              uint8_t *key_arena, uint64_t key_arena_cap, const char *who) {
+  uint64_t n = 0, kat = 0;
+  for (const FilesOut *p : parts) {
+    if (n + p->outs.size() > max_outs)
+      return sstc__fail(SSTC_E_CAPACITY, (std::string(who) + ": more output tables than max_outs").c_str());
+    if (key_arena && kat + p->keys.size() > key_arena_cap)
+      return sstc__fail(SSTC_E_CAPACITY, (std::string(who) + ": key_arena too small").c_str());
+    for (sstc_file_out o : p->outs) {
+      o.smallest_key_off += kat;
+      o.largest_key_off += kat;
+      outs[n++] = o;
+    }
+    if (key_arena && !p->keys.empty()) std::memcpy(key_arena + kat, p->keys.data(), p->keys.size());
+    kat += p->keys.size();
+  }
+  *n_out = static_cast<uint32_t>(n);
+  return SSTC_OK;
+}
+
+} // namespace
+
+extern "C" {
+
+int sstc_compact_files(sstc_pipe *pipe, const char *const *in_paths, const uint64_t *in_file_sizes,
+                       uint32_t n_in, const char *out_prefix, uint64_t first_sst_id,
+                       const sstc_compact_params *params, uint32_t do_fsync, sstc_file_out *outs,
+                       uint32_t max_outs, uint32_t *n_out, uint8_t *key_arena, uint64_t key_arena_cap,
+                       sstc_files_timing *timing) {
+  if (!pipe || (n_in && (!in_paths || !in_file_sizes)) || !out_prefix || !params || !outs || !n_out)
+    return sstc__fail(SSTC_E_INVALID_ARG, "sstc_compact_files: NULL argument");
+  if (params->table_limit == 0 || params->block_threshold == 0)
+    return sstc__fail(SSTC_E_INVALID_ARG, "sstc_compact_files: bad parameters");
+  *n_out = 0;
+  FilesOut r;
+  const int rc = compact_files_impl(
+      pipe, in_paths, in_file_sizes, n_in, out_prefix,
+      [first_sst_id](uint64_t, uint64_t &id) {
+        id = first_sst_id;
+        return SSTC_OK;
+      },
+      params, do_fsync, max_outs, r);
+  if (rc != SSTC_OK) return rc;
+  if (timing) *timing = r.tm;
+  return copy_outs({&r}, outs, max_outs, n_out, key_arena, key_arena_cap, "sstc_compact_files");
+}
+
+int sstc_compact_files_multi(sstc_pipe *const *pipes, uint32_t n_pipes, const char *const *in_paths,
+                             const uint64_t *in_file_sizes, const uint32_t *shard_first, uint32_t n_shards,
+                             const char *out_prefix, uint64_t first_sst_id, const sstc_compact_params *params,
+                             uint32_t do_fsync, sstc_file_out *outs, uint32_t max_outs, uint32_t *n_out,
+                             uint8_t *key_arena, uint64_t key_arena_cap, sstc_files_timing *timing) {
+  const char *who = "sstc_compact_files_multi";
+  if (!pipes || n_pipes == 0 || !shard_first || !out_prefix || !params || !outs || !n_out)
+    return sstc__fail(SSTC_E_INVALID_ARG, "sstc_compact_files_multi: NULL argument");
+  if (params->table_limit == 0 || params->block_threshold == 0)
+    return sstc__fail(SSTC_E_INVALID_ARG, "sstc_compact_files_multi: bad parameters");
+  *n_out = 0;
+  for (uint32_t j = 0; j < n_pipes; j++) {
+    if (!pipes[j]) return sstc__fail(SSTC_E_INVALID_ARG, "sstc_compact_files_multi: NULL pipe");
+    for (uint32_t k = 0; k < j; k++)
+      if (pipes[k] == pipes[j])
+        return sstc__fail(SSTC_E_INVALID_ARG, "sstc_compact_files_multi: a pipe listed twice (one thread per pipe)");
+  }
+  if (shard_first[0] != 0) return sstc__fail(SSTC_E_INVALID_ARG, "sstc_compact_files_multi: shard_first[0] != 0");
+  for (uint32_t s = 0; s < n_shards; s++)
+    if (shard_first[s + 1] < shard_first[s])
+      return sstc__fail(SSTC_E_INVALID_ARG, "sstc_compact_files_multi: shard_first not ascending");
+  if (shard_first[n_shards] && (!in_paths || !in_file_sizes))
+    return sstc__fail(SSTC_E_INVALID_ARG, "sstc_compact_files_multi: NULL argument");
+
+  // the output-id chain: shard s takes the ids after shard s - 1's tables,
+  // exactly the GetNextSSTId() sequence of the shards compacted one after
+  // another; a shard that fails breaks the chain for every shard after it
+  // (those write nothing), the shards before it finish
+  std::mutex m;
+  std::condition_variable cv;
+  std::vector<int> state(n_shards + 1, 0); // 0 pending, 1 ready, -1 broken
+  std::vector<uint64_t> base(n_shards + 1, 0);
+  state[0] = 1;
+  base[0] = first_sst_id;
+  auto publish = [&](uint32_t s, int st, uint64_t b) {
+    std::lock_guard<std::mutex> lk(m);
+    if (state[s + 1] != 0) return;
+    state[s + 1] = st;
+    base[s + 1] = b;
+    cv.notify_all();
+  };
+  std::vector<FilesOut> res(n_shards);
+  std::vector<int> rcs(n_shards, SSTC_OK);
+  std::vector<std::string> errs(n_shards);
+  std::vector<std::thread> th;
+  for (uint32_t j = 0; j < std::min(n_pipes, n_shards); j++)
+    th.emplace_back([&, j] {
+      for (uint32_t sh = j; sh < n_shards; sh += n_pipes) {
+        const FirstId chain = [&, sh](uint64_t nt, uint64_t &id) {
+          std::unique_lock<std::mutex> lk(m);
+          cv.wait(lk, [&] { return state[sh] != 0; });
+          if (state[sh] < 0) return sstc__fail(SSTC_E_INVALID_ARG, "sstc_compact_files_multi: an earlier shard failed");
+          id = base[sh];
+          lk.unlock();
+          publish(sh, 1, id + nt);
+          return static_cast<int>(SSTC_OK);
+        };
+        const uint32_t f = shard_first[sh], n = shard_first[sh + 1] - f;
+        rcs[sh] = compact_files_impl(pipes[j], in_paths + f, in_file_sizes + f, n, out_prefix, chain, params, do_fsync,
+                                     max_outs, res[sh]);
+        if (rcs[sh] != SSTC_OK) {
+          errs[sh] = sstc_last_error_string(); // thread-local: carried to the caller's thread
+          publish(sh, -1, 0);
+        }
+      }
+    });
+  for (auto &t : th) t.join();
+  for (uint32_t sh = 0; sh < n_shards; sh++)
+    if (rcs[sh] != SSTC_OK)
+      return sstc__fail(rcs[sh], ("sstc_compact_files_multi: shard " + std::to_string(sh) + ": " + errs[sh]).c_str());
+  if (timing)
+    for (uint32_t sh = 0; sh < n_shards; sh++) timing[sh] = res[sh].tm;
+  std::vector<const FilesOut *> parts;
+  for (const FilesOut &r : res) parts.push_back(&r);
+  return copy_outs(parts, outs, max_outs, n_out, key_arena, key_arena_cap, who);
 }
 
 } // extern "C"

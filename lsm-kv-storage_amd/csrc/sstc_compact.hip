@@ -1338,6 +1338,7 @@ __global__ __launch_bounds__(256) void ck_run_starts_kernel(const uint64_t *rec_
     }
     __syncthreads();
     if (threadIdx.x == 0) {
+      static_assert(256 / kWave == 4, "the count kernel's per-wave partials: four wave64s");
       *in_bytes = s_part[0] + s_part[1] + s_part[2] + s_part[3];
       for (uint32_t w = 1; w < 256 / kWave; w++) e = s_end[w] > e ? s_end[w] : e;
       *errs = *err_count;

@@ -491,7 +491,8 @@ __global__ void count_kernel(const uint8_t *src, const uint64_t *blk_off, const 
   const uint64_t len = b < nblocks ? blk_len[b] : 0;
   if (len_part) { // uniform: the workgroup's byte sum (bounds the compaction's output counts) and the
                   // end of the source bytes its blocks span (bounds every entry the compaction copies)
-    __shared__ uint64_t s_part[4], s_end[4];
+    static_assert(256 / kWave == 4, "count_kernel: 256-thread workgroups of four wave64s");
+    __shared__ uint64_t s_part[256 / kWave], s_end[256 / kWave];
     const uint64_t v = wave_sum_u64(len);
     uint64_t e = b < nblocks ? blk_off[b] + len : 0;
     for (uint32_t d = kWave / 2; d > 0; d >>= 1) {

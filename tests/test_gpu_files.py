@@ -93,3 +93,46 @@ def test_files_empty_and_errors(pipe, oracle, tmp_path):
         pipe.compact_files([p], [f.size + 1], str(tmp_path) + "/x", 1)
     with pytest.raises(Exception):
         pipe.compact_files([str(tmp_path / "missing.sst")], [1000], str(tmp_path) + "/x", 1)
+
+
+def test_files_capacity_retry_and_bound(oracle, tmp_path):
+    """sstc_compact_files' capacity retry (compact_files.cpp): a first attempt
+    forced one byte short of the output goes through SSTC_E_CAPACITY, the
+    retry at the device-reported size writes the reference's files; a
+    device-reported size past the input-derived bound is SSTC_E_INTERNAL
+    (nothing is allocated for it, no file is written)."""
+    import sstcodec
+    case = CASES["split"]
+    sets = W.compaction_inputs(case["k"], case["n_per"], case["key_space"], vmax=case["vmax"],
+                               distinct=case["distinct"], **case.get("gen", {}))
+    files = [oracle.table_build(r, case["block_threshold"]) for r in sets]
+    paths, sizes = write_inputs(tmp_path, files)
+    want = case["outputs_base1"]
+    need = sum(w["file_size"] - 1 for w in want)
+    codec = sstcodec.Codec(0)
+    p = sstcodec.FilePipe(codec, io_threads=2)
+    try:
+        for first in (1, need - 1, need):
+            od = tmp_path / f"out{first}"
+            od.mkdir()
+            assert p.lib.sstc__pipe_set_test_caps(p.h, first, 0) == 0
+            outs, _ = p.compact_files(paths, sizes, str(od) + "/", 100, case["block_threshold"], case["table_limit"], 1)
+            assert [o[1] for o in outs] == [w["file_size"] for w in want]
+            for (sid, fs, lo, hi), w in zip(outs, want):
+                img = np.fromfile(str(od / f"{sid}.sst"), np.uint8)
+                assert hashlib.sha256(img.tobytes()).hexdigest() == w["sha256"]
+        od = tmp_path / "bound"
+        od.mkdir()
+        assert p.lib.sstc__pipe_set_test_caps(p.h, 1, 1024) == 0
+        with pytest.raises(sstcodec.SstcError, match="bound from the input"):
+            p.compact_files(paths, sizes, str(od) + "/", 100, case["block_threshold"], case["table_limit"], 1)
+        assert not os.listdir(od)
+        # the pipe still works afterwards
+        assert p.lib.sstc__pipe_set_test_caps(p.h, 0, 0) == 0
+        od = tmp_path / "after"
+        od.mkdir()
+        outs, _ = p.compact_files(paths, sizes, str(od) + "/", 100, case["block_threshold"], case["table_limit"], 1)
+        assert [o[1] for o in outs] == [w["file_size"] for w in want]
+    finally:
+        p.close()
+        codec.close()
