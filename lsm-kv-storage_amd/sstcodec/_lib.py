@@ -115,6 +115,9 @@ def load():
         "sstc_pipe_create": (ctypes.c_int, [c_vp, c_u32, P(c_vp)]),
         "sstc_pipe_destroy": (ctypes.c_int, [c_vp]),
         "sstc__pipe_set_test_caps": (ctypes.c_int, [c_vp, c_u64, c_u64]),  # test hook (compact_files.cpp)
+        "sstc_compact_files_multi": (ctypes.c_int, [c_vp, c_u32, c_vp, c_vp, c_vp, c_u32, ctypes.c_char_p, c_u64,
+                                                    P(CompactParams), c_u32, c_vp, c_u32, P(c_u32), c_vp, c_u64,
+                                                    c_vp]),
         "sstc_compact_files": (ctypes.c_int, [c_vp, c_vp, c_vp, c_u32, ctypes.c_char_p, c_u64, P(CompactParams),
                                               c_u32, c_vp, c_u32, P(c_u32), c_vp, c_u64, P(FilesTiming)]),
     }

@@ -380,6 +380,41 @@ class FilePipe:
         return res, {k: getattr(tm, k) for k, _ in FilesTiming._fields_}
 
 
+def compact_files_multi(pipes, shards, out_prefix, first_sst_id, block_threshold=4096, table_limit=32 << 20,
+                        base_level=1, txn_mode=_lib.SSTC_TXN_COMPAT, fsync=True, max_outs=8192):
+    """sstc_compact_files_multi: shards = [[(path, GetFileSize()), ...], ...]
+    (key-range-disjoint input groups), shard s on pipes[s % len(pipes)], one
+    host thread per pipe.  Returns ([(sst_id, file_size, smallest, largest)]
+    in shard order, [timing dict per shard])."""
+    from ._lib import CompactParams, FileOut, FilesTiming
+    lib = pipes[0].lib
+    paths = [p for sh in shards for p, _ in sh]
+    sizes = [int(fs) for sh in shards for _, fs in sh]
+    first = [0]
+    for sh in shards:
+        first.append(first[-1] + len(sh))
+    n = max(len(paths), 1)
+    arr = (ctypes.c_char_p * n)(*[p.encode() for p in paths])
+    sz = (ctypes.c_uint64 * n)(*sizes)
+    sf = (ctypes.c_uint32 * len(first))(*first)
+    ph = (ctypes.c_void_p * len(pipes))(*[p.h for p in pipes])
+    outs = (FileOut * max_outs)()
+    arena = ctypes.create_string_buffer(max_outs * 2 * 4096)
+    nout = ctypes.c_uint32()
+    tm = (FilesTiming * max(len(shards), 1))()
+    prm = CompactParams(block_threshold, table_limit, base_level, txn_mode)
+    check(lib.sstc_compact_files_multi(ctypes.cast(ph, ctypes.c_void_p), len(pipes), ctypes.cast(arr, ctypes.c_void_p),
+                                       ctypes.cast(sz, ctypes.c_void_p), ctypes.cast(sf, ctypes.c_void_p), len(shards),
+                                       out_prefix.encode(), int(first_sst_id), ctypes.byref(prm), 1 if fsync else 0,
+                                       ctypes.cast(outs, ctypes.c_void_p), max_outs, ctypes.byref(nout),
+                                       ctypes.cast(arena, ctypes.c_void_p), len(arena), ctypes.cast(tm, ctypes.c_void_p)),
+          "sstc_compact_files_multi")
+    raw = arena.raw
+    res = [(o.sst_id, o.file_size, raw[o.smallest_key_off:o.smallest_key_off + o.smallest_key_len],
+            raw[o.largest_key_off:o.largest_key_off + o.largest_key_len]) for o in outs[: nout.value]]
+    return res, [{k: getattr(t, k) for k, _ in FilesTiming._fields_} for t in tm[: len(shards)]]
+
+
 def _table_index(f, keys=False):
     """(block offsets, block sizes[, last-key offsets, last-key lengths]) of an
     SST image: footer + meta section walk (reference table_reader.cc:52-156).
