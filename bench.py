@@ -571,7 +571,8 @@ class GpuCompaction:
                                           self.max_t, ct.byref(self.res)), "sstc_compact")
 
     def sync(self):
-        torch.cuda.synchronize()
+        if self.dev.type == "cuda":  # (a host device only in the CPU test of this rank path)
+            torch.cuda.synchronize(self.dev)
 
     def outputs(self):
         """[(sha256, GetFileSize())] of the last call's output SSTs, output bytes."""
@@ -582,7 +583,8 @@ class GpuCompaction:
 
     def free(self):
         del self.src, self.dst
-        torch.cuda.empty_cache()
+        if self.dev.type == "cuda":
+            torch.cuda.empty_cache()
 
 
 def time_job(job, steps, ranks=None, warmup=2):

@@ -15,7 +15,8 @@ done
 python3 - "$out" "$args" <<'PY'
 import csv, glob, json, sys
 out, args = sys.argv[1], sys.argv[2]
-res = {"workload": "config3" if "--config 3" in args else args, "note":
+tag = next((f"config{c}" for c in "345" if f"--config {c}" in args), args)  # what bench.py's legs look up
+res = {"workload": tag, "args": args, "note":
        "one sstc_compact call: every kernel from its last count_kernel dispatch on; FETCH_SIZE x 2 (gfx950), KiB"}
 per = {}
 for c in ("FETCH_SIZE", "WRITE_SIZE"):
