@@ -296,7 +296,10 @@ __global__ __launch_bounds__(256) void ck_check_blocks_kernel(SK *s, const uint6
   // Long groups: the last workgroup to finish repairs them (an in-launch
   // hand-off: every workgroup that lowered a merge txn drains its stores and
   // releases them at agent scope before its ticket; the last arriver acquires
-  // before it reads them).  No workgroup waits on another.
+  // before it reads them).  No workgroup waits on another.  Two-level tickets:
+  // a counter per dispatch group (workgroup i % 8, i.e. per XCD) and one over
+  // the groups, so no address takes more than ~1/8 of the workgroups' atomics
+  // (one same-address atomic per workgroup cost this kernel ~7 us at config 3)
   __shared__ uint32_t s_last;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   const bool any = __syncthreads_or(wrote);
@@ -305,15 +308,24 @@ __global__ __launch_bounds__(256) void ck_check_blocks_kernel(SK *s, const uint6
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-    const uint32_t t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    constexpr uint32_t kG = 8;
+    const uint32_t g = blockIdx.x % kG, groups = gridDim.x < kG ? gridDim.x : kG;
+    const uint32_t in_g = gridDim.x / kG + (g < gridDim.x % kG ? 1u : 0u);
     uint32_t last = 0;
-    if (t == gridDim.x - 1) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    // counters 256 B apart: separate lines / channels
+    if (__hip_atomic_fetch_add(ticket + 64 * g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == in_g - 1) {
+      // the group's last: pass its group's writes on to the last group
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      const unsigned long long g = __hip_atomic_load(guard, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      constexpr unsigned long long kLongInv = kGuardLongGroup | kGuardInv;
-      last = (g & kLongInv) == kLongInv && !stop(); // the job's verdicts are final here
-      __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(ticket + 64 * g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (__hip_atomic_fetch_add(ticket + 64 * kG, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == groups - 1) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned long long gw = __hip_atomic_load(guard, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        constexpr unsigned long long kLongInv = kGuardLongGroup | kGuardInv;
+        last = (gw & kLongInv) == kLongInv && !stop(); // the job's verdicts are final here
+        __hip_atomic_store(ticket + 64 * kG, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
     s_last = last;
   }
@@ -1345,7 +1357,7 @@ __global__ __launch_bounds__(256) void ck_run_starts_kernel(const uint64_t *rec_
       *bad = 0;
       guard[0] = 0; // consistency-guard bits
       guard[1] = e; // the end of the source bytes the input blocks span
-      guard[2] = 0; // ck_check_blocks_kernel's ticket
+      for (int g = 0; g < 9; g++) guard[32 + 32 * g] = 0; // ck_check_blocks_kernel's tickets
     }
   }
   if (i < n) out[i] = rec_base[tfb[i]];
@@ -1452,8 +1464,9 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     unsigned long long *bad = reinterpret_cast<unsigned long long *>(pool.get<uint64_t>(1));
     // consistency guard: [0] bits set by any check of the job, [1] the end of
     // the source bytes its blocks span (both cleared by ck_run_starts_kernel)
-    // guard[0] bits, guard[1] source end, guard[2] the check kernel's ticket
-    unsigned long long *guard = reinterpret_cast<unsigned long long *>(pool.get<uint64_t>(3));
+    // guard[0] bits, guard[1] source end; guard + 32 the check kernel's 9
+    // ticket counters, 256 B apart (u32 at guard + 32 + 32 g)
+    unsigned long long *guard = reinterpret_cast<unsigned long long *>(pool.get<uint64_t>(32 + 9 * 32));
     const uint64_t *src_end = reinterpret_cast<const uint64_t *>(guard + 1);
     // record index of every input table's first record (its run start)
     CK(hipMemcpyAsync(d_tfb, h_tfb, (ntables + 1) * 8, hipMemcpyHostToDevice, s));
@@ -1582,7 +1595,7 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
                                s>>>(A, rb_all, nblocks, rb, nruns, kv, bad, dec_fail, ffws, 1 + 3 * fftiles, guard,
                                                            reinterpret_cast<const uint64_t *>(arena.up_dev),
                                                            reinterpret_cast<uint64_t *>(d_kg), kg_bytes / 8,
-                                                           reinterpret_cast<unsigned int *>(guard + 2));
+                                                           reinterpret_cast<unsigned int *>(guard + 32));
       if (!kg.empty()) {
         const uint32_t max_ids = *std::max_element(pass_ids.begin(), pass_ids.end());
         uint32_t *Cm = pool.get<uint32_t>(static_cast<uint64_t>(max_ids) * kKWay);
