@@ -119,9 +119,23 @@ private:
 
   const TableReader *table_reader_;
 
+  // the table's data section in page-locked host memory (sstc_host_alloc)
+  struct HostBytes {
+    uint8_t *p = nullptr;
+    uint64_t n = 0;
+    int pinned = 0;
+    HostBytes() = default;
+    HostBytes(const HostBytes &) = delete;
+    HostBytes &operator=(const HostBytes &) = delete;
+    ~HostBytes();
+    void reset(uint64_t bytes);
+    uint8_t *data() const { return p; }
+    uint64_t size() const { return n; }
+  };
+
   bool loaded_ = false;
   uint64_t data_begin_ = 0;
-  std::vector<uint8_t> data_;
+  HostBytes data_;
   std::unique_ptr<sstc::DecodedBlocks> rec_;
 };
 

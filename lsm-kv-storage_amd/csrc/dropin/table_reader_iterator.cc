@@ -27,6 +27,8 @@
 #include "sstable/table_reader.h"
 #include "sstc_table.h"
 
+#include <cstdlib>
+#include <new>
 #include <span>
 #include <stdexcept>
 #include <string>
@@ -47,6 +49,18 @@ TableReaderIterator::TableReaderIterator(
 // table_reader_iterator.cc:23
 TableReaderIterator::~TableReaderIterator() { lru_table_item_->Unref(); }
 
+TableReaderIterator::HostBytes::~HostBytes() { sstc_host_free(p, pinned); }
+
+void TableReaderIterator::HostBytes::reset(uint64_t bytes) {
+  sstc_host_free(p, pinned);
+  p = nullptr;
+  pinned = 0;
+  static const bool pageable = std::getenv("SSTC_DROPIN_PAGEABLE") != nullptr; // A/B knob (tools/bench_dropin.py)
+  p = static_cast<uint8_t *>(pageable ? std::malloc(bytes ? bytes : 1) : sstc_host_alloc(bytes ? bytes : 1, &pinned));
+  if (!p) throw std::bad_alloc();
+  n = bytes;
+}
+
 void TableReaderIterator::Load() {
   if (loaded_) return;
   const std::vector<BlockIndex> &index = table_reader_->block_index_;
@@ -60,7 +74,8 @@ void TableReaderIterator::Load() {
   }
   if (nb == 0) lo = hi = 0;
   data_begin_ = lo;
-  data_.resize(hi - lo);
+  // page-locked, so the upload is one DMA at PCIe rate
+  data_.reset(hi - lo);
   for (uint64_t done = 0; done < data_.size();) {
     const uint64_t chunk = std::min<uint64_t>(data_.size() - done, 1ull << 30);
     const ssize_t r = table_reader_->read_file_object_->RandomRead(

@@ -434,34 +434,69 @@ namespace {
 // per-block record counts and status, record fields with offsets into data.
 using HostRecords = DecodedBlocks;
 
-DevBuf upload_raw(sstc_ctx *ctx, const void *h, size_t n) {
-  DevBuf d(n);
-  h2d(ctx, d.p, h, n);
-  return d;
-}
+} // namespace
+
+namespace {
+// per-host-thread, per-device decode staging, grow-only (a reader thread
+// decodes table after table: no hipMalloc / hipFree per table)
+struct DecStage {
+  uint8_t *dev = nullptr;
+  uint64_t cap = 0;
+  ~DecStage() {
+    if (dev) (void)hipFree(dev);
+  }
+  uint8_t *get(uint64_t n) {
+    if (n > cap) {
+      if (dev) (void)hipFree(dev);
+      dev = nullptr;
+      cap = 0;
+      const uint64_t c = n + n / 4;
+      if (hipMalloc(reinterpret_cast<void **>(&dev), c) != hipSuccess) throw std::runtime_error("hipMalloc failed");
+      cap = c;
+    }
+    return dev;
+  }
+};
+thread_local std::map<int, DecStage> g_dec; // device -> staging
 } // namespace
 
 int DecodeBlocks(sstc_ctx *ctx, const uint8_t *data, uint64_t bytes, const uint64_t *off, const uint64_t *len,
                  uint64_t nb, uint32_t txn_mode, DecodedBlocks &out) {
   if (!ctx || (bytes && !data) || (nb && (!off || !len))) return SSTC_E_INVALID_ARG;
-  for (uint64_t b = 0; b < nb; b++)
+  uint64_t sum_len = 0;
+  for (uint64_t b = 0; b < nb; b++) {
     if (off[b] > bytes || len[b] > bytes - off[b]) return SSTC_E_INVALID_ARG;
+    sum_len += len[b];
+  }
   static const uint8_t kZero[16] = {};
   try {
-    DeviceScope on_ctx_device(sstc__ctx_device(ctx));
-    DevBuf d_src = upload_raw(ctx, bytes ? data : kZero, bytes ? bytes : 1), d_off = upload_raw(ctx, off, nb * 8),
-           d_len = upload_raw(ctx, len, nb * 8), d_base((nb + 1) * 8), d_status(nb * 4 + 4);
-    check(sstc_count_records(ctx, d_src.as<uint8_t>(), d_off.as<uint64_t>(), d_len.as<uint64_t>(), nb,
-                             d_base.as<uint64_t>()),
-          "sstc_count_records");
+    const int dev = sstc__ctx_device(ctx);
+    DeviceScope on_ctx_device(dev);
+    // one device region: the bytes, the block index, the counts and the record
+    // arrays sized by the most records the blocks can claim (the count kernel
+    // takes a trailer's n only when 16 n + 16 <= the block's length)
+    const uint64_t nmax = sum_len / 16 + 1;
+    const uint64_t o_src = 0, o_off = align256(bytes + 16), o_len = align256(o_off + 8 * nb),
+                   o_base = align256(o_len + 8 * nb), o_st = align256(o_base + 8 * (nb + 1)),
+                   o_type = align256(o_st + 4 * nb + 4), o_kl = align256(o_type + nmax), o_vl = align256(o_kl + 4 * nmax),
+                   o_txn = align256(o_vl + 4 * nmax), o_ko = align256(o_txn + 8 * nmax),
+                   o_vo = align256(o_ko + 8 * nmax), total = align256(o_vo + 8 * nmax);
+    uint8_t *d = g_dec[dev].get(total);
+    h2d(ctx, d + o_src, bytes ? data : kZero, bytes ? bytes : 1);
+    h2d(ctx, d + o_off, off, nb * 8);
+    h2d(ctx, d + o_len, len, nb * 8);
+    auto *d_off = reinterpret_cast<uint64_t *>(d + o_off), *d_len = reinterpret_cast<uint64_t *>(d + o_len),
+         *d_base = reinterpret_cast<uint64_t *>(d + o_base);
+    check(sstc_count_records(ctx, d + o_src, d_off, d_len, nb, d_base), "sstc_count_records");
     out.base.resize(nb + 1);
-    if (!d2h(ctx, out.base.data(), d_base.p, (nb + 1) * 8) || !sync(ctx)) return SSTC_E_HIP;
+    if (!d2h(ctx, out.base.data(), d_base, (nb + 1) * 8) || !sync(ctx)) return SSTC_E_HIP;
     const uint64_t n = out.base[nb];
-    DevBuf d_type(n + 1), d_kl(4 * n + 4), d_vl(4 * n + 4), d_txn(8 * n + 8), d_ko(8 * n + 8), d_vo(8 * n + 8);
-    sstc_records rec{d_type.as<uint8_t>(), d_kl.as<uint32_t>(), d_vl.as<uint32_t>(),
-                     d_txn.as<uint64_t>(), d_ko.as<uint64_t>(), d_vo.as<uint64_t>()};
-    check(sstc_decode_blocks(ctx, d_src.as<uint8_t>(), d_off.as<uint64_t>(), d_len.as<uint64_t>(), nb,
-                             d_base.as<uint64_t>(), rec, txn_mode, d_status.as<uint32_t>()),
+    if (n > nmax) return SSTC_E_INVALID_ARG; // blocks claiming more entries than their bytes hold
+    sstc_records rec{d + o_type, reinterpret_cast<uint32_t *>(d + o_kl), reinterpret_cast<uint32_t *>(d + o_vl),
+                     reinterpret_cast<uint64_t *>(d + o_txn), reinterpret_cast<uint64_t *>(d + o_ko),
+                     reinterpret_cast<uint64_t *>(d + o_vo)};
+    check(sstc_decode_blocks(ctx, d + o_src, d_off, d_len, nb, d_base, rec, txn_mode,
+                             reinterpret_cast<uint32_t *>(d + o_st)),
           "sstc_decode_blocks");
     out.status.resize(nb);
     out.type.resize(n);
@@ -470,10 +505,10 @@ int DecodeBlocks(sstc_ctx *ctx, const uint8_t *data, uint64_t bytes, const uint6
     out.txn.resize(n);
     out.key_off.resize(n);
     out.val_off.resize(n);
-    bool ok = d2h(ctx, out.status.data(), d_status.p, nb * 4) && d2h(ctx, out.type.data(), d_type.p, n) &&
-              d2h(ctx, out.key_len.data(), d_kl.p, 4 * n) && d2h(ctx, out.val_len.data(), d_vl.p, 4 * n) &&
-              d2h(ctx, out.txn.data(), d_txn.p, 8 * n) && d2h(ctx, out.key_off.data(), d_ko.p, 8 * n) &&
-              d2h(ctx, out.val_off.data(), d_vo.p, 8 * n);
+    bool ok = d2h(ctx, out.status.data(), d + o_st, nb * 4) && d2h(ctx, out.type.data(), d + o_type, n) &&
+              d2h(ctx, out.key_len.data(), d + o_kl, 4 * n) && d2h(ctx, out.val_len.data(), d + o_vl, 4 * n) &&
+              d2h(ctx, out.txn.data(), d + o_txn, 8 * n) && d2h(ctx, out.key_off.data(), d + o_ko, 8 * n) &&
+              d2h(ctx, out.val_off.data(), d + o_vo, 8 * n);
     ok = sync(ctx) && ok;
     return ok ? SSTC_OK : SSTC_E_HIP;
   } catch (const std::exception &) {

@@ -65,6 +65,7 @@
 #include "sstable/block_reader_cache.h"
 #include "sstable/table_reader_cache.h"
 
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <filesystem>
@@ -341,12 +342,15 @@ int main(int argc, char **argv) {
   const kvs::db::Version *version = vm->GetLatestVersion();
   kvs::db::VersionEdit out_edit(levels);
   kvs::db::Compact compact(db->GetBlockReaderCache(), db->GetTableReaderCache(), version, &out_edit, db);
+  const auto t0 = std::chrono::steady_clock::now();
   const bool ok = compact.PickCompact(); // db/compact.cc:35-52 -> DoL0L1Compact -> DoCompactJob
+  const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   for (const auto &del : out_edit.GetImmutableDeletedFiles()) std::printf("in %llu\n", (unsigned long long)del.first);
   for (const auto &level_files : out_edit.GetImmutableNewFiles())
     for (const auto &m : level_files)
       std::printf("out %s %llu %s %s\n", m->filename.c_str(), (unsigned long long)m->file_size,
                   Hex(m->smallest_key).c_str(), Hex(m->largest_key).c_str());
+  std::printf("time %.6f\n", secs); // PickCompact wall time (inputs opened, merged, outputs written + fsync'd)
   std::fflush(stdout);
   _exit(ok ? 0 : 1);
 }

@@ -109,6 +109,22 @@ def test_unmodified_compact_cc_gpu_decode_and_encode(tmp_path, name):
     ins = None
     r = subprocess.run(args, capture_output=True, text=True, timeout=540)
     assert r.returncode == 0, r.stderr[-2000:]
+    if name in TIMED:  # the same PickCompact as written (CPU decode + encode) and the pageable-staging A/B
+        t_gpu = pick_time(r.stdout)
+        env = dict(os.environ, GLIBC_TUNABLES=G.NO_TRIM)
+        times = {}
+        for tag, exe, extra in (("reference_as_written", REF_EXE, {}), ("dropin_pageable", EXE,
+                                                                          {"SSTC_DROPIN_PAGEABLE": "1"})):
+            if not os.path.exists(exe):
+                continue
+            d = tmp_path / f"db_{tag}"
+            d.mkdir()
+            rr = subprocess.run([exe, str(d)] + args[2:], capture_output=True, text=True, timeout=540,
+                                env=dict(env, **extra))
+            assert rr.returncode == 0, (tag, rr.stderr[-1000:])
+            times[tag] = pick_time(rr.stdout)
+        print(f"TIMING {name}: PickCompact with drop-in GPU decode + encode {t_gpu:.3f} s; " +
+              "; ".join(f"{k} {v:.3f} s" for k, v in times.items()), flush=True)
     picked, outs = G.parse_pick_output(r.stdout)
     assert picked == list(range(1, len(case["inputs"]) + 1))
     got = []
@@ -119,6 +135,13 @@ def test_unmodified_compact_cc_gpu_decode_and_encode(tmp_path, name):
     assert got == [(o["sha256"], o["file_size"]) for o in case["fixed_outputs"]]
     print(f"{name}: db/compact.cc + db/merge_iterator.cc unchanged, GPU decode + GPU encode -> "
           f"{len(outs)} outputs equal to the reference's", flush=True)
+
+
+TIMED = ("config3", "config4_rank0", "config5")
+
+
+def pick_time(stdout):
+    return float(next(ln.split()[1] for ln in stdout.splitlines() if ln.startswith("time ")))
 
 
 def run_loop(exe, tmp_path, files, T, limit, base, tag):
