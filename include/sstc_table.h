@@ -65,6 +65,14 @@ using BlockSize = uint64_t;
  * from pool threads, one TableBuilder per thread: db/db_impl.cc:354-362). */
 sstc_ctx *ThreadContext();
 
+/* Page-locked buffers a HostVec outgrew: hipHostFree synchronises the whole
+ * device, so a builder that grows its arrays during AddEntry hands the old
+ * ones here and they are freed at the end of the thread's next Finish() (which
+ * synchronises its own stream anyway) or at thread exit, never between two
+ * AddEntry calls while other threads' builders run. */
+void DeferHostFree(void *p, int pinned);
+void FlushDeferredHostFrees();
+
 /* Growable host array for the builder's pending records: storage from
  * sstc_host_alloc (pinned, so Finish() copies it to the GPU without a pack
  * copy; pageable when pinning fails).  A TableBuilder takes its arrays from a
@@ -106,7 +114,7 @@ private:
     T *q = static_cast<T *>(sstc_host_alloc(c * sizeof(T), &pinned));
     if (!q) throw std::bad_alloc();
     if (n_) std::memcpy(q, p_, n_ * sizeof(T));
-    if (p_) sstc_host_free(p_, pinned_);
+    if (p_) DeferHostFree(p_, pinned_);
     p_ = q;
     cap_ = c;
     pinned_ = pinned;

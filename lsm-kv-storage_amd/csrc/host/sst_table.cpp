@@ -147,6 +147,29 @@ struct BuilderArena {
 };
 
 namespace {
+struct DeferredFrees {
+  std::vector<std::pair<void *, int>> bufs;
+  void flush() {
+    for (auto &[p, pinned] : bufs) sstc_host_free(p, pinned);
+    bufs.clear();
+  }
+  ~DeferredFrees() { flush(); }
+};
+thread_local DeferredFrees g_deferred;
+} // namespace
+
+void DeferHostFree(void *p, int pinned) {
+  if (!p) return;
+  if (!pinned) {
+    sstc_host_free(p, pinned); // pageable: free() does not touch the device
+    return;
+  }
+  g_deferred.bufs.emplace_back(p, pinned);
+}
+
+void FlushDeferredHostFrees() { g_deferred.flush(); }
+
+namespace {
 // per-thread pool of builder arenas: a finished builder's pinned, faulted-in
 // arrays are the next builder's (the flush / compaction threads build SST
 // after SST; round 2 spent most of AddEntries in first-touch page faults)
@@ -160,10 +183,18 @@ BuilderArena *take_arena() {
   return a;
 }
 
+// a surplus arena's pinned arrays are freed with the thread's deferred frees
+// (at its next Finish or exit), not in the destructor of the builder that
+// returned it
+struct SurplusArenas {
+  std::vector<std::unique_ptr<BuilderArena>> v;
+};
+thread_local SurplusArenas g_surplus;
+
 void give_arena(BuilderArena *a) {
   a->clear();
   if (g_arenas.size() < kArenaPool) g_arenas.emplace_back(a);
-  else delete a;
+  else g_surplus.v.emplace_back(a);
 }
 } // namespace
 
@@ -387,6 +418,9 @@ void TableBuilder::Finish() {
   if (!pwrite_all(fd_, h, file_bytes, 0)) throw std::runtime_error("Error when flushing sstable"); // table_builder.cc:155-170
   current_offset_ = file_bytes;
   if (::fsync(fd_) < 0) throw std::runtime_error("fsync failed");
+  // the stream is idle here: free what this thread's builders outgrew
+  g_surplus.v.clear();
+  FlushDeferredHostFrees();
 }
 
 // ----------------------------------------------------------------- TableReader

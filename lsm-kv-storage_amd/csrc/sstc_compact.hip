@@ -1322,45 +1322,53 @@ __global__ __launch_bounds__(256) void ck_pack_kernel(Words w, const uint64_t *a
   if (threadIdx.x == 0) __hip_atomic_store(out + flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// run starts (record index of every input table's first block) to the device
-// (fetched to the host by the pack kernel); thread 0 also snapshots the context's decode
-// error counter and clears the unsorted count for this job; workgroup 0 sums
-// the count kernel's per-workgroup block byte sums into *in_bytes
-__global__ __launch_bounds__(256) void ck_run_starts_kernel(const uint64_t *rec_base, const uint64_t *tfb, uint64_t n,
-                                                            uint64_t *out, const unsigned long long *err_count,
-                                                            uint64_t *errs, unsigned long long *bad,
-                                                            unsigned long long *guard, const uint64_t *len_part,
-                                                            uint64_t nparts, uint64_t *in_bytes) {
-  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (blockIdx.x == 0) { // the count kernel's per-workgroup {byte sum, source end} pairs
-    __shared__ uint64_t s_part[256 / kWave], s_end[256 / kWave];
-    uint64_t v = 0, e = 0;
-    for (uint64_t p = threadIdx.x; p < nparts; p += 256) {
-      v += len_part[2 * p];
-      e = len_part[2 * p + 1] > e ? len_part[2 * p + 1] : e;
-    }
-    v = wave_sum_u64(v);
-    for (uint32_t d = kWave / 2; d > 0; d >>= 1) {
-      const uint64_t y = __shfl_xor(e, d, kWave);
-      e = y > e ? y : e;
-    }
-    if (lane_id() == 0) {
-      s_part[threadIdx.x / kWave] = v;
-      s_end[threadIdx.x / kWave] = e;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      static_assert(256 / kWave == 4, "the count kernel's per-wave partials: four wave64s");
-      *in_bytes = s_part[0] + s_part[1] + s_part[2] + s_part[3];
-      for (uint32_t w = 1; w < 256 / kWave; w++) e = s_end[w] > e ? s_end[w] : e;
-      *errs = *err_count;
-      *bad = 0;
-      guard[0] = 0; // consistency-guard bits
-      guard[1] = e; // the end of the source bytes the input blocks span
-      for (int g = 0; g < 9; g++) guard[32 + 32 * g] = 0; // ck_check_blocks_kernel's tickets
-    }
+// The job's first host hand-off in ONE kernel (round 5: it replaced a
+// tfb copy command, a run-starts kernel and a pack kernel): run starts (record
+// index of every input table's first block, tfb read from the pinned upload
+// words) to the device and, with the input block bytes, to the pinned host
+// words, then the sequence word the host spins on.  Thread 0 also snapshots
+// the context's decode error counter and clears the job's unsorted count,
+// guard bits and the check kernel's tickets.  One workgroup: every host word
+// is stored before the fence that precedes the sequence word.
+__global__ __launch_bounds__(256) void ck_start_kernel(const uint64_t *rec_base, const uint64_t *tfb, uint64_t n,
+                                                       uint64_t *out, const unsigned long long *err_count,
+                                                       uint64_t *errs, unsigned long long *bad,
+                                                       unsigned long long *guard, const uint64_t *len_part,
+                                                       uint64_t nparts, uint64_t *host, uint64_t seq, uint64_t flag) {
+  __shared__ uint64_t s_part[256 / kWave], s_end[256 / kWave];
+  uint64_t v = 0, e = 0;
+  for (uint64_t p = threadIdx.x; p < nparts; p += 256) { // the count kernel's per-workgroup {byte sum, source end}
+    v += len_part[2 * p];
+    e = len_part[2 * p + 1] > e ? len_part[2 * p + 1] : e;
   }
-  if (i < n) out[i] = rec_base[tfb[i]];
+  v = wave_sum_u64(v);
+  for (uint32_t d = kWave / 2; d > 0; d >>= 1) {
+    const uint64_t y = __shfl_xor(e, d, kWave);
+    e = y > e ? y : e;
+  }
+  if (lane_id() == 0) {
+    s_part[threadIdx.x / kWave] = v;
+    s_end[threadIdx.x / kWave] = e;
+  }
+  for (uint64_t i = threadIdx.x; i < n; i += 256) {
+    const uint64_t r = rec_base[tfb[i]];
+    out[i] = r;
+    host[1 + i] = r;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    static_assert(256 / kWave == 4, "the count kernel's per-wave partials: four wave64s");
+    host[0] = s_part[0] + s_part[1] + s_part[2] + s_part[3]; // input block bytes
+    for (uint32_t w = 1; w < 256 / kWave; w++) e = s_end[w] > e ? s_end[w] : e;
+    *errs = *err_count;
+    *bad = 0;
+    guard[0] = 0; // consistency-guard bits
+    guard[1] = e; // the end of the source bytes the input blocks span
+    for (int g = 0; g < 9; g++) guard[32 + 32 * g] = 0; // ck_check_blocks_kernel's tickets
+  }
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(host + flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // pinned, device-mapped, coherent host words: kernels store the job's few
@@ -1409,6 +1417,21 @@ void ensure_up(Arena &arena, uint64_t bytes) {
 // last instead of a stream synchronize (each of the job's mid-job syncs cost
 // ~20-35 us of idle GPU with hipStreamSynchronize); `complete` also waits for
 // the stream to drain (the job's last fetch: the call returns with its work done)
+// the host side of a hand-off: spin until the kernel's sequence word lands
+void wait_seq(Arena &arena, hipStream_t s, uint64_t flag, uint64_t seq) {
+  for (uint64_t it = 1;; it++) {
+    if (__atomic_load_n(arena.host + flag, __ATOMIC_ACQUIRE) == seq) return;
+    if ((it & 255) == 0) { // a failed stream never stores the word
+      const hipError_t q = hipStreamQuery(s);
+      if (q == hipSuccess) {
+        if (__atomic_load_n(arena.host + flag, __ATOMIC_ACQUIRE) == seq) return;
+        throw std::runtime_error("pack kernel finished without its sequence word");
+      }
+      if (q != hipErrorNotReady) throw std::runtime_error(hipGetErrorString(q));
+    }
+  }
+}
+
 void fetch(Arena &arena, hipStream_t s, std::initializer_list<const uint64_t *> src, const uint64_t *arr = nullptr,
            uint64_t narr = 0, bool complete = false) {
   ensure_host(arena, 8 + narr + 1);
@@ -1421,17 +1444,7 @@ void fetch(Arena &arena, hipStream_t s, std::initializer_list<const uint64_t *> 
     CK(hipStreamSynchronize(s));
     return;
   }
-  for (uint64_t it = 1;; it++) {
-    if (__atomic_load_n(arena.host + flag, __ATOMIC_ACQUIRE) == seq) return;
-    if ((it & 255) == 0) { // a failed stream never stores the word
-      const hipError_t q = hipStreamQuery(s);
-      if (q == hipSuccess) {
-        if (__atomic_load_n(arena.host + flag, __ATOMIC_ACQUIRE) == seq) return;
-        throw std::runtime_error("pack kernel finished without its sequence word");
-      }
-      if (q != hipErrorNotReady) throw std::runtime_error(hipGetErrorString(q));
-    }
-  }
+  wait_seq(arena, s, flag, seq);
 }
 
 } // namespace
@@ -1456,23 +1469,31 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     uint64_t *rb_all = pool.get<uint64_t>(nblocks + 1);
     uint64_t *ws = pool.get<uint64_t>(nws);
     uint64_t *errs = pool.get<uint64_t>(2);
-    uint64_t *d_tfb = pool.get<uint64_t>(ntables + 1), *d_rs = pool.get<uint64_t>(ntables + 1);
+    uint64_t *d_rs = pool.get<uint64_t>(ntables + 1);
     const uint64_t nparts = (nblocks + 255) / 256;
-    uint64_t *len_part = pool.get<uint64_t>(2 * nparts + 2), *in_bytes_d = pool.get<uint64_t>(1);
+    uint64_t *len_part = pool.get<uint64_t>(2 * nparts + 2);
     CK(launch_count(d_src, d_blk_off, d_blk_len, nblocks, rb_all, s, ws, len_part));
     CK(launch_scan(rb_all, nblocks, 0, rb_all, ws, s, true));
     unsigned long long *bad = reinterpret_cast<unsigned long long *>(pool.get<uint64_t>(1));
     // consistency guard: [0] bits set by any check of the job, [1] the end of
-    // the source bytes its blocks span (both cleared by ck_run_starts_kernel)
+    // the source bytes its blocks span (both cleared by ck_start_kernel)
     // guard[0] bits, guard[1] source end; guard + 32 the check kernel's 9
     // ticket counters, 256 B apart (u32 at guard + 32 + 32 g)
     unsigned long long *guard = reinterpret_cast<unsigned long long *>(pool.get<uint64_t>(32 + 9 * 32));
     const uint64_t *src_end = reinterpret_cast<const uint64_t *>(guard + 1);
-    // record index of every input table's first record (its run start)
-    CK(hipMemcpyAsync(d_tfb, h_tfb, (ntables + 1) * 8, hipMemcpyHostToDevice, s));
-    ck_run_starts_kernel<<<grid(ntables + 1), 256, 0, s>>>(rb_all, d_tfb, ntables + 1, d_rs, err_count, errs, bad,
-                                                           guard, len_part, nparts, in_bytes_d);
-    fetch(arena, s, {in_bytes_d}, d_rs, ntables + 1);
+    // record index of every input table's first record (its run start): the
+    // table first blocks travel in the pinned upload words (no copy command),
+    // the run starts and the input bytes come back in the pinned host words
+    ensure_up(arena, (ntables + 1) * 8);
+    memcpy(arena.up, h_tfb, (ntables + 1) * 8);
+    ensure_host(arena, 8 + ntables + 2);
+    {
+      const uint64_t flag = arena.host_cap - 1, seq = ++arena.seq;
+      ck_start_kernel<<<1, 256, 0, s>>>(rb_all, reinterpret_cast<const uint64_t *>(arena.up_dev), ntables + 1, d_rs,
+                                         err_count, errs, bad, guard, len_part, nparts, arena.host_dev, seq, flag);
+      CK(hipGetLastError());
+      wait_seq(arena, s, flag, seq);
+    }
     const uint64_t in_bytes = arena.host[0]; // every survivor's entry lies in these bytes
     std::vector<uint64_t> run_start(arena.host + 1, arena.host + 2 + ntables);
     const uint64_t n = run_start[ntables];
