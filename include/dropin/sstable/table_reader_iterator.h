@@ -46,10 +46,6 @@
 #include <string_view>
 #include <vector>
 
-namespace sstc {
-struct DecodedBlocks;
-}
-
 namespace kvs {
 
 namespace sstable {
@@ -101,16 +97,25 @@ private:
   void Load();
   // the block the entry cursor runs over (CreateNewBlockReaderIterator)
   void ShowBlock(uint64_t block);
-  uint64_t EntriesInShownBlock() const;
-  bool EntryValid() const;
-  uint64_t Record() const;
+  bool EntryValid() const { return has_block_ && entry_ < shown_n_; }
+
+  // one decoded record, what the accessors read (one cache line per two
+  // records: MergeIterator walks many tables at once, and six parallel column
+  // arrays per table were six streams each)
+  struct Rec {
+    uint64_t key_off, txn;
+    uint32_t key_len, val_off; // val_off relative to key_off
+    uint32_t val_len;          // SSTC_NO_VALUE: no value fields
+    uint8_t type;
+  };
 
   // block cursor: current_block_offset_index_ of table_reader_iterator.h:64
   uint64_t current_block_offset_index_;
-  // the block an entry cursor exists for (block_reader_iterator_ != nullptr)
-  // and that cursor (BlockReaderIterator::current_offset_index_)
+  // the block an entry cursor exists for (block_reader_iterator_ != nullptr),
+  // its first record and record count, and that cursor
+  // (BlockReaderIterator::current_offset_index_)
   bool has_block_ = false;
-  uint64_t shown_block_ = 0;
+  uint64_t shown_block_ = 0, shown_first_ = 0, shown_n_ = 0;
   uint64_t entry_ = 0;
 
   const std::vector<std::unique_ptr<BlockReaderCache>> &block_reader_cache_;
@@ -119,24 +124,11 @@ private:
 
   const TableReader *table_reader_;
 
-  // the table's data section in page-locked host memory (sstc_host_alloc)
-  struct HostBytes {
-    uint8_t *p = nullptr;
-    uint64_t n = 0;
-    int pinned = 0;
-    HostBytes() = default;
-    HostBytes(const HostBytes &) = delete;
-    HostBytes &operator=(const HostBytes &) = delete;
-    ~HostBytes();
-    void reset(uint64_t bytes);
-    uint8_t *data() const { return p; }
-    uint64_t size() const { return n; }
-  };
-
   bool loaded_ = false;
-  uint64_t data_begin_ = 0;
-  HostBytes data_;
-  std::unique_ptr<sstc::DecodedBlocks> rec_;
+  std::unique_ptr<uint8_t[]> data_; // the table's data section (not zero-filled)
+  uint64_t data_size_ = 0;
+  std::vector<uint64_t> base_;    // per block: its first record
+  std::vector<Rec> rec_;
 };
 
 } // namespace sstable

@@ -854,7 +854,10 @@ __device__ __forceinline__ u32x4 funnel16(const u32x4 &v0, const u32x4 &v1, uint
 // kU = 4 (config 5 encode 232 -> 224 us); kU = 8 is
 // faster on config 5 (210 us) but its 98 VGPRs cost enc_lds_kernel<1> a wave
 // per SIMD: config 3 encode 500 -> 624 us (profiles/r02_ab/encode_ab.md)
-constexpr uint32_t kWaveSpanUnroll = 4;
+#ifndef SSTC_SPAN_U
+#define SSTC_SPAN_U 4
+#endif
+constexpr uint32_t kWaveSpanUnroll = SSTC_SPAN_U;
 template <uint32_t kU>
 __device__ __forceinline__ void copy_span_wave(uint8_t *dp, const uint8_t *sp, uint64_t len) {
   const uint32_t lane = lane_id();
@@ -1317,6 +1320,12 @@ __device__ void enc_wave_offsets(const EncArgs &a, uint64_t b) {
   __threadfence_block(); // the stores complete before any lane of the wave reads them (same CU)
 }
 
+// entry quads of the compaction encode in flight per lane (enc_copy_entries)
+#ifndef SSTC_ENC_Q
+#define SSTC_ENC_Q 4
+#endif
+constexpr uint32_t kEncCopyQ = SSTC_ENC_Q;
+
 // kMode 0: two arenas (key spans in groups of GK lanes, then value spans in
 // groups of GV, kQ span groups in flight); 1: whole-entry copy (compaction)
 template <uint32_t kMode, uint32_t GK = 2, uint32_t GV = 8, uint32_t kQ = 2>
@@ -1400,7 +1409,7 @@ __global__ __launch_bounds__(kEncWaves *kWave) void enc_lds_kernel(EncArgs a) {
       if (lane == 0) atomicOr(a.guard, kGuardBlockRange);
       return;
     }
-    if (!enc_copy_entries<4>(a, img, pad, f0, n, P0, D, b)) return;
+    if (!enc_copy_entries<kEncCopyQ>(a, img, pad, f0, n, P0, D, b)) return;
   } else {
     // mode 0 scans its entry offsets in the wave
     enc_copy_split<GK, GV, kQ>(a, img, s_dummy + threadIdx.x, pad, f0, n, 0, D, s_tbl + wave * kWave);
