@@ -1725,6 +1725,9 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     ea.need = need;
     ea.cap = dst_cap;
     ea.bmeta = bmeta; // block min / max txn (reduced by the encode kernels) and first / last key
+    // output blocks are as large as the input's on average (an entry is copied
+    // whole): past 8 KiB the job's blocks mostly exceed the encode's LDS slot
+    ea.large_blocks = nblocks && in_bytes / nblocks > 8192 ? 1u : 0u;
     ea.src_end = src_end;
     ea.guard = guard;
     CK(launch_enc_emit(ea, s));

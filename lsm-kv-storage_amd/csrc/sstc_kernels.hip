@@ -854,10 +854,7 @@ __device__ __forceinline__ u32x4 funnel16(const u32x4 &v0, const u32x4 &v1, uint
 // kU = 4 (config 5 encode 232 -> 224 us); kU = 8 is
 // faster on config 5 (210 us) but its 98 VGPRs cost enc_lds_kernel<1> a wave
 // per SIMD: config 3 encode 500 -> 624 us (profiles/r02_ab/encode_ab.md)
-#ifndef SSTC_SPAN_U
-#define SSTC_SPAN_U 4
-#endif
-constexpr uint32_t kWaveSpanUnroll = SSTC_SPAN_U;
+constexpr uint32_t kWaveSpanUnroll = 4;
 template <uint32_t kU>
 __device__ __forceinline__ void copy_span_wave(uint8_t *dp, const uint8_t *sp, uint64_t len) {
   const uint32_t lane = lane_id();
@@ -909,6 +906,7 @@ __device__ __forceinline__ void copy_span_wave(uint8_t *dp, const uint8_t *sp, u
 
 // A compaction block past the LDS slot of the enc_lds_kernel<1> wave that met
 // it: entries one after another, each copied by the 64 lanes.
+template <uint32_t kSpanU = kWaveSpanUnroll>
 __device__ bool enc_emit_block_entries_wave(const EncArgs &a, uint64_t b) {
   const uint32_t lane = lane_id();
   const uint64_t f0 = a.blk_first[b], f1 = a.blk_first[b + 1];
@@ -928,7 +926,7 @@ __device__ bool enc_emit_block_entries_wave(const EncArgs &a, uint64_t b) {
   for (uint64_t i = 0; i < n; i++) {
     const uint64_t r = f0 + i;
     const uint64_t o = a.P[r] - P0, sz = a.P[r + 1] - a.P[r];
-    copy_span_wave<kWaveSpanUnroll>(blk + o, a.key_src + a.in.key_off[r] - 5, sz - 8);
+    copy_span_wave<kSpanU>(blk + o, a.key_src + a.in.key_off[r] - 5, sz - 8);
     if (lane < 8) blk[o + sz - 8 + lane] = static_cast<uint8_t>(a.in.txn[r] >> (8 * lane));
   }
   for (uint64_t i = lane; i < n; i += kWave) {
@@ -1320,15 +1318,15 @@ __device__ void enc_wave_offsets(const EncArgs &a, uint64_t b) {
   __threadfence_block(); // the stores complete before any lane of the wave reads them (same CU)
 }
 
-// entry quads of the compaction encode in flight per lane (enc_copy_entries)
-#ifndef SSTC_ENC_Q
-#define SSTC_ENC_Q 4
-#endif
-constexpr uint32_t kEncCopyQ = SSTC_ENC_Q;
-
 // kMode 0: two arenas (key spans in groups of GK lanes, then value spans in
-// groups of GV, kQ span groups in flight); 1: whole-entry copy (compaction)
-template <uint32_t kMode, uint32_t GK = 2, uint32_t GV = 8, uint32_t kQ = 2>
+// groups of GV, kQ span groups in flight); 1: whole-entry copy (compaction),
+// kQ entry quads in flight per lane for the blocks that fit the LDS slot and
+// kU 16 B chunks per lane for the ones past it.  Mode 1 comes in two builds
+// (launch_enc_emit picks by EncArgs::large_blocks): kQ = kU = 2 needs 59 VGPRs,
+// 8 waves / SIMD (config 3 encode 525 -> 512 us, config 4 863 -> 844 us), but
+// copies large blocks slower (config 5 231 -> 255 us); kQ = kU = 4 needs 79,
+// 6 waves (profiles/r05/encode_ab.md)
+template <uint32_t kMode, uint32_t GK = 2, uint32_t GV = 8, uint32_t kQ = 2, uint32_t kU = kWaveSpanUnroll>
 __global__ __launch_bounds__(kEncWaves *kWave) void enc_lds_kernel(EncArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kEncSlotWaves * kEncSlot];
   __shared__ uint32_t s_dummy[kMode == 0 ? kEncWaves * kWave : 1]; // per-lane sink of clipped stores
@@ -1368,7 +1366,7 @@ __global__ __launch_bounds__(kEncWaves *kWave) void enc_lds_kernel(EncArgs a) {
         enc_wave_offsets(a, b);
         enc_emit_block<kWave>(a, b, img, lane); // its LDS image holds the lanes' chunk slots
       } else {
-        if (!enc_emit_block_entries_wave(a, b)) return;
+        if (!enc_emit_block_entries_wave<kU>(a, b)) return;
         if (a.bmeta) { // the block's min / max txn (table footer), reduced by the wave
           const uint64_t f0 = a.blk_first[b], f1 = a.blk_first[b + 1];
           uint64_t mn = ~0ull, mx = 0;
@@ -1409,7 +1407,7 @@ __global__ __launch_bounds__(kEncWaves *kWave) void enc_lds_kernel(EncArgs a) {
       if (lane == 0) atomicOr(a.guard, kGuardBlockRange);
       return;
     }
-    if (!enc_copy_entries<kEncCopyQ>(a, img, pad, f0, n, P0, D, b)) return;
+    if (!enc_copy_entries<kQ>(a, img, pad, f0, n, P0, D, b)) return;
   } else {
     // mode 0 scans its entry offsets in the wave
     enc_copy_split<GK, GV, kQ>(a, img, s_dummy + threadIdx.x, pad, f0, n, 0, D, s_tbl + wave * kWave);
@@ -2462,7 +2460,8 @@ hipError_t launch_enc_emit(const EncArgs &a, hipStream_t s) {
   // (4, 8, 2) / (2, 8, 1) / (4, 8, 4) / (2, 8, 4) and the single pass over
   // (key, value) span pairs were slower (profiles/r02_ab/encode_ab.md)
   if (!a.entries_in_src) enc_lds_kernel<0><<<g, kEncWaves * kWave, 0, s>>>(a);
-  else enc_lds_kernel<1><<<g, kEncWaves * kWave, 0, s>>>(a);
+  else if (a.large_blocks) enc_lds_kernel<1, 2, 8, 4, 4><<<g, kEncWaves * kWave, 0, s>>>(a);
+  else enc_lds_kernel<1, 2, 8, 2, 2><<<g, kEncWaves * kWave, 0, s>>>(a);
   // blocks past an LDS slot are encoded by the wave that met them (a listed
   // pass by a workgroup per block was slower: Zipf set 329 -> 236 us, config 5
   // 319 -> 233 us; profiles/r02_ab/)

@@ -85,6 +85,9 @@ struct EncArgs {
   uint8_t *dst;
   uint32_t entries_in_src = 0; // records decoded from blocks in key_src (== val_src)
   uint32_t xcd = 0;
+  // mode 1: most blocks are past the LDS slot (the build with wider copies,
+  // launch_enc_emit); 0: most fit it (the 8-waves-per-SIMD build)
+  uint32_t large_blocks = 0;
   // optional (compaction, entries_in_src): per block 4 words -- min txn, max
   // txn (table footer, table_builder.cc:47-49), and the first / last entry's
   // key offset | key length << 40 (meta entries, AddIndexBlockEntry): one
