@@ -73,6 +73,12 @@ sstc_ctx *ThreadContext();
 void DeferHostFree(void *p, int pinned);
 void FlushDeferredHostFrees();
 
+/* SSTC_TRACE_HOST=1 in the environment: phase times of the host-side paths
+ * on stderr (diagnostics; off by default) */
+bool TraceHostOn();
+double TraceNowMs();
+void TraceHost(const char *what, double ms);
+
 /* Growable host array for the builder's pending records: storage from
  * sstc_host_alloc (pinned, so Finish() copies it to the GPU without a pack
  * copy; pageable when pinning fails).  A TableBuilder takes its arrays from a

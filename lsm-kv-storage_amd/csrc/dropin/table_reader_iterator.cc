@@ -49,6 +49,8 @@ TableReaderIterator::~TableReaderIterator() { lru_table_item_->Unref(); }
 
 void TableReaderIterator::Load() {
   if (loaded_) return;
+  const bool tr = sstc::TraceHostOn();
+  const double t0 = tr ? sstc::TraceNowMs() : 0;
   const std::vector<BlockIndex> &index = table_reader_->block_index_;
   const uint64_t nb = index.size();
   // the data section: every block the meta section lists, read with the
@@ -71,6 +73,7 @@ void TableReaderIterator::Load() {
       throw std::runtime_error("TableReaderIterator: cannot read the data section of " + table_reader_->filename_);
     done += static_cast<uint64_t>(r);
   }
+  const double t1 = tr ? sstc::TraceNowMs() : 0;
   std::vector<uint64_t> off(nb), len(nb);
   for (uint64_t b = 0; b < nb; b++) {
     off[b] = index[b].GetBlockStartOffset() - lo;
@@ -87,6 +90,7 @@ void TableReaderIterator::Load() {
     if (d.status[b] != SSTC_BLK_OK)
       throw std::runtime_error("TableReaderIterator: corrupt block " + std::to_string(b) + " in " +
                                table_reader_->filename_ + " (SSTC_BLK code " + std::to_string(d.status[b]) + ")");
+  const double t2 = tr ? sstc::TraceNowMs() : 0;
   const uint64_t n = d.type.size();
   rec_.resize(n);
   for (uint64_t i = 0; i < n; i++) {
@@ -100,6 +104,11 @@ void TableReaderIterator::Load() {
   }
   base_ = std::move(d.base);
   loaded_ = true;
+  if (tr) {
+    sstc::TraceHost("iterator read data section", t1 - t0);
+    sstc::TraceHost("iterator GPU decode (H2D, count, decode, D2H)", t2 - t1);
+    sstc::TraceHost("iterator record table", sstc::TraceNowMs() - t2);
+  }
 }
 
 void TableReaderIterator::ShowBlock(uint64_t block) {

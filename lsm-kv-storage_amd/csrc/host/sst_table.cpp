@@ -14,6 +14,8 @@
 #include <unistd.h>
 
 #include <cerrno>
+#include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -108,9 +110,36 @@ bool sync(sstc_ctx *ctx) { return hipStreamSynchronize(stream_of(ctx)) == hipSuc
 
 } // namespace
 
+namespace {
+// SSTC_TRACE_HOST=1: host-side phase times on stderr (diagnostics of the C++
+// drop-in paths; off by default)
+bool trace_host() {
+  static const bool on = std::getenv("SSTC_TRACE_HOST") != nullptr;
+  return on;
+}
+double now_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+thread_local double g_pin_ms = 0;
+thread_local uint64_t g_pin_bytes = 0, g_pin_calls = 0;
+} // namespace
+
+void TraceHost(const char *what, double ms) {
+  if (trace_host()) std::fprintf(stderr, "[sstc] %s %.3f ms\n", what, ms);
+}
+bool TraceHostOn() { return trace_host(); }
+double TraceNowMs() { return now_ms(); }
+
 extern "C" void *sstc_host_alloc(uint64_t bytes, int *pinned) {
   void *p = nullptr;
-  if (bytes && hipHostMalloc(&p, bytes, hipHostMallocPortable) == hipSuccess) {
+  const double t0 = trace_host() ? now_ms() : 0;
+  const bool ok = bytes && hipHostMalloc(&p, bytes, hipHostMallocPortable) == hipSuccess;
+  if (trace_host()) {
+    g_pin_ms += now_ms() - t0;
+    g_pin_bytes += bytes;
+    g_pin_calls++;
+  }
+  if (ok) {
     if (pinned) *pinned = 1;
     return p;
   }
@@ -347,6 +376,7 @@ uint64_t align256(uint64_t x) { return (x + 255) & ~uint64_t(255); }
 
 void TableBuilder::Finish() {
   if (fd_ < 0) throw std::runtime_error("TableBuilder::Finish: file not open");
+  const double t_begin = trace_host() ? now_ms() : 0;
   FlushBlock();
   const uint64_t n = type_.size();
   const uint64_t nb = blk_first_.size() - 1;
@@ -421,6 +451,11 @@ void TableBuilder::Finish() {
   // the stream is idle here: free what this thread's builders outgrew
   g_surplus.v.clear();
   FlushDeferredHostFrees();
+  if (trace_host())
+    std::fprintf(stderr, "[sstc] Finish %llu records %llu B: %.3f ms; page-locked allocs so far %llu calls %llu B %.3f ms\n",
+                 static_cast<unsigned long long>(type_.size()), static_cast<unsigned long long>(file_bytes),
+                 now_ms() - t_begin, static_cast<unsigned long long>(g_pin_calls),
+                 static_cast<unsigned long long>(g_pin_bytes), g_pin_ms);
 }
 
 // ----------------------------------------------------------------- TableReader
