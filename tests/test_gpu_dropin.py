@@ -116,7 +116,8 @@ def test_unmodified_compact_cc_gpu_decode_and_encode(tmp_path, name):
         rr = subprocess.run([REF_EXE, str(d)] + args[2:], capture_output=True, text=True, timeout=540,
                             env=dict(os.environ, GLIBC_TUNABLES=G.NO_TRIM))  # config 5 as written needs the heap mapped
         assert rr.returncode == 0, rr.stderr[-1000:]
-        print(f"TIMING {name}: PickCompact with the drop-in GPU decode + encode {t_gpu:.3f} s, "
+        print(f"TIMING {name}: PickCompact with the drop-in GPU decode + encode {t_gpu:.3f} s "
+              f"(codec context opened before it in {pick_time(r.stdout, 'init'):.3f} s), "
               f"the reference as written {pick_time(rr.stdout):.3f} s", flush=True)
     picked, outs = G.parse_pick_output(r.stdout)
     assert picked == list(range(1, len(case["inputs"]) + 1))
@@ -133,8 +134,8 @@ def test_unmodified_compact_cc_gpu_decode_and_encode(tmp_path, name):
 TIMED = ("config3", "config4_rank0", "config5")
 
 
-def pick_time(stdout):
-    return float(next(ln.split()[1] for ln in stdout.splitlines() if ln.startswith("time ")))
+def pick_time(stdout, tag="time"):
+    return float(next(ln.split()[1] for ln in stdout.splitlines() if ln.startswith(tag + " ")))
 
 
 def run_loop(exe, tmp_path, files, T, limit, base, tag):

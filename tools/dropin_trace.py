@@ -44,7 +44,7 @@ def main():
         cmd += [p, str(fs), lo.hex() or "-", hi.hex() or "-"]
     codec.close()
     r = subprocess.run(cmd, capture_output=True, text=True, env=dict(os.environ, SSTC_TRACE_HOST="1"))
-    print("rc", r.returncode, "time", [ln for ln in r.stdout.splitlines() if ln.startswith("time")])
+    print("rc", r.returncode, [ln for ln in r.stdout.splitlines() if ln.startswith(("time", "init"))])
     tot = collections.defaultdict(float)
     cnt = collections.Counter()
     last = ""
