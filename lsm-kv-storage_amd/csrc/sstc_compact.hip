@@ -722,7 +722,7 @@ __device__ __forceinline__ uint64_t data_bytes(uint32_t kl, uint32_t vl) {
 // flags + tile sums, a scan of the tile sums, compaction): a tile of kFfRows
 // rows keeps its survivors' fields in registers, publishes its three totals
 // (kept records, key+value bytes, entry bytes) through decoupled look-back
-// (one wave per total; ws = [ticket, status[3][tiles]], cleared before the
+// (one wave per total; ws = [unused, status[3][tiles]], cleared before the
 // launch), then writes the survivors row by row at their global positions.
 // The merged keys and the side records are read once.
 constexpr uint32_t kFfRows = 8, kFfTile = kFtThreads * kFfRows;
@@ -792,8 +792,8 @@ __global__ __launch_bounds__(kFtThreads) void ck_filter_kernel(const SK *s, uint
                                                                uint64_t *Pe, uint64_t *ws, uint64_t *totals,
                                                                Abort stop, unsigned long long *guard,
                                                                uint32_t txn_mode) {
-  __shared__ uint64_t s_tile, s_pre[3];
-  if (stop()) { // uniform over the grid: no ticket drawn, the host rejects the job
+  __shared__ uint64_t s_pre[3];
+  if (stop()) { // uniform over the grid: no status published, the host rejects the job
     if (blockIdx.x == 0 && threadIdx.x == 0) { // no survivor: the layout below splits nothing, writes nothing
       totals[0] = totals[1] = totals[2] = 0;
       Pd[0] = Pe[0] = 0;
@@ -801,57 +801,59 @@ __global__ __launch_bounds__(kFtThreads) void ck_filter_kernel(const SK *s, uint
     return;
   }
   const uint32_t tid = threadIdx.x, lane = lane_id(), w = tid / kWave;
-  if (tid == 0) {
-    const uint64_t t = __hip_atomic_fetch_add(ws, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (t + 1 == gridDim.x) __hip_atomic_store(ws, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_tile = t;
-  }
-  __syncthreads();
-  const uint64_t tile = s_tile, t0 = tile * kFfTile;
-  constexpr uint32_t kGroup = 4; // rows whose loads are in flight together
+  // tile = workgroup id: workgroups are dispatched in id order (per XCD, in
+  // order), so the lowest unfinished tile is always resident and its
+  // look-back only waits on finished tiles; a drawn ticket cost 6-20 us
+  // (one device-scope atomic per tile, profiles/r05/filter_ab.md)
+  const uint64_t tile = blockIdx.x, t0 = tile * kFfTile;
   uint32_t km = 0, kl[kFfRows], vl[kFfRows], ty[kFfRows];
   uint64_t tx[kFfRows], ko[kFfRows];
+  // every row's merged keys and side records in flight together; a record's
+  // predecessor is the lane before it (shuffled), a wave's first lane takes
+  // the last lane of the wave before it in merge order through LDS
+  // (s_edge[4 j + w]; [0] = the record before the tile).  Round 4 loaded
+  // every predecessor again and issued the rows in two dependent groups.
+  __shared__ SK s_edge[kFfRows * (kFtThreads / kWave) + 1];
+  {
+    SK x[kFfRows];
+    RecX rr[kFfRows];
 #pragma unroll
-  for (uint32_t j0 = 0; j0 < kFfRows; j0 += kGroup) {
-    SK x[kGroup], pv[kGroup];
-#pragma unroll
-    for (uint32_t g = 0; g < kGroup; g++) { // row j: records t0 + 256 j + [0, 256), lane-consecutive
-      const uint64_t i = t0 + static_cast<uint64_t>(j0 + g) * kFtThreads + tid;
-      const uint64_t ic = i < n ? i : n - 1; // clamped, unconditional: the loads stay in flight together
-      x[g] = s[ic];
-      pv[g] = s[ic ? ic - 1 : 0];
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    RecX rr[kGroup];
-    bool bad_id = false; // a merged record id out of range (never, unless the merge is wrong)
-#pragma unroll
-    for (uint32_t g = 0; g < kGroup; g++) {
-      bad_id |= x[g].id >= n || pv[g].id >= n;
-      rr[g] = kv.rx[x[g].id < n ? x[g].id : 0u]; // unconditional (past n: the last record's)
-    }
-    if (__any(bad_id)) { // no key compare may follow such an id: the job is rejected
-      if (lane == 0) atomicOr(guard, kGuardMergeId);
-      for (uint32_t g = 0; g < kGroup; g++) {
-        x[g].id = pv[g].id = 0;
-        x[g].kl &= ~kSkRead; // and no source read for them
-      }
-    }
-    uint64_t tread[kGroup]; // txns as read (a merge txn lowered by its group: re-read, rare)
-#pragma unroll
-    for (uint32_t g = 0; g < kGroup; g++)
-      tread[g] = x[g].kl & kSkRead ? read_txn(kv, rr[g], x[g].kl & ~kSkRead, txn_mode) : x[g].tx;
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (uint32_t g = 0; g < kGroup; g++) {
-      const uint32_t j = j0 + g;
+    for (uint32_t j = 0; j < kFfRows; j++) {
       const uint64_t i = t0 + static_cast<uint64_t>(j) * kFtThreads + tid;
-      const uint32_t k = i < n ? ff_keep(s, i, x[g], pv[g], rr[g].type, base_level, kv, n, tread[g]) : 0u;
+      x[j] = s[i < n ? i : n - 1]; // clamped, unconditional: the loads stay in flight together
+    }
+    if (tid == 0) s_edge[0] = s[t0 ? t0 - 1 : 0]; // (t0 < n: a tile starts below n)
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (uint32_t j = 0; j < kFfRows; j++) {
+      rr[j] = kv.rx[x[j].id < n ? x[j].id : 0u]; // unconditional (past n: the first record's)
+      if (lane == kWave - 1) s_edge[1 + j * (kFtThreads / kWave) + w] = x[j];
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t j = 0; j < kFfRows; j++) {
+      const uint64_t i = t0 + static_cast<uint64_t>(j) * kFtThreads + tid;
+      SK pv;
+      pv.p0 = __shfl_up(x[j].p0, 1u, kWave);
+      pv.p1 = __shfl_up(x[j].p1, 1u, kWave);
+      pv.tx = __shfl_up(x[j].tx, 1u, kWave);
+      pv.kl = __shfl_up(x[j].kl, 1u, kWave);
+      pv.id = __shfl_up(x[j].id, 1u, kWave);
+      if (lane == 0) pv = s_edge[j * (kFtThreads / kWave) + w];
+      if (__any(x[j].id >= n || pv.id >= n)) { // no key compare may follow such an id: the job is rejected
+        if (lane == 0) atomicOr(guard, kGuardMergeId);
+        x[j].id = pv.id = 0;
+        x[j].kl &= ~kSkRead; // and no source read for it
+      }
+      // the txn as read (a merge txn lowered by its group: re-read, rare)
+      const uint64_t tread = x[j].kl & kSkRead ? read_txn(kv, rr[j], x[j].kl & ~kSkRead, txn_mode) : x[j].tx;
+      const uint32_t k = i < n ? ff_keep(s, i, x[j], pv, rr[j].type, base_level, kv, n, tread) : 0u;
       km |= k << j;
-      kl[j] = x[g].kl & ~kSkRead;
-      tx[j] = tread[g];
-      vl[j] = rr[g].vl;
-      ty[j] = rr[g].type;
-      ko[j] = rr[g].ko;
+      kl[j] = x[j].kl & ~kSkRead;
+      tx[j] = tread;
+      vl[j] = rr[j].vl;
+      ty[j] = rr[j].type;
+      ko[j] = rr[j].ko;
     }
   }
   // per row and wave: kept count and the two byte sums, exchanged once

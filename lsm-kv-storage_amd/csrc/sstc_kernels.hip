@@ -1464,8 +1464,7 @@ struct SegW { // W(x) from an LDS window [base, base + n) or from HBM
 // when the threshold is not reached before the clamp (the bisection then ends
 // at lim - 1 by itself: W is monotone).  Every e < from (>= i) is known to
 // fail: galloping starts there.
-__device__ uint64_t seg_next_at(const SegW &W, uint64_t i, uint64_t lim, uint64_t threshold, uint64_t from) {
-  const uint64_t target = W(i) + threshold;
+__device__ uint64_t seg_next_to(const SegW &W, uint64_t target, uint64_t lim, uint64_t from) {
   uint64_t lo = from, hi = lim - 1;
   for (uint64_t span = 1;; span <<= 1) {
     const uint64_t e = from + span - 1;
@@ -1483,11 +1482,15 @@ __device__ uint64_t seg_next_at(const SegW &W, uint64_t i, uint64_t lim, uint64_
   }
   return lo + 1;
 }
+__device__ __forceinline__ uint64_t seg_next_at(const SegW &W, uint64_t i, uint64_t lim, uint64_t threshold,
+                                                uint64_t from) {
+  return seg_next_to(W, W(i) + threshold, lim, from);
+}
 
 struct SegArgs {
   const uint64_t *Pw;
   uint64_t add, m, threshold;
-  const uint64_t *ends, *nends; // optional clamp: ends[0..*nends], ends[*nends] = m
+  const uint64_t *ends, *nends; // optional clamp: ends[0..*nends], ends[*nends] = m; ends holds >= m + 1 words
   uint32_t *J0, *Fx, *Fc; // by record
   uint64_t *win;          // per tile: entry-window size (scanned into node bases)
   uint64_t *first, *d_count;
@@ -1517,6 +1520,15 @@ __global__ __launch_bounds__(kChThreads) void seg_walk_kernel(SegArgs a) {
     const uint32_t x = tid + r * kChThreads;
     v[r] = x < nlh ? a.Pw[c0 + x] : 0;
   }
+  // in the same round trip: W(c0 - 1) for the entry window (thread 255), and
+  // the table-end count with the first 64 ends (wave 0: the search below
+  // starts from them when there are at most 63 ends, else it reloads)
+  const uint64_t wprev = tid == kChThreads - 1 && c0 ? a.Pw[c0 - 1] + a.add * (c0 - 1) : 0;
+  uint64_t ne_ld = 0, e_ld = 0;
+  if (a.ends && tid < kWave) {
+    ne_ld = *a.nends;
+    e_ld = a.ends[tid < a.m ? tid : a.m];
+  }
   const uint64_t m = a.mp ? *a.mp : a.m;
   if (tid == 0) {
     a.tentry[blockIdx.x] = 0;
@@ -1537,7 +1549,7 @@ __global__ __launch_bounds__(kChThreads) void seg_walk_kernel(SegArgs a) {
     // workgroup's critical path); its last round leaves ends[t0 - 1 ..] in
     // the lanes, cached in LDS for the clamps below
     const uint32_t lane = tid;
-    const uint64_t ne = *a.nends;
+    const uint64_t ne = ne_ld;
     uint64_t lo = 0, n = ne + 1, below = 0, e = 0; // answer in [lo, lo + n); ends[lo - 1] = below
     uint32_t f = 0;
     for (;;) {
@@ -1546,7 +1558,10 @@ __global__ __launch_bounds__(kChThreads) void seg_walk_kernel(SegArgs a) {
       const uint64_t step = n <= kWave ? 1 : (n - 2) / (kWave - 1) + 1;
       const uint64_t off = static_cast<uint64_t>(lane) * step;
       const uint64_t x = step == 1 ? (lo + lane < ne ? lo + lane : ne) : lo + (off < n - 1 ? off : n - 1);
-      e = a.ends[x];
+      if (lo == 0 && n <= kWave) // the first round of <= 64 ends: the loads above (x = min(lane, ne))
+        e = lane <= ne ? e_ld : readlane_u64(e_ld, static_cast<uint32_t>(ne));
+      else
+        e = a.ends[x];
       const uint64_t gt = __ballot(e > c0); // a suffix of the lanes, lane min(n - 1, 63) at least
       // (never empty; a corrupt end list must not turn f into ~0 and send the
       // next round's loads out of range)
@@ -1587,7 +1602,7 @@ __global__ __launch_bounds__(kChThreads) void seg_walk_kernel(SegArgs a) {
     uint64_t lim = m;
     if (a.ends) // first end > c0 - 1: t0, or the one before it when it equals c0
       lim = t0 > 0 && end_at(t0 - 1) == c0 ? c0 : end_at(t0);
-    s_wend = blockIdx.x ? seg_next_at(W, i, lim, a.threshold, i) : c0;
+    s_wend = blockIdx.x ? seg_next_to(W, wprev + a.threshold, lim, i) : c0;
   }
   // J0 of kPer consecutive records per thread: gallop for the first, then from
   // the previous answer (J0 is monotone within an output table)
@@ -1766,18 +1781,22 @@ __global__ __launch_bounds__(kChThreads) void seg_emit_kernel(const uint32_t *J0
   __shared__ uint8_t mk[kChTile];
   __shared__ uint32_t s_wsum[kChThreads / kWave];
   const uint64_t k = blockIdx.x;
-  const uint32_t e = tentry[k];
-  if (!e) return; // a segment spans the whole tile (or the tile is past the device count)
-  if (mp) m = *mp;
-  const uint64_t c0 = k * kChTile, c1 = c0 + kChTile < m ? c0 + kChTile : m;
-  const uint32_t len = static_cast<uint32_t>(c1 - c0), tid = threadIdx.x;
-  {
-    uint32_t v[kPer];
+  const uint64_t c0 = k * kChTile;
+  const uint32_t tid = threadIdx.x;
+  // the tile's J0 goes out on the host bound m (J0 holds m + 1 words) with the
+  // entry and the device count: one round trip instead of three
+  uint32_t v[kPer];
 #pragma unroll
-    for (uint32_t r = 0; r < kPer; r++) {
-      const uint32_t p = tid + r * kChThreads;
-      v[r] = J0[c0 + (p < len ? p : len - 1)];
-    }
+  for (uint32_t r = 0; r < kPer; r++) {
+    const uint64_t x = c0 + tid + r * kChThreads;
+    v[r] = J0[x < m ? x : m];
+  }
+  const uint32_t e = tentry[k];
+  if (mp) m = *mp;
+  if (!e) return; // a segment spans the whole tile (or the tile is past the device count)
+  const uint64_t c1 = c0 + kChTile < m ? c0 + kChTile : m;
+  const uint32_t len = static_cast<uint32_t>(c1 - c0);
+  {
 #pragma unroll
     for (uint32_t r = 0; r < kPer; r++) {
       const uint32_t p = tid + r * kChThreads;
