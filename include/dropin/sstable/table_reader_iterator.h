@@ -14,9 +14,10 @@
  * seen twice.
  *
  * Behaviour (table_reader_iterator.cc:14-149): on the first
- * SeekToFirst / SeekToLast / Seek the whole data section of the table is read
- * through the TableReader's own file object (a friend of TableReader,
- * table_reader.h:105) and every block of its BlockIndex vector is decoded in
+ * SeekToFirst / SeekToLast / Seek the whole data section of the table is
+ * mapped read-only from the TableReader's file (a friend of TableReader,
+ * table_reader.h:105; its own file object reads it when the map fails) and
+ * every block of its BlockIndex vector is decoded in
  * ONE GPU call (sstc::DecodeBlocks on the calling thread's context, txn in the
  * reference's compat mode: an empty-value PUT reads (txn & 0xffffffff) << 32,
  * block_reader.cc:109-111).  Then the iterator walks the decoded records with
@@ -38,6 +39,7 @@
 
 #include "common/base_iterator.h"
 #include "common/macros.h"
+#include "sstcodec.h" // sstc_record32
 
 // libC++
 #include <cassert>
@@ -99,16 +101,6 @@ private:
   void ShowBlock(uint64_t block);
   bool EntryValid() const { return has_block_ && entry_ < shown_n_; }
 
-  // one decoded record, what the accessors read (one cache line per two
-  // records: MergeIterator walks many tables at once, and six parallel column
-  // arrays per table were six streams each)
-  struct Rec {
-    uint64_t key_off, txn;
-    uint32_t key_len, val_off; // val_off relative to key_off
-    uint32_t val_len;          // SSTC_NO_VALUE: no value fields
-    uint8_t type;
-  };
-
   // block cursor: current_block_offset_index_ of table_reader_iterator.h:64
   uint64_t current_block_offset_index_;
   // the block an entry cursor exists for (block_reader_iterator_ != nullptr),
@@ -125,10 +117,16 @@ private:
   const TableReader *table_reader_;
 
   bool loaded_ = false;
-  std::unique_ptr<uint8_t[]> data_; // the table's data section (not zero-filled)
+  const uint8_t *data_ = nullptr;  // the table's data section: a read-only map of the file, or buf_
   uint64_t data_size_ = 0;
+  void *map_ = nullptr;            // mmap of the file's first map_len_ bytes (nullptr: read into buf_)
+  uint64_t map_len_ = 0;
+  std::unique_ptr<uint8_t[]> buf_; // (not zero-filled)
   std::vector<uint64_t> base_;    // per block: its first record
-  std::vector<Rec> rec_;
+  // one 32 B record per entry, packed on the GPU (sstc_record32): what the
+  // accessors read -- one cache line per two records, where six column arrays
+  // per table were six streams each for MergeIterator's walk over many tables
+  std::unique_ptr<sstc_record32[]> rec_;
 };
 
 } // namespace sstable

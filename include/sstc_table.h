@@ -273,9 +273,7 @@ private:
  * sstc_decode_blocks through `ctx`): block b's records are
  * [base[b], base[b+1]), offsets point into the host bytes that were decoded,
  * val_len == SSTC_NO_VALUE marks a record without value fields (a DELETE),
- * status[b] is the block's SSTC_BLK_* code.  What the drop-in
- * kvs::sstable::TableReaderIterator (include/dropin/sstable/
- * table_reader_iterator.h) decodes a whole table with. */
+ * status[b] is the block's SSTC_BLK_* code. */
 struct DecodedBlocks {
   std::vector<uint64_t> base;
   std::vector<uint32_t> status;
@@ -287,6 +285,19 @@ struct DecodedBlocks {
  * SSTC_E_* code (bad arguments, HIP failure) */
 int DecodeBlocks(sstc_ctx *ctx, const uint8_t *data, uint64_t bytes, const uint64_t *off, const uint64_t *len,
                  uint64_t nb, uint32_t txn_mode, DecodedBlocks &out);
+
+/* The same decode with the records packed on the GPU (sstc_pack_records) and
+ * copied back in one piece: 32 B per record instead of six columns, no host
+ * repacking.  What the drop-in kvs::sstable::TableReaderIterator serves its
+ * entries from. */
+struct DecodedTable {
+  std::vector<uint64_t> base;            // nb + 1: block b's records are [base[b], base[b + 1])
+  std::vector<uint32_t> status;          // SSTC_BLK_* per block
+  std::unique_ptr<sstc_record32[]> rec;  // n records
+  uint64_t n = 0;
+};
+int DecodeTable(sstc_ctx *ctx, const uint8_t *data, uint64_t bytes, const uint64_t *off, const uint64_t *len,
+                uint64_t nb, uint32_t txn_mode, DecodedTable &out);
 
 /* table_reader_iterator.cc:46-149 over a table decoded whole on the GPU at the
  * first Seek (one sstc_count_records + sstc_decode_blocks call instead of a

@@ -93,6 +93,19 @@ typedef struct sstc_records {
   uint64_t *val_off;
 } sstc_records;
 
+/* One decoded record packed in 32 B: what a host-side iterator serves per
+ * entry (sstc_pack_records).  Offsets into the decoded bytes; the value starts
+ * at key_off + val_rel. */
+typedef struct sstc_record32 {
+  uint64_t key_off;
+  uint64_t txn;
+  uint32_t key_len;
+  uint32_t val_rel;  /* value offset - key offset; 0 without value fields */
+  uint32_t val_len;  /* SSTC_NO_VALUE = no value fields (a DELETE) */
+  uint8_t type;
+  uint8_t pad[3];
+} sstc_record32;
+
 uint32_t sstc_version(void);
 const char *sstc_last_error_string(void);
 
@@ -134,6 +147,12 @@ int sstc_count_records(sstc_ctx *ctx, const uint8_t *d_src, const uint64_t *d_bl
 int sstc_decode_blocks(sstc_ctx *ctx, const uint8_t *d_src, const uint64_t *d_blk_off,
                        const uint64_t *d_blk_len, uint64_t nblocks, const uint64_t *d_rec_base,
                        sstc_records out, uint32_t txn_mode, uint32_t *d_block_status);
+
+/* Pack records [0, nrec) of a device record table (sstc_decode_blocks output)
+ * into d_out[0, nrec) (device, 32 B each), for one device-to-host copy of what
+ * a table iterator serves (BlockReaderIterator's accessors,
+ * sstable/block_reader_iterator.cc:30-71). */
+int sstc_pack_records(sstc_ctx *ctx, sstc_records in, uint64_t nrec, sstc_record32 *d_out);
 
 /* ---- encode (replaces BlockBuilder::AddEntry/EncodeExtraInfo and the block
  *      write of TableBuilder::FlushBlock, sstable/block_builder.cc:12-109,

@@ -27,6 +27,11 @@
 #include "sstable/table_reader.h"
 #include "sstc_table.h"
 
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
 #include <algorithm>
 #include <span>
 #include <stdexcept>
@@ -45,7 +50,10 @@ TableReaderIterator::TableReaderIterator(
 }
 
 // table_reader_iterator.cc:23
-TableReaderIterator::~TableReaderIterator() { lru_table_item_->Unref(); }
+TableReaderIterator::~TableReaderIterator() {
+  if (map_) munmap(map_, map_len_);
+  lru_table_item_->Unref();
+}
 
 void TableReaderIterator::Load() {
   if (loaded_) return;
@@ -53,10 +61,14 @@ void TableReaderIterator::Load() {
   const double t0 = tr ? sstc::TraceNowMs() : 0;
   const std::vector<BlockIndex> &index = table_reader_->block_index_;
   const uint64_t nb = index.size();
-  // the data section: every block the meta section lists, read with the
-  // TableReader's own file object (table_reader.cc:220-221 reads them one by
-  // one).  Pageable: page-locking a fresh buffer per table cost more than the
-  // staged copy (config 4's 128 tables: 6.2 s vs 4.6 s per PickCompact)
+  // the data section: every block the meta section lists (table_reader.cc:
+  // 220-221 reads them one by one).  Mapped read-only, pages populated in the
+  // one call: a read into fresh memory paid a page fault (and the kernel's
+  // zeroing) per 4 KiB of the destination, ~180 ms of config 5's 1 GB.  An SST
+  // is immutable once written (db_impl.cc:430-436), so the map is its bytes.
+  // Fallback: the TableReader's own file object into a pageable buffer
+  // (page-locking a fresh buffer per table cost more than the staged copy:
+  // config 4's 128 tables, 6.2 s vs 4.6 s per PickCompact).
   uint64_t lo = UINT64_MAX, hi = 0;
   for (const BlockIndex &bi : index) {
     lo = std::min<uint64_t>(lo, bi.GetBlockStartOffset());
@@ -64,14 +76,30 @@ void TableReaderIterator::Load() {
   }
   if (nb == 0) lo = hi = 0;
   data_size_ = hi - lo;
-  data_.reset(new uint8_t[data_size_ ? data_size_ : 1]);
-  for (uint64_t done = 0; done < data_size_;) {
-    const uint64_t chunk = std::min<uint64_t>(data_size_ - done, 1ull << 30);
-    const ssize_t r = table_reader_->read_file_object_->RandomRead(
-        std::span<Byte>(data_.get() + done, chunk), lo + done);
-    if (r <= 0)
-      throw std::runtime_error("TableReaderIterator: cannot read the data section of " + table_reader_->filename_);
-    done += static_cast<uint64_t>(r);
+  if (data_size_) {
+    const int fd = open(table_reader_->filename_.c_str(), O_RDONLY | O_CLOEXEC);
+    struct stat st;
+    if (fd >= 0 && fstat(fd, &st) == 0 && static_cast<uint64_t>(st.st_size) >= hi) { // (no page past EOF)
+      void *p = mmap(nullptr, hi, PROT_READ, MAP_PRIVATE | MAP_POPULATE, fd, 0);
+      if (p != MAP_FAILED) {
+        map_ = p;
+        map_len_ = hi;
+        data_ = static_cast<const uint8_t *>(p) + lo;
+      }
+    }
+    if (fd >= 0) close(fd);
+  }
+  if (!map_) {
+    buf_.reset(new uint8_t[data_size_ ? data_size_ : 1]);
+    for (uint64_t done = 0; done < data_size_;) {
+      const uint64_t chunk = std::min<uint64_t>(data_size_ - done, 1ull << 30);
+      const ssize_t r =
+          table_reader_->read_file_object_->RandomRead(std::span<Byte>(buf_.get() + done, chunk), lo + done);
+      if (r <= 0)
+        throw std::runtime_error("TableReaderIterator: cannot read the data section of " + table_reader_->filename_);
+      done += static_cast<uint64_t>(r);
+    }
+    data_ = buf_.get();
   }
   const double t1 = tr ? sstc::TraceNowMs() : 0;
   std::vector<uint64_t> off(nb), len(nb);
@@ -79,10 +107,11 @@ void TableReaderIterator::Load() {
     off[b] = index[b].GetBlockStartOffset() - lo;
     len[b] = index[b].GetBlockSize();
   }
-  // every block of the table in ONE GPU decode, txn as the reference reads it
-  sstc::DecodedBlocks d;
-  const int rc = sstc::DecodeBlocks(sstc::ThreadContext(), data_.get(), data_size_, off.data(), len.data(), nb,
-                                    SSTC_TXN_COMPAT, d);
+  // every block of the table in ONE GPU decode, txn as the reference reads
+  // it, the records packed on the GPU into what the accessors read
+  sstc::DecodedTable d;
+  const int rc = sstc::DecodeTable(sstc::ThreadContext(), data_, data_size_, off.data(), len.data(), nb,
+                                   SSTC_TXN_COMPAT, d);
   if (rc != SSTC_OK)
     throw std::runtime_error("TableReaderIterator: GPU decode of " + table_reader_->filename_ +
                              " failed: " + sstc_last_error_string());
@@ -91,23 +120,12 @@ void TableReaderIterator::Load() {
       throw std::runtime_error("TableReaderIterator: corrupt block " + std::to_string(b) + " in " +
                                table_reader_->filename_ + " (SSTC_BLK code " + std::to_string(d.status[b]) + ")");
   const double t2 = tr ? sstc::TraceNowMs() : 0;
-  const uint64_t n = d.type.size();
-  rec_.resize(n);
-  for (uint64_t i = 0; i < n; i++) {
-    Rec &r = rec_[i];
-    r.key_off = d.key_off[i];
-    r.txn = d.txn[i];
-    r.key_len = d.key_len[i];
-    r.val_len = d.val_len[i];
-    r.val_off = d.val_len[i] == SSTC_NO_VALUE ? 0u : static_cast<uint32_t>(d.val_off[i] - d.key_off[i]);
-    r.type = d.type[i];
-  }
+  rec_ = std::move(d.rec);
   base_ = std::move(d.base);
   loaded_ = true;
   if (tr) {
-    sstc::TraceHost("iterator read data section", t1 - t0);
-    sstc::TraceHost("iterator GPU decode (H2D, count, decode, D2H)", t2 - t1);
-    sstc::TraceHost("iterator record table", sstc::TraceNowMs() - t2);
+    sstc::TraceHost(map_ ? "iterator map data section" : "iterator read data section", t1 - t0);
+    sstc::TraceHost("iterator GPU decode (H2D, count, decode, pack, D2H)", t2 - t1);
   }
 }
 
@@ -121,18 +139,18 @@ void TableReaderIterator::ShowBlock(uint64_t block) {
 // block_reader_iterator.cc:30-40
 std::string_view TableReaderIterator::GetKey() {
   if (!EntryValid()) return std::string_view{};
-  const Rec &r = rec_[shown_first_ + entry_];
-  return {reinterpret_cast<const char *>(data_.get()) + r.key_off, r.key_len};
+  const sstc_record32 &r = rec_[shown_first_ + entry_];
+  return {reinterpret_cast<const char *>(data_) + r.key_off, r.key_len};
 }
 
 // block_reader_iterator.cc:42-52 + block_reader.cc:84-102: a DELETE has no
 // value (null view), a PUT a view into the block even when empty
 std::string_view TableReaderIterator::GetValue() {
   if (!EntryValid()) return std::string_view{};
-  const Rec &r = rec_[shown_first_ + entry_];
+  const sstc_record32 &r = rec_[shown_first_ + entry_];
   if (r.type == static_cast<uint8_t>(db::ValueType::DELETED) || r.val_len == SSTC_NO_VALUE)
     return std::string_view{};
-  return {reinterpret_cast<const char *>(data_.get()) + r.key_off + r.val_off, r.val_len};
+  return {reinterpret_cast<const char *>(data_) + r.key_off + r.val_rel, r.val_len};
 }
 
 // block_reader_iterator.cc:54-61

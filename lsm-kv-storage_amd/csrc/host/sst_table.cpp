@@ -529,8 +529,13 @@ struct DecStage {
 thread_local std::map<int, DecStage> g_dec; // device -> staging
 } // namespace
 
-int DecodeBlocks(sstc_ctx *ctx, const uint8_t *data, uint64_t bytes, const uint64_t *off, const uint64_t *len,
-                 uint64_t nb, uint32_t txn_mode, DecodedBlocks &out) {
+namespace {
+// H2D of the bytes and the block index, count + decode on the device; on
+// SSTC_OK `base` holds the per-block record bases (host) and `rec` / `d_st`
+// the device record table and block codes (in the thread's staging region)
+int decode_on_device(sstc_ctx *ctx, const uint8_t *data, uint64_t bytes, const uint64_t *off, const uint64_t *len,
+                     uint64_t nb, uint32_t txn_mode, std::vector<uint64_t> &base, sstc_records &rec,
+                     uint32_t *&d_st, uint8_t *&d_extra, uint64_t extra_per_rec) {
   if (!ctx || (bytes && !data) || (nb && (!off || !len))) return SSTC_E_INVALID_ARG;
   uint64_t sum_len = 0;
   for (uint64_t b = 0; b < nb; b++) {
@@ -538,35 +543,46 @@ int DecodeBlocks(sstc_ctx *ctx, const uint8_t *data, uint64_t bytes, const uint6
     sum_len += len[b];
   }
   static const uint8_t kZero[16] = {};
-  try {
-    const int dev = sstc__ctx_device(ctx);
-    DeviceScope on_ctx_device(dev);
-    // one device region: the bytes, the block index, the counts and the record
-    // arrays sized by the most records the blocks can claim (the count kernel
-    // takes a trailer's n only when 16 n + 16 <= the block's length)
-    const uint64_t nmax = sum_len / 16 + 1;
-    const uint64_t o_src = 0, o_off = align256(bytes + 16), o_len = align256(o_off + 8 * nb),
-                   o_base = align256(o_len + 8 * nb), o_st = align256(o_base + 8 * (nb + 1)),
-                   o_type = align256(o_st + 4 * nb + 4), o_kl = align256(o_type + nmax), o_vl = align256(o_kl + 4 * nmax),
-                   o_txn = align256(o_vl + 4 * nmax), o_ko = align256(o_txn + 8 * nmax),
-                   o_vo = align256(o_ko + 8 * nmax), total = align256(o_vo + 8 * nmax);
-    uint8_t *d = g_dec[dev].get(total);
-    h2d(ctx, d + o_src, bytes ? data : kZero, bytes ? bytes : 1);
-    h2d(ctx, d + o_off, off, nb * 8);
-    h2d(ctx, d + o_len, len, nb * 8);
-    auto *d_off = reinterpret_cast<uint64_t *>(d + o_off), *d_len = reinterpret_cast<uint64_t *>(d + o_len),
-         *d_base = reinterpret_cast<uint64_t *>(d + o_base);
-    check(sstc_count_records(ctx, d + o_src, d_off, d_len, nb, d_base), "sstc_count_records");
-    out.base.resize(nb + 1);
-    if (!d2h(ctx, out.base.data(), d_base, (nb + 1) * 8) || !sync(ctx)) return SSTC_E_HIP;
-    const uint64_t n = out.base[nb];
-    if (n > nmax) return SSTC_E_INVALID_ARG; // blocks claiming more entries than their bytes hold
-    sstc_records rec{d + o_type, reinterpret_cast<uint32_t *>(d + o_kl), reinterpret_cast<uint32_t *>(d + o_vl),
+  const int dev = sstc__ctx_device(ctx);
+  DeviceScope on_ctx_device(dev);
+  // one device region: the bytes, the block index, the counts and the record
+  // arrays sized by the most records the blocks can claim (the count kernel
+  // takes a trailer's n only when 16 n + 16 <= the block's length)
+  const uint64_t nmax = sum_len / 16 + 1;
+  const uint64_t o_src = 0, o_off = align256(bytes + 16), o_len = align256(o_off + 8 * nb),
+                 o_base = align256(o_len + 8 * nb), o_st = align256(o_base + 8 * (nb + 1)),
+                 o_type = align256(o_st + 4 * nb + 4), o_kl = align256(o_type + nmax), o_vl = align256(o_kl + 4 * nmax),
+                 o_txn = align256(o_vl + 4 * nmax), o_ko = align256(o_txn + 8 * nmax),
+                 o_vo = align256(o_ko + 8 * nmax), o_x = align256(o_vo + 8 * nmax),
+                 total = align256(o_x + extra_per_rec * nmax);
+  uint8_t *d = g_dec[dev].get(total);
+  h2d(ctx, d + o_src, bytes ? data : kZero, bytes ? bytes : 1);
+  h2d(ctx, d + o_off, off, nb * 8);
+  h2d(ctx, d + o_len, len, nb * 8);
+  auto *d_off = reinterpret_cast<uint64_t *>(d + o_off), *d_len = reinterpret_cast<uint64_t *>(d + o_len),
+       *d_base = reinterpret_cast<uint64_t *>(d + o_base);
+  check(sstc_count_records(ctx, d + o_src, d_off, d_len, nb, d_base), "sstc_count_records");
+  base.resize(nb + 1);
+  if (!d2h(ctx, base.data(), d_base, (nb + 1) * 8) || !sync(ctx)) return SSTC_E_HIP;
+  if (base[nb] > nmax) return SSTC_E_INVALID_ARG; // blocks claiming more entries than their bytes hold
+  rec = sstc_records{d + o_type, reinterpret_cast<uint32_t *>(d + o_kl), reinterpret_cast<uint32_t *>(d + o_vl),
                      reinterpret_cast<uint64_t *>(d + o_txn), reinterpret_cast<uint64_t *>(d + o_ko),
                      reinterpret_cast<uint64_t *>(d + o_vo)};
-    check(sstc_decode_blocks(ctx, d + o_src, d_off, d_len, nb, d_base, rec, txn_mode,
-                             reinterpret_cast<uint32_t *>(d + o_st)),
-          "sstc_decode_blocks");
+  d_st = reinterpret_cast<uint32_t *>(d + o_st);
+  d_extra = d + o_x;
+  check(sstc_decode_blocks(ctx, d + o_src, d_off, d_len, nb, d_base, rec, txn_mode, d_st), "sstc_decode_blocks");
+  return SSTC_OK;
+}
+} // namespace
+
+int DecodeBlocks(sstc_ctx *ctx, const uint8_t *data, uint64_t bytes, const uint64_t *off, const uint64_t *len,
+                 uint64_t nb, uint32_t txn_mode, DecodedBlocks &out) {
+  try {
+    sstc_records rec{};
+    uint32_t *d_st = nullptr;
+    uint8_t *d_x = nullptr;
+    if (int r = decode_on_device(ctx, data, bytes, off, len, nb, txn_mode, out.base, rec, d_st, d_x, 0)) return r;
+    const uint64_t n = out.base[nb];
     out.status.resize(nb);
     out.type.resize(n);
     out.key_len.resize(n);
@@ -574,10 +590,33 @@ int DecodeBlocks(sstc_ctx *ctx, const uint8_t *data, uint64_t bytes, const uint6
     out.txn.resize(n);
     out.key_off.resize(n);
     out.val_off.resize(n);
-    bool ok = d2h(ctx, out.status.data(), d + o_st, nb * 4) && d2h(ctx, out.type.data(), d + o_type, n) &&
-              d2h(ctx, out.key_len.data(), d + o_kl, 4 * n) && d2h(ctx, out.val_len.data(), d + o_vl, 4 * n) &&
-              d2h(ctx, out.txn.data(), d + o_txn, 8 * n) && d2h(ctx, out.key_off.data(), d + o_ko, 8 * n) &&
-              d2h(ctx, out.val_off.data(), d + o_vo, 8 * n);
+    bool ok = d2h(ctx, out.status.data(), d_st, nb * 4) && d2h(ctx, out.type.data(), rec.type, n) &&
+              d2h(ctx, out.key_len.data(), rec.key_len, 4 * n) && d2h(ctx, out.val_len.data(), rec.val_len, 4 * n) &&
+              d2h(ctx, out.txn.data(), rec.txn, 8 * n) && d2h(ctx, out.key_off.data(), rec.key_off, 8 * n) &&
+              d2h(ctx, out.val_off.data(), rec.val_off, 8 * n);
+    ok = sync(ctx) && ok;
+    return ok ? SSTC_OK : SSTC_E_HIP;
+  } catch (const std::exception &) {
+    return SSTC_E_HIP;
+  }
+}
+
+int DecodeTable(sstc_ctx *ctx, const uint8_t *data, uint64_t bytes, const uint64_t *off, const uint64_t *len,
+                uint64_t nb, uint32_t txn_mode, DecodedTable &out) {
+  try {
+    sstc_records rec{};
+    uint32_t *d_st = nullptr;
+    uint8_t *d_x = nullptr;
+    if (int r = decode_on_device(ctx, data, bytes, off, len, nb, txn_mode, out.base, rec, d_st, d_x,
+                                 sizeof(sstc_record32)))
+      return r;
+    const uint64_t n = out.base[nb];
+    auto *d_rec = reinterpret_cast<sstc_record32 *>(d_x);
+    check(sstc_pack_records(ctx, rec, n, d_rec), "sstc_pack_records");
+    out.status.resize(nb);
+    out.n = n;
+    out.rec.reset(new sstc_record32[n ? n : 1]); // default-initialised: the copy below fills it
+    bool ok = d2h(ctx, out.status.data(), d_st, nb * 4) && d2h(ctx, out.rec.get(), d_rec, n * sizeof(sstc_record32));
     ok = sync(ctx) && ok;
     return ok ? SSTC_OK : SSTC_E_HIP;
   } catch (const std::exception &) {

@@ -300,6 +300,13 @@ int sstc_decode_blocks(sstc_ctx *c, const uint8_t *d_src, const uint64_t *d_blk_
   return SSTC_OK;
 }
 
+int sstc_pack_records(sstc_ctx *c, sstc_records in, uint64_t nrec, sstc_record32 *d_out) {
+  if (!c || (nrec && (!d_out || bad_records(in)))) return fail(SSTC_E_INVALID_ARG, "sstc_pack_records: NULL argument");
+  if (int r = bind_device(c)) return r;
+  SSTC_HIP(sstc::launch_pack_records(in, nrec, d_out, c->stream), "pack kernel");
+  return SSTC_OK;
+}
+
 int sstc_segment_records(sstc_ctx *c, const uint32_t *d_key_len, const uint32_t *d_val_len,
                          uint64_t nrec, uint64_t block_threshold, uint64_t *d_blk_first,
                          uint64_t *d_nblocks) {

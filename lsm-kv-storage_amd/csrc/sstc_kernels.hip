@@ -2291,6 +2291,28 @@ hipError_t launch_decode(const DecArgs &a, hipStream_t s) {
   return hipGetLastError();
 }
 
+// SoA record table -> 32 B records (sstc_record32), one record per thread:
+// 33 B of columns read, 32 B written, both coalesced
+static_assert(sizeof(sstc_record32) == 32, "sstc_record32 is 32 B");
+__global__ __launch_bounds__(256) void pack_records_kernel(sstc_records in, uint64_t n, sstc_record32 *out) {
+  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
+       i += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
+    const uint64_t ko = in.key_off[i], vo = in.val_off[i], tx = in.txn[i];
+    const uint32_t kl = in.key_len[i], vl = in.val_len[i], ty = in.type[i];
+    const uint32_t rel = vl == kNoValue ? 0u : static_cast<uint32_t>(vo - ko);
+    u32x4 *q = reinterpret_cast<u32x4 *>(out + i);
+    q[0] = u32x4{static_cast<uint32_t>(ko), static_cast<uint32_t>(ko >> 32), static_cast<uint32_t>(tx),
+                 static_cast<uint32_t>(tx >> 32)};
+    q[1] = u32x4{kl, rel, vl, ty};
+  }
+}
+
+hipError_t launch_pack_records(const sstc_records &in, uint64_t nrec, sstc_record32 *out, hipStream_t s) {
+  if (nrec) pack_records_kernel<<<static_cast<uint32_t>(std::min<uint64_t>(grid_for(nrec, 256), 8192)), 256, 0, s>>>(
+      in, nrec, out);
+  return hipGetLastError();
+}
+
 // sized for the smallest tile any scan uses (kScanThreads x 4 items)
 uint64_t scan_workspace_elems(uint64_t n) { return (n + 4 * kScanThreads - 1) / (4 * kScanThreads) + 2; }
 

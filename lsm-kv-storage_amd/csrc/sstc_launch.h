@@ -148,6 +148,7 @@ hipError_t launch_count(const uint8_t *src, const uint64_t *blk_off, const uint6
                         uint64_t nblocks, uint64_t *counts, hipStream_t s, uint64_t *scan_ws = nullptr,
                         uint64_t *len_part = nullptr); // len_part: per workgroup of 256 blocks, {sum of blk_len, max blk_off + blk_len}
 hipError_t launch_decode(const DecArgs &a, hipStream_t s);
+hipError_t launch_pack_records(const sstc_records &in, uint64_t nrec, sstc_record32 *out, hipStream_t s);
 uint64_t scan_workspace_elems(uint64_t n);
 // look-back status words a scan of n items needs cleared (0: single-workgroup scan)
 uint64_t scan_status_words(uint64_t n);

@@ -122,7 +122,7 @@ def test_dropin_builds_unmodified_compact_cc():
     assert "kvs::db::Compact::DoCompactJob()" in defined
     # the decode side: compact.cc constructs sstable::TableReaderIterator with
     # the reference's signature (compact.cc:201-203,223-225), and the one in the
-    # binary is the drop-in (its Load() decodes through sstc::DecodeBlocks), not
+    # binary is the drop-in (its Load() decodes through sstc::DecodeTable), not
     # the reference's (whose CreateNewBlockReaderIterator reads block by block)
     assert ("kvs::sstable::TableReaderIterator::TableReaderIterator(std::vector<std::unique_ptr<"
             "kvs::sstable::BlockReaderCache") in undef
@@ -131,7 +131,7 @@ def test_dropin_builds_unmodified_compact_cc():
     assert "TableReaderIterator::CreateNewBlockReaderIterator" not in defined
     tri = os.path.join(ROOT, "oracle", "_ref", "dropin_obj", "sstc", "table_reader_iterator.o")
     tri_undef = subprocess.run(["nm", "-C", "-u", tri], capture_output=True, text=True, check=True).stdout
-    assert "sstc::DecodeBlocks(" in tri_undef
+    assert "sstc::DecodeTable(" in tri_undef
     # the compiled TUs are the reference's own files, byte for byte
     mk = ["make", "-C", os.path.join(ROOT, "oracle"), "-n", "-B"]
     dep = subprocess.run(mk + [obj], capture_output=True, text=True).stdout
