@@ -52,12 +52,14 @@ def relaunch(n, script, argv, extra_env=None):
 
 
 class Ranks:
-    def __init__(self, world, rank, local, device, backend):
+    def __init__(self, world, rank, local, device, backend, pg=None):
         self.world, self.rank, self.local, self.device, self.backend = world, rank, local, device, backend
+        # a process group exists: world > 1, or SSTC_PG_SINGLE at world 1
+        self.pg = world > 1 if pg is None else pg
 
     @property
     def on(self):
-        return self.world > 1
+        return self.pg
 
     def barrier(self):
         if self.on:
@@ -110,11 +112,17 @@ def init_ranks(n_expected, backend="nccl"):
             raise SystemExit(f"{world} ranks need {world} GPUs, {torch.cuda.device_count()} visible")
         torch.cuda.set_device(local)
         device = torch.device("cuda", local)
-    if world > 1:
+    # SSTC_PG_SINGLE=1 under a launcher: a one-rank process group as well, so
+    # the collective path (RCCL init with device_id, barrier, max / sum /
+    # gather) runs on a one-GPU box (tests/test_gpu_bench_rank.py)
+    pg = world > 1 or (under_launcher() and os.environ.get("SSTC_PG_SINGLE") == "1")
+    if pg:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=device)
         else:
             dist.init_process_group("gloo")
         assert dist.get_world_size() == n_expected
-    return Ranks(world, rank, local, device, backend)
+        print(f"[sstc] process group: {dist.get_backend()}, world {dist.get_world_size()}", file=sys.stderr,
+              flush=True)
+    return Ranks(world, rank, local, device, backend, pg)
