@@ -1732,6 +1732,7 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     ea.large_blocks = nblocks && in_bytes / nblocks > 8192 ? 1u : 0u;
     ea.src_end = src_end;
     ea.guard = guard;
+    ea.xcd = 2; // XCD-chunked block order (the grid is the nb_max bound)
     CK(launch_enc_emit(ea, s));
     ck_meta_kernel<<<static_cast<uint32_t>((nb_max + 255) / 256), 256, 0, s>>>(bmeta, L, btab, BL, MS, blen, tbf,
                                                                               d_table_off, tdata, d_dst, need,

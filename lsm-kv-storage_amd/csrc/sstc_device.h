@@ -55,6 +55,18 @@ __device__ __forceinline__ uint32_t xcd_logical_block(uint32_t i, uint32_t n) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + k;
 }
 
+// XCD-chunked order for grids sized by a bound (the real count is on the
+// device): within every run of kNumXcd * C workgroups, XCD x (= i % 8, the
+// dispatch round robin) takes the x-th chunk of C consecutive logical ids, so
+// neighbouring ids run at the same time behind one L2; a last partial run
+// keeps dispatch order (workgroups past the real count leave)
+__device__ __forceinline__ uint32_t xcd_chunk_block(uint32_t i, uint32_t n, uint32_t C) {
+  const uint32_t run = kNumXcd * C, r0 = i / run * run;
+  if (r0 + run > n) return i;
+  const uint32_t j = i - r0;
+  return r0 + (j % kNumXcd) * C + j / kNumXcd;
+}
+
 // ---- LDS image reads / writes at arbitrary byte offsets ---------------------
 // Reads: aligned dwords + v_alignbyte (the image is padded by >= 16 bytes past
 // its last byte).  gfx950 runs LDS in unaligned mode (the compiler's default

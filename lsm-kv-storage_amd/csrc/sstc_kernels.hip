@@ -1326,6 +1326,13 @@ __device__ void enc_wave_offsets(const EncArgs &a, uint64_t b) {
 // 8 waves / SIMD (config 3 encode 525 -> 512 us, config 4 863 -> 844 us), but
 // copies large blocks slower (config 5 231 -> 255 us); kQ = kU = 4 needs 79,
 // 6 waves (profiles/r05/encode_ab.md)
+// EncArgs::xcd == 2 (the compaction job, whose grid is a bound): 16
+// consecutive workgroups per XCD chunk.  Neighbouring output blocks copy
+// neighbouring entries of the same inputs (config 4: 1-entry runs from 128
+// inputs), so their source lines are fetched once per L2: config 4 encode
+// FETCH 3.89 -> 2.33 GB, 845 -> 832 us (profiles/r05/encode_xcd.md)
+constexpr uint32_t kEncXcdChunk = 16;
+
 template <uint32_t kMode, uint32_t GK = 2, uint32_t GV = 8, uint32_t kQ = 2, uint32_t kU = kWaveSpanUnroll>
 __global__ __launch_bounds__(kEncWaves *kWave) void enc_lds_kernel(EncArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kEncSlotWaves * kEncSlot];
@@ -1333,7 +1340,9 @@ __global__ __launch_bounds__(kEncWaves *kWave) void enc_lds_kernel(EncArgs a) {
   __shared__ u32x4 s_tbl[kMode == 0 ? kEncWaves * kWave : 1]; // span tuples (copy_spans)
   const uint32_t wave = uniform(threadIdx.x / kWave);
   const uint32_t lane = lane_id();
-  const uint32_t wg = a.xcd ? xcd_logical_block(blockIdx.x, gridDim.x) : blockIdx.x;
+  const uint32_t wg = a.xcd == 2   ? xcd_chunk_block(blockIdx.x, gridDim.x, kEncXcdChunk)
+                      : a.xcd == 1 ? xcd_logical_block(blockIdx.x, gridDim.x)
+                                   : blockIdx.x;
   const uint64_t b = static_cast<uint64_t>(wg) * kEncWaves + wave;
   if (b >= a.nblocks) return;
   uint8_t *img = lds + wave * kEncSlot;

@@ -84,7 +84,7 @@ struct EncArgs {
   const uint64_t *out_blk_len;
   uint8_t *dst;
   uint32_t entries_in_src = 0; // records decoded from blocks in key_src (== val_src)
-  uint32_t xcd = 0;
+  uint32_t xcd = 0; // block order: 0 dispatch, 1 XCD-grouped ranges (exact grid), 2 XCD chunks (bound grid)
   // mode 1: most blocks are past the LDS slot (the build with wider copies,
   // launch_enc_emit); 0: most fit it (the 8-waves-per-SIMD build)
   uint32_t large_blocks = 0;
