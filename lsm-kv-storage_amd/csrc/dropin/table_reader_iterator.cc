@@ -33,6 +33,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <span>
 #include <stdexcept>
 #include <string>
@@ -76,7 +77,8 @@ void TableReaderIterator::Load() {
   }
   if (nb == 0) lo = hi = 0;
   data_size_ = hi - lo;
-  if (data_size_) {
+  static const bool no_map = std::getenv("SSTC_DROPIN_NO_MAP") != nullptr; // (tests: the read path)
+  if (data_size_ && !no_map) {
     const int fd = open(table_reader_->filename_.c_str(), O_RDONLY | O_CLOEXEC);
     struct stat st;
     if (fd >= 0 && fstat(fd, &st) == 0 && static_cast<uint64_t>(st.st_size) >= hi) { // (no page past EOF)

@@ -97,6 +97,7 @@ def load():
         "sstc_ctx_reset_errors": (ctypes.c_int, [c_vp]),
         "sstc_count_records": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_u64, c_vp]),
         "sstc_decode_blocks": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_u64, c_vp, Records, c_u32, c_vp]),
+        "sstc_pack_records": (ctypes.c_int, [c_vp, Records, c_u64, c_vp]),
         "sstc_segment_records": (ctypes.c_int, [c_vp, c_vp, c_vp, c_u64, c_u64, c_vp, c_vp]),
         "sstc_encode_blocks": (ctypes.c_int, [c_vp, c_vp, c_vp, Records, c_u64, c_vp, c_u64, c_u64,
                                               c_vp, c_vp, c_vp]),

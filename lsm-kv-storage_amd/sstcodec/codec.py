@@ -156,6 +156,14 @@ class Codec:
                                           table.c(), txn_mode, _p(status)), "sstc_decode_blocks")
         return table, rec_base, status
 
+    def pack(self, table):
+        """sstc_pack_records: the record table as n x 32 B sstc_record32 rows
+        (uint8 tensor [n, 32]) -- what the drop-in TableReaderIterator reads."""
+        out = torch.empty((max(table.n, 1), 32), dtype=torch.uint8, device=self.device)
+        self._stream()
+        check(self.lib.sstc_pack_records(self.h, table.c(), table.n, _p(out)), "sstc_pack_records")
+        return out[: table.n]
+
     # ---- encode ------------------------------------------------------------
     def segment(self, table, threshold):
         n = table.n

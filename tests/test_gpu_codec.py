@@ -192,6 +192,34 @@ def test_decode_random_vs_oracle(codec, oracle, seed):
     assert np.array_equal(got["txn"], rec["txn"]) and np.array_equal(got["type"], rec["type"])
 
 
+@pytest.mark.parametrize("mode", [0, 1])
+def test_pack_records_equals_decoded_columns(codec, oracle, mode):
+    """sstc_pack_records, what the drop-in TableReaderIterator serves: every
+    32 B sstc_record32 row holds the decoded record's key offset, txn (the
+    compat quirk in mode 0, block_reader.cc:109-111), key length, value offset
+    relative to the key (0 for a DELETE), value length (SSTC_NO_VALUE for a
+    DELETE) and type -- DELETEs, empty keys and empty values included."""
+    rec = W.mixed_records(6000, seed=41, max_val=700)
+    first = oracle.segment(rec, 4096)
+    src, offs, lens = oracle.encode_blocks(rec, first, base=3)
+    src = np.concatenate([[1, 2, 3], src]).astype(np.uint8)
+    table, _, status = codec.decode(t8(src), t64(offs), t64(lens), txn_mode=mode)
+    assert int(status.max().item()) == 0
+    rows = codec.pack(table).cpu().numpy()
+    got = table.to_numpy()
+    n = len(got["type"])
+    assert rows.shape == (n, 32) and n == len(rec["type"])
+    u64 = rows[:, :16].copy().view("<u8")
+    u32 = rows[:, 16:28].copy().view("<u4")
+    nv = got["val_len"] == np.uint32(0xFFFFFFFF)
+    assert nv.any() and (got["val_len"] == 0).any() and (got["key_len"] == 0).any()
+    assert np.array_equal(u64[:, 0], got["key_off"]) and np.array_equal(u64[:, 1], got["txn"])
+    assert np.array_equal(u32[:, 0], got["key_len"]) and np.array_equal(u32[:, 2], got["val_len"])
+    rel = np.where(nv, 0, got["val_off"] - got["key_off"]).astype(np.uint32)
+    assert np.array_equal(u32[:, 1], rel)
+    assert np.array_equal(rows[:, 28], got["type"])
+
+
 # -------------------------------------------------------------------- encode
 def records_table(rec):
     from sstcodec.codec import RecordTable

@@ -134,6 +134,30 @@ def test_unmodified_compact_cc_gpu_decode_and_encode(tmp_path, name):
 TIMED = ("config3", "config4_rank0", "config5")
 
 
+@pytest.mark.parametrize("name", [n for n in ("cj_small", "probe100") if n in RUNNABLE])
+def test_unmodified_compact_cc_read_path(tmp_path, name):
+    """The drop-in iterator's fallback when its table cannot be mapped: the
+    data section read through the TableReader's own file object
+    (SSTC_DROPIN_NO_MAP forces it), outputs still the reference's."""
+    need(EXE)
+    from oracle import table_key_range
+    case = MANIFEST[name]
+    sets, T, limit = case_inputs(name)
+    ins = build_inputs(tmp_path, sets, T)
+    args = [EXE, str(tmp_path / "db"), str(T), str(limit)]
+    (tmp_path / "db").mkdir()
+    for p, fs, rec in ins:
+        lo, hi = table_key_range(rec)
+        args += [p, str(fs), lo.hex() or "-", hi.hex() or "-"]
+    r = subprocess.run(args, capture_output=True, text=True, timeout=240,
+                       env=dict(os.environ, SSTC_DROPIN_NO_MAP="1", SSTC_TRACE_HOST="1"))
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "iterator read data section" in r.stderr and "iterator map data section" not in r.stderr
+    _, outs = G.parse_pick_output(r.stdout)
+    got = [(sha(np.fromfile(p, np.uint8)), fs) for p, fs, _, _ in outs]
+    assert got == [(o["sha256"], o["file_size"]) for o in case["fixed_outputs"]]
+
+
 def pick_time(stdout, tag="time"):
     return float(next(ln.split()[1] for ln in stdout.splitlines() if ln.startswith(tag + " ")))
 
