@@ -583,7 +583,9 @@ struct MgDesc {
 };
 static_assert(kKWay == 8, "MgDesc holds 8 sub-runs");
 
-__global__ __launch_bounds__(kMgThreads) void ck_mg_merge_kernel(const SK *__restrict__ in, SK *__restrict__ out,
+// (waves_per_eu(8): the p1-only instantiation took 102 SGPRs, 7 waves per
+// SIMD; 8 spills 25 SGPRs to VGPR lanes)
+__global__ __launch_bounds__(kMgThreads) __attribute__((amdgpu_waves_per_eu(8))) void ck_mg_merge_kernel(const SK *__restrict__ in, SK *__restrict__ out,
                                                                    const KWin *__restrict__ win, KeyView kv) {
   __shared__ u32x4 pf[kKRegion];
   __shared__ uint16_t ix[2][kKRegion];
@@ -609,6 +611,12 @@ __global__ __launch_bounds__(kMgThreads) void ck_mg_merge_kernel(const SK *__res
   // second half (txn, key length, id) kept in registers for the output
   constexpr uint32_t kPer = kKRegion / kMgThreads;
   u32x4 rest[kPer];
+  // the window's first 8 key bytes, when every record shares them (a window
+  // is a narrow key range: keys with a common prefix of 8+ bytes, e.g. every
+  // config-3 / 4 key, "k0000000..."), let the merge read only the second 8
+  // bytes of each prefix from LDS: half the LDS bytes per probe
+  const uint64_t c0 = reinterpret_cast<const uint64_t *>(in + d.gidx(0))[0];
+  bool same = true;
 #pragma unroll
   for (uint32_t j = 0; j < kPer; j++) {
     const uint32_t i = threadIdx.x + j * kMgThreads;
@@ -616,14 +624,19 @@ __global__ __launch_bounds__(kMgThreads) void ck_mg_merge_kernel(const SK *__res
       const u32x4 *r = reinterpret_cast<const u32x4 *>(in + d.gidx(i));
       pf[i] = r[0];
       rest[j] = r[1];
+      same &= (static_cast<uint64_t>(r[0].x) | (static_cast<uint64_t>(r[0].y) << 32)) == c0;
     }
   }
+  // the verdict through ix[0] (free until the second level writes it): one
+  // word per wave, no extra LDS (__syncthreads_and took 256 B: 8 -> 7
+  // workgroups per CU)
+  const bool wall = __all(same);
+  if (lane_id() == 0) ix[0][threadIdx.x / kWave] = wall ? 1 : 0;
   __syncthreads();
-  auto pfx = [&](uint32_t sl) __attribute__((always_inline)) -> MgPf {
-    const u32x4 h = pf[sl];
-    return {static_cast<uint64_t>(h.x) | (static_cast<uint64_t>(h.y) << 32),
-            static_cast<uint64_t>(h.z) | (static_cast<uint64_t>(h.w) << 32)};
-  };
+  bool p1only = true;
+#pragma unroll
+  for (uint32_t w = 0; w < kMgThreads / kWave; w++) p1only &= ix[0][w] != 0;
+  const uint64_t *pf64 = reinterpret_cast<const uint64_t *>(pf);
   // slot sa (prefix a) before slot sb (prefix b); the whole records on a tie
   auto less = [&](uint32_t sa, const MgPf &a, uint32_t sb, const MgPf &b) __attribute__((always_inline)) {
     if (a.p0 != b.p0) return a.p0 < b.p0;
@@ -637,6 +650,14 @@ __global__ __launch_bounds__(kMgThreads) void ck_mg_merge_kernel(const SK *__res
   };
   const uint32_t per = (total + kMgThreads - 1) / kMgThreads; // outputs per thread
   const uint32_t p0 = threadIdx.x * per;
+  auto levels = [&](auto p1tag) __attribute__((always_inline)) -> uint32_t {
+  constexpr bool kP1 = decltype(p1tag)::value;
+  auto pfx = [&](uint32_t sl) __attribute__((always_inline)) -> MgPf {
+    if constexpr (kP1) return {c0, pf64[2 * sl + 1]};
+    const u32x4 h = pf[sl];
+    return {static_cast<uint64_t>(h.x) | (static_cast<uint64_t>(h.y) << 32),
+            static_cast<uint64_t>(h.z) | (static_cast<uint64_t>(h.w) << 32)};
+  };
   uint32_t src = 0;
   for (uint32_t wd = 1; wd < k; wd <<= 1) {
     const bool first = wd == 1;
@@ -684,6 +705,9 @@ __global__ __launch_bounds__(kMgThreads) void ck_mg_merge_kernel(const SK *__res
     __syncthreads();
     src ^= 1;
   }
+  return src;
+  };
+  const uint32_t src = p1only ? levels(std::true_type{}) : levels(std::false_type{});
   // output: the inverse permutation, then every thread writes its own staged
   // records at their merged positions (prefix from LDS, second half from its
   // registers) -- reading the records again from the input after the merge
