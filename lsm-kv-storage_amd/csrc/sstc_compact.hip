@@ -1111,12 +1111,20 @@ __global__ __launch_bounds__(kTiThreads) void ck_table_info_kernel(const uint64_
   }
 }
 
+// per block: its output offset (bo, the encode's), its offset inside its
+// table and the output offset of its meta entry (brel / mo, the meta
+// kernel's: the dependent table lookups are taken here, off the meta
+// kernel's chain of loads)
 __global__ void ck_block_off_kernel(const uint32_t *btab, Lay L, BlkOff BL, const uint64_t *tbf,
-                                    const uint64_t *toff, uint64_t *bo) {
+                                    const uint64_t *toff, const uint64_t *tdata, const uint64_t *MS, uint64_t *bo,
+                                    uint64_t *brel, uint64_t *mo) {
   const uint64_t b = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (b >= L.nb_max || !L.ok() || b >= L.nb()) return;
   const uint32_t t = btab[b];
-  bo[b] = toff[t] + (BL[b] - BL[tbf[t]]);
+  const uint64_t f = tbf[t], rel = BL[b] - BL[f];
+  bo[b] = toff[t] + rel;
+  brel[b] = rel;
+  mo[b] = toff[t] + tdata[t] + (MS[b] - MS[f]);
 }
 
 __device__ __forceinline__ void put_le(uint8_t *p, uint64_t v, int n) {
@@ -1154,23 +1162,20 @@ __device__ __forceinline__ bool meta_keys(uint64_t b, const uint64_t *bmeta, con
   if (!ok) atomicOr(guard, kGuardMeta);
   return ok;
 }
-__device__ __forceinline__ void meta_entry(uint8_t *p, uint64_t b, const uint32_t *btab, const BlkOff &BL,
-                                           const uint64_t *blen, const uint64_t *tbf, const MKeys &m) {
-  const uint32_t t = btab[b];
+__device__ __forceinline__ void meta_entry(uint8_t *p, uint64_t rel, uint64_t len, const MKeys &m) {
   put_le(p, m.fk, 4);
   for (uint32_t j = 0; j < m.fk; j++) p[4 + j] = m.k0[j];
   put_le(p + 4 + m.fk, m.lk, 4);
   for (uint32_t j = 0; j < m.lk; j++) p[8 + m.fk + j] = m.k1[j];
-  put_le(p + 8 + m.fk + m.lk, BL[b] - BL[tbf[t]], 8);
-  put_le(p + 16 + m.fk + m.lk, blen[b], 8);
+  put_le(p + 8 + m.fk + m.lk, rel, 8);
+  put_le(p + 16 + m.fk + m.lk, len, 8);
 }
 
 __global__ __launch_bounds__(256) void ck_meta_kernel(const uint64_t *bmeta, Lay L, const uint32_t *btab,
-                                                      BlkOff BL, const uint64_t *MS, const uint64_t *blen,
-                                                      const uint64_t *tbf, const uint64_t *toff,
-                                                      const uint64_t *tdata, uint8_t *dst, const uint64_t *need,
-                                                      uint64_t cap, unsigned long long *guard, const uint8_t *src,
-                                                      const uint64_t *src_end) {
+                                                      const uint64_t *brel, const uint64_t *mo, const uint64_t *MS,
+                                                      const uint64_t *blen, const uint64_t *tbf, uint8_t *dst,
+                                                      const uint64_t *need, uint64_t cap, unsigned long long *guard,
+                                                      const uint8_t *src, const uint64_t *src_end) {
   __shared__ __attribute__((aligned(16))) uint8_t img[kMetaLds + 16];
   if (*need > cap || !L.ok()) return; // output capacity exceeded / corrupt layout: nothing is written
   const uint64_t nb = L.nb();
@@ -1180,9 +1185,8 @@ __global__ __launch_bounds__(256) void ck_meta_kernel(const uint64_t *bmeta, Lay
   const uint64_t b = b0 + threadIdx.x;
   const uint64_t m0 = MS[b0];
   const uint64_t send = *src_end;
-  // a table's meta section must end inside the output buffer
-  auto in_cap = [&](uint64_t t, uint64_t at, uint64_t len) {
-    const uint64_t o = toff[t] + tdata[t] + at;
+  // a table's meta section must end inside the output buffer (o = mo[...])
+  auto in_cap = [&](uint64_t o, uint64_t len) {
     const bool ok = o <= cap && len <= cap - o;
     if (!ok) atomicOr(guard, kGuardMeta);
     return ok;
@@ -1190,33 +1194,33 @@ __global__ __launch_bounds__(256) void ck_meta_kernel(const uint64_t *bmeta, Lay
   MKeys mk{};
   if (MS[bend] - m0 > kMetaLds) {  // long keys: direct per-thread writes
     if (b < bend && meta_keys(b, bmeta, MS, src, send, guard, mk)) {
-      const uint32_t t = btab[b];
-      if (in_cap(t, MS[b] - MS[tbf[t]], MS[b + 1] - MS[b]))
-        meta_entry(dst + toff[t] + tdata[t] + (MS[b] - MS[tbf[t]]), b, btab, BL, blen, tbf, mk);
+      const uint64_t o = mo[b];
+      if (in_cap(o, MS[b + 1] - MS[b])) meta_entry(dst + o, brel[b], blen[b], mk);
     }
     return;
   }
   const bool ok = b >= bend || meta_keys(b, bmeta, MS, src, send, guard, mk);
-  if (b < bend && ok) meta_entry(img + (MS[b] - m0), b, btab, BL, blen, tbf, mk);
+  if (b < bend && ok) meta_entry(img + (MS[b] - m0), brel[b], blen[b], mk);
   if (__syncthreads_or(!ok)) return; // a bad entry: the workgroup writes nothing
   for (uint64_t bs = b0; bs < bend;) {  // one run per output table touched
     const uint32_t t = btab[bs];
     const uint64_t be = tbf[t + 1] < bend ? tbf[t + 1] : bend;
     const uint32_t l0 = static_cast<uint32_t>(MS[bs] - m0);
     const int64_t len = static_cast<int64_t>(MS[be] - MS[bs]);
-    if (!in_cap(t, MS[bs] - MS[tbf[t]], static_cast<uint64_t>(len))) return; // uniform
-    uint8_t *g = dst + toff[t] + tdata[t] + (MS[bs] - MS[tbf[t]]);
+    const uint64_t o = mo[bs];
+    if (!in_cap(o, static_cast<uint64_t>(len))) return; // uniform
+    uint8_t *g = dst + o;
     const uint32_t pad = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(g) & 15u);
     const uint32_t nchunk = static_cast<uint32_t>((pad + len + 15) >> 4);
     for (uint32_t c = threadIdx.x; c < nchunk; c += 256u) {
       const int64_t lo = 16 * static_cast<int64_t>(c) - pad;
       if (lo >= 0 && lo + 16 <= len) {
-        const uint32_t o = l0 + static_cast<uint32_t>(lo);
+        const uint32_t o2 = l0 + static_cast<uint32_t>(lo);
         u32x4 v;
-        v.x = lds_u32u(img, o);
-        v.y = lds_u32u(img, o + 4);
-        v.z = lds_u32u(img, o + 8);
-        v.w = lds_u32u(img, o + 12);
+        v.x = lds_u32u(img, o2);
+        v.y = lds_u32u(img, o2 + 4);
+        v.z = lds_u32u(img, o2 + 8);
+        v.w = lds_u32u(img, o2 + 12);
         *reinterpret_cast<u32x4 *>(g + lo) = v;
       } else {
         const int64_t x1 = lo + 16 < len ? lo + 16 : len;
@@ -1742,7 +1746,8 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     // when it exceeds dst_cap) and by the host after the last sync
     const uint64_t *need = d_table_off + nt_max; // = d_table_off[nt]: the lengths past nt are zero
     uint64_t *bo = pool.get<uint64_t>(nb_max);
-    ck_block_off_kernel<<<grid(nb_max), 256, 0, s>>>(btab, L, BL, tbf, d_table_off, bo);
+    uint64_t *brel = pool.get<uint64_t>(nb_max), *mo = pool.get<uint64_t>(nb_max);
+    ck_block_off_kernel<<<grid(nb_max), 256, 0, s>>>(btab, L, BL, tbf, d_table_off, tdata, MS, bo, brel, mo);
     // 6. encode blocks, meta entries, footers
     EncArgs ea{d_src, d_src, sstc_records{KR.type, KR.kl, KR.vl, KR.tx, KR.ko, KR.vo}, bf, nb_max, Pe, bo, blen, d_dst, 1};
     ea.nb_dev = dn + 1;
@@ -1758,9 +1763,9 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     ea.guard = guard;
     ea.xcd = 2; // XCD-chunked block order (the grid is the nb_max bound)
     CK(launch_enc_emit(ea, s));
-    ck_meta_kernel<<<static_cast<uint32_t>((nb_max + 255) / 256), 256, 0, s>>>(bmeta, L, btab, BL, MS, blen, tbf,
-                                                                              d_table_off, tdata, d_dst, need,
-                                                                              dst_cap, guard, d_src, src_end);
+    ck_meta_kernel<<<static_cast<uint32_t>((nb_max + 255) / 256), 256, 0, s>>>(bmeta, L, btab, brel, mo, MS, blen,
+                                                                              tbf, d_dst, need, dst_cap, guard,
+                                                                              d_src, src_end);
     ck_footer_kernel<<<static_cast<uint32_t>(nt_max), kFootThreads, 0, s>>>(L, tbf, d_table_off, tdata, tmeta, bmeta,
                                                                            d_dst, dst_cap, guard);
     CK(hipGetLastError());
