@@ -431,6 +431,35 @@ def test_segment_tiles_vs_oracle(codec, oracle, case):
         assert np.array_equal(got, want), (case, T)
 
 
+@pytest.mark.parametrize("case", ["serial_gate", "serial_fallback"])
+def test_segment_serial_walk_vs_oracle(codec, oracle, case):
+    """seg_walk_kernel's short-chain path (round 5): a 1024-record tile whose
+    first segment predicts <= 48 segments walks its window chains serially,
+    a walk past 64 segments falls back to pointer jumping.  serial_gate:
+    constant-weight runs of 22 / 21 / 16 / 32-record blocks at T = 4096 (both
+    sides of the 48 gate); serial_fallback: every tile starts with 600 tiny
+    records (one ~565-record segment, so the gate says serial) and ends with
+    424 one-record blocks (the walk passes 64 and the tile is redone by
+    pointer jumping)."""
+    if case == "serial_gate":
+        n = 40_000
+        w = np.array([190, 200, 256, 128])[(np.arange(n) // 5000) % 4]  # weight = 33 + key + value bytes
+        klen, vlen, T = np.zeros(n, np.int64), w - 33, 4096
+    else:
+        n = 1024 * 40
+        tiny = (np.arange(n) % 1024) < 600
+        klen = np.zeros(n, np.int64)
+        vlen = np.where(tiny, 0xFFFFFFFF, 20_000)  # no-value records weigh 29 B
+        T = 16384
+    rec = length_records(klen, vlen)
+    want = oracle.segment(rec, T)
+    got = cpu_u64(codec.segment(records_table(rec), T))
+    assert np.array_equal(got, want), case
+    if case == "serial_gate":  # the block lengths the runs were built for
+        L = np.diff(want)
+        assert {22, 21, 16, 32} <= set(L.tolist())
+
+
 @pytest.mark.parametrize("seed", range(3))
 def test_encode_span_alignments_vs_oracle(codec, oracle, seed):
     """Keys / values at every source alignment (arena offsets shuffled, so
