@@ -526,7 +526,9 @@ struct DecStage {
     return dev;
   }
 };
-thread_local std::map<int, DecStage> g_dec; // device -> staging
+// device -> staging: the input bytes + block index, and the record arrays
+// (sized by the real record count, known after the count kernel)
+thread_local std::map<int, DecStage> g_dec, g_dec_rec;
 } // namespace
 
 namespace {
@@ -545,16 +547,15 @@ int decode_on_device(sstc_ctx *ctx, const uint8_t *data, uint64_t bytes, const u
   static const uint8_t kZero[16] = {};
   const int dev = sstc__ctx_device(ctx);
   DeviceScope on_ctx_device(dev);
-  // one device region: the bytes, the block index, the counts and the record
-  // arrays sized by the most records the blocks can claim (the count kernel
-  // takes a trailer's n only when 16 n + 16 <= the block's length)
+  // one device region for the bytes, the block index, the counts and the
+  // block codes; the record arrays in a second one sized by the real count
+  // (the count kernel takes a trailer's n only when 16 n + 16 <= the block's
+  // length, so n <= nmax; round 5 sized them by nmax: ~4x the records of
+  // 150 B entries, 65 B each with the packed rows)
   const uint64_t nmax = sum_len / 16 + 1;
   const uint64_t o_src = 0, o_off = align256(bytes + 16), o_len = align256(o_off + 8 * nb),
                  o_base = align256(o_len + 8 * nb), o_st = align256(o_base + 8 * (nb + 1)),
-                 o_type = align256(o_st + 4 * nb + 4), o_kl = align256(o_type + nmax), o_vl = align256(o_kl + 4 * nmax),
-                 o_txn = align256(o_vl + 4 * nmax), o_ko = align256(o_txn + 8 * nmax),
-                 o_vo = align256(o_ko + 8 * nmax), o_x = align256(o_vo + 8 * nmax),
-                 total = align256(o_x + extra_per_rec * nmax);
+                 total = align256(o_st + 4 * nb + 4);
   uint8_t *d = g_dec[dev].get(total);
   h2d(ctx, d + o_src, bytes ? data : kZero, bytes ? bytes : 1);
   h2d(ctx, d + o_off, off, nb * 8);
@@ -564,12 +565,18 @@ int decode_on_device(sstc_ctx *ctx, const uint8_t *data, uint64_t bytes, const u
   check(sstc_count_records(ctx, d + o_src, d_off, d_len, nb, d_base), "sstc_count_records");
   base.resize(nb + 1);
   if (!d2h(ctx, base.data(), d_base, (nb + 1) * 8) || !sync(ctx)) return SSTC_E_HIP;
-  if (base[nb] > nmax) return SSTC_E_INVALID_ARG; // blocks claiming more entries than their bytes hold
-  rec = sstc_records{d + o_type, reinterpret_cast<uint32_t *>(d + o_kl), reinterpret_cast<uint32_t *>(d + o_vl),
-                     reinterpret_cast<uint64_t *>(d + o_txn), reinterpret_cast<uint64_t *>(d + o_ko),
-                     reinterpret_cast<uint64_t *>(d + o_vo)};
+  const uint64_t n = base[nb];
+  if (n > nmax) return SSTC_E_INVALID_ARG; // blocks claiming more entries than their bytes hold
+  const uint64_t r_type = 0, r_kl = align256(n + 1), r_vl = align256(r_kl + 4 * n + 4),
+                 r_txn = align256(r_vl + 4 * n + 4), r_ko = align256(r_txn + 8 * n + 8),
+                 r_vo = align256(r_ko + 8 * n + 8), r_x = align256(r_vo + 8 * n + 8),
+                 r_total = align256(r_x + extra_per_rec * n + 16);
+  uint8_t *r = g_dec_rec[dev].get(r_total);
+  rec = sstc_records{r + r_type, reinterpret_cast<uint32_t *>(r + r_kl), reinterpret_cast<uint32_t *>(r + r_vl),
+                     reinterpret_cast<uint64_t *>(r + r_txn), reinterpret_cast<uint64_t *>(r + r_ko),
+                     reinterpret_cast<uint64_t *>(r + r_vo)};
   d_st = reinterpret_cast<uint32_t *>(d + o_st);
-  d_extra = d + o_x;
+  d_extra = r + r_x;
   check(sstc_decode_blocks(ctx, d + o_src, d_off, d_len, nb, d_base, rec, txn_mode, d_st), "sstc_decode_blocks");
   return SSTC_OK;
 }
