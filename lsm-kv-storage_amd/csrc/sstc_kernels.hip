@@ -2184,10 +2184,14 @@ __global__ __launch_bounds__(kScanThreads) void scan_apply_kernel(In in, uint64_
 // the launch's: a context tags every scan on its own workspace with a new
 // epoch, so stale words of earlier calls are ignored and no memset precedes
 // the scan (epoch 0 = the caller cleared the words in an earlier kernel).
-// Tiles are numbered by a ticket counter so every tile a workgroup waits on is
-// already resident; the tile that draws the last ticket resets the counter
-// for the next launch.  ws = [ticket, status[tiles]].
+// Tile = workgroup id: workgroups are dispatched in id order, so every tile a
+// workgroup waits on is resident or done (round 4 drew a ticket per tile from
+// a device-scope counter; SSTC_SCAN_TICKET=1 builds that for A/B).
+// ws = [unused, status[tiles]].
 constexpr uint32_t kLbItems = 16;
+#ifndef SSTC_SCAN_TICKET
+#define SSTC_SCAN_TICKET 0
+#endif
 
 __device__ __forceinline__ uint32_t lb_idx(uint32_t i) { return i + (i >> 4); } // 1 pad per 16
 
@@ -2197,8 +2201,10 @@ __global__ __launch_bounds__(kScanThreads) void scan_lookback_kernel(In in, uint
   constexpr uint32_t kTile = kScanThreads * kItems;
   __shared__ uint64_t sm[kTile + kTile / 16];
   __shared__ uint64_t s_wsum[kScanThreads / kWave];
-  __shared__ uint64_t s_tile, s_prefix;
+  __shared__ uint64_t s_prefix;
   const uint32_t tid = threadIdx.x, lane = lane_id(), w = tid / kWave;
+#if SSTC_SCAN_TICKET
+  __shared__ uint64_t s_tile;
   if (tid == 0) {
     const uint64_t t = __hip_atomic_fetch_add(ws, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (t + 1 == gridDim.x) __hip_atomic_store(ws, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2206,6 +2212,11 @@ __global__ __launch_bounds__(kScanThreads) void scan_lookback_kernel(In in, uint
   }
   __syncthreads();
   const uint64_t tile = s_tile;
+#else
+  // tile = workgroup id (dispatched in id order: the lowest unfinished tile
+  // is resident, as in ck_filter_kernel; ws[0] is unused)
+  const uint64_t tile = blockIdx.x;
+#endif
   const uint64_t base = tile * kTile;
   const uint64_t tag = static_cast<uint64_t>(epoch) << kLbEpochShift;
   uint64_t *status = ws + 1;
