@@ -46,6 +46,28 @@ def test_bench_launches_n_ranks(n):
     assert c4["GiBps_aggregate"] > 0 and all(p["GiBps"] > 0 for p in c4["per_rank"])
 
 
+def test_one_rank_process_group_under_a_launcher():
+    """SSTC_PG_SINGLE=1 under torch.distributed.run: a one-rank process group
+    is built (gloo here; tests/test_gpu_bench_rank.py does the same with
+    RCCL on the GPU box), and the collectives run through it."""
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    env = os.environ.copy()
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    env["SSTC_PG_SINGLE"] = "1"
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+                        "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.join(ROOT, "bench.py"),
+                        "--gpus", "1", "--plumbing", "--steps", "2", "--warmup", "1"],
+                       capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "[sstc] process group: gloo, world 1" in r.stderr
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert out["n_gpus"] == 1 and out["compact_config4"]["n_gpus"] == 1
+
+
 def test_bench_refuses_world_mismatch():
     # an external launcher with WORLD_SIZE=1 while --gpus 2 was asked for
     r = run_bench(["--gpus", "2", "--plumbing", "--steps", "1"],
