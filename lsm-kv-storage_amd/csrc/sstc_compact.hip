@@ -1231,6 +1231,16 @@ __global__ __launch_bounds__(256) void ck_meta_kernel(const uint64_t *bmeta, Lay
   }
 }
 
+struct FootWords { // (ck_footer_kernel's copy of Words: declared before it)
+  const uint64_t *p[8];
+  uint32_t n;
+};
+struct FootDone {
+  FootWords w;     // the device words the host reads after the job
+  uint64_t *host;  // pinned, device-mapped host words
+  unsigned int *ticket; // zeroed by ck_start_kernel
+};
+
 // footer of table t (table_builder.cc:179-211), one workgroup per table: its
 // min / max txn (table_builder.cc:47-49) reduced from the blocks' (the encode
 // wrote every block's), then the 40 B footer.  (Round 4: folded the separate
@@ -1239,49 +1249,64 @@ constexpr uint32_t kFootThreads = 1024;
 __global__ __launch_bounds__(kFootThreads) void ck_footer_kernel(Lay L, const uint64_t *tbf, const uint64_t *toff,
                                                                  const uint64_t *tdata, const uint64_t *tmeta,
                                                                  const uint64_t *bmeta, uint8_t *dst, uint64_t cap,
-                                                                 unsigned long long *guard) {
+                                                                 unsigned long long *guard, FootDone done) {
   __shared__ uint64_t smn[kFootThreads / kWave], smx[kFootThreads / kWave];
   const uint64_t t = blockIdx.x;
-  if (!L.ok()) return;
-  const uint64_t nt = L.nt();
-  if (t >= nt || toff[nt] > cap) return; // uniform over the workgroup
-  const uint64_t f = tbf[t], e = tbf[t + 1];
-  const uint64_t o = toff[t], dbytes = tdata[t], mbytes = tmeta[t]; // in flight with the reduction's loads
-  uint64_t mn = ~0ull, mx = 0;
+  const uint64_t nt = L.ok() ? L.nt() : 0;
+  if (L.ok() && t < nt && toff[nt] <= cap) { // uniform over the workgroup
+    const uint64_t f = tbf[t], e = tbf[t + 1];
+    const uint64_t o = toff[t], dbytes = tdata[t], mbytes = tmeta[t]; // in flight with the reduction's loads
+    uint64_t mn = ~0ull, mx = 0;
 #pragma unroll 4
-  for (uint64_t b = f + threadIdx.x; b < e; b += kFootThreads) {
-    const u32x4 v = *reinterpret_cast<const u32x4 *>(bmeta + 4 * b); // min, max
-    const uint64_t x = static_cast<uint64_t>(v.x) | static_cast<uint64_t>(v.y) << 32;
-    const uint64_t y = static_cast<uint64_t>(v.z) | static_cast<uint64_t>(v.w) << 32;
-    mn = x < mn ? x : mn;
-    mx = y > mx ? y : mx;
+    for (uint64_t b = f + threadIdx.x; b < e; b += kFootThreads) {
+      const u32x4 v = *reinterpret_cast<const u32x4 *>(bmeta + 4 * b); // min, max
+      const uint64_t x = static_cast<uint64_t>(v.x) | static_cast<uint64_t>(v.y) << 32;
+      const uint64_t y = static_cast<uint64_t>(v.z) | static_cast<uint64_t>(v.w) << 32;
+      mn = x < mn ? x : mn;
+      mx = y > mx ? y : mx;
+    }
+    for (uint32_t d = kWave / 2; d > 0; d >>= 1) {
+      const uint64_t x = __shfl_xor(mn, d, kWave), y = __shfl_xor(mx, d, kWave);
+      mn = x < mn ? x : mn;
+      mx = y > mx ? y : mx;
+    }
+    if (lane_id() == 0) {
+      smn[threadIdx.x / kWave] = mn;
+      smx[threadIdx.x / kWave] = mx;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      for (uint32_t w = 1; w < kFootThreads / kWave; w++) {
+        mn = smn[w] < mn ? smn[w] : mn;
+        mx = smx[w] > mx ? smx[w] : mx;
+      }
+      const uint64_t at = o + dbytes + mbytes;
+      if (at < o || at > cap || cap - at < 40) { // the footer must end inside the output buffer
+        atomicOr(guard, kGuardFooter);
+      } else {
+        uint8_t *p = dst + at;
+        put_le(p, e - f, 8);
+        put_le(p + 8, dbytes, 8);
+        put_le(p + 16, mbytes, 8);
+        put_le(p + 24, mn, 8);
+        put_le(p + 32, mx, 8);
+      }
+    }
   }
-  for (uint32_t d = kWave / 2; d > 0; d >>= 1) {
-    const uint64_t x = __shfl_xor(mn, d, kWave), y = __shfl_xor(mx, d, kWave);
-    mn = x < mn ? x : mn;
-    mx = y > mx ? y : mx;
+  // the job's completion words to the pinned host words by the last footer
+  // workgroup to finish (round 5: a one-workgroup pack kernel after this
+  // one); a footer's guard bit is released before its ticket, the last
+  // arriver acquires before it reads the words.  The host synchronises the
+  // stream, then reads them.
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    if (__hip_atomic_fetch_add(done.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      for (uint32_t i = 0; i < done.w.n; i++)
+        done.host[i] = __hip_atomic_load(done.w.p[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __threadfence_system();
+    }
   }
-  if (lane_id() == 0) {
-    smn[threadIdx.x / kWave] = mn;
-    smx[threadIdx.x / kWave] = mx;
-  }
-  __syncthreads();
-  if (threadIdx.x != 0) return;
-  for (uint32_t w = 1; w < kFootThreads / kWave; w++) {
-    mn = smn[w] < mn ? smn[w] : mn;
-    mx = smx[w] > mx ? smx[w] : mx;
-  }
-  const uint64_t at = o + dbytes + mbytes;
-  if (at < o || at > cap || cap - at < 40) { // the footer must end inside the output buffer
-    atomicOr(guard, kGuardFooter);
-    return;
-  }
-  uint8_t *p = dst + at;
-  put_le(p, e - f, 8);
-  put_le(p + 8, dbytes, 8);
-  put_le(p + 16, mbytes, 8);
-  put_le(p + 24, mn, 8);
-  put_le(p + 32, mx, 8);
 }
 
 // ------------------------------------------------------------------ host side
@@ -1394,7 +1419,7 @@ __global__ __launch_bounds__(256) void ck_start_kernel(const uint64_t *rec_base,
     *bad = 0;
     guard[0] = 0; // consistency-guard bits
     guard[1] = e; // the end of the source bytes the input blocks span
-    for (int g = 0; g < 9; g++) guard[32 + 32 * g] = 0; // ck_check_blocks_kernel's tickets
+    for (int g = 0; g < 10; g++) guard[32 + 32 * g] = 0; // the check kernel's 9 tickets, the footer's
   }
   __threadfence_system();
   __syncthreads();
@@ -1508,8 +1533,8 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     // consistency guard: [0] bits set by any check of the job, [1] the end of
     // the source bytes its blocks span (both cleared by ck_start_kernel)
     // guard[0] bits, guard[1] source end; guard + 32 the check kernel's 9
-    // ticket counters, 256 B apart (u32 at guard + 32 + 32 g)
-    unsigned long long *guard = reinterpret_cast<unsigned long long *>(pool.get<uint64_t>(32 + 9 * 32));
+    // ticket counters, then the footer's, 256 B apart (u32 at guard + 32 + 32 g)
+    unsigned long long *guard = reinterpret_cast<unsigned long long *>(pool.get<uint64_t>(32 + 10 * 32));
     const uint64_t *src_end = reinterpret_cast<const uint64_t *>(guard + 1);
     // record index of every input table's first record (its run start): the
     // table first blocks travel in the pinned upload words (no copy command),
@@ -1766,13 +1791,20 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     ck_meta_kernel<<<static_cast<uint32_t>((nb_max + 255) / 256), 256, 0, s>>>(bmeta, L, btab, brel, mo, MS, blen,
                                                                               tbf, d_dst, need, dst_cap, guard,
                                                                               d_src, src_end);
+    ensure_host(arena, 9);
+    FootDone done{};
+    {
+      const std::initializer_list<const uint64_t *> words = {
+          reinterpret_cast<const uint64_t *>(err_count), errs, reinterpret_cast<const uint64_t *>(bad),
+          reinterpret_cast<const uint64_t *>(guard), need, dn, dn + 1, totals};
+      for (const uint64_t *p : words) done.w.p[done.w.n++] = p;
+    }
+    done.host = arena.host_dev;
+    done.ticket = reinterpret_cast<unsigned int *>(guard + 32 + 32 * 9);
     ck_footer_kernel<<<static_cast<uint32_t>(nt_max), kFootThreads, 0, s>>>(L, tbf, d_table_off, tdata, tmeta, bmeta,
-                                                                           d_dst, dst_cap, guard);
+                                                                           d_dst, dst_cap, guard, done);
     CK(hipGetLastError());
-    fetch(arena, s,
-          {reinterpret_cast<const uint64_t *>(err_count), errs, reinterpret_cast<const uint64_t *>(bad),
-           reinterpret_cast<const uint64_t *>(guard), need, dn, dn + 1, totals},
-          nullptr, 0, true);
+    CK(hipStreamSynchronize(s));
     if (const int r = job_error(arena.host)) return r;
     res[1] = arena.host[7];
     res[4] = arena.host[4];
