@@ -132,6 +132,35 @@ def test_unmodified_compact_cc_gpu_decode_and_encode(tmp_path, name):
 
 
 TIMED = ("config3", "config4_rank0", "config5")
+ASAN_EXE = os.path.join(ROOT, "oracle", "_ref", "compact_dropin_asan")
+ASAN_ENV = {"ASAN_OPTIONS": "detect_leaks=0:halt_on_error=1"}
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("name", [n for n in ("cj_small", "cj_zipf", "probe100", "config5") if n in RUNNABLE])
+def test_dropin_host_code_under_asan(tmp_path, name):
+    """The drop-in's host code -- the unmodified compact.cc / merge_iterator.cc
+    and the drop-in iterator over its mapped data sections -- built with
+    AddressSanitizer (`make -C oracle dropin-asan`; libsstcodec.so itself
+    uninstrumented): no report, outputs the reference's.  Includes cj_zipf and
+    config 5, where the reference as written reads freed memory
+    (compact.cc:250, aswritten.json)."""
+    need(ASAN_EXE)
+    from oracle import table_key_range
+    case = MANIFEST[name]
+    sets, T, limit = case_inputs(name)
+    ins = build_inputs(tmp_path, sets, T)
+    args = [ASAN_EXE, str(tmp_path / "db"), str(T), str(limit)]
+    (tmp_path / "db").mkdir()
+    for p, fs, rec in ins:
+        lo, hi = table_key_range(rec)
+        args += [p, str(fs), lo.hex() or "-", hi.hex() or "-"]
+    r = subprocess.run(args, capture_output=True, text=True, timeout=540, env=dict(os.environ, **ASAN_ENV))
+    assert "AddressSanitizer" not in r.stderr, r.stderr[-3000:]
+    assert r.returncode == 0, r.stderr[-2000:]
+    _, outs = G.parse_pick_output(r.stdout)
+    got = [(sha(np.fromfile(p, np.uint8)), fs) for p, fs, _, _ in outs]
+    assert got == [(o["sha256"], o["file_size"]) for o in case["fixed_outputs"]]
 
 
 @pytest.mark.parametrize("name", [n for n in ("cj_small", "probe100") if n in RUNNABLE])
@@ -238,11 +267,14 @@ def test_iterator_trace_equals_reference(oracle, tmp_path):
     need(REF_EXE)
     args = trace_tables(oracle, tmp_path)
     dumps = []
-    for exe, tag in ((REF_EXE, "ref"), (EXE, "dropin")):
+    runs = [(REF_EXE, "ref"), (EXE, "dropin")] + ([(ASAN_EXE, "dropin_asan")] if os.path.exists(ASAN_EXE) else [])
+    for exe, tag in runs:
         d = str(tmp_path / f"{tag}.dump")
-        r = subprocess.run([exe, "--iter", d] + args, capture_output=True, text=True, timeout=120)
+        r = subprocess.run([exe, "--iter", d] + args, capture_output=True, text=True, timeout=240,
+                           env=dict(os.environ, **ASAN_ENV))
+        assert "AddressSanitizer" not in r.stderr, (tag, r.stderr[-3000:])
         assert r.returncode == 0, (tag, r.stderr[-2000:])
         dumps.append((r.stdout.strip(), open(d, "rb").read()))
-    assert dumps[0][0] == dumps[1][0] and dumps[0][0].startswith("iter ok ")
-    assert len(dumps[0][1]) > 1_000_000
-    assert dumps[0][1] == dumps[1][1]
+    assert dumps[0][0].startswith("iter ok ") and len(dumps[0][1]) > 1_000_000
+    for out, dump in dumps[1:]:  # the drop-in (and its ASan build) walk exactly as the reference does
+        assert out == dumps[0][0] and dump == dumps[0][1]
