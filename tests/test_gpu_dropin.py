@@ -133,24 +133,28 @@ def test_unmodified_compact_cc_gpu_decode_and_encode(tmp_path, name):
 
 TIMED = ("config3", "config4_rank0", "config5")
 ASAN_EXE = os.path.join(ROOT, "oracle", "_ref", "compact_dropin_asan")
+# tools/build_asan.sh: the same harness with libsstcodec.so's own host code
+# (TableBuilder, DecodeTable, the compaction job's host side) under ASan too
+ASAN_LIB_EXE = os.path.join(ROOT, "oracle", "_ref", "compact_dropin_asan_lib")
 ASAN_ENV = {"ASAN_OPTIONS": "detect_leaks=0:halt_on_error=1"}
 
 
 @pytest.mark.timeout(600)
+@pytest.mark.parametrize("exe", [ASAN_EXE, ASAN_LIB_EXE], ids=["engine", "engine+lib"])
 @pytest.mark.parametrize("name", [n for n in ("cj_small", "cj_zipf", "probe100", "config5") if n in RUNNABLE])
-def test_dropin_host_code_under_asan(tmp_path, name):
+def test_dropin_host_code_under_asan(tmp_path, name, exe):
     """The drop-in's host code -- the unmodified compact.cc / merge_iterator.cc
     and the drop-in iterator over its mapped data sections -- built with
     AddressSanitizer (`make -C oracle dropin-asan`; libsstcodec.so itself
     uninstrumented): no report, outputs the reference's.  Includes cj_zipf and
     config 5, where the reference as written reads freed memory
     (compact.cc:250, aswritten.json)."""
-    need(ASAN_EXE)
+    need(exe)
     from oracle import table_key_range
     case = MANIFEST[name]
     sets, T, limit = case_inputs(name)
     ins = build_inputs(tmp_path, sets, T)
-    args = [ASAN_EXE, str(tmp_path / "db"), str(T), str(limit)]
+    args = [exe, str(tmp_path / "db"), str(T), str(limit)]
     (tmp_path / "db").mkdir()
     for p, fs, rec in ins:
         lo, hi = table_key_range(rec)
@@ -267,7 +271,8 @@ def test_iterator_trace_equals_reference(oracle, tmp_path):
     need(REF_EXE)
     args = trace_tables(oracle, tmp_path)
     dumps = []
-    runs = [(REF_EXE, "ref"), (EXE, "dropin")] + ([(ASAN_EXE, "dropin_asan")] if os.path.exists(ASAN_EXE) else [])
+    runs = [(REF_EXE, "ref"), (EXE, "dropin")] + [(x, os.path.basename(x)) for x in (ASAN_EXE, ASAN_LIB_EXE)
+                                                   if os.path.exists(x)]
     for exe, tag in runs:
         d = str(tmp_path / f"{tag}.dump")
         r = subprocess.run([exe, "--iter", d] + args, capture_output=True, text=True, timeout=240,
