@@ -117,7 +117,8 @@ int next_epoch(sstc_ctx *c, uint32_t &epoch) {
 // one-kernel block offsets (a tile per 256 blocks, finer than the scans'), so
 // that no call after sstc_ctx_reserve grows the workspace
 int ensure_blocks(sstc_ctx *c, uint64_t nb) {
-  return ensure_scan_words(c, std::max(sstc::scan_workspace_elems(nb + 1), sstc::enc_offsets_workspace(nb)));
+  return ensure_scan_words(c, std::max({sstc::scan_workspace_elems(nb + 1), sstc::enc_offsets_workspace(nb),
+                                        sstc::count_scan_workspace(nb)}));
 }
 
 int ensure_records(sstc_ctx *c, uint64_t nr) {
@@ -217,7 +218,7 @@ int sstc_ctx_destroy(sstc_ctx *c) {
     delete hp;
   }
   if (c->switch_ev) (void)hipEventDestroy(c->switch_ev);
-  for (void *p : {c->counters, c->arena.base,
+  for (void *p : {c->counters, c->arena.base, static_cast<void *>(c->arena.lb),
                   static_cast<void *>(c->scan_ws),
                   static_cast<void *>(c->P), static_cast<void *>(c->jump)})
     if (p) (void)hipFree(p);
@@ -279,11 +280,18 @@ int sstc_count_records(sstc_ctx *c, const uint8_t *d_src, const uint64_t *d_blk_
   if (!c || !d_rec_base || (nblocks && (!d_src || !d_blk_off || !d_blk_len)))
     return fail(SSTC_E_INVALID_ARG, "sstc_count_records: NULL argument");
   if (int r = bind_device(c)) return r;
-  if (int r = ensure_scan(c, nblocks + 1)) return r;
+  if (int r = ensure_scan_words(c, sstc::count_scan_workspace(nblocks))) return r;
   uint32_t ep = 0;
   if (int r = next_epoch(c, ep)) return r;
-  SSTC_HIP(sstc::launch_count(d_src, d_blk_off, d_blk_len, nblocks, d_rec_base, c->stream), "count kernel");
-  SSTC_HIP(sstc::launch_scan(d_rec_base, nblocks, 0, d_rec_base, c->scan_ws, c->stream, false, ep), "scan");
+  sstc::CountScanArgs a{};
+  a.src = d_src;
+  a.blk_off = d_blk_off;
+  a.blk_len = d_blk_len;
+  a.nblocks = nblocks;
+  a.rec_base = d_rec_base;
+  a.ws = c->scan_ws;
+  a.epoch = ep;
+  SSTC_HIP(sstc::launch_count_scan(a, false, c->stream), "count + scan kernel");
   return SSTC_OK;
 }
 

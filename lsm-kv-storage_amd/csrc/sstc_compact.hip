@@ -1238,7 +1238,7 @@ struct FootWords { // (ck_footer_kernel's copy of Words: declared before it)
 struct FootDone {
   FootWords w;     // the device words the host reads after the job
   uint64_t *host;  // pinned, device-mapped host words
-  unsigned int *ticket; // zeroed by ck_start_kernel
+  unsigned int *ticket; // zeroed by count_scan_kernel<true>
 };
 
 // footer of table t (table_builder.cc:179-211), one workgroup per table: its
@@ -1377,53 +1377,20 @@ __global__ __launch_bounds__(256) void ck_pack_kernel(Words w, const uint64_t *a
   if (threadIdx.x == 0) __hip_atomic_store(out + flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// The job's first host hand-off in ONE kernel (round 5: it replaced a
-// tfb copy command, a run-starts kernel and a pack kernel): run starts (record
-// index of every input table's first block, tfb read from the pinned upload
-// words) to the device and, with the input block bytes, to the pinned host
-// words, then the sequence word the host spins on.  Thread 0 also snapshots
-// the context's decode error counter and clears the job's unsorted count,
-// guard bits and the check kernel's tickets.  One workgroup: every host word
-// is stored before the fence that precedes the sequence word.
-__global__ __launch_bounds__(256) void ck_start_kernel(const uint64_t *rec_base, const uint64_t *tfb, uint64_t n,
-                                                       uint64_t *out, const unsigned long long *err_count,
-                                                       uint64_t *errs, unsigned long long *bad,
-                                                       unsigned long long *guard, const uint64_t *len_part,
-                                                       uint64_t nparts, uint64_t *host, uint64_t seq, uint64_t flag) {
-  __shared__ uint64_t s_part[256 / kWave], s_end[256 / kWave];
-  uint64_t v = 0, e = 0;
-  for (uint64_t p = threadIdx.x; p < nparts; p += 256) { // the count kernel's per-workgroup {byte sum, source end}
-    v += len_part[2 * p];
-    e = len_part[2 * p + 1] > e ? len_part[2 * p + 1] : e;
+// the persistent region of count_scan_kernel<true> (Arena::lb): zero when
+// (re)allocated, left zero by every launch (its last tile clears it)
+void ensure_lb(Arena &arena, uint64_t words, hipStream_t s) {
+  if (arena.lb && arena.lb_cap >= words) return;
+  if (arena.lb) {
+    CK(hipStreamSynchronize(s));
+    (void)hipFree(arena.lb);
   }
-  v = wave_sum_u64(v);
-  for (uint32_t d = kWave / 2; d > 0; d >>= 1) {
-    const uint64_t y = __shfl_xor(e, d, kWave);
-    e = y > e ? y : e;
-  }
-  if (lane_id() == 0) {
-    s_part[threadIdx.x / kWave] = v;
-    s_end[threadIdx.x / kWave] = e;
-  }
-  for (uint64_t i = threadIdx.x; i < n; i += 256) {
-    const uint64_t r = rec_base[tfb[i]];
-    out[i] = r;
-    host[1 + i] = r;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    static_assert(256 / kWave == 4, "the count kernel's per-wave partials: four wave64s");
-    host[0] = s_part[0] + s_part[1] + s_part[2] + s_part[3]; // input block bytes
-    for (uint32_t w = 1; w < 256 / kWave; w++) e = s_end[w] > e ? s_end[w] : e;
-    *errs = *err_count;
-    *bad = 0;
-    guard[0] = 0; // consistency-guard bits
-    guard[1] = e; // the end of the source bytes the input blocks span
-    for (int g = 0; g < 10; g++) guard[32 + 32 * g] = 0; // the check kernel's 9 tickets, the footer's
-  }
-  __threadfence_system();
-  __syncthreads();
-  if (threadIdx.x == 0) __hip_atomic_store(host + flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  arena.lb = nullptr;
+  arena.lb_cap = 0;
+  const uint64_t cap = words < 1024 ? 1024 : words + words / 4;
+  CK(hipMalloc(reinterpret_cast<void **>(&arena.lb), cap * sizeof(uint64_t)));
+  arena.lb_cap = cap;
+  CK(hipMemsetAsync(arena.lb, 0, cap * sizeof(uint64_t), s));
 }
 
 // pinned, device-mapped, coherent host words: kernels store the job's few
@@ -1512,7 +1479,6 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
                  uint64_t *res, std::string &err) {
   try {
     Pool pool(arena);
-    const uint64_t nws = scan_workspace_elems(nblocks + 1) + 64;
     // Host syncs: (1) the run starts and the input block bytes (they size
     // every array and bound the output counts), (2) completion with the
     // output size, the table / block counts and the error flags (the
@@ -1522,16 +1488,13 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     // the host enqueues the whole tail while the merge runs.
     // 1. decode every block
     uint64_t *rb_all = pool.get<uint64_t>(nblocks + 1);
-    uint64_t *ws = pool.get<uint64_t>(nws);
     uint64_t *errs = pool.get<uint64_t>(2);
     uint64_t *d_rs = pool.get<uint64_t>(ntables + 1);
-    const uint64_t nparts = (nblocks + 255) / 256;
-    uint64_t *len_part = pool.get<uint64_t>(2 * nparts + 2);
-    CK(launch_count(d_src, d_blk_off, d_blk_len, nblocks, rb_all, s, ws, len_part));
-    CK(launch_scan(rb_all, nblocks, 0, rb_all, ws, s, true));
+    uint64_t *part = pool.get<uint64_t>(2 * count_scan_tiles(nblocks));
+    ensure_lb(arena, count_scan_workspace(nblocks), s);
     unsigned long long *bad = reinterpret_cast<unsigned long long *>(pool.get<uint64_t>(1));
     // consistency guard: [0] bits set by any check of the job, [1] the end of
-    // the source bytes its blocks span (both cleared by ck_start_kernel)
+    // the source bytes its blocks span (both set by count_scan_kernel<true>)
     // guard[0] bits, guard[1] source end; guard + 32 the check kernel's 9
     // ticket counters, then the footer's, 256 B apart (u32 at guard + 32 + 32 g)
     unsigned long long *guard = reinterpret_cast<unsigned long long *>(pool.get<uint64_t>(32 + 10 * 32));
@@ -1544,9 +1507,26 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     ensure_host(arena, 8 + ntables + 2);
     {
       const uint64_t flag = arena.host_cap - 1, seq = ++arena.seq;
-      ck_start_kernel<<<1, 256, 0, s>>>(rb_all, reinterpret_cast<const uint64_t *>(arena.up_dev), ntables + 1, d_rs,
-                                         err_count, errs, bad, guard, len_part, nparts, arena.host_dev, seq, flag);
-      CK(hipGetLastError());
+      CountScanArgs ca{};
+      ca.src = d_src;
+      ca.blk_off = d_blk_off;
+      ca.blk_len = d_blk_len;
+      ca.nblocks = nblocks;
+      ca.rec_base = rb_all;
+      ca.ws = arena.lb;
+      ca.epoch = 0;
+      ca.part = part;
+      ca.tfb = reinterpret_cast<const uint64_t *>(arena.up_dev);
+      ca.ntfb = ntables + 1;
+      ca.run_start = d_rs;
+      ca.err_count = err_count;
+      ca.errs = errs;
+      ca.bad = bad;
+      ca.guard = guard;
+      ca.host = arena.host_dev;
+      ca.seq = seq;
+      ca.flag = flag;
+      CK(launch_count_scan(ca, true, s));
       wait_seq(arena, s, flag, seq);
     }
     const uint64_t in_bytes = arena.host[0]; // every survivor's entry lies in these bytes

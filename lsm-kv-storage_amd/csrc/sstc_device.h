@@ -177,6 +177,43 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
   return v;
 }
 
+// One wave of tile `tile`: publishes the tile's total, looks back over the
+// status words of the tiles before it (64 per round) until an inclusive one,
+// publishes its own inclusive prefix and returns the exclusive prefix
+// (wave-uniform; tile 0: 0).  Words of another epoch are not published yet.
+__device__ __forceinline__ uint64_t lb_publish_lookback(uint64_t *status, uint64_t tile, uint64_t total,
+                                                        uint32_t epoch) {
+  const uint32_t lane = lane_id();
+  const uint64_t tag = static_cast<uint64_t>(epoch) << kLbEpochShift;
+  if (tile == 0) {
+    if (lane == 0) __hip_atomic_store(&status[0], kLbInc | tag | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return 0;
+  }
+  if (lane == 0) __hip_atomic_store(&status[tile], kLbAgg | tag | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  uint64_t prefix = 0;
+  int64_t p = static_cast<int64_t>(tile) - 1; // window [p - 63, p]
+  uint64_t spins = 0;
+  for (;;) {
+    const int64_t q = p - static_cast<int64_t>(lane);
+    uint64_t st = q >= 0 ? __hip_atomic_load(&status[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kLbInc | tag;
+    if (((st >> kLbEpochShift) & 0x3FFFu) != epoch) st = 0; // a stale word: not published yet
+    const uint64_t inc = __ballot((st >> 62) == 2);
+    const uint32_t need = inc ? static_cast<uint32_t>(__ffsll(static_cast<long long>(inc))) : kWave;
+    const uint64_t zero = __ballot((st >> 62) == 0 && lane < need);
+    if (zero) {
+      if (++spins > kLbSpinLimit) break; // a predecessor never published: give up (wrong sums, no hang)
+      __builtin_amdgcn_s_sleep(1);
+      continue;
+    }
+    prefix += wave_sum_u64(lane < need ? (st & kLbVal) : 0);
+    if (inc) break;
+    p -= kWave;
+  }
+  if (lane == 0)
+    __hip_atomic_store(&status[tile], kLbInc | tag | (prefix + total), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return prefix;
+}
+
 // LDS writes of one lane are made visible to the other lanes of the SAME wave:
 // LDS executes a wave's DS instructions in order, so only a compiler barrier
 // and the lgkmcnt drain are needed (no s_barrier).

@@ -6,9 +6,10 @@
 //                       large ones parsed from HBM and streamed through the
 //                       wave's LDS slot (replaces the per-block work of
 //                       db/compact.cc:254-302 on surviving records).
-//   count_kernel        per-block entry count from the 16 B extra
+//   count_scan_kernel   per-block entry counts from the 16 B extras
 //                       (TableReader::CreateAndSetupDataForBlockReader,
-//                       sstable/table_reader.cc:226-232).
+//                       sstable/table_reader.cc:226-232) scanned into
+//                       record bases, one kernel.
 //   decode_kernel       per-entry parse into a record table
 //                       (BlockReader accessors, sstable/block_reader.cc:59-114).
 //   enc_*_kernel        records -> blocks (BlockBuilder, block_builder.cc:12-109).
@@ -477,49 +478,6 @@ __global__ __launch_bounds__(kRtWaves *kWave, 8) void rt_kernel(RtArgs a) {
 // ---------------------------------------------------------------------------
 // Decode to the record table.
 // ---------------------------------------------------------------------------
-// grid-stride clear of nz words (a following scan's look-back status words),
-// folded into a kernel that runs anyway instead of a memset command
-__device__ __forceinline__ void zero_words(uint64_t *w, uint64_t nz) {
-  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
-  for (uint64_t z = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; z < nz; z += stride) w[z] = 0;
-}
-
-__global__ void count_kernel(const uint8_t *src, const uint64_t *blk_off, const uint64_t *blk_len,
-                             uint64_t nblocks, uint64_t *counts, uint64_t *zws, uint64_t nz, uint64_t *len_part) {
-  const uint64_t b = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  zero_words(zws, nz); // the look-back status words of the scan that follows
-  const uint64_t len = b < nblocks ? blk_len[b] : 0;
-  if (len_part) { // uniform: the workgroup's byte sum (bounds the compaction's output counts) and the
-                  // end of the source bytes its blocks span (bounds every entry the compaction copies)
-    static_assert(256 / kWave == 4, "count_kernel: 256-thread workgroups of four wave64s");
-    __shared__ uint64_t s_part[256 / kWave], s_end[256 / kWave];
-    const uint64_t v = wave_sum_u64(len);
-    uint64_t e = b < nblocks ? blk_off[b] + len : 0;
-    for (uint32_t d = kWave / 2; d > 0; d >>= 1) {
-      const uint64_t y = __shfl_xor(e, d, kWave);
-      e = y > e ? y : e;
-    }
-    if (lane_id() == 0) {
-      s_part[threadIdx.x / kWave] = v;
-      s_end[threadIdx.x / kWave] = e;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      len_part[2 * blockIdx.x] = s_part[0] + s_part[1] + s_part[2] + s_part[3];
-      const uint64_t e01 = s_end[0] > s_end[1] ? s_end[0] : s_end[1], e23 = s_end[2] > s_end[3] ? s_end[2] : s_end[3];
-      len_part[2 * blockIdx.x + 1] = e01 > e23 ? e01 : e23;
-    }
-  }
-  if (b >= nblocks) return;
-  uint64_t c = 0;
-  if (len >= 16) {
-    const uint8_t *blk = src + blk_off[b];
-    const uint64_t n = g_u64u(blk + len - 16), doff = g_u64u(blk + len - 8);
-    if (check_extra(len, n, doff) == kBlkOk) c = n;
-  }
-  counts[b] = c;
-}
-
 constexpr uint32_t kDecWaves = 4;
 
 // Parse one block into the record table (and, when asked, the 32 B sort keys
@@ -2218,7 +2176,6 @@ __global__ __launch_bounds__(kScanThreads) void scan_lookback_kernel(In in, uint
   const uint64_t tile = blockIdx.x;
 #endif
   const uint64_t base = tile * kTile;
-  const uint64_t tag = static_cast<uint64_t>(epoch) << kLbEpochShift;
   uint64_t *status = ws + 1;
 #pragma unroll
   for (uint32_t j = 0; j < kItems; j++) {
@@ -2243,34 +2200,7 @@ __global__ __launch_bounds__(kScanThreads) void scan_lookback_kernel(In in, uint
     total += x;
   }
   if (w == 0) {
-    uint64_t prefix = 0;
-    if (tile == 0) {
-      if (lane == 0) __hip_atomic_store(&status[0], kLbInc | tag | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      if (lane == 0) __hip_atomic_store(&status[tile], kLbAgg | tag | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      int64_t p = static_cast<int64_t>(tile) - 1; // window [p - 63, p]
-      uint64_t spins = 0;
-      for (;;) {
-        const int64_t q = p - static_cast<int64_t>(lane);
-        uint64_t st = q >= 0 ? __hip_atomic_load(&status[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                             : kLbInc | tag;
-        if (((st >> kLbEpochShift) & 0x3FFFu) != epoch) st = 0; // a stale word: not published yet
-        const uint64_t inc = __ballot((st >> 62) == 2);
-        const uint32_t need = inc ? static_cast<uint32_t>(__ffsll(static_cast<long long>(inc))) : kWave;
-        const uint64_t zero = __ballot((st >> 62) == 0 && lane < need);
-        if (zero) {
-          if (++spins > kLbSpinLimit) break; // a predecessor never published: give up (wrong sums, no hang)
-          __builtin_amdgcn_s_sleep(1);
-          continue;
-        }
-        prefix += wave_sum_u64(lane < need ? (st & kLbVal) : 0);
-        if (inc) break;
-        p -= kWave;
-      }
-      if (lane == 0)
-        __hip_atomic_store(&status[tile], kLbInc | tag | (prefix + total), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-    }
+    const uint64_t prefix = lb_publish_lookback(status, tile, total, epoch);
     if (lane == 0) s_prefix = prefix;
   }
   __syncthreads();
@@ -2287,6 +2217,191 @@ __global__ __launch_bounds__(kScanThreads) void scan_lookback_kernel(In in, uint
     if (base + i < n) out[base + i] = sm[lb_idx(i)];
   }
   if (tid == 0 && base < n && n <= base + kTile) out[n] = carry_in + s_prefix + total;
+}
+
+// Record bases of the blocks in ONE kernel (count_kernel + a scan of its
+// counts were two launches): a workgroup reads the 16 B extras of kCsTile
+// blocks (n and the offset section start, table_reader.cc:11-20; an extra
+// that fails check_extra counts 0, as in count_kernel), scans the counts by
+// decoupled look-back (tile = workgroup id, status words at ws + kCsStatus)
+// and writes rec_base[0..n].
+// kStart, the compaction job's first kernel (ck_start_kernel's work folded in
+// as well: one launch where there were three): every tile also reduces its
+// blocks' byte sum and source end into part[], and the last tile to finish
+// (ws[0] is the ticket) does the job's first host hand-off -- the run starts
+// rec_base[tfb[i]] to the device and the pinned host words with the input
+// bytes, the error-counter snapshot, the cleared unsorted count, guard words
+// and the check / footer kernels' tickets, then the sequence word the host
+// spins on.  Its ws is the context's persistent region (Arena::lb), zero at
+// entry (epoch 0): the last tile clears the ticket and the status words again
+// once every tile has finished its look-back.
+#ifndef SSTC_CS_ITEMS
+#define SSTC_CS_ITEMS 8
+#endif
+constexpr uint32_t kCsItems = SSTC_CS_ITEMS, kCsTile = kScanThreads * kCsItems, kCsStatus = 32;
+
+uint64_t count_scan_tiles(uint64_t nblocks) { return nblocks ? (nblocks + kCsTile - 1) / kCsTile : 1; }
+uint64_t count_scan_workspace(uint64_t nblocks) { return kCsStatus + count_scan_tiles(nblocks); }
+
+template <bool kStart>
+__global__ __launch_bounds__(kScanThreads) void count_scan_kernel(CountScanArgs a) {
+  __shared__ uint64_t sm[kCsTile + kCsTile / 16];
+  __shared__ uint64_t s_wsum[kScanThreads / kWave], s_bytes[kScanThreads / kWave], s_end[kScanThreads / kWave];
+  __shared__ uint64_t s_prefix;
+  __shared__ uint32_t s_last;
+  const uint32_t tid = threadIdx.x, lane = lane_id(), w = tid / kWave;
+  const uint64_t n = a.nblocks, tile = blockIdx.x, base = tile * kCsTile;
+  // masked-off extras read 16 B of the ticket line no thread writes
+  const uint8_t *safe = reinterpret_cast<const uint8_t *>(a.ws + 8);
+  uint64_t len[kCsItems], off[kCsItems];
+#pragma unroll
+  for (uint32_t j = 0; j < kCsItems; j++) {
+    const uint64_t i = base + j * kScanThreads + tid;
+    len[j] = i < n ? a.blk_len[i] : 0;
+    off[j] = i < n ? a.blk_off[i] : 0;
+  }
+  // every extra's loads issued before any is used (clamped, not branched)
+  uint64_t xn[kCsItems], xd[kCsItems];
+#pragma unroll
+  for (uint32_t j = 0; j < kCsItems; j++) {
+    const uint8_t *p = len[j] >= 16 ? a.src + off[j] + len[j] - 16 : safe;
+    xn[j] = g_u64u(p);
+    xd[j] = g_u64u(p + 8);
+  }
+  uint64_t bytes = 0, end = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < kCsItems; j++) {
+    const uint32_t x = j * kScanThreads + tid;
+    sm[lb_idx(x)] = len[j] >= 16 && check_extra(len[j], xn[j], xd[j]) == kBlkOk ? xn[j] : 0;
+    if constexpr (kStart) {
+      bytes += len[j];
+      const uint64_t e = base + x < n ? off[j] + len[j] : 0;
+      end = e > end ? e : end;
+    }
+  }
+  __syncthreads();
+  uint64_t v[kCsItems], sum = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < kCsItems; j++) {
+    v[j] = sm[lb_idx(tid * kCsItems + j)];
+    sum += v[j];
+  }
+  const uint64_t incl = wave_incl_scan_u64(sum);
+  if (lane == kWave - 1) s_wsum[w] = incl;
+  if constexpr (kStart) {
+    bytes = wave_sum_u64(bytes);
+    for (uint32_t d = kWave / 2; d > 0; d >>= 1) {
+      const uint64_t y = __shfl_xor(end, d, kWave);
+      end = y > end ? y : end;
+    }
+    if (lane == 0) {
+      s_bytes[w] = bytes;
+      s_end[w] = end;
+    }
+  }
+  __syncthreads();
+  uint64_t wbase = 0, total = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < kScanThreads / kWave; k++) {
+    const uint64_t x = s_wsum[k];
+    if (k < w) wbase += x;
+    total += x;
+  }
+  if (w == 0) {
+    const uint64_t prefix = lb_publish_lookback(a.ws + kCsStatus, tile, total, a.epoch);
+    if (lane == 0) s_prefix = prefix;
+  }
+  __syncthreads();
+  uint64_t run = s_prefix + wbase + incl - sum;
+#pragma unroll
+  for (uint32_t j = 0; j < kCsItems; j++) {
+    sm[lb_idx(tid * kCsItems + j)] = run;
+    run += v[j];
+  }
+  __syncthreads();
+#pragma unroll
+  for (uint32_t j = 0; j < kCsItems; j++) {
+    const uint32_t i = j * kScanThreads + tid;
+    if (base + i < n) a.rec_base[base + i] = sm[lb_idx(i)];
+  }
+  // rec_base[n] = the record count: the tile holding item n - 1 (tile 0 when n = 0)
+  if (tid == 0 && (n == 0 ? tile == 0 : base < n && n <= base + kCsTile)) a.rec_base[n] = s_prefix + total;
+  if constexpr (kStart) {
+    if (tid == 0) {
+      uint64_t by = 0, e = 0;
+      for (uint32_t k = 0; k < kScanThreads / kWave; k++) {
+        by += s_bytes[k];
+        e = s_end[k] > e ? s_end[k] : e;
+      }
+      a.part[2 * tile] = by;
+      a.part[2 * tile + 1] = e;
+    }
+    // the tile's stores drained, then released at agent scope before its
+    // ticket; the last tile acquires before it reads the others' (as the
+    // check kernel's long-group hand-off)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const bool last =
+          __hip_atomic_fetch_add(a.ws, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1ull;
+      if (last) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      s_last = last;
+    }
+    __syncthreads();
+    if (!s_last) return;
+    uint64_t by = 0, e = 0;
+    for (uint64_t p = tid; p < gridDim.x; p += kScanThreads) {
+      by += __hip_atomic_load(a.part + 2 * p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint64_t x = __hip_atomic_load(a.part + 2 * p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      e = x > e ? x : e;
+    }
+    by = wave_sum_u64(by);
+    for (uint32_t d = kWave / 2; d > 0; d >>= 1) {
+      const uint64_t y = __shfl_xor(e, d, kWave);
+      e = y > e ? y : e;
+    }
+    if (lane == 0) {
+      s_bytes[w] = by;
+      s_end[w] = e;
+    }
+    for (uint64_t i = tid; i < a.ntfb; i += kScanThreads) {
+      const uint64_t r = __hip_atomic_load(a.rec_base + a.tfb[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      a.run_start[i] = r;
+      a.host[1 + i] = r;
+    }
+    for (uint64_t x = tid; x < gridDim.x; x += kScanThreads) a.ws[kCsStatus + x] = 0; // for the next job
+    __syncthreads();
+    if (tid == 0) {
+      by = 0;
+      e = 0;
+      for (uint32_t k = 0; k < kScanThreads / kWave; k++) {
+        by += s_bytes[k];
+        e = s_end[k] > e ? s_end[k] : e;
+      }
+      a.host[0] = by; // input block bytes
+      *a.errs = *a.err_count;
+      *a.bad = 0;
+      a.guard[0] = 0; // consistency-guard bits
+      a.guard[1] = e; // the end of the source bytes the input blocks span
+      for (int g = 0; g < 10; g++) a.guard[32 + 32 * g] = 0; // the check kernel's 9 tickets, the footer's
+      a.ws[0] = 0; // the ticket, for the next job
+    }
+    __threadfence_system();
+    __syncthreads();
+    if (tid == 0) __hip_atomic_store(a.host + a.flag, a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+hipError_t launch_count_scan(const CountScanArgs &a, bool start, hipStream_t s) {
+  const uint32_t g = static_cast<uint32_t>(count_scan_tiles(a.nblocks));
+  if (start) count_scan_kernel<true><<<g, kScanThreads, 0, s>>>(a);
+  else count_scan_kernel<false><<<g, kScanThreads, 0, s>>>(a);
+  return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------
@@ -2319,14 +2434,6 @@ hipError_t launch_roundtrip(const RtArgs &a, hipStream_t s) {
   // VGPRs instead of LDS-DMA, and storing the staged block before the parse
   // were all slower: profiles/r02_ab/rt_ab.md, profiles/r03_ab/rt_1gib.md)
   if (a.nblocks) rt_kernel<<<grid_for(a.nblocks, kRtWaves), kRtWaves * kWave, 0, s>>>(a);
-  return hipGetLastError();
-}
-
-hipError_t launch_count(const uint8_t *src, const uint64_t *blk_off, const uint64_t *blk_len,
-                        uint64_t nblocks, uint64_t *counts, hipStream_t s, uint64_t *scan_ws, uint64_t *len_part) {
-  const uint64_t nz = scan_ws ? scan_status_words(nblocks) : 0;
-  if (nblocks)
-    count_kernel<<<grid_for(nblocks, 256), 256, 0, s>>>(src, blk_off, blk_len, nblocks, counts, scan_ws, nz, len_part);
   return hipGetLastError();
 }
 

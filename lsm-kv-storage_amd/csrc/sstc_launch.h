@@ -144,16 +144,40 @@ hipError_t launch_get(const GetArgs &a, hipStream_t s);
 
 hipError_t launch_roundtrip(const RtArgs &a, hipStream_t s);
 hipError_t launch_copy_probe(const uint8_t *src, uint8_t *dst, uint64_t n16, hipStream_t s);
-hipError_t launch_count(const uint8_t *src, const uint64_t *blk_off, const uint64_t *blk_len,
-                        uint64_t nblocks, uint64_t *counts, hipStream_t s, uint64_t *scan_ws = nullptr,
-                        uint64_t *len_part = nullptr); // len_part: per workgroup of 256 blocks, {sum of blk_len, max blk_off + blk_len}
+// record bases rec_base[0..nblocks] (exclusive scan of the blocks' entry
+// counts) in one kernel; start: the compaction job's first host hand-off as
+// well (count_scan_kernel<true>, sstc_kernels.hip)
+struct CountScanArgs {
+  const uint8_t *src;
+  const uint64_t *blk_off, *blk_len;
+  uint64_t nblocks;
+  uint64_t *rec_base; // nblocks + 1
+  // count_scan_workspace(nblocks) words: [0] ticket (start), status words at
+  // + 32.  start: zero at entry, left zero (epoch 0); else epoch-tagged words
+  // (a context's scan workspace, next_epoch)
+  uint64_t *ws;
+  uint32_t epoch;
+  // start only
+  uint64_t *part;                       // 2 x count_scan_tiles(nblocks)
+  const uint64_t *tfb;                  // ntfb table first blocks (device-readable)
+  uint64_t ntfb;
+  uint64_t *run_start;                  // ntfb: rec_base[tfb[i]]
+  const unsigned long long *err_count;  // snapshot into *errs
+  uint64_t *errs;
+  unsigned long long *bad, *guard;      // cleared (guard[1] = the source end)
+  uint64_t *host;                       // pinned: [0] input bytes, [1..ntfb] run starts
+  uint64_t seq, flag;                   // host[flag] = seq last
+};
+uint64_t count_scan_tiles(uint64_t nblocks);
+uint64_t count_scan_workspace(uint64_t nblocks);
+hipError_t launch_count_scan(const CountScanArgs &a, bool start, hipStream_t s);
 hipError_t launch_decode(const DecArgs &a, hipStream_t s);
 hipError_t launch_pack_records(const sstc_records &in, uint64_t nrec, sstc_record32 *out, hipStream_t s);
 uint64_t scan_workspace_elems(uint64_t n);
 // look-back status words a scan of n items needs cleared (0: single-workgroup scan)
 uint64_t scan_status_words(uint64_t n);
 // ws_zeroed: the caller cleared scan_status_words(n) words of ws in an earlier
-// kernel on the same stream (launch_count's scan_ws, ...), no memset here.
+// kernel on the same stream (seg_walk_kernel's zws, ...), no memset here.
 // epoch (1..kScanEpochs-1): ws holds status words of earlier scans tagged with
 // other epochs (a context's own workspace, see sstc_api.hip next_epoch): no
 // memset either.  Neither: the status words are cleared with a memset.
@@ -196,6 +220,10 @@ struct Arena {
   uint8_t *up = nullptr;
   uint8_t *up_dev = nullptr;
   uint64_t up_cap = 0;
+  // the first kernel's ticket + look-back status words (count_scan_kernel
+  // <true>): zeroed when allocated, left zero by every launch
+  uint64_t *lb = nullptr;
+  uint64_t lb_cap = 0;
   // fault injection for tests (sstc__ctx_set_fault): corrupts the compaction
   // job's filter output on the device so its consistency guard can be tested
   // (1: survivor key offsets, 2: entry prefix sums); 0 in production

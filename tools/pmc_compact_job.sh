@@ -2,7 +2,7 @@
 # HBM traffic of ONE sstc_compact call (config 3 by default) from two rocprofv3
 # PMC passes (FETCH_SIZE, WRITE_SIZE: separate passes, MI355X_MICROARCH.md
 # TCC slots), summed over the kernels of the job's last call (from its last
-# count_kernel dispatch on); FETCH_SIZE doubled (gfx950 wide-stream correction).
+# count_scan_kernel / count_kernel dispatch on); FETCH_SIZE doubled (gfx950 wide-stream correction).
 # Writes gpurun_out/pmc_compact/summary.json; copy it to profiles/pmc_compact.json.
 cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 2
 export TMPDIR=/tmp
@@ -17,14 +17,14 @@ import csv, glob, json, sys
 out, args = sys.argv[1], sys.argv[2]
 tag = next((f"config{c}" for c in "345" if f"--config {c}" in args), args)  # what bench.py's legs look up
 res = {"workload": tag, "args": args, "note":
-       "one sstc_compact call: every kernel from its last count_kernel dispatch on; FETCH_SIZE x 2 (gfx950), KiB"}
+       "one sstc_compact call: every kernel from its last count_scan_kernel (count_kernel) dispatch on; FETCH_SIZE x 2 (gfx950), KiB"}
 per = {}
 for c in ("FETCH_SIZE", "WRITE_SIZE"):
     rows = []
     for f in glob.glob(f"{out}/{c}/**/*counter_collection.csv", recursive=True):
         rows += [r for r in csv.DictReader(open(f)) if r["Counter_Name"] == c]
     rows.sort(key=lambda r: int(r["Dispatch_Id"]))
-    start = max(i for i, r in enumerate(rows) if "count_kernel" in r["Kernel_Name"])
+    start = max(i for i, r in enumerate(rows) if "count_kernel" in r["Kernel_Name"] or "count_scan_kernel" in r["Kernel_Name"])
     tot = 0.0
     for r in rows[start:]:
         if r["Kernel_Name"].startswith("__amd_rocclr"):  # the caller's copies after the call, not the job

@@ -6,7 +6,10 @@ import sys
 rows = list(csv.DictReader(open(sys.argv[1])))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 idx = [i for i, r in enumerate(rows) if "sstc::decode_kernel" in r["Kernel_Name"]]
-start = idx[-1] - 2
+# the job's first kernel: count_scan_kernel (count_kernel + scan + ck_start_kernel
+# before round 5's end), the last one before the job's decode
+start = max(i for i in range(idx[-1]) if "count_kernel" in rows[i]["Kernel_Name"]
+            or "count_scan_kernel" in rows[i]["Kernel_Name"])
 t0 = int(rows[start]["Start_Timestamp"])
 last = t0
 agg = {}
