@@ -1465,6 +1465,7 @@ struct SegArgs {
   uint64_t nz;
   uint32_t *tentry;       // cleared here: tiles + 1 entry counters
   const uint64_t *mp;     // optional: the record count on the device (m is then its bound)
+  const uint64_t *skip;   // *skip != 0: the arithmetic chain held (seg_arith_*), nothing to do
 };
 
 // table ends cached in LDS by seg_walk_kernel: ends[t0 - 1 + j], j < kEndCache
@@ -1477,6 +1478,7 @@ __global__ __launch_bounds__(kChThreads) void seg_walk_kernel(SegArgs a) {
   __shared__ uint64_t s_wend, s_t0, s_e[kEndCache], s_ec;
   const uint32_t tid = threadIdx.x;
   const uint64_t c0 = static_cast<uint64_t>(blockIdx.x) * kChTile;
+  if (*a.skip) return;
   // the window's loads go out on the host bound a.m (Pw holds a.m + 1 words),
   // together with the device count's: one round trip instead of two
   constexpr uint32_t kFill = kLw / kChThreads;
@@ -1674,9 +1676,11 @@ struct NodeArgs {
   uint64_t m, tiles;
   uint32_t *Nx, *Nc, *Nt; // level 0: next node, segments, tile
   const uint64_t *mp;     // optional device record count
+  const uint64_t *skip;   // as SegArgs::skip
 };
 
 __global__ void seg_node_kernel(NodeArgs a) {
+  if (*a.skip) return;
   const uint64_t k = blockIdx.x;
   const uint64_t b0 = a.base[k], nw = a.base[k + 1] - b0, c0 = k * kChTile;
   const uint64_t m = a.mp ? *a.mp : a.m;
@@ -1695,7 +1699,8 @@ __global__ void seg_node_kernel(NodeArgs a) {
 
 // level k + 1 = 8 hops of level k (node count from the device)
 __global__ void seg_npow_kernel(const uint32_t *Nx, const uint32_t *Nc, uint32_t *Nx1, uint32_t *Nc1,
-                                const uint64_t *nnodes) {
+                                const uint64_t *nnodes, const uint64_t *skip) {
+  if (*skip) return;
   const uint64_t n = *nnodes;
   for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
        i += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
@@ -1719,7 +1724,8 @@ __global__ void seg_npow_kernel(const uint32_t *Nx, const uint32_t *Nc, uint32_t
 __global__ void seg_nentry_kernel(const uint32_t *Nx, const uint32_t *Nc, const uint32_t *Nt, const uint64_t *base,
                                   uint32_t levels, uint64_t stride, uint64_t m, const uint64_t *mp,
                                   uint64_t tiles, uint32_t *tentry, uint32_t *tbefore, uint64_t *first,
-                                  uint64_t *d_count) {
+                                  uint64_t *d_count, const uint64_t *skip) {
+  if (*skip) return;
   if (mp) m = *mp;
   const uint64_t h = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (h == 0) {
@@ -1767,7 +1773,8 @@ __global__ void seg_nentry_kernel(const uint32_t *Nx, const uint32_t *Nc, const 
 // (e.g. 4 KiB blocks of small records: ~73 per tile) are walked by one thread.
 __global__ __launch_bounds__(kChThreads) void seg_emit_kernel(const uint32_t *J0, uint64_t m, const uint64_t *mp,
                                                               const uint32_t *tentry, const uint32_t *tbefore,
-                                                              uint64_t *first) {
+                                                              uint64_t *first, const uint64_t *skip) {
+  if (*skip) return;
   constexpr uint32_t kPer = kChTile / kChThreads;
   constexpr uint16_t kOut = 0xFFFF; // successor outside the tile
   constexpr uint32_t kSerialChain = 128;
@@ -2112,7 +2119,9 @@ struct EntryIn {
 // out[i] = carry_in + sum(in[0..i)), out[n] = carry_in + total.  in may alias out.
 template <class In>
 __global__ __launch_bounds__(kScanThreads) void scan_apply_kernel(In in, uint64_t n, const uint64_t *tile_base,
-                                                                  uint64_t carry_in, uint64_t *out) {
+                                                                  uint64_t carry_in, uint64_t *out,
+                                                                  const uint64_t *skip) {
+  if (skip && *skip) return; // (launch_segment: the arithmetic chain held)
   const uint64_t t0 = static_cast<uint64_t>(blockIdx.x) * kScanTile + threadIdx.x * kScanItems;
   uint64_t v[kScanItems];
   uint64_t s = 0;
@@ -2155,7 +2164,9 @@ __device__ __forceinline__ uint32_t lb_idx(uint32_t i) { return i + (i >> 4); } 
 
 template <class In, uint32_t kItems = kLbItems>
 __global__ __launch_bounds__(kScanThreads) void scan_lookback_kernel(In in, uint64_t n, uint64_t carry_in,
-                                                                     uint64_t *out, uint64_t *ws, uint32_t epoch) {
+                                                                     uint64_t *out, uint64_t *ws, uint32_t epoch,
+                                                                     const uint64_t *skip) {
+  if (skip && *skip) return; // uniform: every tile returns (launch_segment: the arithmetic chain held)
   constexpr uint32_t kTile = kScanThreads * kItems;
   __shared__ uint64_t sm[kTile + kTile / 16];
   __shared__ uint64_t s_wsum[kScanThreads / kWave];
@@ -2479,10 +2490,10 @@ uint64_t scan_status_words(uint64_t n) { return n <= kScanTile ? 0 : (n + kArrTi
 
 template <class In, uint32_t kItems = kLbItems>
 static hipError_t scan_any(In in, uint64_t n, uint64_t carry_in, uint64_t *out, uint64_t *ws, hipStream_t s,
-                           bool ws_zeroed, uint32_t epoch) {
+                           bool ws_zeroed, uint32_t epoch, const uint64_t *skip = nullptr) {
   constexpr uint64_t kTile = kScanThreads * kItems;
   if (n <= kScanTile) {
-    scan_apply_kernel<In><<<1, kScanThreads, 0, s>>>(in, n, nullptr, carry_in, out);
+    scan_apply_kernel<In><<<1, kScanThreads, 0, s>>>(in, n, nullptr, carry_in, out, skip);
     return hipGetLastError();
   }
   const uint64_t tiles = (n + kTile - 1) / kTile;
@@ -2493,7 +2504,7 @@ static hipError_t scan_any(In in, uint64_t n, uint64_t carry_in, uint64_t *out, 
     if (e != hipSuccess) return e;
   }
   scan_lookback_kernel<In, kItems><<<static_cast<uint32_t>(tiles), kScanThreads, 0, s>>>(in, n, carry_in, out, ws,
-                                                                                        epoch);
+                                                                                        epoch, skip);
   return hipGetLastError();
 }
 
@@ -2663,11 +2674,137 @@ hipError_t launch_enc_emit(const EncArgs &a, hipStream_t s) {
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// Arithmetic block chains.  When the records of an output table have equal
+// entry sizes (fixed-size keys and values, configs 2-4, db_bench's default),
+// its segments all hold the same number of records but the last: the chain
+// through table a is T_a, T_a + g_a, T_a + 2 g_a, ... (T_a its first record)
+// up to T_{a+1}.  seg_arith_kernel predicts g_a from the table's first record
+// (the least k with k w >= threshold, w = W(T_a + 1) - W(T_a)) and scans the
+// predicted segment counts; seg_arith_check_kernel writes every predicted
+// start and checks its hop exactly against W -- the hop from p is
+// q = min(p + g_a, T_{a+1}) iff W(q - 1) < W(p) + threshold (or q - 1 = p) and,
+// unless q = T_{a+1}, W(q) >= W(p) + threshold: three loads, no walk, every
+// hop checked (the first included), so a wrong prediction only costs the
+// fallback.  One failed check (or more than kArMax tables) clears the verdict
+// word and the general chain walk above runs; when every hop checks, its
+// kernels (seg_walk, the window scan, seg_node, seg_npow, seg_nentry,
+// seg_emit) return at once.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kArMax = 1024, kArThreads = 512;
+
+struct ArithArgs {
+  const uint64_t *Pw;
+  uint64_t add, m, threshold;   // m: the host bound
+  const uint64_t *ends, *nends; // optional table starts ends[0..*nends] (ends[*nends] = the record count)
+  const uint64_t *mp;           // optional device record count
+  // ar[0]: verdict (1: every predicted hop holds), ar[1]: segment count,
+  // ar[2 ..]: g_a (kArMax), then the segment bases of the tables (kArMax + 1)
+  uint64_t *ar;
+  uint64_t *first, *d_count;
+};
+
+__device__ __forceinline__ uint64_t ar_w(const ArithArgs &a, uint64_t x) { return a.Pw[x] + a.add * x; }
+
+// table t's predicted hop and segment count (0: not a table the chain can take)
+__device__ __forceinline__ void ar_predict(const ArithArgs &a, uint64_t t, uint64_t nt, uint64_t m, uint64_t &g,
+                                           uint64_t &cnt) {
+  g = cnt = 0;
+  if (t >= nt) return;
+  const uint64_t T0 = a.ends ? a.ends[t] : 0, T1 = a.ends ? a.ends[t + 1] : m;
+  if (!(T0 < T1 && T1 <= m)) return;
+  const uint64_t w = ar_w(a, T0 + 1) - ar_w(a, T0), len = T1 - T0;
+  uint64_t k = w ? (a.threshold + w - 1) / w : len;
+  k = k < 1 ? 1 : (k > len ? len : k);
+  g = k;
+  cnt = (len + k - 1) / k;
+}
+
+__global__ __launch_bounds__(kArThreads) void seg_arith_kernel(ArithArgs a) {
+  __shared__ uint64_t s_w[kArThreads / kWave];
+  __shared__ uint32_t s_bad;
+  const uint32_t tid = threadIdx.x, lane = lane_id(), wv = tid / kWave;
+  const uint64_t m = a.mp ? *a.mp : a.m;
+  const uint64_t nt = a.ends ? *a.nends : 1;
+  if (m == 0 || nt == 0 || nt > kArMax) { // no records: the general path's m = 0 case; too many tables
+    if (tid == 0) a.ar[0] = 0;
+    return;
+  }
+  if (tid == 0) s_bad = 0;
+  __syncthreads();
+  uint64_t *g = a.ar + 2, *tb = a.ar + 2 + kArMax;
+  uint64_t g0, c0, g1, c1; // tables 2 tid, 2 tid + 1
+  ar_predict(a, 2 * tid, nt, m, g0, c0);
+  ar_predict(a, 2 * tid + 1, nt, m, g1, c1);
+  if ((2 * tid < nt && !c0) || (2 * tid + 1 < nt && !c1)) s_bad = 1; // an empty or out-of-range table
+  const uint64_t inc = wave_incl_scan_u64(c0 + c1);
+  if (lane == kWave - 1) s_w[wv] = inc;
+  __syncthreads();
+  uint64_t before = 0, total = 0;
+  for (uint32_t k = 0; k < kArThreads / kWave; k++) {
+    before += k < wv ? s_w[k] : 0;
+    total += s_w[k];
+  }
+  const uint64_t b0 = before + inc - (c0 + c1);
+  if (2 * tid < nt) {
+    g[2 * tid] = g0;
+    tb[2 * tid] = b0;
+  }
+  if (2 * tid + 1 < nt) {
+    g[2 * tid + 1] = g1;
+    tb[2 * tid + 1] = b0 + c0;
+  }
+  if (tid == 0) {
+    tb[nt] = total;
+    a.ar[1] = total;
+    a.ar[0] = s_bad ? 0 : 1;
+    if (!s_bad) { // the general path writes both when it runs
+      *a.d_count = total;
+      a.first[total] = m;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void seg_arith_check_kernel(ArithArgs a) {
+  __shared__ uint64_t s_tb[kArMax + 1], s_t[kArMax + 1], s_g[kArMax];
+  // the verdict, the count and the tables' words in one round of loads
+  const uint64_t ok0 = a.ar[0], total = a.ar[1];
+  const uint64_t m = a.mp ? *a.mp : a.m;
+  const uint64_t nt = a.ends ? *a.nends : 1;
+  const uint64_t *g = a.ar + 2, *tb = a.ar + 2 + kArMax;
+  if (!ok0 || nt > kArMax) return; // not eligible, or a hop already failed: the general path writes everything
+  for (uint64_t t = threadIdx.x; t <= nt; t += 256) {
+    s_tb[t] = tb[t];
+    s_t[t] = a.ends ? a.ends[t] : (t ? m : 0);
+    if (t < nt) s_g[t] = g[t];
+  }
+  __syncthreads();
+  bool ok = true;
+  for (uint64_t h = static_cast<uint64_t>(blockIdx.x) * 256 + threadIdx.x; h < total;
+       h += static_cast<uint64_t>(gridDim.x) * 256) {
+    uint64_t lo = 0, hi = nt; // the table: s_tb[lo] <= h < s_tb[lo + 1]
+    while (lo + 1 < hi) {
+      const uint64_t mid = (lo + hi) >> 1;
+      if (s_tb[mid] <= h) lo = mid;
+      else hi = mid;
+    }
+    const uint64_t T1 = s_t[lo + 1], gg = s_g[lo];
+    const uint64_t p = s_t[lo] + (h - s_tb[lo]) * gg;
+    const uint64_t q = p + gg < T1 ? p + gg : T1;
+    const uint64_t wp = ar_w(a, p), wq1 = ar_w(a, q - 1), wq = ar_w(a, q);
+    const uint64_t target = wp + a.threshold;
+    ok &= p < T1 && (q - 1 == p || wq1 < target) && (q == T1 || wq >= target);
+    a.first[h] = p;
+  }
+  if (!ok) a.ar[0] = 0; // (every failing thread stores the same 0)
+}
+
 namespace {
 struct SegLayout { // u32 offsets into the segmentation workspace
   uint64_t tiles, levels, J0, Fx, Fc, Nx, Nc, Nt, tentry, tbefore, u64, total;
-  // u64 region (8-aligned): win[tiles + 1], base[tiles + 1], nn, visits, scan ws
-  uint64_t win, base, nn, visits, sws;
+  // u64 region (8-aligned): win[tiles + 1], base[tiles + 1], nn, visits, scan
+  // ws, the arithmetic chain's words (ArithArgs::ar)
+  uint64_t win, base, nn, visits, sws, ar;
   explicit SegLayout(uint64_t m) {
     tiles = (m + kChTile - 1) / kChTile;
     levels = 1;
@@ -2687,7 +2824,8 @@ struct SegLayout { // u32 offsets into the segmentation workspace
     nn = base + tiles + 1;
     visits = nn + 1;
     sws = visits + 1;
-    total = u64 + 2 * (sws + scan_workspace_elems(tiles + 1) + 1);
+    ar = sws + scan_workspace_elems(tiles + 1) + 1;
+    total = u64 + 2 * (ar + 2 + 2 * kArMax + 1 + 1);
   }
 };
 } // namespace
@@ -2716,23 +2854,30 @@ hipError_t launch_segment(const uint64_t *Pw, uint64_t nrec, uint64_t threshold,
   uint64_t *win = U + L.win, *base = U + L.base, *sws = U + L.sws;
   uint32_t *tentry = J + L.tentry, *tbefore = J + L.tbefore;
   const uint64_t stride = nrec + 1;
+  // equal-sized entries: the arithmetic chain, checked hop by hop; the
+  // general walk below runs only when a check fails (ar[0] = 0)
+  uint64_t *ar = U + L.ar;
+  const uint32_t pg = static_cast<uint32_t>(std::min<uint64_t>(grid_for(nrec + 1, 256), 2048));
+  const ArithArgs aa{Pw, add, nrec, threshold, ends, d_nends, d_nrec, ar, blk_first, d_nblocks};
+  seg_arith_kernel<<<1, kArThreads, 0, s>>>(aa);
+  seg_arith_check_kernel<<<pg, 256, 0, s>>>(aa);
   SegArgs a{Pw, add, nrec, threshold, ends, d_nends, J + L.J0, J + L.Fx, J + L.Fc, win, blk_first, d_nblocks,
-            sws, scan_status_words(L.tiles), tentry, d_nrec};
+            sws, scan_status_words(L.tiles), tentry, d_nrec, ar};
   seg_walk_kernel<<<static_cast<uint32_t>(L.tiles), kChThreads, 0, s>>>(a);
-  hipError_t e = launch_scan(win, L.tiles, 0, base, sws, s, true); // base[tiles] = node count
+  // base[tiles] = node count
+  hipError_t e = scan_any<ArrIn, kArrItems>(ArrIn{win}, L.tiles, 0, base, sws, s, true, 0, ar);
   if (e != hipSuccess) return e;
   const uint64_t *nn = base + L.tiles;
-  NodeArgs na{J + L.Fx, J + L.Fc, base, nrec, L.tiles, J + L.Nx, J + L.Nc, J + L.Nt, d_nrec};
+  NodeArgs na{J + L.Fx, J + L.Fc, base, nrec, L.tiles, J + L.Nx, J + L.Nc, J + L.Nt, d_nrec, ar};
   seg_node_kernel<<<static_cast<uint32_t>(L.tiles), 256, 0, s>>>(na);
-  const uint32_t pg = static_cast<uint32_t>(std::min<uint64_t>(grid_for(nrec + 1, 256), 2048));
   for (uint64_t k = 0; k + 1 < L.levels; k++)
     seg_npow_kernel<<<pg, 256, 0, s>>>(J + L.Nx + k * stride, J + L.Nc + k * stride, J + L.Nx + (k + 1) * stride,
-                                       J + L.Nc + (k + 1) * stride, nn);
+                                       J + L.Nc + (k + 1) * stride, nn, ar);
   seg_nentry_kernel<<<grid_for(L.tiles, 256), 256, 0, s>>>(J + L.Nx, J + L.Nc, J + L.Nt, base,
                                                            static_cast<uint32_t>(L.levels), stride, nrec, d_nrec,
-                                                           L.tiles, tentry, tbefore, blk_first, d_nblocks);
+                                                           L.tiles, tentry, tbefore, blk_first, d_nblocks, ar);
   seg_emit_kernel<<<static_cast<uint32_t>(L.tiles), kChThreads, 0, s>>>(J + L.J0, nrec, d_nrec, tentry, tbefore,
-                                                                        blk_first);
+                                                                        blk_first, ar);
   return hipGetLastError();
 }
 

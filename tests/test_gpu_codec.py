@@ -460,6 +460,43 @@ def test_segment_serial_walk_vs_oracle(codec, oracle, case):
         assert {22, 21, 16, 32} <= set(L.tolist())
 
 
+@pytest.mark.parametrize("case", ["uniform", "exact_fit", "one_record_blocks", "one_off_late", "one_off_first",
+                                  "no_value"])
+def test_segment_arithmetic_chain_vs_oracle(codec, oracle, case):
+    """seg_arith_kernel / seg_arith_check_kernel (end of round 5): equal-sized
+    entries take the arithmetic chain T, T + g, T + 2g, ... checked hop by hop;
+    any other input must fall back to the general walk.  uniform: 149 B entries
+    (config 2's shape, 28-record blocks, a short last block); exact_fit: blocks
+    that reach the threshold exactly (W(q) == W(p) + T on every hop);
+    one_record_blocks: values past the threshold (g = 1); one_off_late /
+    one_off_first: equal entries but one record 3000 B heavier near the end /
+    in the first block, so that block closes early (the chain's check fails on
+    one hop / the first hop predicts the wrong g: the general walk); no_value:
+    equal DELETE-shaped records."""
+    n = 100_003
+    klen = np.full(n, 16, np.int64)
+    vlen = np.full(n, 100, np.int64)
+    Ts = (4096, 32768)
+    if case == "exact_fit":
+        vlen[:] = 128 - 33 - 16  # weight (entry + offset entry) 33 + 16 + 79 = 128 B: T / 128 records per block
+        Ts = (4096, 128 * 7)
+    elif case == "one_record_blocks":
+        vlen[:] = 5000
+    elif case == "one_off_late":
+        vlen[n - 777] += 3000
+    elif case == "one_off_first":
+        vlen[3] += 3000
+    elif case == "no_value":
+        vlen[:] = 0xFFFFFFFF
+    rec = length_records(klen, vlen)
+    for T in Ts:
+        want = oracle.segment(rec, T)
+        got = cpu_u64(codec.segment(records_table(rec), T))
+        assert np.array_equal(got, want), (case, T)
+        if case == "uniform":
+            assert len(set(np.diff(want[:-1]).tolist())) == 1  # the arithmetic shape the fast path takes
+
+
 @pytest.mark.parametrize("seed", range(3))
 def test_encode_span_alignments_vs_oracle(codec, oracle, seed):
     """Keys / values at every source alignment (arena offsets shuffled, so
