@@ -45,10 +45,15 @@
 #include <cassert>
 #include <cstdint>
 #include <memory>
+#include <string>
 #include <string_view>
 #include <vector>
 
 namespace kvs {
+
+namespace db {
+class MergeIterator;
+}
 
 namespace sstable {
 
@@ -95,6 +100,11 @@ public:
   void SeekToLast() override;
 
 private:
+  // the drop-in MergeIterator (include/dropin/db/merge_iterator.h) merges the
+  // tables on the device from their files: it reads the table's file name and
+  // block index through Describe (this class is TableReader's friend)
+  friend class kvs::db::MergeIterator;
+  void Describe(std::string *path, std::vector<uint64_t> *off, std::vector<uint64_t> *len) const;
   // decodes the table on first use (one GPU call)
   void Load();
   // the block the entry cursor runs over (CreateNewBlockReaderIterator)

@@ -42,12 +42,14 @@
 #include "sstcodec.h"
 
 #ifdef __cplusplus
+#include <atomic>
 #include <cstdint>
 #include <cstring>
 #include <memory>
 #include <new>
 #include <string>
 #include <string_view>
+#include <thread>
 #include <type_traits>
 #include <utility>
 #include <vector>
@@ -133,6 +135,76 @@ private:
 /* one TableBuilder's pending records (sst_table.cpp keeps a per-thread pool) */
 struct BuilderArena;
 
+/* The inputs of one merge (a compaction's input SSTs, db/compact.cc:186-230)
+ * made resident for the drop-in MergeIterator (include/dropin/db/
+ * merge_iterator.h): every input's data section is mapped read-only into ONE
+ * host address range, uploaded once to the device at the same offsets, and
+ * its records decoded and merged there (sstc_merge_records) into the order
+ * the reference's MergeIterator walks them.  Host views (keys, values) point
+ * into the mapping; offsets are the same on both sides, so a TableBuilder on
+ * the same thread that is handed such views records (offset) instead of
+ * copying bytes and encodes its blocks from the device copy (Activate). */
+class ResidentInputs : public std::enable_shared_from_this<ResidentInputs> {
+public:
+  struct Input {                      // one input table, iterator order
+    std::string path;                 // its SST file
+    std::vector<uint64_t> off, len;   // its data blocks (BlockIndex order), file offsets
+  };
+  /* Map, upload, decode + merge (txn as the reference's iterator reads it).
+   * nullptr when the merged order cannot be produced on the device (a file
+   * that cannot be mapped, a table without blocks, a corrupt block, keys out
+   * of order, no HIP device); *why says which. */
+  static std::shared_ptr<ResidentInputs> Create(sstc_ctx *ctx, const std::vector<Input> &inputs, uint32_t txn_mode,
+                                                std::string *why);
+  ~ResidentInputs();
+  ResidentInputs(const ResidentInputs &) = delete;
+  ResidentInputs &operator=(const ResidentInputs &) = delete;
+
+  uint64_t NumRecords() const { return n_; }
+  /* the merged records, downloaded in chunks behind the caller's walk by a
+   * helper thread: Records()[0, WaitRecords(k)) are in host memory, and
+   * WaitRecords(k) returns >= min(k, NumRecords()) (throws std::runtime_error
+   * when the download failed) */
+  const sstc_merged_record *Records() const { return rec_.get(); }
+  uint64_t WaitRecords(uint64_t k);
+  const uint8_t *Host() const { return host_; }
+  uint64_t Bytes() const { return bytes_; }
+  const uint8_t *DeviceBytes() const { return dev_; }
+  int Device() const { return device_; }
+  /* equal (key, merge txn) neighbours from different inputs / differing ones
+   * (sstc_merge_result): both non-zero = the reference heap's order may differ */
+  uint64_t CrossTies() const { return cross_ties_; }
+  uint64_t TieDiffs() const { return tie_diffs_; }
+  /* the input a record's key lies in */
+  uint32_t InputOf(uint64_t key_off) const;
+  /* host-side phase times of Create (ms): map, upload, device merge, download */
+  double ms[4] = {0, 0, 0, 0};
+
+  /* TableBuilders on the calling thread may reference this region from now
+   * until Deactivate (the drop-in MergeIterator activates it for its life) */
+  void Activate();
+  void Deactivate();
+  static ResidentInputs *Active(); /* the calling thread's, or nullptr */
+
+private:
+  ResidentInputs() = default;
+  uint8_t *host_ = nullptr;   // reserved range (PROT_NONE) with the files mapped in it
+  uint64_t bytes_ = 0;
+  uint8_t *dev_ = nullptr;    // device copy, same offsets
+  int device_ = -1;
+  uint64_t n_ = 0, cross_ties_ = 0, tie_diffs_ = 0;
+  std::unique_ptr<sstc_merged_record[]> rec_;
+  std::vector<uint64_t> table_base_; // offset of table t's file in the range
+  // the download: device records (the creating thread's merge buffer, lent to
+  // this object until the helper is done), records ready, failure flag
+  void Download();
+  void *drec_ = nullptr;
+  uint64_t drec_cap_ = 0;
+  std::atomic<uint64_t> ready_{0};
+  std::atomic<int> failed_{0};
+  std::thread helper_;
+};
+
 /* One meta entry (reference sstable/block_index.h:22-57). */
 struct BlockIndex {
   std::string smallest_key;
@@ -170,11 +242,12 @@ public:
                   const uint64_t *val_off);
 
   std::string_view GetSmallestKey() const { return table_smallest_key_; }
-  /* the last key added (a view into the builder's key arena; no string copy
-   * per AddEntry, the reference's #1 host hotspot, table_builder.cc:37-53) */
+  /* the last key added (a view into the builder's key arena or the resident
+   * inputs; no string copy per AddEntry, the reference's #1 host hotspot,
+   * table_builder.cc:37-53) */
   std::string_view GetLargestKey() const {
     if (type_.empty()) return {};
-    return {reinterpret_cast<const char *>(keys_.data()) + key_off_.back(), key_len_.back()};
+    return {reinterpret_cast<const char *>(KeyPtr(type_.size() - 1)), key_len_.back()};
   }
   std::string_view GetFilename() const { return filename_; }
   uint64_t GetFileSize() const { return current_offset_ + 1; } /* table_builder.cc:228 */
@@ -198,6 +271,23 @@ private:
   uint64_t min_txn_ = UINT64_MAX, max_txn_ = 0;
   uint64_t data_size_ = 0;
   uint64_t current_offset_ = 0;
+  /* Resident inputs (ResidentInputs::Activate on this thread, same device as
+   * ctx_): a record whose key and value views lie in them is kept as offsets
+   * into them (no copy; Finish encodes from the device copy); one that does not
+   * is copied into the arenas with kArenaRef in its offsets. */
+  static constexpr uint64_t kArenaRef = 1ull << 63;
+  std::shared_ptr<ResidentInputs> res_;
+  const uint8_t *res_host_ = nullptr;
+  uint64_t res_bytes_ = 0, arena_recs_ = 0;
+  bool AdoptResident();
+  const uint8_t *KeyPtr(size_t i) const {
+    const uint64_t o = key_off_[i];
+    return res_host_ && !(o & kArenaRef) ? res_host_ + o : keys_.data() + (o & ~kArenaRef);
+  }
+  const uint8_t *ValPtr(size_t i) const {
+    const uint64_t o = val_off_[i];
+    return res_host_ && !(o & kArenaRef) ? res_host_ + o : vals_.data() + (o & ~kArenaRef);
+  }
 };
 
 /* The records of one data block, decoded on the GPU (BlockReaderData +

@@ -278,6 +278,42 @@ int sstc_compact(sstc_ctx *ctx, const uint8_t *d_src, const uint64_t *d_blk_off,
                  const sstc_compact_params *params, uint8_t *d_dst, uint64_t dst_cap, uint64_t *d_table_off,
                  uint64_t *d_table_len, uint64_t max_tables, sstc_compact_result *result);
 
+/* ---- merge order (replaces db::MergeIterator's SeekToFirst + Next walk,
+ *      db/merge_iterator.cc:34-46,79-92, over the TableReaderIterators that
+ *      Compact::CreateMergeIterator makes, db/compact.cc:186-230) ----------- */
+
+/* One record of the merged order: the key's offset in d_src (the entry's type
+ * byte and u32 key length precede it, its u32 value length and value follow
+ * it, block format above) and its txn as the reference's iterator reads it
+ * (txn_mode). */
+typedef struct sstc_merged_record {
+  uint64_t key_off;
+  uint64_t txn;
+} sstc_merged_record;
+
+typedef struct sstc_merge_result {
+  uint64_t records;    /* records of all inputs = merged records                  */
+  uint64_t cross_ties; /* merged neighbours with equal key and merge txn from      */
+                       /* different inputs                                        */
+  uint64_t tie_diffs;  /* merged neighbours with equal key and merge txn whose     */
+                       /* type, txn as read or value differ                       */
+} sstc_merge_result;
+
+/* Decode every block of the `ntables` inputs (given as for sstc_compact) and
+ * write their records to d_out[0, records) in MergeIterator order: key
+ * ascending, then txn descending, where an input's versions of a key compete
+ * under the smallest txn before them in that input (the order the reference's
+ * heap pops them when the compat reader returns them out of txn order), then
+ * the lower input first.  The heap orders records with equal (key, txn) from
+ * different inputs by heap history (merge_iterator.h:91-95); such ties are
+ * counted, and when both counts are non-zero this order may differ from the
+ * reference's heap (the caller then takes the heap's order).  Inputs whose
+ * keys are not ascending, or with a block that fails to decode:
+ * SSTC_E_INVALID_ARG.  More records than max_records: SSTC_E_CAPACITY with
+ * result->records set and nothing written.  Synchronises the stream. */
+int sstc_merge_records(sstc_ctx *ctx, const uint8_t *d_src, const uint64_t *d_blk_off, const uint64_t *d_blk_len,
+                       uint64_t nblocks, const uint64_t *h_table_first_block, uint32_t ntables, uint32_t txn_mode,
+                       sstc_merged_record *d_out, uint64_t max_records, sstc_merge_result *result);
 
 /* ---- point lookups (replaces TableReader::GetValue without a block cache,
  *      sstable/table_reader.cc:168-210, with BlockReader::GetValue,

@@ -26,7 +26,7 @@ ARCH = os.environ.get("SSTC_OFFLOAD_ARCH", "gfx950")
 REFERENCE = os.environ.get("SSTC_REFERENCE", "/root/reference")  # headers for the drop-in test TU only
 
 HIP_SOURCES = ["sstc_kernels.hip", "sstc_compact.hip", "sstc_get.hip", "sstc_api.hip"]
-HOST_SOURCES = ["host/sst_table.cpp", "host/compact_files.cpp"]
+HOST_SOURCES = ["host/sst_table.cpp", "host/compact_files.cpp", "host/resident.cpp"]
 
 
 def _hipcc():

@@ -131,6 +131,17 @@ void TableReaderIterator::Load() {
   }
 }
 
+void TableReaderIterator::Describe(std::string *path, std::vector<uint64_t> *off, std::vector<uint64_t> *len) const {
+  *path = table_reader_->filename_;
+  const std::vector<BlockIndex> &index = table_reader_->block_index_;
+  off->resize(index.size());
+  len->resize(index.size());
+  for (size_t b = 0; b < index.size(); b++) {
+    (*off)[b] = index[b].GetBlockStartOffset();
+    (*len)[b] = index[b].GetBlockSize();
+  }
+}
+
 void TableReaderIterator::ShowBlock(uint64_t block) {
   has_block_ = true;
   shown_block_ = block;

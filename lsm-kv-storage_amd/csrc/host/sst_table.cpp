@@ -18,6 +18,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
 #include <map>
 #include <memory>
 #include <stdexcept>
@@ -249,26 +250,47 @@ bool TableBuilder::Open() {
   return fd_ >= 0;
 }
 
+bool TableBuilder::AdoptResident() {
+  ResidentInputs *r = ResidentInputs::Active();
+  if (!r || r->Device() != sstc__ctx_device(ctx_)) return false;
+  res_ = r->shared_from_this();
+  res_host_ = r->Host();
+  res_bytes_ = r->Bytes();
+  return true;
+}
+
 void TableBuilder::AddEntry(std::string_view key, std::string_view value, uint64_t txn_id,
                             uint8_t value_type) {
   // table_builder.cc:35-60
   if (table_smallest_key_.empty()) table_smallest_key_ = std::string(key);
+  const uint8_t *kp = reinterpret_cast<const uint8_t *>(key.data());
+  const uint8_t *vp = reinterpret_cast<const uint8_t *>(value.data());
+  // views into the resident inputs (what the drop-in MergeIterator hands out):
+  // offsets only, the bytes are already on the device
+  if ((res_host_ || (type_.empty() && AdoptResident())) &&
+      static_cast<uint64_t>(kp - res_host_) < res_bytes_ &&
+      (!vp || static_cast<uint64_t>(vp - res_host_) < res_bytes_)) {
+    key_off_.push_back(static_cast<uint64_t>(kp - res_host_));
+    val_off_.push_back(vp ? static_cast<uint64_t>(vp - res_host_) : 0);
+  } else {
+    const uint64_t tag = res_host_ ? kArenaRef : 0;
+    arena_recs_ += tag != 0;
+    key_off_.push_back(keys_.size() | tag);
+    keys_.append(kp, key.size());
+    if (vp) {
+      val_off_.push_back(vals_.size() | tag);
+      vals_.append(vp, value.size());
+    } else {
+      val_off_.push_back(tag);
+    }
+  }
   type_.push_back(value_type);
   key_len_.push_back(static_cast<uint32_t>(key.size()));
-  key_off_.push_back(keys_.size());
-  keys_.append(reinterpret_cast<const uint8_t *>(key.data()), key.size());
-  if (value.data()) {
-    val_len_.push_back(static_cast<uint32_t>(value.size()));
-    val_off_.push_back(vals_.size());
-    vals_.append(reinterpret_cast<const uint8_t *>(value.data()), value.size());
-  } else {
-    val_len_.push_back(SSTC_NO_VALUE);
-    val_off_.push_back(0);
-  }
+  val_len_.push_back(vp ? static_cast<uint32_t>(value.size()) : SSTC_NO_VALUE);
   txn_.push_back(txn_id);
   if (txn_id < min_txn_) min_txn_ = txn_id;
   if (txn_id > max_txn_) max_txn_ = txn_id;
-  data_size_ += key.size() + (value.data() ? value.size() : 0);
+  data_size_ += key.size() + (vp ? value.size() : 0);
   block_size_ += entry_size(key_len_.back(), val_len_.back()) + 16; // block_builder.cc:33
   if (block_size_ >= threshold_) FlushBlock();
 }
@@ -291,18 +313,20 @@ void TableBuilder::AddEntries(uint64_t n, const uint8_t *type, const uint32_t *k
   }
   keys_.reserve(keys_.size() + kb);
   vals_.reserve(vals_.size() + vb);
+  const uint64_t tag = res_host_ ? kArenaRef : 0; // (a resident builder: these are arena records)
+  arena_recs_ += tag ? n : 0;
   for (uint64_t i = 0; i < n; i++) {
     const uint32_t kl = key_len[i], vl = val_len[i];
     if (table_smallest_key_.empty()) table_smallest_key_.assign(reinterpret_cast<const char *>(key_src + key_off[i]), kl);
     type_.push_back(type[i]);
     key_len_.push_back(kl);
-    key_off_.push_back(keys_.size());
+    key_off_.push_back(keys_.size() | tag);
     keys_.append(key_src + key_off[i], kl);
     if (vl != SSTC_NO_VALUE) {
-      val_off_.push_back(vals_.size());
+      val_off_.push_back(vals_.size() | tag);
       vals_.append(val_src + val_off[i], vl);
     } else {
-      val_off_.push_back(0);
+      val_off_.push_back(tag);
     }
     val_len_.push_back(vl);
     txn_.push_back(txn[i]);
@@ -328,9 +352,19 @@ namespace {
 struct Staging {
   uint8_t *host = nullptr, *dev = nullptr;
   uint64_t host_cap = 0, dev_cap = 0;
+  std::vector<hipEvent_t> ev; // one per D2H chunk of a Finish
   ~Staging() {
     if (host) (void)hipHostFree(host);
     if (dev) (void)hipFree(dev);
+    for (hipEvent_t e : ev) (void)hipEventDestroy(e);
+  }
+  hipEvent_t Event(uint64_t i) {
+    while (ev.size() <= i) {
+      hipEvent_t e = nullptr;
+      if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) throw std::runtime_error("hipEventCreate");
+      ev.push_back(e);
+    }
+    return ev[i];
   }
   uint8_t *Host(uint64_t n) {
     if (n > host_cap) {
@@ -358,6 +392,55 @@ struct Staging {
 };
 thread_local std::map<int, Staging> g_stage; // device -> staging
 
+// Finish() writes the file image in chunks as they arrive from the device
+constexpr uint64_t kWriteChunk = 8ull << 20;
+constexpr uint64_t kDirectAlign = 4096;
+
+// Writes the image h[0, file_bytes) of an SST at offset 0: the 4 KiB-aligned
+// part through a second O_DIRECT descriptor (the page-locked image goes to
+// the device without a copy into the page cache: a buffered pwrite of a
+// 44 MB table cost 4-5 ms of memcpy on top of the fsync), the unaligned tail
+// through the builder's own descriptor.  Same bytes, same offsets, same
+// durability (Finish fsyncs after); a file system without O_DIRECT, or a
+// direct write it refuses, takes buffered pwrites.  SSTC_NO_DIRECT_IO=1: always buffered.
+class FileWriter {
+public:
+  FileWriter(int fd, const std::string &path, const uint8_t *h) : fd_(fd), h_(h) {
+    static const bool off = std::getenv("SSTC_NO_DIRECT_IO") != nullptr;
+    if (!off && !(reinterpret_cast<uintptr_t>(h) & (kDirectAlign - 1)))
+      dfd_ = ::open(path.c_str(), O_WRONLY | O_DIRECT | O_CLOEXEC);
+  }
+  ~FileWriter() {
+    if (dfd_ >= 0) ::close(dfd_);
+  }
+  bool direct() const { return direct_used_; }
+  // write [done_, end); `last`: end is the file's end (write the unaligned tail too)
+  void WriteUpTo(uint64_t end, bool last) {
+    if (dfd_ >= 0) {
+      const uint64_t a = end & ~(kDirectAlign - 1);
+      if (a > done_) {
+        if (pwrite_all(dfd_, h_ + done_, a - done_, done_)) {
+          direct_used_ = true;
+          done_ = a;
+        } else { // refused (alignment rules of this file system): buffered from here on
+          ::close(dfd_);
+          dfd_ = -1;
+        }
+      }
+      if (!last) return;
+    }
+    if (end > done_ && !pwrite_all(fd_, h_ + done_, end - done_, done_))
+      throw std::runtime_error("Error when flushing sstable"); // table_builder.cc:155-170
+    done_ = end;
+  }
+
+private:
+  int fd_, dfd_ = -1;
+  const uint8_t *h_;
+  uint64_t done_ = 0;
+  bool direct_used_ = false;
+};
+
 // makes `dev` current for the scope and restores the caller's device
 struct DeviceScope {
   int prev = -1;
@@ -377,6 +460,7 @@ uint64_t align256(uint64_t x) { return (x + 255) & ~uint64_t(255); }
 void TableBuilder::Finish() {
   if (fd_ < 0) throw std::runtime_error("TableBuilder::Finish: file not open");
   const double t_begin = trace_host() ? now_ms() : 0;
+  double t_enc = t_begin, t_d2h = t_begin, t_write = t_begin;
   FlushBlock();
   const uint64_t n = type_.size();
   const uint64_t nb = blk_first_.size() - 1;
@@ -409,26 +493,63 @@ void TableBuilder::Finish() {
     h2d(ctx_, d + o_kl, key_len_.data(), 4 * n);
     h2d(ctx_, d + o_vl, val_len_.data(), 4 * n);
     h2d(ctx_, d + o_txn, txn_.data(), 8 * n);
-    h2d(ctx_, d + o_ko, key_off_.data(), 8 * n);
-    h2d(ctx_, d + o_vo, val_off_.data(), 8 * n);
     h2d(ctx_, d + o_first, blk_first_.data(), 8 * (nb + 1));
-    h2d(ctx_, d + o_keys, keys_.data(), keys_.size());
-    h2d(ctx_, d + o_vals, vals_.data(), vals_.size());
+    const uint8_t *key_src = d + o_keys, *val_src = d + o_vals;
+    std::vector<uint64_t> ko2, vo2; // (a resident builder with arena records: offsets from one base)
+    if (!res_host_) {
+      h2d(ctx_, d + o_ko, key_off_.data(), 8 * n);
+      h2d(ctx_, d + o_vo, val_off_.data(), 8 * n);
+      h2d(ctx_, d + o_keys, keys_.data(), keys_.size());
+      h2d(ctx_, d + o_vals, vals_.data(), vals_.size());
+    } else if (arena_recs_ == 0) {
+      // every record is in the resident inputs: their device copy is the
+      // source, nothing but the record columns goes up
+      key_src = val_src = res_->DeviceBytes();
+      h2d(ctx_, d + o_ko, key_off_.data(), 8 * n);
+      h2d(ctx_, d + o_vo, val_off_.data(), 8 * n);
+    } else {
+      h2d(ctx_, d + o_keys, keys_.data(), keys_.size());
+      h2d(ctx_, d + o_vals, vals_.data(), vals_.size());
+      const uint8_t *rdev = res_->DeviceBytes();
+      const uint8_t *base = std::min<const uint8_t *>({rdev, key_src, val_src});
+      ko2.resize(n);
+      vo2.resize(n);
+      for (uint64_t i = 0; i < n; i++) {
+        const uint64_t k = key_off_[i], v = val_off_[i];
+        ko2[i] = k & kArenaRef ? static_cast<uint64_t>(key_src - base) + (k & ~kArenaRef)
+                               : static_cast<uint64_t>(rdev - base) + k;
+        vo2[i] = v & kArenaRef ? static_cast<uint64_t>(val_src - base) + (v & ~kArenaRef)
+                               : static_cast<uint64_t>(rdev - base) + v;
+      }
+      key_src = val_src = base;
+      h2d(ctx_, d + o_ko, ko2.data(), 8 * n);
+      h2d(ctx_, d + o_vo, vo2.data(), 8 * n);
+    }
     sstc_records rec{d + o_type, reinterpret_cast<uint32_t *>(d + o_kl), reinterpret_cast<uint32_t *>(d + o_vl),
                      reinterpret_cast<uint64_t *>(d + o_txn), reinterpret_cast<uint64_t *>(d + o_ko),
                      reinterpret_cast<uint64_t *>(d + o_vo)};
-    check(sstc_encode_blocks(ctx_, d + o_keys, d + o_vals, rec, n, reinterpret_cast<uint64_t *>(d + o_first), nb, 0,
+    check(sstc_encode_blocks(ctx_, key_src, val_src, rec, n, reinterpret_cast<uint64_t *>(d + o_first), nb, 0,
                              d + o_dst, reinterpret_cast<uint64_t *>(d + o_off), reinterpret_cast<uint64_t *>(d + o_len)),
           "sstc_encode_blocks");
     uint64_t errs = 0;
     check(sstc_ctx_error_count(ctx_, &errs), "sstc_ctx_error_count"); // synchronises the stream
-    // blocks straight into the file image, the block index beside it
-    if (!d2h(ctx_, h, d + o_dst, data_bytes) || !d2h(ctx_, blk_off.data(), d + o_off, (nb + 1) * 8) ||
-        !d2h(ctx_, blk_len.data(), d + o_len, nb * 8) || !sync(ctx_))
+    if (trace_host()) t_enc = now_ms();
+    // the block index first (the meta section below needs it), then the
+    // blocks straight into the file image in chunks, each chunk's arrival an
+    // event: the file is written chunk by chunk behind the copies
+    if (!d2h(ctx_, blk_off.data(), d + o_off, (nb + 1) * 8) || !d2h(ctx_, blk_len.data(), d + o_len, nb * 8))
       throw std::runtime_error("hipMemcpyAsync D2H failed");
+    for (uint64_t c = 0; c * kWriteChunk < data_bytes; c++) {
+      const uint64_t at = c * kWriteChunk, len = std::min(kWriteChunk, data_bytes - at);
+      if (!d2h(ctx_, h + at, d + o_dst + at, len) || hipEventRecord(stage.Event(c), stream_of(ctx_)) != hipSuccess)
+        throw std::runtime_error("hipMemcpyAsync D2H failed");
+    }
+    // (the block index is in once the first chunk's event has fired)
+    if (hipEventSynchronize(stage.Event(0)) != hipSuccess) throw std::runtime_error("hipEventSynchronize failed");
   }
   // meta section: one entry per block (table_builder.cc:101-145), then the
   // footer (table_builder.cc:179-211), appended to the file image in place
+  if (trace_host()) t_d2h = now_ms();
   uint8_t *w = h + data_bytes;
   auto put = [&w](const void *p, uint64_t len) {
     std::memcpy(w, p, len);
@@ -437,25 +558,38 @@ void TableBuilder::Finish() {
   for (uint64_t b = 0; b < nb; b++) {
     const uint64_t f = blk_first_[b], l = blk_first_[b + 1] - 1;
     put(&key_len_[f], 4);
-    put(keys_.data() + key_off_[f], key_len_[f]);
+    put(KeyPtr(f), key_len_[f]);
     put(&key_len_[l], 4);
-    put(keys_.data() + key_off_[l], key_len_[l]);
+    put(KeyPtr(l), key_len_[l]);
     put(&blk_off[b], 8);
     put(&blk_len[b], 8);
   }
   const uint64_t meta_off = data_bytes, foot[5] = {nb, meta_off, meta_bytes, min_txn_, max_txn_};
   put(foot, 40);
-  if (!pwrite_all(fd_, h, file_bytes, 0)) throw std::runtime_error("Error when flushing sstable"); // table_builder.cc:155-170
+  const double t_meta = trace_host() ? now_ms() : 0;
+  // the data blocks as their chunks land, then the rest (table_builder.cc:
+  // 155-170 writes the same bytes block by block)
+  FileWriter out(fd_, filename_, h);
+  for (uint64_t c = 0; nb && c * kWriteChunk < data_bytes; c++) {
+    if (hipEventSynchronize(stage.Event(c)) != hipSuccess) throw std::runtime_error("hipEventSynchronize failed");
+    out.WriteUpTo(std::min((c + 1) * kWriteChunk, data_bytes), false);
+  }
+  out.WriteUpTo(file_bytes, true);
+  if (trace_host()) t_write = now_ms();
   current_offset_ = file_bytes;
   if (::fsync(fd_) < 0) throw std::runtime_error("fsync failed");
   // the stream is idle here: free what this thread's builders outgrew
   g_surplus.v.clear();
   FlushDeferredHostFrees();
   if (trace_host())
-    std::fprintf(stderr, "[sstc] Finish %llu records %llu B: %.3f ms; page-locked allocs so far %llu calls %llu B %.3f ms\n",
+    std::fprintf(stderr,
+                 "[sstc] Finish %llu records %llu B: %.3f ms (H2D + encode %.3f, D2H %.3f, meta %.3f, pwrite %.3f, "
+                 "fsync %.3f%s%s); page-locked allocs so far %llu calls %llu B %.3f ms\n",
                  static_cast<unsigned long long>(type_.size()), static_cast<unsigned long long>(file_bytes),
-                 now_ms() - t_begin, static_cast<unsigned long long>(g_pin_calls),
-                 static_cast<unsigned long long>(g_pin_bytes), g_pin_ms);
+                 now_ms() - t_begin, t_enc - t_begin, t_d2h - t_enc, t_meta - t_d2h, t_write - t_meta,
+                 now_ms() - t_write, res_host_ ? (arena_recs_ ? ", resident + arena" : ", resident") : "",
+                 out.direct() ? ", direct" : "",
+                 static_cast<unsigned long long>(g_pin_calls), static_cast<unsigned long long>(g_pin_bytes), g_pin_ms);
 }
 
 // ----------------------------------------------------------------- TableReader
@@ -660,6 +794,18 @@ sstc_ctx *ThreadContext() {
     if (hipStreamCreateWithFlags(&h.stream, hipStreamNonBlocking) != hipSuccess)
       throw std::runtime_error("hipStreamCreateWithFlags failed");
     check(sstc_ctx_create(dev, h.stream, &h.ctx), "sstc_ctx_create");
+    // the runtime's pageable-copy paths set themselves up on first use (~10 ms
+    // each way): once here, when the engine opens the codec, not inside the
+    // first compaction's merge (ResidentInputs uploads from the file maps and
+    // downloads into ordinary memory)
+    void *d = nullptr;
+    uint64_t word = 0;
+    if (hipMalloc(&d, 64) == hipSuccess) {
+      (void)hipMemcpyAsync(d, &word, 8, hipMemcpyHostToDevice, h.stream);
+      (void)hipMemcpyAsync(&word, d, 8, hipMemcpyDeviceToHost, h.stream);
+      (void)hipStreamSynchronize(h.stream);
+      (void)hipFree(d);
+    }
   }
   return h.ctx;
 }

@@ -512,6 +512,35 @@ int sstc_compact(sstc_ctx *c, const uint8_t *d_src, const uint64_t *d_blk_off, c
   return SSTC_OK;
 }
 
+int sstc_merge_records(sstc_ctx *c, const uint8_t *d_src, const uint64_t *d_blk_off, const uint64_t *d_blk_len,
+                       uint64_t nblocks, const uint64_t *h_table_first_block, uint32_t ntables, uint32_t txn_mode,
+                       sstc_merged_record *d_out, uint64_t max_records, sstc_merge_result *result) {
+  if (!c || !h_table_first_block || !result || (nblocks && (!d_src || !d_blk_off || !d_blk_len)) ||
+      (max_records && !d_out))
+    return fail(SSTC_E_INVALID_ARG, "sstc_merge_records: NULL argument");
+  if (txn_mode > SSTC_TXN_CORRECT) return fail(SSTC_E_INVALID_ARG, "sstc_merge_records: bad txn mode");
+  if (ntables == 0 || h_table_first_block[0] != 0 || h_table_first_block[ntables] != nblocks)
+    return fail(SSTC_E_INVALID_ARG, "sstc_merge_records: table ranges must cover the block list");
+  for (uint32_t t = 0; t < ntables; t++)
+    if (h_table_first_block[t] > h_table_first_block[t + 1])
+      return fail(SSTC_E_INVALID_ARG, "sstc_merge_records: table ranges must be ascending");
+  if (int r = bind_device(c)) return r;
+  uint64_t res[5] = {0, 0, 0, 0, 0};
+  std::string err;
+  sstc::MergeOut mo{d_out, max_records, {0, 0}};
+  const int rc = sstc::compact_impl(c->arena, c->stream, c->err_count, d_src, d_blk_off, d_blk_len, nblocks,
+                                    h_table_first_block, ntables, 1, 1, 1, txn_mode, nullptr, 0, nullptr, nullptr,
+                                    0, res, err, &mo);
+  result->records = res[0];
+  result->cross_ties = mo.ties[0];
+  result->tie_diffs = mo.ties[1];
+  if (rc != SSTC_OK) {
+    (void)hipStreamSynchronize(c->stream);
+    return fail(rc, ("sstc_merge_records: " + err).c_str());
+  }
+  return SSTC_OK;
+}
+
 int sstc_copy_probe(sstc_ctx *c, const uint8_t *d_src, uint8_t *d_dst, uint64_t nbytes) {
   if (!c || (nbytes && (!d_src || !d_dst))) return fail(SSTC_E_INVALID_ARG, "sstc_copy_probe: NULL argument");
   if ((nbytes | reinterpret_cast<uintptr_t>(d_src) | reinterpret_cast<uintptr_t>(d_dst)) & 15u)

@@ -980,6 +980,60 @@ __global__ __launch_bounds__(kFtThreads) void ck_filter_kernel(const SK *s, uint
   }
 }
 
+// The merged order itself (sstc_merge_records: MergeIterator's SeekToFirst +
+// Next sequence, merge_iterator.cc:34-46,79-92, without the compaction's
+// filter): a thread per merged position writes the record's key offset and
+// its txn as the reference's iterator reads it (the merge txn unless the
+// decode lowered it, kSkRead).  Equal (key, merge txn) neighbours are where
+// the reference's std::priority_queue decides the order by heap history
+// (merge_iterator.h:91-95 compares only key and txn), so they are counted:
+// ties[0] = such neighbours from different inputs, ties[1] = such neighbours
+// (any inputs) whose type, txn as read or value differ.  Both rare; the host
+// takes the heap's own order when both are non-zero.
+__device__ __forceinline__ uint32_t run_of_record(const uint64_t *rs, uint32_t nruns, uint64_t id) {
+  uint32_t lo = 0, hi = nruns; // last run start <= id
+  while (lo + 1 < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (rs[mid] <= id) lo = mid;
+    else hi = mid;
+  }
+  return lo;
+}
+
+__global__ __launch_bounds__(256) void ck_merged_kernel(const SK *s, uint64_t n, KeyView kv, const uint64_t *rs,
+                                                        uint32_t nruns, sstc_merged_record *out,
+                                                        unsigned long long *ties, Abort stop,
+                                                        unsigned long long *guard, uint32_t txn_mode) {
+  if (stop()) return; // a rejected job: the host reads the verdicts, nothing here is used
+  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const SK x = s[i];
+  if (x.id >= n) { // a broken merge: rejected by the guard, no source read
+    atomicOr(guard, kGuardMergeId);
+    return;
+  }
+  const RecX rr = kv.rx[x.id];
+  const uint32_t kl = x.kl & ~kSkRead;
+  const uint64_t tread = x.kl & kSkRead ? read_txn(kv, rr, kl, txn_mode) : x.tx;
+  sstc_merged_record m;
+  m.key_off = rr.ko;
+  m.txn = tread;
+  out[i] = m;
+  if (i == 0) return;
+  const SK pv = s[i - 1];
+  if (pv.id >= n || pv.tx != x.tx || !ff_same_key(pv, x, kv)) return;
+  // equal (key, merge txn): the rare path
+  if (run_of_record(rs, nruns, pv.id) != run_of_record(rs, nruns, x.id)) atomicAdd(&ties[0], 1ull);
+  const RecX pr = kv.rx[pv.id];
+  const uint64_t ptread = pv.kl & kSkRead ? read_txn(kv, pr, kl, txn_mode) : pv.tx;
+  bool diff = pr.type != rr.type || pr.vl != rr.vl || ptread != tread;
+  if (!diff && rr.vl != kNoValue) {
+    const uint8_t *a = kv.src + rr.ko + kl + 4, *b = kv.src + pr.ko + kl + 4;
+    for (uint32_t j = 0; j < rr.vl && !diff; j++) diff = a[j] != b[j];
+  }
+  if (diff) atomicAdd(&ties[1], 1ull);
+}
+
 // The output table and block counts stay on the device (dn[0], dn[1]): the
 // layout kernels run on host-side upper bounds (nt_max, nb_max: every table
 // but the last holds >= table_limit key+value bytes, every block but a
@@ -1476,7 +1530,7 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
                  const uint64_t *d_blk_len, uint64_t nblocks, const uint64_t *h_tfb, uint32_t ntables,
                  uint64_t block_threshold, uint64_t table_limit, uint32_t base_level, uint32_t txn_mode,
                  uint8_t *d_dst, uint64_t dst_cap, uint64_t *d_table_off, uint64_t *d_table_len, uint64_t max_tables,
-                 uint64_t *res, std::string &err) {
+                 uint64_t *res, std::string &err, MergeOut *mo) {
   try {
     Pool pool(arena);
     // Host syncs: (1) the run starts and the input block bytes (they size
@@ -1537,6 +1591,10 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
       err = "too many records";
       return SSTC_E_INVALID_ARG;
     }
+    if (mo && n > mo->cap) { // (nothing else is enqueued yet)
+      err = "more records than max_records";
+      return SSTC_E_CAPACITY;
+    }
     const uint64_t wsn = scan_workspace_elems(n + 1) + 64;
     uint64_t *ws2 = pool.get<uint64_t>(wsn);
     RecX *RX = pool.get<RecX>(n);
@@ -1552,6 +1610,11 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
       if (arena.host[0] != arena.host[1]) {
         err = "an input block failed to decode";
         return SSTC_E_INVALID_ARG;
+      }
+      if (mo) { // nothing to merge
+        CK(hipStreamSynchronize(s));
+        mo->ties[0] = mo->ties[1] = 0;
+        return SSTC_OK;
       }
       if (max_tables < 1 || dst_cap < 40) {
         err = "output capacity";
@@ -1681,12 +1744,6 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
         }
       }
     }
-    // 3. keep / drop and the survivors gathered in merge order with their
-    // prefix sums (sized by n: the kept count is known after the pass)
-    ck_filter_kernel<<<static_cast<uint32_t>(fftiles), kFtThreads, 0, s>>>(A, n, kv, base_level, KR, Pd, Pe, ffws,
-                                                                        totals, stop, guard, txn_mode);
-    if (arena.fault == 1) CK(hipMemsetAsync(KR.ko, 0xFF, n * sizeof(uint64_t), s)); // test: bad key offsets
-    if (arena.fault == 2) CK(hipMemsetAsync(Pe, 0x5A, (n + 1) * sizeof(uint64_t), s)); // test: bad prefix sums
     // the job's error words (decode errors, unsorted inputs, guard bits) are
     // read after the last kernel: a rejected job writes nothing (the filter
     // of a stopped job reports no survivor)
@@ -1708,6 +1765,27 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
       }
       return SSTC_OK;
     };
+    if (mo) { // sstc_merge_records: the merged order, no filter
+      unsigned long long *ties = reinterpret_cast<unsigned long long *>(pool.get<uint64_t>(2));
+      CK(hipMemsetAsync(ties, 0, 2 * sizeof(uint64_t), s));
+      ck_merged_kernel<<<grid(n), 256, 0, s>>>(A, n, kv, rb, static_cast<uint32_t>(nruns), mo->out, ties, stop, guard,
+                                               txn_mode);
+      CK(hipGetLastError());
+      fetch(arena, s, {reinterpret_cast<const uint64_t *>(err_count), errs, reinterpret_cast<const uint64_t *>(bad),
+                       reinterpret_cast<const uint64_t *>(guard), reinterpret_cast<const uint64_t *>(ties),
+                       reinterpret_cast<const uint64_t *>(ties + 1)},
+            nullptr, 0, true);
+      if (const int r = job_error(arena.host)) return r;
+      mo->ties[0] = arena.host[4];
+      mo->ties[1] = arena.host[5];
+      return SSTC_OK;
+    }
+    // 3. keep / drop and the survivors gathered in merge order with their
+    // prefix sums (sized by n: the kept count is known after the pass)
+    ck_filter_kernel<<<static_cast<uint32_t>(fftiles), kFtThreads, 0, s>>>(A, n, kv, base_level, KR, Pd, Pe, ffws,
+                                                                        totals, stop, guard, txn_mode);
+    if (arena.fault == 1) CK(hipMemsetAsync(KR.ko, 0xFF, n * sizeof(uint64_t), s)); // test: bad key offsets
+    if (arena.fault == 2) CK(hipMemsetAsync(Pe, 0x5A, (n + 1) * sizeof(uint64_t), s)); // test: bad prefix sums
     if (max_tables == 0) { // no room for the first table (m >= 1 unless the job is rejected)
       fetch(arena, s, err_words, nullptr, 0, true);
       if (const int r = job_error(arena.host)) return r;

@@ -230,12 +230,20 @@ struct Arena {
   uint32_t fault = 0;
 };
 
+// sstc_merge_records: compact_impl stops after the merge and writes the merged
+// order (out, up to cap records) instead of filtering and encoding
+struct MergeOut {
+  sstc_merged_record *out;
+  uint64_t cap;
+  uint64_t ties[2]; // result: cross-input (key, merge txn) ties, ties whose records differ
+};
+
 int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, const uint8_t *d_src,
                  const uint64_t *d_blk_off,
                  const uint64_t *d_blk_len, uint64_t nblocks, const uint64_t *h_tfb, uint32_t ntables,
                  uint64_t block_threshold, uint64_t table_limit, uint32_t base_level, uint32_t txn_mode,
                  uint8_t *d_dst, uint64_t dst_cap, uint64_t *d_table_off, uint64_t *d_table_len, uint64_t max_tables,
-                 uint64_t *res, std::string &err);
+                 uint64_t *res, std::string &err, MergeOut *mo = nullptr);
 
 // SST open on the device (sstc_open_tables): block index outputs
 struct OpenOut {

@@ -308,7 +308,138 @@ int RunIter(int argc, char **argv) {
 }
 } // namespace
 
+// usage: <exe> --merge <dump> <mid_key_hex> [<file> <file_size>]...
+//   db::MergeIterator over TableReaderIterators of every file (as
+//   CreateMergeIterator makes them), every step's IsValid / key / value /
+//   type / txn written to <dump>: (1) SeekToFirst + Next to the end (the whole
+//   merged order), then SeekToLast + Prev while IsValid, as the reference's
+//   tests/test_mergeIterator.cc:154-182 walks it; (2) a second iterator
+//   walked half way, then SeekToLast, Prev x 3 (IsValid is the min heap's,
+//   the accessors read the min heap's top), Seek(mid key) + Next x 3,
+//   SeekToFirst + Next x 2 (only steps whose outcome the reference defines:
+//   no min-heap pop after SeekToLast, whose table iterators then hold new
+//   blocks while the min heap's keys still view the freed ones).  Linked against the reference's merge_iterator.cc
+//   this is the reference's trace; linked as the drop-in it is the device
+//   merge's, and the two must be equal.
+int RunMerge(int argc, char **argv) {
+  using namespace kvs;
+  std::FILE *dump = std::fopen(argv[2], "wb");
+  if (!dump) return 4;
+  const std::string mid = Unhex(argv[3]);
+  char tmpl[] = "/tmp/sstref_mergeXXXXXX";
+  if (!mkdtemp(tmpl)) return 3;
+  g_db_path = std::string(tmpl) + "/";
+  auto *db = new db::DBImpl(true);
+  auto put = [&](const void *p, size_t n) { std::fwrite(p, 1, n, dump); };
+  auto view = [&](std::string_view v) {
+    const uint8_t has = v.data() != nullptr;
+    const uint32_t n = static_cast<uint32_t>(v.size());
+    put(&has, 1), put(&n, 4);
+    if (n) put(v.data(), n);
+  };
+  auto make = [&](int pass) {
+    std::vector<std::unique_ptr<sstable::TableReaderIterator>> its;
+    for (int i = 4; i + 1 < argc; i += 2) {
+      its.push_back(OpenIterator(db, static_cast<SSTId>(100 * pass + i), argv[i],
+                                 std::strtoull(argv[i + 1], nullptr, 10)));
+      if (!its.back()) std::exit(4);
+    }
+    return std::make_unique<db::MergeIterator>(std::move(its));
+  };
+  uint64_t steps = 0, walked = 0;
+  auto step = [&](db::MergeIterator &it, char op, bool read = true) {
+    const uint8_t valid = it.IsValid();
+    put(&op, 1), put(&valid, 1);
+    if (read) {
+      const uint8_t type = static_cast<uint8_t>(it.GetType());
+      const TxnId txn = it.GetTransactionId();
+      put(&type, 1), put(&txn, 8);
+      view(it.GetKey());
+      view(it.GetValue());
+    }
+    steps++;
+  };
+  {
+    auto it = make(1);
+    for (it->SeekToFirst(); it->IsValid(); it->Next(), walked++) step(*it, 'N');
+    step(*it, 'E', false);
+    for (it->SeekToLast(); it->IsValid(); it->Prev()) step(*it, 'P');
+    step(*it, 'L', false);
+  }
+  if (walked >= 8) {
+    auto it = make(2);
+    it->SeekToFirst();
+    for (uint64_t i = 0; i < walked / 2; i++) it->Next();
+    step(*it, 'H');
+    it->SeekToLast(), step(*it, 'L');
+    for (int j = 0; j < 3; j++) it->Prev(), step(*it, 'P');
+    // (a Next here would pop the min heap, whose keys SeekToLast left
+    // dangling in the reference: its table iterators freed those blocks)
+    it->Seek(mid), step(*it, 'S');
+    for (int j = 0; j < 3; j++) it->Next(), step(*it, 'N');
+    it->SeekToFirst(), step(*it, 'F');
+    for (int j = 0; j < 2; j++) it->Next(), step(*it, 'N');
+  }
+  std::fclose(dump);
+  std::printf("merge ok %llu %llu\n", (unsigned long long)walked, (unsigned long long)steps);
+  std::fflush(stdout);
+  _exit(0);
+}
+
+// usage: <exe> --walk <level> [<file> <file_size>]...
+//   Diagnostic: the time of DoCompactJob's loop parts over db::MergeIterator
+//   (level 0: SeekToFirst + Next + the four accessors; 1: + the key compare of
+//   ShouldKeepEntry; 2: + TableBuilder::AddEntry into builders split at 32 MiB
+//   that are never finished -- no encode, no file written).
+int RunWalk(int argc, char **argv) {
+  using namespace kvs;
+  const int level = std::atoi(argv[2]);
+  char tmpl[] = "/tmp/sstref_walkXXXXXX";
+  if (!mkdtemp(tmpl)) return 3;
+  g_db_path = std::string(tmpl) + "/";
+  auto *db = new db::DBImpl(true);
+  std::vector<std::unique_ptr<sstable::TableReaderIterator>> its;
+  for (int i = 3; i + 1 < argc; i += 2) {
+    its.push_back(OpenIterator(db, static_cast<SSTId>(i), argv[i], std::strtoull(argv[i + 1], nullptr, 10)));
+    if (!its.back()) return 4;
+  }
+#ifdef SSTC_DROPIN
+  sstc::ThreadContext();
+#endif
+  auto it = std::make_unique<db::MergeIterator>(std::move(its));
+  const auto t0 = std::chrono::steady_clock::now();
+  it->SeekToFirst();
+  const auto t1 = std::chrono::steady_clock::now();
+  uint64_t n = 0, sum = 0, kept = 0;
+  std::string_view last;
+  std::unique_ptr<sstable::TableBuilder> b;
+  for (; it->IsValid(); it->Next(), n++) {
+    std::string_view key = it->GetKey(), value = it->GetValue();
+    const db::ValueType type = it->GetType();
+    const TxnId txn = it->GetTransactionId();
+    sum += key.size() + value.size() + static_cast<int>(type) + txn;
+    if (level >= 1) {
+      kept += last != key;
+      last = key;
+    }
+    if (level >= 2) {
+      if (!b) b = std::make_unique<sstable::TableBuilder>(g_db_path + "walk.sst", db->GetConfig());
+      b->AddEntry(key, value, txn, type);
+      if (b->GetDataSize() >= (32ull << 20)) b.reset();
+    }
+  }
+  const auto t2 = std::chrono::steady_clock::now();
+  std::printf("walk level %d: %llu records (%llu keys, sum %llu): SeekToFirst %.6f s, loop %.6f s = %.1f ns/record\n",
+              level, (unsigned long long)n, (unsigned long long)kept, (unsigned long long)sum,
+              std::chrono::duration<double>(t1 - t0).count(), std::chrono::duration<double>(t2 - t1).count(),
+              1e9 * std::chrono::duration<double>(t2 - t1).count() / (n ? n : 1));
+  std::fflush(stdout);
+  _exit(0);
+}
+
 int main(int argc, char **argv) {
+  if (argc >= 3 && std::string(argv[1]) == "--walk" && (argc - 3) % 2 == 0) return RunWalk(argc, argv);
+  if (argc >= 4 && std::string(argv[1]) == "--merge" && (argc - 4) % 2 == 0) return RunMerge(argc, argv);
   if (argc >= 6 && std::string(argv[1]) == "--loop" && (argc - 6) % 2 == 0) return RunLoop(argc, argv);
   if (argc >= 3 && std::string(argv[1]) == "--iter" && (argc - 3) % 2 == 0) return RunIter(argc, argv);
   if (argc < 4 || (argc - 4) % 4) {

@@ -171,7 +171,9 @@ def test_dropin_host_code_under_asan(tmp_path, name, exe):
 def test_unmodified_compact_cc_read_path(tmp_path, name):
     """The drop-in iterator's fallback when its table cannot be mapped: the
     data section read through the TableReader's own file object
-    (SSTC_DROPIN_NO_MAP forces it), outputs still the reference's."""
+    (SSTC_DROPIN_NO_MAP forces it; SSTC_DROPIN_HEAP_MERGE makes the drop-in
+    MergeIterator walk the table iterators, as it does when the device merge
+    cannot take the inputs), outputs still the reference's."""
     need(EXE)
     from oracle import table_key_range
     case = MANIFEST[name]
@@ -183,7 +185,7 @@ def test_unmodified_compact_cc_read_path(tmp_path, name):
         lo, hi = table_key_range(rec)
         args += [p, str(fs), lo.hex() or "-", hi.hex() or "-"]
     r = subprocess.run(args, capture_output=True, text=True, timeout=240,
-                       env=dict(os.environ, SSTC_DROPIN_NO_MAP="1", SSTC_TRACE_HOST="1"))
+                       env=dict(os.environ, SSTC_DROPIN_NO_MAP="1", SSTC_TRACE_HOST="1", SSTC_DROPIN_HEAP_MERGE="1"))
     assert r.returncode == 0, r.stderr[-2000:]
     assert "iterator read data section" in r.stderr and "iterator map data section" not in r.stderr
     _, outs = G.parse_pick_output(r.stdout)
@@ -283,3 +285,95 @@ def test_iterator_trace_equals_reference(oracle, tmp_path):
     assert dumps[0][0].startswith("iter ok ") and len(dumps[0][1]) > 1_000_000
     for out, dump in dumps[1:]:  # the drop-in (and its ASan build) walk exactly as the reference does
         assert out == dumps[0][0] and dump == dumps[0][1]
+
+
+def _merge_sets(name, oracle):
+    """(file images, block threshold) of the --merge trace cases"""
+    from sstcodec import workload as W
+    if name in CJ:
+        c = CJ[name]
+        sets = W.compaction_inputs(c["k"], c["n_per"], c["key_space"], vmax=c["vmax"], distinct=c["distinct"],
+                                   **c.get("gen", {}))
+        return [oracle.table_build(r, c["block_threshold"]) for r in sets]
+    if name.startswith("ties_"):
+        return tie_case(load_golden("compact_ties.npz"), name[5:], 1)[0]
+    if name == "versions":  # a key's versions out of txn order as read (empty-value PUTs, block_reader.cc:109-111)
+        sets = W.compaction_inputs(3, 1500, 50, seed=70, p_delete=0.1, vmin=0, vmax=3, distinct=False)
+        return [oracle.table_build(r, 256) for r in sets]
+    if name == "ragged":  # ragged keys 0-48 B (the empty key repeats), empty values, DELETEs
+        from test_gpu_compact_fuzz import ragged_sorted
+        return [oracle.table_build(ragged_sorted(900 + 300 * t, 610 + t), 4096) for t in range(4)]
+    if name == "one_table":
+        return [oracle.table_build(W.compaction_inputs(1, 3000, 9000, seed=9)[0], 4096)]
+    raise KeyError(name)
+
+
+MERGE_CASES = sorted(CJ) + ["ties_same", "ties_diff", "versions", "ragged", "one_table"]
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("name", MERGE_CASES)
+def test_merge_iterator_trace_equals_reference(oracle, tmp_path, name):
+    """the drop-in db::MergeIterator (device merge,
+    include/dropin/db/merge_iterator.h) against the reference's own
+    merge_iterator.cc over the same TableReaderIterators: the whole
+    SeekToFirst + Next walk (key, value incl. null vs empty views, type, txn
+    as read, IsValid) and the reference's quirks after it -- SeekToLast +
+    Prev gated by the MIN heap's IsValid (tests/test_mergeIterator.cc walks it
+    so), a half walk then SeekToLast / Prev / Next / Seek / SeekToFirst --
+    equal at every step.  The device merge serves every case but the
+    differing-tie one, which takes the heap's own order (heap mode)."""
+    need(EXE)
+    need(REF_EXE)
+    files = _merge_sets(name, oracle)
+    args = []
+    for i, f in enumerate(files):
+        p = str(tmp_path / f"m{i}.sst")
+        f.tofile(p)
+        args += [p, str(f.size + 1)]
+    mid = first_last_key(files[0])[1].hex() or "-"
+    dumps = []
+    runs = [(REF_EXE, "ref", {}), (EXE, "dropin", {"SSTC_TRACE_HOST": "1"}),
+            (EXE, "heap", {"SSTC_DROPIN_HEAP_MERGE": "1"})]
+    if name in ("small", "versions", "ties_diff") and os.path.exists(ASAN_EXE):
+        runs.append((ASAN_EXE, "asan", ASAN_ENV))
+    for exe, tag, env in runs:
+        d = str(tmp_path / f"{tag}.dump")
+        r = subprocess.run([exe, "--merge", d, mid] + args, capture_output=True, text=True, timeout=240,
+                           env=dict(os.environ, **env))
+        assert "AddressSanitizer" not in r.stderr, (tag, r.stderr[-3000:])
+        assert r.returncode == 0, (tag, r.stderr[-2000:])
+        if tag == "dropin":
+            mode = "heap mode" if name == "ties_diff" else "device merge"
+            assert f"MergeIterator over {len(files)} tables: {mode}" in r.stderr, r.stderr[-2000:]
+        dumps.append((tag, r.stdout.strip(), open(d, "rb").read()))
+    assert dumps[0][1].startswith("merge ok ") and len(dumps[0][2]) > 1000
+    want = merge_steps(dumps[0][2])
+    for tag, out, dump in dumps[1:]:
+        got = merge_steps(dump)
+        bad = next((i for i, (a, b) in enumerate(zip(got, want)) if a != b), None)
+        assert bad is None, (tag, bad, len(want), got[bad], want[bad])
+        assert out == dumps[0][1] and dump == dumps[0][2], tag
+
+
+def merge_steps(dump):
+    """the --merge dump as (op, valid, type, txn, key, value) steps"""
+    import struct
+    out, i = [], 0
+
+    def view():
+        nonlocal i
+        has, n = dump[i], struct.unpack_from("<I", dump, i + 1)[0]
+        v = (has, bytes(dump[i + 5:i + 5 + n]))
+        i += 5 + n
+        return v
+    while i < len(dump):
+        op, valid = chr(dump[i]), dump[i + 1]
+        i += 2
+        if op in "EL" and (i >= len(dump) or chr(dump[i]) in "NPHLSF"):  # the no-read steps
+            out.append((op, valid))
+            continue
+        typ, txn = dump[i], struct.unpack_from("<Q", dump, i + 1)[0]
+        i += 9
+        out.append((op, valid, typ, txn, view(), view()))
+    return out

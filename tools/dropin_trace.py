@@ -28,6 +28,9 @@ def key_range(rec):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", type=int, default=5)
+    ap.add_argument("--repeat", type=int, default=1)
+    ap.add_argument("--walk", type=int, nargs="*", default=[])
+    ap.add_argument("--pf", nargs="*", default=["24"])
     args = ap.parse_args()
     import sstcodec
     from sstcodec import workload as W
@@ -43,6 +46,21 @@ def main():
         lo, hi = key_range(rec)
         cmd += [p, str(fs), lo.hex() or "-", hi.hex() or "-"]
     codec.close()
+    ref = os.path.join(ROOT, "oracle", "_ref", "ref_pick_compact")
+    files = cmd[4:]
+    walk = [a for i, a in enumerate(files) if i % 4 < 2]
+    for level in args.walk:  # the loop's parts (ref_pick_compact.cc --walk)
+        for e, tag, pf in [(exe, "dropin", p) for p in args.pf] + [(ref, "reference", None)]:
+            if level == 2 and tag == "reference":
+                continue
+            env = dict(os.environ, **({"SSTC_DROPIN_PF": pf} if pf is not None else {}))
+            r = subprocess.run([e, "--walk", str(level)] + walk, capture_output=True, text=True, env=env)
+            print(tag, "pf", pf, r.stdout.strip(), r.stderr[-500:] if r.returncode else "", flush=True)
+    for rep in range(args.repeat - 1):  # untraced runs: PickCompact time only
+        d = os.path.join(td, f"db{rep}")
+        os.makedirs(d)
+        r = subprocess.run([exe, d] + cmd[2:], capture_output=True, text=True)
+        print("untraced", [ln for ln in r.stdout.splitlines() if ln.startswith("time")], flush=True)
     r = subprocess.run(cmd, capture_output=True, text=True, env=dict(os.environ, SSTC_TRACE_HOST="1"))
     print("rc", r.returncode, [ln for ln in r.stdout.splitlines() if ln.startswith(("time", "init"))])
     tot = collections.defaultdict(float)
@@ -56,6 +74,9 @@ def main():
         elif ln.startswith("[sstc] Finish"):
             tot["Finish"] += float(ln.split(": ")[1].split(" ms")[0])
             cnt["Finish"] += 1
+            for part, v in re.findall(r"(H2D \+ encode|D2H|meta|pwrite|fsync) ([0-9.]+)", ln):
+                tot["Finish: " + part] += float(v)
+                cnt["Finish: " + part] += 1
             last = ln
     for k, v in tot.items():
         print(f"{k}: {v:.1f} ms over {cnt[k]}")
