@@ -505,7 +505,7 @@ def codec_legs(codec, dev, stream, src, off, ln, steps):
 def read_compact_traffic(workload):
     """HBM bytes per sstc_compact call from the PMC passes of
     tools/pmc_compact_job.sh (profiles/pmc_compact*.json), or None."""
-    for name in ("pmc_compact.json", "pmc_compact_c4.json"):
+    for name in ("pmc_compact.json", "pmc_compact_c4.json", "pmc_compact_c5.json"):
         try:
             with open(os.path.join(ROOT, "profiles", name)) as f:
                 d = json.load(f)
@@ -676,25 +676,39 @@ def files_leg(codec, paths, td, fixture, in_bytes, reps=3, io_threads=8):
             "verified_vs_reference": bool(ok)}
 
 
-def compact_leg(codec, dev, stream, steps, cpu_ref=True, files=True):
-    """BASELINE config 3 -- the compaction hot path north_star replaces
-    (db/compact.cc:232-322): 8 SSTs x 1 M records (16 B keys, 100 B values,
-    disjoint interleave) -> sstc_compact (decode, k-way merge, keep/drop,
-    32 MiB table split, 4 KiB block split, encode, meta, footers) -> 28 output
-    SSTs.  Inputs are written by the flush-path sstc::TableBuilder and must
-    hash to the reference TableBuilder's files; every output must hash to the
-    reference's compaction (tests/golden/compaction_configs.json "config3").
-    Device-resident time = median of `steps` calls, each bracketed by device
-    syncs.  Roofline: the job must read every input byte once and write every
-    output byte once: algorithmic bytes = input + output bytes.  `files`: the
-    same job file -> file (sstc_compact_files, fsync on) beside the
-    reference's own loop on the same files (cpu_baseline, like for like)."""
+COMPACT_WORKLOADS = {
+    3: "config3: 8 SSTs x 1 M records (16 B keys, 100 B values) -> 28 SSTs, sstc_compact, device-resident",
+    5: "config5: 8 SSTs x 5000 records over a shared 20 000-key space (Zipf 8 B - 64 KiB values, 10 % DELETE, "
+       "overlapping keys: the drop / overwrite path) -> 14 SSTs, sstc_compact, device-resident",
+}
+
+
+def compact_leg(codec, dev, stream, steps, cpu_ref=True, files=True, config=3, dropin=True):
+    """BASELINE config 3 (or 5) -- the compaction hot path north_star replaces
+    (db/compact.cc:232-322): config 3 = 8 SSTs x 1 M records (16 B keys, 100 B
+    values, disjoint interleave) -> 28 output SSTs; config 5 = Zipf values
+    8 B - 64 KiB with overlapping keys and DELETEs -> 14 SSTs.  sstc_compact
+    (decode, k-way merge, keep/drop, 32 MiB table split, 4 KiB block split,
+    encode, meta, footers).  Inputs are written by the flush-path
+    sstc::TableBuilder and must hash to the reference TableBuilder's files;
+    every output must hash to the reference's compaction
+    (tests/golden/compaction_configs.json).  Device-resident time = median of
+    `steps` calls, each bracketed by device syncs.  Roofline: the job must
+    read every input byte once and write every output byte once: algorithmic
+    bytes = input + output bytes.  `files`: the same job file -> file
+    (sstc_compact_files, fsync on) beside the reference's own loop on the
+    same files (cpu_baseline, like for like).  `dropin`: PickCompact under the
+    UNCHANGED db/compact.cc with the drop-ins (dropin_leg)."""
     import shutil
     import tempfile
-    fx = json.load(open(os.path.join(ROOT, "tests", "golden", "compaction_configs.json")))["config3"]
-    td = tempfile.mkdtemp(prefix="sstc_bench_c3_", dir=os.environ.get("TMPDIR", "/tmp"))
+    tag = f"config{config}"
+    fx = json.load(open(os.path.join(ROOT, "tests", "golden", "compaction_configs.json")))[tag]
+    td = tempfile.mkdtemp(prefix=f"sstc_bench_c{config}_", dir=os.environ.get("TMPDIR", "/tmp"))
     try:
-        job = GpuCompaction(codec, dev, stream, td, W.config_inputs(3), fx)
+        sets = W.config_inputs(config)
+        ranges = [record_key_range(r) for r in sets]
+        job = GpuCompaction(codec, dev, stream, td, sets, fx)
+        del sets
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         _, t = time_job(job, steps)
         e0.record(stream)
@@ -707,29 +721,106 @@ def compact_leg(codec, dev, stream, steps, cpu_ref=True, files=True):
         paths = job.paths
         job.free()
         alg = in_bytes + out_bytes
-        leg = {"workload": "config3: 8 SSTs x 1 M records (16 B keys, 100 B values) -> 28 SSTs, sstc_compact, "
-                           "device-resident", "steps": steps, "ms_median": round(t * 1e3, 4),
+        leg = {"workload": COMPACT_WORKLOADS[config], "steps": steps, "ms_median": round(t * 1e3, 4),
                "ms_events_one_call": round(e0.elapsed_time(e1), 4),
                "GiBps_in": round(in_bytes / t / 2 ** 30, 1), "records_in": res.records_in,
                "records_kept": res.records_kept, "tables_out": res.tables_out, "input_bytes": in_bytes,
                "output_bytes": out_bytes, "verified_vs_reference": ok, "inputs_equal_reference": job.inputs_ok,
                "roofline": {"bound": "hbm", "achieved": round(alg / t / 1e9, 1), "peak": HBM_PEAK_GBPS,
                             "unit": "GB/s", "frac": round(alg / t / 1e9 / HBM_PEAK_GBPS, 4),
-                            "traffic": read_compact_traffic("config3"), "alg_bytes_per_call": alg,
+                            "traffic": read_compact_traffic(tag), "alg_bytes_per_call": alg,
                             "alg": "input bytes read once + output bytes written once (a copy's traffic)",
                             "kernel": "sstc_compact (whole job, ~30 kernels; wall time incl. its host syncs)"}}
         if not ok:
-            raise SystemExit("compact leg: outputs differ from the reference's compaction: timing invalid")
+            raise SystemExit(f"{tag} compact leg: outputs differ from the reference's compaction: timing invalid")
         if files:
             leg["files"] = files_leg(codec, paths, td, fx, in_bytes)
         if cpu_ref:
             base = ref_compact_baseline(paths, td, in_bytes)
             if base:
-                base["compare_with"] = "legs.compact.files (file -> file, fsync on): the like-for-like GPU number"
+                base["compare_with"] = "legs.*.files (file -> file, fsync on): the like-for-like GPU number"
                 leg["cpu_baseline"] = base
+        if dropin:
+            leg["dropin"] = dropin_leg(paths, ranges, fx, td, in_bytes)
         return leg
     finally:
         shutil.rmtree(td, ignore_errors=True)
+
+
+def record_key_range(rec):
+    """first and last key of a record set (what VersionEdit records for an input SST)"""
+    ko, kl, ks = rec["key_off"], rec["key_len"], rec["key_src"]
+    return (bytes(ks[int(ko[0]):int(ko[0]) + int(kl[0])]), bytes(ks[int(ko[-1]):int(ko[-1]) + int(kl[-1])]))
+
+
+def dropin_leg(paths, ranges, fixture, td, in_bytes, reps=2):
+    """Compact::PickCompact -> DoCompactJob, the reference's
+    own db/compact.cc compiled UNCHANGED with include/dropin/ first on the
+    include path (oracle/Makefile target `dropin`: the engine build, linked
+    with libsstcodec.so), so its MergeIterator merges on the device
+    (include/dropin/db/merge_iterator.h: inputs mapped + uploaded once,
+    sstc_merge_records), its TableReaderIterators are the drop-in readers and
+    every output SST is built by sstc::TableBuilder (device encode from the
+    resident inputs, O_DIRECT write + fsync); timed beside the reference AS
+    WRITTEN (oracle/_ref/ref_pick_compact: the same compact.cc with the
+    reference's merge_iterator.cc, table_reader_iterator.cc and
+    table_builder.cc) on the same input files, same host, one process each,
+    dirty pages synced before every run.  The drop-in's outputs are verified
+    against the reference's fixed-semantics outputs; seconds = PickCompact
+    wall time as the harness prints it (codec context opened before the timer,
+    as an engine does at DB open)."""
+    import subprocess
+    exe = os.path.join(ROOT, "oracle", "_ref", "compact_dropin")
+    ref = os.path.join(ROOT, "oracle", "_ref", "ref_pick_compact")
+    if not os.path.exists(exe):
+        return None
+    args = [str(fixture["block_threshold"]), str(fixture["table_limit"])]
+    for (p, fs), (lo, hi) in zip(paths, ranges):
+        args += [p, str(fs), lo.hex() or "-", hi.hex() or "-"]
+
+    def run(binary, tag, i, env=None):
+        d = os.path.join(td, f"pick_{tag}_{i}")
+        os.makedirs(d)
+        os.sync()
+        r = subprocess.run([binary, d] + args, capture_output=True, text=True, timeout=600,
+                           env=dict(os.environ, **(env or {})))
+        if r.returncode != 0:
+            raise SystemExit(f"dropin leg: {tag} failed: {r.stderr[-500:]}")
+        t = float(next(ln.split()[1] for ln in r.stdout.splitlines() if ln.startswith("time ")))
+        outs = [ln.split() for ln in r.stdout.splitlines() if ln.startswith("out ")]
+        return t, outs, d
+
+    gpu, cpu, ok = [], [], True
+    for i in range(reps):
+        t, outs, d = run(exe, "dropin", i)
+        got = []
+        for o in outs:
+            with open(o[1], "rb") as f:
+                got.append((_sha(f.read()), int(o[2])))
+        ok &= got == [(w["sha256"], w["file_size"]) for w in fixture["outputs_base1"]]
+        gpu.append(t)
+        import shutil
+        shutil.rmtree(d, ignore_errors=True)
+        if os.path.exists(ref):  # (config 5 as written needs its freed blocks kept mapped, else it crashes)
+            tr, _, d = run(ref, "ref", i, {"GLIBC_TUNABLES": "glibc.malloc.trim_threshold=17179869184"})
+            cpu.append(tr)
+            shutil.rmtree(d, ignore_errors=True)
+    if not ok:
+        raise SystemExit("dropin leg: the unchanged compact.cc with the drop-ins wrote other bytes than the reference")
+    g = float(np.median(gpu))
+    leg = {"what": "Compact::PickCompact (db/compact.cc unchanged) with the drop-in MergeIterator (device merge), "
+                   "TableReaderIterator and TableBuilder (device encode), input files page-cache-hot, outputs "
+                   "written + fsync'd", "s_runs": [round(x, 4) for x in gpu], "s_median": round(g, 4),
+           "GiBps_in": round(in_bytes / g / 2 ** 30, 3), "verified_vs_reference": bool(ok)}
+    if cpu:
+        c = float(np.median(cpu))
+        leg["cpu_baseline"] = {"value": round(c, 4), "unit": "s", "s_runs": [round(x, 4) for x in cpu],
+                               "cores": 1, "kind": "reference",
+                               "sample": "the same PickCompact with the reference's own merge_iterator.cc, "
+                                         "table_reader_iterator.cc and table_builder.cc (oracle/_ref/"
+                                         "ref_pick_compact), same input files, same host"}
+        leg["ratio_to_reference"] = round(g / c, 3)
+    return leg
 
 
 class HostPlumbing:
@@ -809,6 +900,9 @@ def main():
     ap.add_argument("--compact-steps", type=int, default=10)
     ap.add_argument("--no-files-leg", action="store_true", help="skip the config-3 file -> file compaction leg")
     ap.add_argument("--no-compact4", action="store_true", help="skip the config-4 (128 SSTs per GPU) leg")
+    ap.add_argument("--no-compact5", action="store_true", help="skip the config-5 (Zipf values) leg")
+    ap.add_argument("--no-dropin", action="store_true",
+                    help="skip PickCompact under the unchanged compact.cc (drop-ins vs the reference as written)")
     ap.add_argument("--c4-steps", type=int, default=5)
     ap.add_argument("--c4-keys", type=int, default=100_000, help="records per SST of the config-4 leg")
     ap.add_argument("--plumbing", action="store_true",
@@ -894,7 +988,12 @@ def main():
                 out["legs"] = codec_legs(codec, dev, stream, src, off, ln, max(10, args.steps // 2))
             if not args.no_compact:
                 out.setdefault("legs", {})["compact"] = compact_leg(codec, dev, stream, args.compact_steps,
-                                                                     not args.no_cpu_baseline, not args.no_files_leg)
+                                                                     not args.no_cpu_baseline, not args.no_files_leg,
+                                                                     dropin=not args.no_dropin)
+            if not args.no_compact5:
+                out.setdefault("legs", {})["compact_config5"] = compact_leg(
+                    codec, dev, stream, args.compact_steps, not args.no_cpu_baseline, False, config=5,
+                    dropin=not args.no_dropin)
             if not args.no_hbm_variant:
                 out["roofline"]["hbm_1gib"] = hbm_variant(codec, dev, 4 * nb)
             if not args.no_e2e:
@@ -934,6 +1033,14 @@ def compact4(args, ranks, codec, dev, stream):
         make = lambda r: GpuCompaction(codec, dev, stream, td, W.config_inputs(4, r, keys=args.c4_keys),  # noqa: E731
                                        _c4_fixture(r, args.c4_keys))
         leg = config4_leg(ranks, make, args.c4_steps, lambda r: _c4_fixture(r, args.c4_keys))
+        fx = _c4_fixture(ranks.rank, args.c4_keys)
+        if ranks.world == 1 and fx is not None and not args.no_dropin:  # rank 0's shard through the unchanged caller
+            sets = W.config_inputs(4, ranks.rank, keys=args.c4_keys)
+            ranges = [record_key_range(r) for r in sets]
+            del sets
+            paths = [(os.path.join(td, f"in{i}.sst"), os.path.getsize(os.path.join(td, f"in{i}.sst")) + 1)
+                     for i in range(len(ranges))]
+            leg["dropin_rank0"] = dropin_leg(paths, ranges, fx, td, sum(fs - 1 for _, fs in paths))
     finally:
         shutil.rmtree(td, ignore_errors=True)
     bad = [p["rank"] for p in leg["per_rank"] if p["verified_vs_reference"] is False]

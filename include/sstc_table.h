@@ -171,13 +171,15 @@ public:
   uint64_t Bytes() const { return bytes_; }
   const uint8_t *DeviceBytes() const { return dev_; }
   int Device() const { return device_; }
-  /* equal (key, merge txn) neighbours from different inputs / differing ones
-   * (sstc_merge_result): both non-zero = the reference heap's order may differ */
+  /* runs of equal (key, merge txn) records spanning inputs / those whose
+   * records differ (sstc_merge_result): TieDiffs() > 0 = the reference heap's
+   * order may give other bytes */
   uint64_t CrossTies() const { return cross_ties_; }
   uint64_t TieDiffs() const { return tie_diffs_; }
   /* the input a record's key lies in */
   uint32_t InputOf(uint64_t key_off) const;
-  /* host-side phase times of Create (ms): map, upload, device merge, download */
+  /* host-side phase times of Create (ms): waits for the maps, maps + uploads,
+   * device merge, download start */
   double ms[4] = {0, 0, 0, 0};
 
   /* TableBuilders on the calling thread may reference this region from now

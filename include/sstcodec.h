@@ -58,6 +58,13 @@ extern "C" {
 #define SSTC_E_CAPACITY -5 /* workspace too small: call sstc_ctx_reserve */
 #define SSTC_E_INTERNAL -6 /* a device-side consistency check of a job failed: no out-of-range access was made,
                               but d_dst and the output table arrays are undefined (partly written) */
+#define SSTC_E_TIE_ORDER -7 /* sstc_compact / sstc_compact_files: the inputs hold records with equal key and txn
+                               in different tables whose contents differ, so the reference's MergeIterator heap
+                               orders them by its push / pop history (merge_iterator.h:91-95), which this job does
+                               not reproduce: nothing was written (d_dst untouched, no output file created or
+                               changed); the output table arrays are undefined.  The engine never writes such
+                               inputs (its txn ids are unique per write); a caller that must handle them runs
+                               the drop-in MergeIterator path, which takes the heap's order */
 
 /* per-block status, d_block_status[b] */
 #define SSTC_BLK_OK 0
@@ -258,10 +265,11 @@ void sstc_host_free(void *p, int pinned);
  * input in file order under the smallest txn before it, for groups of up to
  * 64 blocks (longer out-of-order groups: SSTC_E_INVALID_ARG).  Records merge
  * in MergeIterator order (key asc, txn desc; equal (key, txn): lower input
- * table first -- the reference's
- * std::priority_queue orders such ties by heap history, so inputs holding the
- * same (key, txn) with different contents may differ in order; identical
- * copies, the only kind the engine writes, give the same bytes), ShouldKeepEntry filters
+ * table first -- the reference's std::priority_queue orders such ties by heap
+ * history: identical copies, the only kind the engine writes, give the same
+ * bytes in any order; inputs holding the same (key, txn) with different
+ * contents in different tables are refused with SSTC_E_TIE_ORDER and nothing
+ * written), ShouldKeepEntry filters
  * them, and the survivors are written as complete SST images (blocks, meta
  * section, 40 B footer) back to back into d_dst: table t at d_table_off[t]
  * with d_table_len[t] bytes (TableBuilder::GetFileSize() = d_table_len[t] + 1).
@@ -293,10 +301,10 @@ typedef struct sstc_merged_record {
 
 typedef struct sstc_merge_result {
   uint64_t records;    /* records of all inputs = merged records                  */
-  uint64_t cross_ties; /* merged neighbours with equal key and merge txn from      */
-                       /* different inputs                                        */
-  uint64_t tie_diffs;  /* merged neighbours with equal key and merge txn whose     */
-                       /* type, txn as read or value differ                       */
+  uint64_t cross_ties; /* runs of merged records with equal key and merge txn     */
+                       /* that span two or more inputs                            */
+  uint64_t tie_diffs;  /* those of them whose records are not all alike (type,    */
+                       /* txn as read, value): the heap's order may differ        */
 } sstc_merge_result;
 
 /* Decode every block of the `ntables` inputs (given as for sstc_compact) and
@@ -305,8 +313,8 @@ typedef struct sstc_merge_result {
  * under the smallest txn before them in that input (the order the reference's
  * heap pops them when the compat reader returns them out of txn order), then
  * the lower input first.  The heap orders records with equal (key, txn) from
- * different inputs by heap history (merge_iterator.h:91-95); such ties are
- * counted, and when both counts are non-zero this order may differ from the
+ * different inputs by heap history (merge_iterator.h:91-95); such runs are
+ * counted, and when tie_diffs is non-zero this order may differ from the
  * reference's heap (the caller then takes the heap's order).  Inputs whose
  * keys are not ascending, or with a block that fails to decode:
  * SSTC_E_INVALID_ARG.  More records than max_records: SSTC_E_CAPACITY with
@@ -435,11 +443,16 @@ int sstc_compact_files(sstc_pipe *pipe, const char *const *in_paths, const uint6
  * of its own per pipe.  No data crosses devices.  Output ids continue from
  * shard to shard: shard 0 takes first_sst_id.., shard s the ids after shard
  * s - 1's last (the GetNextSSTId() sequence of the shards compacted one after
- * another; a shard writes only once the shards before it know their table
- * counts).  outs / key_arena receive the outputs in shard order; timing, when
- * not NULL, has n_shards entries.  A failing shard fails the call with its
- * error; the shards after it write nothing, the ones before it complete.
- * The pipes must be distinct (each is used by one thread). */
+ * another).  The device work of the shards overlaps; their writes do not: a
+ * shard writes only once the shard before it has written all of its
+ * outputs, and only after max_outs and key_arena_cap hold for the outputs of
+ * every shard up to it (checked before any of its files is touched).  outs /
+ * key_arena receive the outputs in shard order; timing, when not NULL, has
+ * n_shards entries.  A failing shard -- whatever fails: its inputs, its
+ * device job, a check above or one of its writes -- fails the call with its
+ * error; the shards after it write nothing; the ones before it complete and
+ * their outputs are still reported in outs / n_out / key_arena.  The pipes
+ * must be distinct (each is used by one thread). */
 int sstc_compact_files_multi(sstc_pipe *const *pipes, uint32_t n_pipes, const char *const *in_paths,
                              const uint64_t *in_file_sizes, const uint32_t *shard_first, uint32_t n_shards,
                              const char *out_prefix, uint64_t first_sst_id, const sstc_compact_params *params,

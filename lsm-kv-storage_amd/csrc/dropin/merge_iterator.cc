@@ -46,7 +46,7 @@ void MergeIterator::SeekToFirst() {
     std::string why;
     std::shared_ptr<sstc::ResidentInputs> r =
         num_iterators_ ? sstc::ResidentInputs::Create(sstc::ThreadContext(), in, SSTC_TXN_COMPAT, &why) : nullptr;
-    if (r && r->CrossTies() && r->TieDiffs()) {
+    if (r && r->TieDiffs()) {
       why = "equal (key, txn) records with different contents in different tables: the heap's own order";
       r.reset();
     }

@@ -237,10 +237,43 @@ struct FilesOut {
   sstc_files_timing tm{};
 };
 
-// first_id(nt, id): called once the output table count nt is known and before
-// any output is written; sets the first output id or returns an error code
+// first_id(nt, key_bytes, id): called once the output tables are in host
+// memory (their count nt and the bytes of their smallest + largest keys,
+// what the caller's outs / key_arena receive, are known) and before any
+// output file is touched; sets the first output id or returns an error code
 // (then nothing is written)
-using FirstId = std::function<int(uint64_t, uint64_t &)>;
+using FirstId = std::function<int(uint64_t, uint64_t, uint64_t &)>;
+
+constexpr uint64_t kDirectAlign = 4096;
+
+// One output table: created, or opened WITHOUT O_TRUNC when the path exists
+// (io/linux_file.cc:99-119, LinuxWriteOnlyFile::Open: a longer stale file
+// keeps its tail past the new table's bytes, as the reference's compaction
+// leaves it), then written at offset 0.  With fsync on, the 4 KiB-aligned
+// part goes through a second O_DIRECT descriptor straight from the pinned
+// image (no page-cache copy before the flush: the fsync'd buffered write of a
+// 44 MB table cost its memcpy on top of the device write), the tail through
+// the ordinary one; a file system that refuses O_DIRECT takes buffered
+// writes.  img must be 4 KiB aligned for the direct part.
+bool write_table(const std::string &path, const uint8_t *img, uint64_t bytes, bool do_fsync) {
+  ::chmod(path.c_str(), 0644);
+  const bool create = ::access(path.c_str(), F_OK) != 0;
+  const int fd = ::open(path.c_str(), create ? (O_WRONLY | O_CREAT | O_TRUNC) : O_WRONLY, 0644);
+  if (fd < 0) return false;
+  uint64_t done = 0;
+  if (do_fsync && !(reinterpret_cast<uintptr_t>(img) & (kDirectAlign - 1))) {
+    const int dfd = ::open(path.c_str(), O_WRONLY | O_DIRECT | O_CLOEXEC);
+    const uint64_t a = bytes & ~(kDirectAlign - 1);
+    if (dfd >= 0) {
+      if (a && pwrite_full(dfd, img, a, 0)) done = a;
+      ::close(dfd);
+    }
+  }
+  bool ok = done == bytes || pwrite_full(fd, img + done, bytes - done, done);
+  if (ok && do_fsync && ::fsync(fd) < 0) ok = false;
+  ::close(fd);
+  return ok;
+}
 
 int compact_files_impl(sstc_pipe *pipe, const char *const *in_paths, const uint64_t *in_file_sizes, uint32_t n_in,
                        const char *out_prefix, const FirstId &first_id, const sstc_compact_params *params,
@@ -387,20 +420,25 @@ int compact_files_impl(sstc_pipe *pipe, const char *const *in_paths, const uint6
   }
   const auto t3 = clk::now();
 
-  // ---- store: per-table D2H with an event, writer threads pwrite + fsync
+  // ---- store: per-table D2H with an event (each table at a 4 KiB-aligned
+  // place of the pinned staging, for the O_DIRECT writes), the tables' keys
+  // read from their images, then -- once first_id has accepted the count and
+  // the key bytes -- writer threads write + fsync (no output file is touched
+  // before every check has passed)
   const uint64_t nt = res.tables_out;
   if (nt > max_outs) return sstc__fail(SSTC_E_CAPACITY, "sstc_compact_files: more output tables than max_outs");
-  uint64_t first_sst_id = 0;
-  if (const int r = first_id(nt, first_sst_id)) return r;
-  std::vector<uint64_t> toff(nt + 1);
+  std::vector<uint64_t> toff(nt + 1), hoff(nt + 1, 0);
   if (hipMemcpy(toff.data(), d_toff, 8 * (nt + 1), hipMemcpyDeviceToHost) != hipSuccess)
     return sstc__fail(SSTC_E_HIP, "sstc_compact_files: table offsets");
-  if (grow_pinned(pipe->h_out, pipe->cap_h_out, toff[nt] + 16))
+  for (uint64_t t = 0; t < nt; t++)
+    hoff[t + 1] = hoff[t] + (toff[t + 1] - toff[t] + kDirectAlign - 1) / kDirectAlign * kDirectAlign;
+  if (grow_pinned(pipe->h_out, pipe->cap_h_out, hoff[nt] + kDirectAlign))
     return sstc__fail(SSTC_E_NOMEM, "sstc_compact_files: output staging");
+  uint8_t *h_out = pipe->h_out + ((kDirectAlign - reinterpret_cast<uintptr_t>(pipe->h_out) % kDirectAlign) % kDirectAlign);
   std::vector<hipEvent_t> ev(nt);
   for (uint64_t t = 0; t < nt; t++) {
     if (hipEventCreateWithFlags(&ev[t], hipEventDisableTiming) != hipSuccess ||
-        hipMemcpyAsync(pipe->h_out + toff[t], pipe->d_dst + toff[t], toff[t + 1] - toff[t], hipMemcpyDeviceToHost,
+        hipMemcpyAsync(h_out + hoff[t], pipe->d_dst + toff[t], toff[t + 1] - toff[t], hipMemcpyDeviceToHost,
                        s) != hipSuccess ||
         hipEventRecord(ev[t], s) != hipSuccess) {
       (void)hipStreamSynchronize(s);
@@ -410,37 +448,38 @@ int compact_files_impl(sstc_pipe *pipe, const char *const *in_paths, const uint6
     }
   }
   std::vector<std::string> lo(nt), hi(nt);
-  std::atomic<uint64_t> tnext{0};
   std::atomic<int> werr{0};
-  std::vector<std::thread> writers;
-  const std::string prefix(out_prefix);
   const uint32_t nw = static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>(pipe->io_threads, nt)));
-  for (uint32_t w = 0; w < nw; w++)
-    writers.emplace_back([&] {
-      (void)hipSetDevice(pipe->device);
-      for (uint64_t t; (t = tnext.fetch_add(1)) < nt;) {
-        if (hipEventSynchronize(ev[t]) != hipSuccess) {
-          werr = 1;
-          continue;
-        }
-        const uint8_t *img = pipe->h_out + toff[t];
-        const uint64_t bytes = toff[t + 1] - toff[t];
-        const std::string path = prefix + std::to_string(first_sst_id + t) + ".sst";
-        // io/linux_file.cc:99-119 (LinuxWriteOnlyFile::Open): an output path
-        // that already exists is opened WITHOUT O_TRUNC, so a longer stale
-        // file keeps its tail past the new table's bytes, as the reference's
-        // compaction leaves it (GetFileSize and the table image are unchanged)
-        ::chmod(path.c_str(), 0644);
-        const bool create = ::access(path.c_str(), F_OK) != 0;
-        const int fd = ::open(path.c_str(), create ? (O_WRONLY | O_CREAT | O_TRUNC) : O_WRONLY, 0644);
-        if (fd < 0 || !pwrite_full(fd, img, bytes, 0) || (do_fsync && ::fsync(fd) < 0)) werr = 2;
-        if (fd >= 0) ::close(fd);
-        table_keys(img, bytes, lo[t], hi[t]);
-      }
-    });
-  for (auto &t : writers) t.join();
+  auto parallel = [&](const std::function<void(uint64_t)> &work) {
+    std::atomic<uint64_t> tnext{0};
+    std::vector<std::thread> th;
+    for (uint32_t w = 0; w < nw; w++)
+      th.emplace_back([&] {
+        (void)hipSetDevice(pipe->device);
+        for (uint64_t t; (t = tnext.fetch_add(1)) < nt;) work(t);
+      });
+    for (auto &x : th) x.join();
+  };
+  parallel([&](uint64_t t) {
+    if (hipEventSynchronize(ev[t]) != hipSuccess) {
+      werr = 1;
+      return;
+    }
+    table_keys(h_out + hoff[t], toff[t + 1] - toff[t], lo[t], hi[t]);
+  });
   for (auto &e : ev) (void)hipEventDestroy(e);
-  if (werr) return sstc__fail(werr == 1 ? SSTC_E_HIP : SSTC_E_INVALID_ARG, "sstc_compact_files: output write failed");
+  if (werr) return sstc__fail(SSTC_E_HIP, "sstc_compact_files: D2H of the outputs failed");
+  uint64_t key_bytes = 0;
+  for (uint64_t t = 0; t < nt; t++) key_bytes += lo[t].size() + hi[t].size();
+  uint64_t first_sst_id = 0;
+  if (const int r = first_id(nt, key_bytes, first_sst_id)) return r;
+  const std::string prefix(out_prefix);
+  parallel([&](uint64_t t) {
+    if (!write_table(prefix + std::to_string(first_sst_id + t) + ".sst", h_out + hoff[t], toff[t + 1] - toff[t],
+                     do_fsync))
+      werr = 2;
+  });
+  if (werr) return sstc__fail(SSTC_E_INVALID_ARG, "sstc_compact_files: output write failed");
   result.outs.resize(nt);
   result.keys.clear();
   for (uint64_t t = 0; t < nt; t++) {
@@ -501,9 +540,12 @@ int sstc_compact_files(sstc_pipe *pipe, const char *const *in_paths, const uint6
   FilesOut r;
   const int rc = compact_files_impl(
       pipe, in_paths, in_file_sizes, n_in, out_prefix,
-      [first_sst_id](uint64_t, uint64_t &id) {
+      [&](uint64_t nt, uint64_t key_bytes, uint64_t &id) {
+        if (nt > max_outs) return sstc__fail(SSTC_E_CAPACITY, "sstc_compact_files: more output tables than max_outs");
+        if (key_arena && key_bytes > key_arena_cap)
+          return sstc__fail(SSTC_E_CAPACITY, "sstc_compact_files: key_arena too small");
         id = first_sst_id;
-        return SSTC_OK;
+        return static_cast<int>(SSTC_OK);
       },
       params, do_fsync, max_outs, r);
   if (rc != SSTC_OK) return rc;
@@ -537,19 +579,23 @@ int sstc_compact_files_multi(sstc_pipe *const *pipes, uint32_t n_pipes, const ch
 
   // the output-id chain: shard s takes the ids after shard s - 1's tables,
   // exactly the GetNextSSTId() sequence of the shards compacted one after
-  // another; a shard that fails breaks the chain for every shard after it
-  // (those write nothing), the shards before it finish
+  // another.  A shard writes only once the shard before it has written all
+  // of its outputs, and only after the call-wide checks (max_outs, key_arena
+  // for the shards so far) pass; a shard that fails -- before or while
+  // writing -- breaks the chain, so every shard after it writes nothing (the
+  // device work of all shards still overlaps).
   std::mutex m;
   std::condition_variable cv;
-  std::vector<int> state(n_shards + 1, 0); // 0 pending, 1 ready, -1 broken
-  std::vector<uint64_t> base(n_shards + 1, 0);
+  std::vector<int> state(n_shards + 1, 0); // 0 pending, 1 written, -1 broken
+  std::vector<uint64_t> base(n_shards + 1, 0), kbase(n_shards + 1, 0);
   state[0] = 1;
   base[0] = first_sst_id;
-  auto publish = [&](uint32_t s, int st, uint64_t b) {
+  auto publish = [&](uint32_t s, int st, uint64_t b, uint64_t kb) {
     std::lock_guard<std::mutex> lk(m);
     if (state[s + 1] != 0) return;
     state[s + 1] = st;
     base[s + 1] = b;
+    kbase[s + 1] = kb;
     cv.notify_all();
   };
   std::vector<FilesOut> res(n_shards);
@@ -559,13 +605,17 @@ int sstc_compact_files_multi(sstc_pipe *const *pipes, uint32_t n_pipes, const ch
   for (uint32_t j = 0; j < std::min(n_pipes, n_shards); j++)
     th.emplace_back([&, j] {
       for (uint32_t sh = j; sh < n_shards; sh += n_pipes) {
-        const FirstId chain = [&, sh](uint64_t nt, uint64_t &id) {
+        uint64_t my_id = 0, my_keys = 0;
+        const FirstId chain = [&, sh](uint64_t nt, uint64_t key_bytes, uint64_t &id) {
           std::unique_lock<std::mutex> lk(m);
           cv.wait(lk, [&] { return state[sh] != 0; });
           if (state[sh] < 0) return sstc__fail(SSTC_E_INVALID_ARG, "sstc_compact_files_multi: an earlier shard failed");
-          id = base[sh];
-          lk.unlock();
-          publish(sh, 1, id + nt);
+          if (base[sh] - first_sst_id + nt > max_outs)
+            return sstc__fail(SSTC_E_CAPACITY, "sstc_compact_files_multi: more output tables than max_outs");
+          if (key_arena && kbase[sh] + key_bytes > key_arena_cap)
+            return sstc__fail(SSTC_E_CAPACITY, "sstc_compact_files_multi: key_arena too small");
+          id = my_id = base[sh];
+          my_keys = kbase[sh] + key_bytes;
           return static_cast<int>(SSTC_OK);
         };
         const uint32_t f = shard_first[sh], n = shard_first[sh + 1] - f;
@@ -573,19 +623,25 @@ int sstc_compact_files_multi(sstc_pipe *const *pipes, uint32_t n_pipes, const ch
                                      max_outs, res[sh]);
         if (rcs[sh] != SSTC_OK) {
           errs[sh] = sstc_last_error_string(); // thread-local: carried to the caller's thread
-          publish(sh, -1, 0);
+          publish(sh, -1, 0, 0);
+        } else {
+          publish(sh, 1, my_id + res[sh].outs.size(), my_keys);
         }
       }
     });
   for (auto &t : th) t.join();
-  for (uint32_t sh = 0; sh < n_shards; sh++)
-    if (rcs[sh] != SSTC_OK)
-      return sstc__fail(rcs[sh], ("sstc_compact_files_multi: shard " + std::to_string(sh) + ": " + errs[sh]).c_str());
   if (timing)
     for (uint32_t sh = 0; sh < n_shards; sh++) timing[sh] = res[sh].tm;
+  // the shards before the first failing one completed: their outputs are
+  // reported (outs / n_out / key_arena) whatever the call returns
+  uint32_t done = 0;
+  while (done < n_shards && rcs[done] == SSTC_OK) done++;
   std::vector<const FilesOut *> parts;
-  for (const FilesOut &r : res) parts.push_back(&r);
-  return copy_outs(parts, outs, max_outs, n_out, key_arena, key_arena_cap, who);
+  for (uint32_t sh = 0; sh < done; sh++) parts.push_back(&res[sh]);
+  const int rc = copy_outs(parts, outs, max_outs, n_out, key_arena, key_arena_cap, who);
+  if (done < n_shards)
+    return sstc__fail(rcs[done], ("sstc_compact_files_multi: shard " + std::to_string(done) + ": " + errs[done]).c_str());
+  return rc;
 }
 
 } // extern "C"

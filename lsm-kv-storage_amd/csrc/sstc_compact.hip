@@ -811,11 +811,67 @@ __device__ __forceinline__ uint64_t read_txn(const KeyView &kv, const RecX &rx, 
   return g_u64u(kv.src + rx.ko + kl + (after_value ? 4ull + rx.vl : 0ull));
 }
 
+__device__ __forceinline__ uint32_t run_of_record(const uint64_t *rs, uint32_t nruns, uint64_t id) {
+  uint32_t lo = 0, hi = nruns; // last run start <= id
+  while (lo + 1 < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (rs[mid] <= id) lo = mid;
+    else hi = mid;
+  }
+  return lo;
+}
+
+// A run of merged records with equal key and merge txn: where the reference's
+// heap decides the order by its history (merge_iterator.h:91-95 compares key
+// and txn only).  Any order of the run gives the same bytes unless the run
+// holds records of two or more inputs AND not all of its records are alike
+// (type, txn as read, value).  Called for merged neighbours i - 1, i with equal
+// key and merge txn (rare: txns are unique per write); the run's first pair
+// walks the run once: ties[0] counts runs spanning inputs, ties[1] those of
+// them whose records differ, and such a run sets kGuardTieBoth.
+__device__ __forceinline__ uint64_t txn_as_read(const SK &x, const RecX &r, const KeyView &kv, uint32_t txn_mode) {
+  return x.kl & kSkRead ? read_txn(kv, r, x.kl & ~kSkRead, txn_mode) : x.tx;
+}
+
+__device__ __forceinline__ void note_tie(const SK *s, uint64_t n, uint64_t i, const KeyView &kv, const uint64_t *rs,
+                                         uint32_t nruns, uint32_t txn_mode, unsigned long long *ties,
+                                         unsigned long long *guard) {
+  const SK h = s[i - 1];
+  if (h.id >= n) return;
+  if (i >= 2) { // not the run's first pair: the pair that is walks it
+    const SK q = s[i - 2];
+    if (q.id < n && q.tx == h.tx && ff_same_key(q, h, kv)) return;
+  }
+  const uint32_t kl = h.kl & ~kSkRead;
+  const RecX hr = kv.rx[h.id];
+  const uint64_t htx = txn_as_read(h, hr, kv, txn_mode);
+  const uint32_t hin = run_of_record(rs, nruns, h.id);
+  bool cross = false, diff = false;
+  for (uint64_t j = i; j < n; j++) {
+    const SK x = s[j];
+    if (x.id >= n || x.tx != h.tx || !ff_same_key(h, x, kv)) break;
+    cross |= run_of_record(rs, nruns, x.id) != hin;
+    if (diff) continue;
+    const RecX r = kv.rx[x.id];
+    diff = r.type != hr.type || r.vl != hr.vl || txn_as_read(x, r, kv, txn_mode) != htx;
+    if (!diff && r.vl != kNoValue) {
+      const uint8_t *a = kv.src + r.ko + kl + 4, *b = kv.src + hr.ko + kl + 4;
+      for (uint32_t k = 0; k < r.vl && !diff; k++) diff = a[k] != b[k];
+    }
+  }
+  if (!cross) return;
+  if (ties) atomicAdd(&ties[0], 1ull);
+  if (!diff) return;
+  if (ties) atomicAdd(&ties[1], 1ull);
+  if (guard) atomicOr(guard, kGuardTieBoth);
+}
+
 __global__ __launch_bounds__(kFtThreads) void ck_filter_kernel(const SK *s, uint64_t n, KeyView kv,
                                                                uint32_t base_level, Rec out, uint64_t *Pd,
                                                                uint64_t *Pe, uint64_t *ws, uint64_t *totals,
                                                                Abort stop, unsigned long long *guard,
-                                                               uint32_t txn_mode) {
+                                                               uint32_t txn_mode, const uint64_t *rs,
+                                                               uint32_t nruns) {
   __shared__ uint64_t s_pre[3];
   if (stop()) { // uniform over the grid: no status published, the host rejects the job
     if (blockIdx.x == 0 && threadIdx.x == 0) { // no survivor: the layout below splits nothing, writes nothing
@@ -872,6 +928,8 @@ __global__ __launch_bounds__(kFtThreads) void ck_filter_kernel(const SK *s, uint
       // the txn as read (a merge txn lowered by its group: re-read, rare)
       const uint64_t tread = x[j].kl & kSkRead ? read_txn(kv, rr[j], x[j].kl & ~kSkRead, txn_mode) : x[j].tx;
       const uint32_t k = i < n ? ff_keep(s, i, x[j], pv, rr[j].type, base_level, kv, n, tread) : 0u;
+      if (i < n && i > 0 && pv.tx == x[j].tx && ff_same_key(pv, x[j], kv)) // (rare: txns are unique per write)
+        note_tie(s, n, i, kv, rs, nruns, txn_mode, nullptr, guard);
       km |= k << j;
       kl[j] = x[j].kl & ~kSkRead;
       tx[j] = tread;
@@ -986,20 +1044,9 @@ __global__ __launch_bounds__(kFtThreads) void ck_filter_kernel(const SK *s, uint
 // its txn as the reference's iterator reads it (the merge txn unless the
 // decode lowered it, kSkRead).  Equal (key, merge txn) neighbours are where
 // the reference's std::priority_queue decides the order by heap history
-// (merge_iterator.h:91-95 compares only key and txn), so they are counted:
-// ties[0] = such neighbours from different inputs, ties[1] = such neighbours
-// (any inputs) whose type, txn as read or value differ.  Both rare; the host
-// takes the heap's own order when both are non-zero.
-__device__ __forceinline__ uint32_t run_of_record(const uint64_t *rs, uint32_t nruns, uint64_t id) {
-  uint32_t lo = 0, hi = nruns; // last run start <= id
-  while (lo + 1 < hi) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if (rs[mid] <= id) lo = mid;
-    else hi = mid;
-  }
-  return lo;
-}
-
+// (merge_iterator.h:91-95 compares only key and txn), so their runs are
+// counted (note_tie): ties[0] = runs spanning inputs, ties[1] = those of them
+// whose records differ -- where the heap's order may give other bytes.
 __global__ __launch_bounds__(256) void ck_merged_kernel(const SK *s, uint64_t n, KeyView kv, const uint64_t *rs,
                                                         uint32_t nruns, sstc_merged_record *out,
                                                         unsigned long long *ties, Abort stop,
@@ -1022,16 +1069,7 @@ __global__ __launch_bounds__(256) void ck_merged_kernel(const SK *s, uint64_t n,
   if (i == 0) return;
   const SK pv = s[i - 1];
   if (pv.id >= n || pv.tx != x.tx || !ff_same_key(pv, x, kv)) return;
-  // equal (key, merge txn): the rare path
-  if (run_of_record(rs, nruns, pv.id) != run_of_record(rs, nruns, x.id)) atomicAdd(&ties[0], 1ull);
-  const RecX pr = kv.rx[pv.id];
-  const uint64_t ptread = pv.kl & kSkRead ? read_txn(kv, pr, kl, txn_mode) : pv.tx;
-  bool diff = pr.type != rr.type || pr.vl != rr.vl || ptread != tread;
-  if (!diff && rr.vl != kNoValue) {
-    const uint8_t *a = kv.src + rr.ko + kl + 4, *b = kv.src + pr.ko + kl + 4;
-    for (uint32_t j = 0; j < rr.vl && !diff; j++) diff = a[j] != b[j];
-  }
-  if (diff) atomicAdd(&ties[1], 1ull);
+  note_tie(s, n, i, kv, rs, nruns, txn_mode, ties, nullptr); // equal (key, merge txn): the rare path
 }
 
 // The output table and block counts stay on the device (dn[0], dn[1]): the
@@ -1231,7 +1269,8 @@ __global__ __launch_bounds__(256) void ck_meta_kernel(const uint64_t *bmeta, Lay
                                                       const uint64_t *need, uint64_t cap, unsigned long long *guard,
                                                       const uint8_t *src, const uint64_t *src_end) {
   __shared__ __attribute__((aligned(16))) uint8_t img[kMetaLds + 16];
-  if (*need > cap || !L.ok()) return; // output capacity exceeded / corrupt layout: nothing is written
+  if (*need > cap || !L.ok() || (*guard & kGuardTieBoth) == kGuardTieBoth)
+    return; // output capacity exceeded / corrupt layout / heap-order ties: nothing is written
   const uint64_t nb = L.nb();
   const uint64_t b0 = static_cast<uint64_t>(blockIdx.x) * 256u;
   if (b0 >= nb) return;
@@ -1307,7 +1346,7 @@ __global__ __launch_bounds__(kFootThreads) void ck_footer_kernel(Lay L, const ui
   __shared__ uint64_t smn[kFootThreads / kWave], smx[kFootThreads / kWave];
   const uint64_t t = blockIdx.x;
   const uint64_t nt = L.ok() ? L.nt() : 0;
-  if (L.ok() && t < nt && toff[nt] <= cap) { // uniform over the workgroup
+  if (L.ok() && t < nt && toff[nt] <= cap && (*guard & kGuardTieBoth) != kGuardTieBoth) { // uniform
     const uint64_t f = tbf[t], e = tbf[t + 1];
     const uint64_t o = toff[t], dbytes = tdata[t], mbytes = tmeta[t]; // in flight with the reduction's loads
     uint64_t mn = ~0ull, mx = 0;
@@ -1763,6 +1802,11 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
         err = "device consistency check failed after the merge (merged record ids out of range)";
         return SSTC_E_INTERNAL;
       }
+      if (!mo && (h[3] & kGuardTieBoth) == kGuardTieBoth) {
+        err = "inputs hold equal (key, txn) records with different contents in different tables: the "
+              "reference's heap orders them by its history; nothing was written";
+        return SSTC_E_TIE_ORDER;
+      }
       return SSTC_OK;
     };
     if (mo) { // sstc_merge_records: the merged order, no filter
@@ -1783,7 +1827,8 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     // 3. keep / drop and the survivors gathered in merge order with their
     // prefix sums (sized by n: the kept count is known after the pass)
     ck_filter_kernel<<<static_cast<uint32_t>(fftiles), kFtThreads, 0, s>>>(A, n, kv, base_level, KR, Pd, Pe, ffws,
-                                                                        totals, stop, guard, txn_mode);
+                                                                        totals, stop, guard, txn_mode, rb,
+                                                                        static_cast<uint32_t>(nruns));
     if (arena.fault == 1) CK(hipMemsetAsync(KR.ko, 0xFF, n * sizeof(uint64_t), s)); // test: bad key offsets
     if (arena.fault == 2) CK(hipMemsetAsync(Pe, 0x5A, (n + 1) * sizeof(uint64_t), s)); // test: bad prefix sums
     if (max_tables == 0) { // no room for the first table (m >= 1 unless the job is rejected)
@@ -1872,7 +1917,7 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
       err = "more output tables than max_tables";
       return SSTC_E_CAPACITY;
     }
-    if (arena.host[3] & ~(kGuardLongGroup | kGuardInv)) {
+    if (arena.host[3] & ~(kGuardLongGroup | kGuardInv | kGuardTieCross | kGuardTieDiff)) {
       err = "device consistency check failed (guard bits 0x" + [](uint64_t v) {
         char b[24];
         snprintf(b, sizeof b, "%llx", static_cast<unsigned long long>(v));

@@ -70,6 +70,17 @@ struct DecArgs {
   unsigned long long *inv = nullptr;
 };
 
+// consistency-guard bits of the compaction job (sstc_compact.hip)
+constexpr unsigned long long kGuardMergeId = 1, kGuardEntry = 2, kGuardBlockRange = 4, kGuardMeta = 8,
+                             kGuardFooter = 16, kGuardLayout = 32, kGuardLongGroup = 64,
+                             kGuardInv = 128, kGuardTieCross = 256, kGuardTieDiff = 512;
+// Equal (key, merge txn) neighbours in the merged order from different inputs
+// (kGuardTieCross) and such neighbours whose records differ (kGuardTieDiff):
+// with both, the reference's heap (merge_iterator.h:91-95) may order them
+// otherwise than this job, so the job writes nothing and returns
+// SSTC_E_TIE_ORDER (the writers stand down on both bits).
+constexpr unsigned long long kGuardTieBoth = kGuardTieCross | kGuardTieDiff;
+
 struct EncArgs {
   const uint8_t *key_src;
   const uint8_t *val_src;
@@ -96,7 +107,9 @@ struct EncArgs {
   // optional capacity guard (compaction): nothing is written when *need > cap
   const uint64_t *need = nullptr;
   uint64_t cap = 0;
-  __device__ bool over() const { return need && *need > cap; }
+  __device__ bool over() const {
+    return (need && *need > cap) || (guard && (*guard & kGuardTieBoth) == kGuardTieBoth);
+  }
   // optional consistency guard (compaction, mode 1): every block's output range
   // must lie in [0, cap), every entry inside its block image (offset + size
   // <= data bytes, size >= its header + key) and its source inside
@@ -109,10 +122,6 @@ struct EncArgs {
   const uint64_t *nb_dev = nullptr;
 };
 
-// consistency-guard bits of the compaction job (sstc_compact.hip)
-constexpr unsigned long long kGuardMergeId = 1, kGuardEntry = 2, kGuardBlockRange = 4, kGuardMeta = 8,
-                             kGuardFooter = 16, kGuardLayout = 32, kGuardLongGroup = 64,
-                             kGuardInv = 128;
 // kGuardLongGroup / kGuardInv are notes, not faults: a key's versions continue
 // over more than kGroupCarryBlocks blocks / some group is out of txn order as
 // read.  Both together send the check kernel's last workgroup through the

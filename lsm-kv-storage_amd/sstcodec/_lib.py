@@ -64,12 +64,15 @@ class FilesTiming(ctypes.Structure):
 
 
 SSTC_E_INTERNAL = -6  # include/sstcodec.h: a device-side consistency check failed
+SSTC_E_TIE_ORDER = -7  # include/sstcodec.h: equal (key, txn) records with different contents in different inputs
 
 SSTC_TAB_OK, SSTC_TAB_BAD_FOOTER, SSTC_TAB_BAD_META, SSTC_TAB_BAD_BLOCK, SSTC_TAB_TOO_LARGE = 0, 1, 2, 3, 4
 
 
 class SstcError(RuntimeError):
-    pass
+    def __init__(self, msg, code=None):
+        super().__init__(msg)
+        self.code = code  # the SSTC_E_* return code
 
 
 _lib = None
@@ -133,4 +136,4 @@ def load():
 def check(rc, what):
     if rc != SSTC_OK:
         msg = load().sstc_last_error_string()
-        raise SstcError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")
+        raise SstcError(f"{what} failed ({rc}): {msg.decode() if msg else ''}", rc)

@@ -243,9 +243,11 @@ class Codec:
 
     # ---- compaction ----------------------------------------------------------
     def compact(self, tables, block_threshold=4096, table_limit=32 << 20, base_level=1,
-                txn_mode=_lib.SSTC_TXN_COMPAT):
+                txn_mode=_lib.SSTC_TXN_COMPAT, probe=None):
         """Compact SST images (list of numpy u8 arrays, iterator order) on the
-        GPU.  Returns (list of output SST images as numpy arrays, result)."""
+        GPU.  Returns (list of output SST images as numpy arrays, result).
+        probe (tests): a list that receives the output buffer before the call's
+        status is checked."""
         import numpy as np
         from ._lib import CompactParams, CompactResult
         if isinstance(tables, (list, tuple)):
@@ -266,9 +268,12 @@ class Codec:
         prm = CompactParams(block_threshold, table_limit, base_level, txn_mode)
         res = CompactResult()
         self._stream()
-        check(self.lib.sstc_compact(self.h, _p(src), _p(blk_off), _p(blk_len), int(blk_off.numel()),
-                                    h_tfb.ctypes.data_as(ctypes.c_void_p), len(files), ctypes.byref(prm), _p(dst),
-                                    cap, _p(toff), _p(tlen), max_t, ctypes.byref(res)), "sstc_compact")
+        rc = self.lib.sstc_compact(self.h, _p(src), _p(blk_off), _p(blk_len), int(blk_off.numel()),
+                                   h_tfb.ctypes.data_as(ctypes.c_void_p), len(files), ctypes.byref(prm), _p(dst),
+                                   cap, _p(toff), _p(tlen), max_t, ctypes.byref(res))
+        if probe is not None:
+            probe.append(dst)
+        check(rc, "sstc_compact")
         nt = res.tables_out
         o = toff[: nt + 1].cpu().numpy()
         d = dst[: int(o[nt])].cpu().numpy()
@@ -411,15 +416,19 @@ def compact_files_multi(pipes, shards, out_prefix, first_sst_id, block_threshold
     nout = ctypes.c_uint32()
     tm = (FilesTiming * max(len(shards), 1))()
     prm = CompactParams(block_threshold, table_limit, base_level, txn_mode)
-    check(lib.sstc_compact_files_multi(ctypes.cast(ph, ctypes.c_void_p), len(pipes), ctypes.cast(arr, ctypes.c_void_p),
-                                       ctypes.cast(sz, ctypes.c_void_p), ctypes.cast(sf, ctypes.c_void_p), len(shards),
-                                       out_prefix.encode(), int(first_sst_id), ctypes.byref(prm), 1 if fsync else 0,
-                                       ctypes.cast(outs, ctypes.c_void_p), max_outs, ctypes.byref(nout),
-                                       ctypes.cast(arena, ctypes.c_void_p), len(arena), ctypes.cast(tm, ctypes.c_void_p)),
-          "sstc_compact_files_multi")
+    rc = lib.sstc_compact_files_multi(ctypes.cast(ph, ctypes.c_void_p), len(pipes), ctypes.cast(arr, ctypes.c_void_p),
+                                      ctypes.cast(sz, ctypes.c_void_p), ctypes.cast(sf, ctypes.c_void_p), len(shards),
+                                      out_prefix.encode(), int(first_sst_id), ctypes.byref(prm), 1 if fsync else 0,
+                                      ctypes.cast(outs, ctypes.c_void_p), max_outs, ctypes.byref(nout),
+                                      ctypes.cast(arena, ctypes.c_void_p), len(arena), ctypes.cast(tm, ctypes.c_void_p))
     raw = arena.raw
     res = [(o.sst_id, o.file_size, raw[o.smallest_key_off:o.smallest_key_off + o.smallest_key_len],
             raw[o.largest_key_off:o.largest_key_off + o.largest_key_len]) for o in outs[: nout.value]]
+    try:
+        check(rc, "sstc_compact_files_multi")
+    except _lib.SstcError as e:
+        e.outs = res  # the outputs of the shards that completed before the failing one
+        raise
     return res, [{k: getattr(t, k) for k, _ in FilesTiming._fields_} for t in tm[: len(shards)]]
 
 

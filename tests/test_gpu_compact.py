@@ -167,22 +167,24 @@ def test_compact_large_vs_oracle(codec, oracle, k, n_per, space, dup):
 
 @pytest.mark.parametrize("base", [1, 0])
 def test_ties_vs_reference(codec, oracle, base):
-    """Equal (key, txn) records across inputs: identical copies give the
-    reference's bytes; differing copies equal the reference up to the order
-    inside equal-(key, txn) runs (input order here, heap history there) and
-    equal the oracle's bytes."""
-    from conftest import same_up_to_tie_order, sst_records, tie_case
+    """Equal (key, txn) records across inputs: identical
+    copies give the reference's bytes; differing copies -- whose order the
+    reference's heap decides by its history, merge_iterator.h:91-95 -- are
+    refused with SSTC_E_TIE_ORDER and not one byte of the output buffer is
+    written (the caller routes such a job to the drop-in MergeIterator, which
+    takes the heap's order: tests/test_gpu_dropin.py ties cases)."""
+    from sstcodec._lib import SSTC_E_TIE_ORDER, SstcError
+    from conftest import tie_case
     g = load_golden("compact_ties.npz")
     ins, want = tie_case(g, "same", base)
     outs, _ = codec.compact(ins, 4096, 6000, base)
     assert len(outs) == len(want) and all(np.array_equal(o, w) for o, w in zip(outs, want))
     ins, want = tie_case(g, "diff", base)
-    outs, _ = codec.compact(ins, 4096, 6000, base)
-    worc, _ = oracle.compact(ins, 4096, 6000, base)
-    assert len(outs) == len(worc) and all(np.array_equal(o, w) for o, w in zip(outs, worc))
-    a = [r for o in outs for r in sst_records(oracle, o)]
-    b = [r for w in want for r in sst_records(oracle, w)]
-    assert same_up_to_tie_order(a, b, [sst_records(oracle, i) for i in ins])
+    probe = []
+    with pytest.raises(SstcError) as e:
+        codec.compact(ins, 4096, 6000, base, probe=probe)
+    assert e.value.code == SSTC_E_TIE_ORDER, str(e.value)
+    assert bool((probe[0] == 0xA5).all()), "a refused job wrote output bytes"
 
 
 @pytest.mark.parametrize("base", [1, 0])

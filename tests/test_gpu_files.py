@@ -136,3 +136,26 @@ def test_files_capacity_retry_and_bound(oracle, tmp_path):
     finally:
         p.close()
         codec.close()
+
+
+def test_files_refuse_differing_ties(pipe, tmp_path):
+    """SSTC_E_TIE_ORDER through the file pipeline: inputs
+    holding equal (key, txn) records with different contents in different
+    tables are refused before any output file is created; identical copies
+    compact as the reference does."""
+    from conftest import load_golden, tie_case
+    from sstcodec._lib import SSTC_E_TIE_ORDER, SstcError
+    g = load_golden("compact_ties.npz")
+    ins, _ = tie_case(g, "diff", 1)
+    paths, sizes = write_inputs(tmp_path, ins)
+    od = tmp_path / "out"
+    od.mkdir()
+    with pytest.raises(SstcError) as e:
+        pipe.compact_files(paths, sizes, str(od) + "/", 100, 4096, 6000, 1)
+    assert e.value.code == SSTC_E_TIE_ORDER
+    assert os.listdir(od) == []
+    ins, want = tie_case(g, "same", 1)
+    paths, sizes = write_inputs(tmp_path, ins)
+    outs, _ = pipe.compact_files(paths, sizes, str(od) + "/", 100, 4096, 6000, 1)
+    got = [np.fromfile(str(od / f"{sid}.sst"), np.uint8) for sid, _, _, _ in outs]
+    assert len(got) == len(want) and all(np.array_equal(a, b) for a, b in zip(got, want))

@@ -97,7 +97,7 @@ def test_multi_failing_shard(oracle, tmp_path):
     try:
         od = tmp_path / "out"
         od.mkdir()
-        with pytest.raises(sstcodec.SstcError, match="shard 1"):
+        with pytest.raises(sstcodec.SstcError, match="shard 1") as e:
             compact_files_multi(pipes, shards, str(od) + "/", 1, 4096, 1 << 20, 1, fsync=False)
     finally:
         close(codecs, pipes)
@@ -105,6 +105,52 @@ def test_multi_failing_shard(oracle, tmp_path):
     assert written == list(range(1, 1 + len(want[0])))  # shard 0 only
     for sid in written:
         assert np.array_equal(np.fromfile(str(od / f"{sid}.sst"), np.uint8), want[0][sid - 1])
+    assert [o[0] for o in e.value.outs] == written  # and reported
+
+
+def _run_multi(tmp_path, shards, n_pipes, **kw):
+    from sstcodec.codec import compact_files_multi
+    codecs, pipes, _ = make_pipes(n_pipes)
+    od = tmp_path / "out"
+    try:
+        return compact_files_multi(pipes, shards, str(od) + "/", 1, 4096, 1 << 20, 1, **kw)
+    finally:
+        close(codecs, pipes)
+
+
+@pytest.mark.parametrize("fsync", [False, True])
+def test_multi_store_failure_stops_later_shards(oracle, tmp_path, fsync):
+    """a shard whose WRITE fails (its first output path is a
+    directory) fails the call; the shards after it write nothing, the one
+    before it completes and is reported (fsync on: the O_DIRECT writes)."""
+    import sstcodec
+    shards, want = small_shards(tmp_path, oracle, 4)
+    od = tmp_path / "out"
+    od.mkdir()
+    n0 = len(want[0])
+    os.mkdir(od / f"{1 + n0}.sst")  # shard 1's first output
+    with pytest.raises(sstcodec.SstcError, match="shard 1") as e:
+        _run_multi(tmp_path, shards, 4, fsync=fsync)
+    files = sorted(int(f.split(".")[0]) for f in os.listdir(od) if os.path.isfile(od / f))
+    assert max(files) <= n0 + len(want[1])  # nothing of shards 2 and 3
+    assert [o[0] for o in e.value.outs] == list(range(1, 1 + n0))  # shard 0: complete and reported
+    for sid in range(1, 1 + n0):
+        assert np.array_equal(np.fromfile(str(od / f"{sid}.sst"), np.uint8), want[0][sid - 1])
+
+
+def test_multi_max_outs_across_shards(oracle, tmp_path):
+    """max_outs holds per shard but not for the call: the shard
+    that would pass it fails before touching a file; the shards before it are
+    written and reported, the ones after write nothing."""
+    import sstcodec
+    shards, want = small_shards(tmp_path, oracle, 3)
+    n0, n1 = len(want[0]), len(want[1])
+    assert n1 > 1
+    (tmp_path / "out").mkdir()
+    with pytest.raises(sstcodec.SstcError, match="max_outs") as e:
+        _run_multi(tmp_path, shards, 3, fsync=False, max_outs=n0 + n1 - 1)
+    files = sorted(int(f.split(".")[0]) for f in os.listdir(tmp_path / "out"))
+    assert files == list(range(1, 1 + n0)) and [o[0] for o in e.value.outs] == files
 
 
 @pytest.mark.timeout(600)
