@@ -388,18 +388,29 @@ def test_compact_long_equal_runs(codec, oracle):
     """Runs of identical (key, txn) records far longer than the inputs count
     (ShouldKeepEntry keeps them all: last_txn == txn, compact.cc:357-362): the
     keep test finds a record's group head by galloping, O(log run) per record
-    (a walk back over the run was O(run^2) in total)."""
+    (a walk back over the run was O(run^2) in total); the tie check walks the
+    run once.  With different values per input the job is refused
+    (SSTC_E_TIE_ORDER: the reference's heap would order them by history)."""
+    from sstcodec._lib import SSTC_E_TIE_ORDER, SstcError
     n = 60_000
-    sets = []
-    for t in range(3):
-        rec = W.uniform_records(n, key_index=np.zeros(n, np.uint64), seed=t + 1, value_len=20)
-        rec["txn"][:] = 77  # one key, one txn, every record
-        sets.append(rec)
-    extra = W.uniform_records(1000, key_index=np.arange(1, 1001, dtype=np.uint64), seed=9, value_len=20,
-                              txn_start=10)
-    sets.append(extra)
-    ins = [oracle.table_build(r, 4096) for r in sets]
-    want, kept = oracle.compact(ins, 4096, 1 << 20, 1)
-    outs, res = codec.compact(ins, 4096, 1 << 20, 1)
-    assert res.records_kept == kept == 3 * n + 1000
-    assert len(outs) == len(want) and all(np.array_equal(o, w) for o, w in zip(outs, want))
+    for same in (True, False):
+        sets = []
+        for t in range(3):
+            # identical copies in every input (any heap order gives the same
+            # bytes), or each input its own values (SSTC_E_TIE_ORDER)
+            rec = W.uniform_records(n, key_index=np.zeros(n, np.uint64), seed=1 if same else t + 1, value_len=20)
+            rec["txn"][:] = 77  # one key, one txn, every record
+            sets.append(rec)
+        extra = W.uniform_records(1000, key_index=np.arange(1, 1001, dtype=np.uint64), seed=9, value_len=20,
+                                  txn_start=10)
+        sets.append(extra)
+        ins = [oracle.table_build(r, 4096) for r in sets]
+        if not same:
+            with pytest.raises(SstcError) as e:
+                codec.compact(ins, 4096, 1 << 20, 1)
+            assert e.value.code == SSTC_E_TIE_ORDER
+            continue
+        want, kept = oracle.compact(ins, 4096, 1 << 20, 1)
+        outs, res = codec.compact(ins, 4096, 1 << 20, 1)
+        assert res.records_kept == kept == 3 * n + 1000
+        assert len(outs) == len(want) and all(np.array_equal(o, w) for o, w in zip(outs, want))
