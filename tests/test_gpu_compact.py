@@ -396,10 +396,12 @@ def test_compact_long_equal_runs(codec, oracle):
     for same in (True, False):
         sets = []
         for t in range(3):
-            # identical copies in every input (any heap order gives the same
-            # bytes), or each input its own values (SSTC_E_TIE_ORDER)
-            rec = W.uniform_records(n, key_index=np.zeros(n, np.uint64), seed=1 if same else t + 1, value_len=20)
+            # identical records (any heap order gives the same bytes), or
+            # values that differ (SSTC_E_TIE_ORDER: the run spans inputs)
+            rec = W.uniform_records(n, key_index=np.zeros(n, np.uint64), seed=t + 1, value_len=20)
             rec["txn"][:] = 77  # one key, one txn, every record
+            if same:
+                rec["val_off"][:] = 0  # every record the same value: all copies alike
             sets.append(rec)
         extra = W.uniform_records(1000, key_index=np.arange(1, 1001, dtype=np.uint64), seed=9, value_len=20,
                                   txn_start=10)
