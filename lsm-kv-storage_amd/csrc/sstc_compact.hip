@@ -823,12 +823,22 @@ __device__ __forceinline__ uint32_t run_of_record(const uint64_t *rs, uint32_t n
 
 // A run of merged records with equal key and merge txn: where the reference's
 // heap decides the order by its history (merge_iterator.h:91-95 compares key
-// and txn only).  Any order of the run gives the same bytes unless the run
-// holds records of two or more inputs AND not all of its records are alike
-// (type, txn as read, value).  Called for merged neighbours i - 1, i with equal
-// key and merge txn (rare: txns are unique per write); the run's first pair
-// walks the run once: ties[0] counts runs spanning inputs, ties[1] those of
-// them whose records differ, and such a run sets kGuardTieBoth.
+// and txn only).  Every order of the run gives the same records in the same
+// order unless the run holds records of two or more inputs AND not all of
+// them are alike (type, txn as read, value).  Called for merged neighbours
+// i - 1, i with equal key and merge txn (rare: txns are unique per write); the
+// run's first pair walks the run once.
+//   ties != null (sstc_merge_records, the iterator's whole order is
+//   observable): ties[0] counts runs spanning inputs, ties[1] those of them
+//   whose records differ.
+//   guard != null (the compaction filter): only the order of what
+//   ShouldKeepEntry keeps can reach an output (compact.cc:324-363): the
+//   run's records whose txn as read is not below the key group's first
+//   record's (the group head: the run's own merge txn when the run starts
+//   the group -- every input's first version in it has that txn -- else the
+//   group's first record's, galloped to as ff_keep does).  A run whose kept
+//   records span inputs and are not alike sets kGuardTieBoth: the job is
+//   refused (SSTC_E_TIE_ORDER).
 __device__ __forceinline__ uint64_t txn_as_read(const SK &x, const RecX &r, const KeyView &kv, uint32_t txn_mode) {
   return x.kl & kSkRead ? read_txn(kv, r, x.kl & ~kSkRead, txn_mode) : x.tx;
 }
@@ -838,24 +848,59 @@ __device__ __forceinline__ void note_tie(const SK *s, uint64_t n, uint64_t i, co
                                          unsigned long long *guard) {
   const SK h = s[i - 1];
   if (h.id >= n) return;
-  if (i >= 2) { // not the run's first pair: the pair that is walks it
+  bool group_head = true; // the run starts its key group
+  if (i >= 2) {
     const SK q = s[i - 2];
-    if (q.id < n && q.tx == h.tx && ff_same_key(q, h, kv)) return;
+    if (q.id < n && ff_same_key(q, h, kv)) {
+      if (q.tx == h.tx) return; // not the run's first pair: the pair that is walks it
+      group_head = false;
+    }
+  }
+  uint64_t head_txn = h.tx;
+  if (guard && !group_head) { // the group's first record (s[hi] has the key, s[lo] not)
+    uint64_t hi = i - 2;
+    int64_t lo = -1;
+    for (uint64_t step = 1;; step <<= 1) {
+      if (hi == 0) break;
+      const uint64_t p = hi > step ? hi - step : 0;
+      if (ff_same_key_at(s[p], h, kv, n)) {
+        hi = p;
+      } else {
+        lo = static_cast<int64_t>(p);
+        break;
+      }
+    }
+    while (lo + 1 < static_cast<int64_t>(hi)) {
+      const uint64_t mid = static_cast<uint64_t>((lo + static_cast<int64_t>(hi)) >> 1);
+      if (ff_same_key_at(s[mid], h, kv, n)) hi = mid;
+      else lo = static_cast<int64_t>(mid);
+    }
+    head_txn = s[hi].tx;
   }
   const uint32_t kl = h.kl & ~kSkRead;
-  const RecX hr = kv.rx[h.id];
-  const uint64_t htx = txn_as_read(h, hr, kv, txn_mode);
-  const uint32_t hin = run_of_record(rs, nruns, h.id);
-  bool cross = false, diff = false;
-  for (uint64_t j = i; j < n; j++) {
+  bool have = false, cross = false, diff = false;
+  uint32_t fin = 0;
+  RecX fr{};
+  uint64_t ftx = 0;
+  for (uint64_t j = i - 1; j < n; j++) {
     const SK x = s[j];
     if (x.id >= n || x.tx != h.tx || !ff_same_key(h, x, kv)) break;
-    cross |= run_of_record(rs, nruns, x.id) != hin;
-    if (diff) continue;
     const RecX r = kv.rx[x.id];
-    diff = r.type != hr.type || r.vl != hr.vl || txn_as_read(x, r, kv, txn_mode) != htx;
+    const uint64_t tx = txn_as_read(x, r, kv, txn_mode);
+    if (guard && tx < head_txn) continue; // dropped whatever the order (!(last_txn > txn), compact.cc:357-362)
+    const uint32_t in = run_of_record(rs, nruns, x.id);
+    if (!have) {
+      have = true;
+      fin = in;
+      fr = r;
+      ftx = tx;
+      continue;
+    }
+    cross |= in != fin;
+    if (diff) continue;
+    diff = r.type != fr.type || r.vl != fr.vl || tx != ftx;
     if (!diff && r.vl != kNoValue) {
-      const uint8_t *a = kv.src + r.ko + kl + 4, *b = kv.src + hr.ko + kl + 4;
+      const uint8_t *a = kv.src + r.ko + kl + 4, *b = kv.src + fr.ko + kl + 4;
       for (uint32_t k = 0; k < r.vl && !diff; k++) diff = a[k] != b[k];
     }
   }

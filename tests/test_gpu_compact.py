@@ -398,7 +398,7 @@ def test_compact_long_equal_runs(codec, oracle):
         for t in range(3):
             # identical records (any heap order gives the same bytes), or
             # values that differ (SSTC_E_TIE_ORDER: the run spans inputs)
-            rec = W.uniform_records(n, key_index=np.zeros(n, np.uint64), seed=t + 1, value_len=20)
+            rec = W.uniform_records(n, key_index=np.zeros(n, np.uint64), seed=1 if same else t + 1, value_len=20)
             rec["txn"][:] = 77  # one key, one txn, every record
             if same:
                 rec["val_off"][:] = 0  # every record the same value: all copies alike
