@@ -159,6 +159,15 @@ int sstc__ctx_set_fault(sstc_ctx *c, uint32_t fault) {
   c->arena.fault = fault;
   return SSTC_OK;
 }
+// test hook: the compaction block split's plan for the context's next job
+// (0 both paths, 1 the arithmetic chain alone, 2 the general walk alone) and
+// how many jobs had to run their tail twice (a chain-alone plan that failed)
+int sstc__ctx_seg_stats(sstc_ctx *c, uint32_t *mode, uint64_t *redos) {
+  if (!c || !mode || !redos) return SSTC_E_INVALID_ARG;
+  *mode = static_cast<uint32_t>(c->arena.seg_mode);
+  *redos = c->arena.seg_redo_count;
+  return SSTC_OK;
+}
 int sstc__ctx_sync(sstc_ctx *c) {
   if (!c || bind_device(c)) return SSTC_E_NO_DEVICE;
   return hipStreamSynchronize(c->stream) == hipSuccess ? SSTC_OK : SSTC_E_HIP;

@@ -1314,8 +1314,8 @@ __global__ __launch_bounds__(256) void ck_meta_kernel(const uint64_t *bmeta, Lay
                                                       const uint64_t *need, uint64_t cap, unsigned long long *guard,
                                                       const uint8_t *src, const uint64_t *src_end) {
   __shared__ __attribute__((aligned(16))) uint8_t img[kMetaLds + 16];
-  if (*need > cap || !L.ok() || (*guard & kGuardTieBoth) == kGuardTieBoth)
-    return; // output capacity exceeded / corrupt layout / heap-order ties: nothing is written
+  if (*need > cap || !L.ok() || writers_stand_down(*guard))
+    return; // output capacity exceeded / corrupt layout / heap-order ties / a redone split: nothing is written
   const uint64_t nb = L.nb();
   const uint64_t b0 = static_cast<uint64_t>(blockIdx.x) * 256u;
   if (b0 >= nb) return;
@@ -1391,7 +1391,7 @@ __global__ __launch_bounds__(kFootThreads) void ck_footer_kernel(Lay L, const ui
   __shared__ uint64_t smn[kFootThreads / kWave], smx[kFootThreads / kWave];
   const uint64_t t = blockIdx.x;
   const uint64_t nt = L.ok() ? L.nt() : 0;
-  if (L.ok() && t < nt && toff[nt] <= cap && (*guard & kGuardTieBoth) != kGuardTieBoth) { // uniform
+  if (L.ok() && t < nt && toff[nt] <= cap && !writers_stand_down(*guard)) { // uniform
     const uint64_t f = tbf[t], e = tbf[t + 1];
     const uint64_t o = toff[t], dbytes = tdata[t], mbytes = tmeta[t]; // in flight with the reduction's loads
     uint64_t mn = ~0ull, mx = 0;
@@ -1888,7 +1888,15 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     uint64_t *tf = pool.get<uint64_t>(n + 1), *dn = pool.get<uint64_t>(2);
     segment(pool, Pd, 0, n, totals, table_limit, nullptr, nullptr, tf, dn, s, true);
     uint64_t *bf = pool.get<uint64_t>(n + 1);
-    segment(pool, Pe, 16, n, totals, block_threshold, tf, dn, bf, dn + 1, s, false); // blocks end at table ends
+    uint32_t *Jb = pool.get<uint32_t>(segment_workspace_u32(n));
+    // the block split's launch plan: this context's last job decides (kArithOnly
+    // while the equal-size chain held: none of the general walk's nine
+    // launches; kGeneralOnly while it failed, retrying both every kSegProbe jobs)
+    SegMode mode = arena.seg_mode;
+    if (mode == SegMode::kGeneralOnly && ++arena.seg_general_jobs >= kSegProbe) {
+      mode = SegMode::kBoth;
+      arena.seg_general_jobs = 0;
+    }
     // 5. layout over count bounds (no host fetch: see Lay): the survivors'
     // key+value and entry + offset-entry bytes are at most the input block bytes
     const uint64_t tl = table_limit ? table_limit : 1, bt = block_threshold ? block_threshold : 1;
@@ -1900,45 +1908,15 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     const uint64_t nzb = scan_status_words(nb_max); // <= nb_max
     uint64_t *ws3 = pool.get<uint64_t>(2 * nzb);
     uint64_t *tbf = pool.get<uint64_t>(nt_max + 1);
-    ck_block_info_kernel<<<grid(nb_max), 256, 0, s>>>(bf, L, Pe, KR.kl, tf, blen, msz, btab, tbf, ws3, 2 * nzb,
-                                                      guard);
     const BlkOff BL{Pe, bf}; // block offsets in closed form (Pe[0] = 0)
     uint64_t *MS = pool.get<uint64_t>(nb_max + 1);
-    CK(launch_scan(msz, nb_max, 0, MS, ws3 + nzb, s, true));
-    uint64_t *tdata = pool.get<uint64_t>(nt_max),
-             *tmeta = pool.get<uint64_t>(nt_max);
-    if (nt_max + 1 <= kTiThreads) {
-      ck_table_info_kernel<true><<<1, kTiThreads, 0, s>>>(tf, L, bf, BL, MS, tbf, tdata, tmeta, d_table_len,
-                                                          d_table_off);
-    } else {
-      ck_table_info_kernel<false><<<grid(nt_max + 1), 256, 0, s>>>(tf, L, bf, BL, MS, tbf, tdata, tmeta, d_table_len,
-                                                                   nullptr);
-      CK(launch_scan(d_table_len, nt_max, 0, d_table_off, ws2, s)); // nt_max + 1 <= max_tables + 1 elements
-    }
+    uint64_t *tdata = pool.get<uint64_t>(nt_max), *tmeta = pool.get<uint64_t>(nt_max);
     // the output size is checked on the device (every writer below stands down
     // when it exceeds dst_cap) and by the host after the last sync
     const uint64_t *need = d_table_off + nt_max; // = d_table_off[nt]: the lengths past nt are zero
     uint64_t *bo = pool.get<uint64_t>(nb_max);
     uint64_t *brel = pool.get<uint64_t>(nb_max), *mo = pool.get<uint64_t>(nb_max);
-    ck_block_off_kernel<<<grid(nb_max), 256, 0, s>>>(btab, L, BL, tbf, d_table_off, tdata, MS, bo, brel, mo);
-    // 6. encode blocks, meta entries, footers
-    EncArgs ea{d_src, d_src, sstc_records{KR.type, KR.kl, KR.vl, KR.tx, KR.ko, KR.vo}, bf, nb_max, Pe, bo, blen, d_dst, 1};
-    ea.nb_dev = dn + 1;
     uint64_t *bmeta = pool.get<uint64_t>(4 * nb_max); // per block: min / max txn, first / last key
-    // blocks past an LDS slot are encoded by the wave that met them (config 5 319 -> 233 us)
-    ea.need = need;
-    ea.cap = dst_cap;
-    ea.bmeta = bmeta; // block min / max txn (reduced by the encode kernels) and first / last key
-    // output blocks are as large as the input's on average (an entry is copied
-    // whole): past 8 KiB the job's blocks mostly exceed the encode's LDS slot
-    ea.large_blocks = nblocks && in_bytes / nblocks > 8192 ? 1u : 0u;
-    ea.src_end = src_end;
-    ea.guard = guard;
-    ea.xcd = 2; // XCD-chunked block order (the grid is the nb_max bound)
-    CK(launch_enc_emit(ea, s));
-    ck_meta_kernel<<<static_cast<uint32_t>((nb_max + 255) / 256), 256, 0, s>>>(bmeta, L, btab, brel, mo, MS, blen,
-                                                                              tbf, d_dst, need, dst_cap, guard,
-                                                                              d_src, src_end);
     ensure_host(arena, 9);
     FootDone done{};
     {
@@ -1949,11 +1927,63 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
     }
     done.host = arena.host_dev;
     done.ticket = reinterpret_cast<unsigned int *>(guard + 32 + 32 * 9);
-    ck_footer_kernel<<<static_cast<uint32_t>(nt_max), kFootThreads, 0, s>>>(L, tbf, d_table_off, tdata, tmeta, bmeta,
-                                                                           d_dst, dst_cap, guard, done);
-    CK(hipGetLastError());
-    CK(hipStreamSynchronize(s));
+    // the block split (entry + offset-entry bytes, table_builder.cc:57-59,
+    // clamped at the table ends) and everything after it: enqueued once, and
+    // once more with the general walk when a kArithOnly chain failed
+    auto tail = [&](SegMode m) {
+      CK(launch_segment(Pe, n, block_threshold, Jb, dn + 1, bf, s, tf, dn, 16, false, totals, m, guard));
+      ck_block_info_kernel<<<grid(nb_max), 256, 0, s>>>(bf, L, Pe, KR.kl, tf, blen, msz, btab, tbf, ws3, 2 * nzb,
+                                                        guard);
+      CK(launch_scan(msz, nb_max, 0, MS, ws3 + nzb, s, true));
+      if (nt_max + 1 <= kTiThreads) {
+        ck_table_info_kernel<true><<<1, kTiThreads, 0, s>>>(tf, L, bf, BL, MS, tbf, tdata, tmeta, d_table_len,
+                                                            d_table_off);
+      } else {
+        ck_table_info_kernel<false><<<grid(nt_max + 1), 256, 0, s>>>(tf, L, bf, BL, MS, tbf, tdata, tmeta,
+                                                                     d_table_len, nullptr);
+        CK(launch_scan(d_table_len, nt_max, 0, d_table_off, ws2, s)); // nt_max + 1 <= max_tables + 1 elements
+      }
+      ck_block_off_kernel<<<grid(nb_max), 256, 0, s>>>(btab, L, BL, tbf, d_table_off, tdata, MS, bo, brel, mo);
+      // 6. encode blocks, meta entries, footers
+      EncArgs ea{d_src, d_src, sstc_records{KR.type, KR.kl, KR.vl, KR.tx, KR.ko, KR.vo}, bf, nb_max, Pe, bo, blen,
+                 d_dst, 1};
+      ea.nb_dev = dn + 1;
+      // blocks past an LDS slot are encoded by the wave that met them (config 5 319 -> 233 us)
+      ea.need = need;
+      ea.cap = dst_cap;
+      ea.bmeta = bmeta; // block min / max txn (reduced by the encode kernels) and first / last key
+      // output blocks are as large as the input's on average (an entry is copied
+      // whole): past 8 KiB the job's blocks mostly exceed the encode's LDS slot
+      ea.large_blocks = nblocks && in_bytes / nblocks > 8192 ? 1u : 0u;
+      ea.src_end = src_end;
+      ea.guard = guard;
+      ea.xcd = 2; // XCD-chunked block order (the grid is the nb_max bound)
+      CK(launch_enc_emit(ea, s));
+      ck_meta_kernel<<<static_cast<uint32_t>((nb_max + 255) / 256), 256, 0, s>>>(bmeta, L, btab, brel, mo, MS, blen,
+                                                                                tbf, d_dst, need, dst_cap, guard,
+                                                                                d_src, src_end);
+      ck_footer_kernel<<<static_cast<uint32_t>(nt_max), kFootThreads, 0, s>>>(L, tbf, d_table_off, tdata, tmeta,
+                                                                             bmeta, d_dst, dst_cap, guard, done);
+      CK(hipGetLastError());
+      CK(hipStreamSynchronize(s));
+    };
+    tail(mode);
     if (const int r = job_error(arena.host)) return r;
+    if (arena.host[3] & kGuardSplitRedo) { // the chain failed and nothing was written: the walk this time
+      const uint64_t g = arena.host[3] & (kGuardLongGroup | kGuardInv | kGuardTieCross | kGuardTieDiff);
+      CK(hipMemcpyAsync(guard, &g, sizeof g, hipMemcpyHostToDevice, s));
+      CK(hipMemsetAsync(done.ticket, 0, sizeof(unsigned int), s));
+      arena.seg_redo_count++;
+      mode = SegMode::kGeneralOnly;
+      tail(mode);
+      if (const int r = job_error(arena.host)) return r;
+    }
+    // the next job's plan: the chain alone after a job whose chain held
+    if (mode != SegMode::kGeneralOnly)
+      arena.seg_mode = arena.host[3] & (kGuardArithFail | kGuardSplitRedo) ? SegMode::kGeneralOnly
+                                                                            : SegMode::kArithOnly;
+    else if (arena.seg_mode != SegMode::kGeneralOnly)
+      arena.seg_mode = SegMode::kGeneralOnly;
     res[1] = arena.host[7];
     res[4] = arena.host[4];
     res[2] = arena.host[6];
@@ -1962,7 +1992,7 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
       err = "more output tables than max_tables";
       return SSTC_E_CAPACITY;
     }
-    if (arena.host[3] & ~(kGuardLongGroup | kGuardInv | kGuardTieCross | kGuardTieDiff)) {
+    if (arena.host[3] & ~(kGuardLongGroup | kGuardInv | kGuardTieCross | kGuardTieDiff | kGuardArithFail)) {
       err = "device consistency check failed (guard bits 0x" + [](uint64_t v) {
         char b[24];
         snprintf(b, sizeof b, "%llx", static_cast<unsigned long long>(v));

@@ -1465,7 +1465,7 @@ struct SegArgs {
   uint64_t nz;
   uint32_t *tentry;       // cleared here: tiles + 1 entry counters
   const uint64_t *mp;     // optional: the record count on the device (m is then its bound)
-  const uint64_t *skip;   // *skip != 0: the arithmetic chain held (seg_arith_*), nothing to do
+  const uint64_t *skip;   // *skip != 0: the arithmetic chain held (seg_arith_*), nothing to do (null: run)
 };
 
 // table ends cached in LDS by seg_walk_kernel: ends[t0 - 1 + j], j < kEndCache
@@ -1478,7 +1478,7 @@ __global__ __launch_bounds__(kChThreads) void seg_walk_kernel(SegArgs a) {
   __shared__ uint64_t s_wend, s_t0, s_e[kEndCache], s_ec;
   const uint32_t tid = threadIdx.x;
   const uint64_t c0 = static_cast<uint64_t>(blockIdx.x) * kChTile;
-  if (*a.skip) return;
+  if (a.skip && *a.skip) return;
   // the window's loads go out on the host bound a.m (Pw holds a.m + 1 words),
   // together with the device count's: one round trip instead of two
   constexpr uint32_t kFill = kLw / kChThreads;
@@ -1680,7 +1680,7 @@ struct NodeArgs {
 };
 
 __global__ void seg_node_kernel(NodeArgs a) {
-  if (*a.skip) return;
+  if (a.skip && *a.skip) return;
   const uint64_t k = blockIdx.x;
   const uint64_t b0 = a.base[k], nw = a.base[k + 1] - b0, c0 = k * kChTile;
   const uint64_t m = a.mp ? *a.mp : a.m;
@@ -1700,7 +1700,7 @@ __global__ void seg_node_kernel(NodeArgs a) {
 // level k + 1 = 8 hops of level k (node count from the device)
 __global__ void seg_npow_kernel(const uint32_t *Nx, const uint32_t *Nc, uint32_t *Nx1, uint32_t *Nc1,
                                 const uint64_t *nnodes, const uint64_t *skip) {
-  if (*skip) return;
+  if (skip && *skip) return;
   const uint64_t n = *nnodes;
   for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
        i += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
@@ -1725,7 +1725,7 @@ __global__ void seg_nentry_kernel(const uint32_t *Nx, const uint32_t *Nc, const 
                                   uint32_t levels, uint64_t stride, uint64_t m, const uint64_t *mp,
                                   uint64_t tiles, uint32_t *tentry, uint32_t *tbefore, uint64_t *first,
                                   uint64_t *d_count, const uint64_t *skip) {
-  if (*skip) return;
+  if (skip && *skip) return;
   if (mp) m = *mp;
   const uint64_t h = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (h == 0) {
@@ -1774,7 +1774,7 @@ __global__ void seg_nentry_kernel(const uint32_t *Nx, const uint32_t *Nc, const 
 __global__ __launch_bounds__(kChThreads) void seg_emit_kernel(const uint32_t *J0, uint64_t m, const uint64_t *mp,
                                                               const uint32_t *tentry, const uint32_t *tbefore,
                                                               uint64_t *first, const uint64_t *skip) {
-  if (*skip) return;
+  if (skip && *skip) return;
   constexpr uint32_t kPer = kChTile / kChThreads;
   constexpr uint16_t kOut = 0xFFFF; // successor outside the tile
   constexpr uint32_t kSerialChain = 128;
@@ -2702,6 +2702,14 @@ struct ArithArgs {
   // ar[2 ..]: g_a (kArMax), then the segment bases of the tables (kArMax + 1)
   uint64_t *ar;
   uint64_t *first, *d_count;
+  // optional: a chain that fails (here or in the check) ORs fail_bit into
+  // *fail (the compaction job's guard word: a note, or -- when the general
+  // walk was not enqueued -- the bit that makes the job's writers stand down)
+  unsigned long long *fail = nullptr;
+  unsigned long long fail_bit = 0;
+  __device__ void failed() const {
+    if (fail) atomicOr(fail, fail_bit);
+  }
 };
 
 __device__ __forceinline__ uint64_t ar_w(const ArithArgs &a, uint64_t x) { return a.Pw[x] + a.add * x; }
@@ -2727,7 +2735,10 @@ __global__ __launch_bounds__(kArThreads) void seg_arith_kernel(ArithArgs a) {
   const uint64_t m = a.mp ? *a.mp : a.m;
   const uint64_t nt = a.ends ? *a.nends : 1;
   if (m == 0 || nt == 0 || nt > kArMax) { // no records: the general path's m = 0 case; too many tables
-    if (tid == 0) a.ar[0] = 0;
+    if (tid == 0) {
+      a.ar[0] = 0;
+      a.failed();
+    }
     return;
   }
   if (tid == 0) s_bad = 0;
@@ -2758,6 +2769,7 @@ __global__ __launch_bounds__(kArThreads) void seg_arith_kernel(ArithArgs a) {
     tb[nt] = total;
     a.ar[1] = total;
     a.ar[0] = s_bad ? 0 : 1;
+    if (s_bad) a.failed();
     if (!s_bad) { // the general path writes both when it runs
       *a.d_count = total;
       a.first[total] = m;
@@ -2796,7 +2808,10 @@ __global__ __launch_bounds__(256) void seg_arith_check_kernel(ArithArgs a) {
     ok &= p < T1 && (q - 1 == p || wq1 < target) && (q == T1 || wq >= target);
     a.first[h] = p;
   }
-  if (!ok) a.ar[0] = 0; // (every failing thread stores the same 0)
+  if (!ok) { // (every failing thread stores the same 0)
+    a.ar[0] = 0;
+    a.failed();
+  }
 }
 
 namespace {
@@ -2836,7 +2851,8 @@ uint64_t segment_workspace_u32(uint64_t nrec) {
 
 hipError_t launch_segment(const uint64_t *Pw, uint64_t nrec, uint64_t threshold, uint32_t *J,
                           uint64_t *d_nblocks, uint64_t *blk_first, hipStream_t s, const uint64_t *ends,
-                          const uint64_t *d_nends, uint64_t add, bool long_segments, const uint64_t *d_nrec) {
+                          const uint64_t *d_nends, uint64_t add, bool long_segments, const uint64_t *d_nrec,
+                          SegMode mode, unsigned long long *fail) {
   if (nrec == 0) { // no records: no segment, first[0] = 0
     hipError_t e = hipMemsetAsync(d_nblocks, 0, sizeof(uint64_t), s);
     if (e == hipSuccess) e = hipMemsetAsync(blk_first, 0, sizeof(uint64_t), s);
@@ -2858,9 +2874,16 @@ hipError_t launch_segment(const uint64_t *Pw, uint64_t nrec, uint64_t threshold,
   // general walk below runs only when a check fails (ar[0] = 0)
   uint64_t *ar = U + L.ar;
   const uint32_t pg = static_cast<uint32_t>(std::min<uint64_t>(grid_for(nrec + 1, 256), 2048));
-  const ArithArgs aa{Pw, add, nrec, threshold, ends, d_nends, d_nrec, ar, blk_first, d_nblocks};
-  seg_arith_kernel<<<1, kArThreads, 0, s>>>(aa);
-  seg_arith_check_kernel<<<pg, 256, 0, s>>>(aa);
+  if (mode != SegMode::kGeneralOnly) {
+    ArithArgs aa{Pw, add, nrec, threshold, ends, d_nends, d_nrec, ar, blk_first, d_nblocks};
+    aa.fail = fail;
+    aa.fail_bit = mode == SegMode::kArithOnly ? kGuardSplitRedo : kGuardArithFail;
+    seg_arith_kernel<<<1, kArThreads, 0, s>>>(aa);
+    seg_arith_check_kernel<<<pg, 256, 0, s>>>(aa);
+    if (mode == SegMode::kArithOnly) return hipGetLastError(); // a failed chain: *fail |= kGuardSplitRedo
+  } else {
+    ar = nullptr; // no verdict: the general walk runs
+  }
   SegArgs a{Pw, add, nrec, threshold, ends, d_nends, J + L.J0, J + L.Fx, J + L.Fc, win, blk_first, d_nblocks,
             sws, scan_status_words(L.tiles), tentry, d_nrec, ar};
   seg_walk_kernel<<<static_cast<uint32_t>(L.tiles), kChThreads, 0, s>>>(a);

@@ -80,6 +80,19 @@ constexpr unsigned long long kGuardMergeId = 1, kGuardEntry = 2, kGuardBlockRang
 // otherwise than this job, so the job writes nothing and returns
 // SSTC_E_TIE_ORDER (the writers stand down on both bits).
 constexpr unsigned long long kGuardTieBoth = kGuardTieCross | kGuardTieDiff;
+// The block split's arithmetic chain (seg_arith_*) failed: kGuardArithFail is
+// a note (the general walk ran behind it); kGuardSplitRedo means the general
+// walk was NOT enqueued (the context's last job took the chain, SegMode::
+// kArithOnly), so the split is not the greedy one: every writer stands down
+// and the host runs the job's tail again with the general walk.
+constexpr unsigned long long kGuardArithFail = 1024, kGuardSplitRedo = 2048;
+// the job's writers (encode, meta, footer) write nothing
+__host__ __device__ inline bool writers_stand_down(unsigned long long g) {
+  return (g & kGuardSplitRedo) || (g & kGuardTieBoth) == kGuardTieBoth;
+}
+// block split launch plan (launch_segment): both paths (the general walk's
+// kernels return at once when the chain holds), the chain alone, the walk alone
+enum class SegMode : uint32_t { kBoth = 0, kArithOnly = 1, kGeneralOnly = 2 };
 
 struct EncArgs {
   const uint8_t *key_src;
@@ -107,9 +120,7 @@ struct EncArgs {
   // optional capacity guard (compaction): nothing is written when *need > cap
   const uint64_t *need = nullptr;
   uint64_t cap = 0;
-  __device__ bool over() const {
-    return (need && *need > cap) || (guard && (*guard & kGuardTieBoth) == kGuardTieBoth);
-  }
+  __device__ bool over() const { return (need && *need > cap) || (guard && writers_stand_down(*guard)); }
   // optional consistency guard (compaction, mode 1): every block's output range
   // must lie in [0, cap), every entry inside its block image (offset + size
   // <= data bytes, size >= its header + key) and its source inside
@@ -212,7 +223,8 @@ uint64_t segment_workspace_u32(uint64_t nrec);
 hipError_t launch_segment(const uint64_t *Pw, uint64_t nrec, uint64_t threshold, uint32_t *J,
                           uint64_t *d_nblocks, uint64_t *blk_first, hipStream_t s,
                           const uint64_t *ends = nullptr, const uint64_t *d_nends = nullptr, uint64_t add = 0,
-                          bool long_segments = false, const uint64_t *d_nrec = nullptr);
+                          bool long_segments = false, const uint64_t *d_nrec = nullptr,
+                          SegMode mode = SegMode::kBoth, unsigned long long *fail = nullptr);
 // d_nrec: the record count on the device (nrec is then only its upper bound:
 // grids and workspace are sized by nrec, the kernels segment *d_nrec records)
 
@@ -237,7 +249,14 @@ struct Arena {
   // job's filter output on the device so its consistency guard can be tested
   // (1: survivor key offsets, 2: entry prefix sums); 0 in production
   uint32_t fault = 0;
+  // the block split plan of this context's next compaction job: the chain
+  // alone while the last job's chain held, the walk alone while it failed
+  // (with a retry of both every kSegProbe jobs), both when unknown
+  SegMode seg_mode = SegMode::kBoth;
+  uint32_t seg_general_jobs = 0;
+  uint64_t seg_redo_count = 0; // jobs whose tail ran twice (diagnostics / tests)
 };
+constexpr uint32_t kSegProbe = 8;
 
 // sstc_merge_records: compact_impl stops after the merge and writes the merged
 // order (out, up to cap records) instead of filtering and encoding

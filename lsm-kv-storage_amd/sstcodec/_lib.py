@@ -113,6 +113,7 @@ def load():
                                                c_vp]),
         "sstc_copy_probe": (ctypes.c_int, [c_vp, c_vp, c_vp, c_u64]),
         "sstc__ctx_set_fault": (ctypes.c_int, [c_vp, c_u32]),  # test hooks (sstc_api.hip), not in the header
+        "sstc__ctx_seg_stats": (ctypes.c_int, [c_vp, c_vp, c_vp]),
         "sstc__ctx_set_scan_epoch": (ctypes.c_int, [c_vp, c_u32]),
         "sstc_open_tables": (ctypes.c_int, [c_vp, c_vp, c_u64, c_vp, c_vp, c_u32, c_u64, c_vp, c_vp, c_vp, c_vp,
                                             c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),

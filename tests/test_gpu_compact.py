@@ -416,3 +416,39 @@ def test_compact_long_equal_runs(codec, oracle):
         outs, res = codec.compact(ins, 4096, 1 << 20, 1)
         assert res.records_kept == kept == 3 * n + 1000
         assert len(outs) == len(want) and all(np.array_equal(o, w) for o, w in zip(outs, want))
+
+
+def _seg_stats(codec):
+    import ctypes
+    mode, redos = ctypes.c_uint32(), ctypes.c_uint64()
+    assert codec.lib.sstc__ctx_seg_stats(codec.h, ctypes.byref(mode), ctypes.byref(redos)) == 0
+    return mode.value, redos.value
+
+
+def test_block_split_plan_follows_the_workload(oracle):
+    """the block split's launch plan per context.  A job whose
+    equal-size chain held makes the next job enqueue the chain alone (none of
+    the general walk's launches); when that next job's records do not fit the
+    chain (Zipf sizes) its writers stand down, the tail runs again with the
+    general walk, and the outputs are still the oracle's; jobs after a failed
+    chain take the walk alone, retrying both every kSegProbe jobs."""
+    import sstcodec
+    codec = sstcodec.Codec(0)  # a fresh context: plan "both"
+    try:
+        uni = [oracle.table_build(r, 4096) for r in W.config_inputs(3, ssts=4, keys=20_000)]
+        zipf = [oracle.table_build(r, 4096) for r in
+                W.compaction_inputs(4, 600, 1200, seed=5, vmin=8, vmax=65536, zipf=1.1, p_delete=0.1)]
+        want_u, _ = oracle.compact(uni, 4096, 1 << 20, 1)
+        want_z, _ = oracle.compact(zipf, 4096, 1 << 20, 1)
+        plans = []
+        for ins, want in [(uni, want_u), (uni, want_u), (zipf, want_z), (zipf, want_z), (uni, want_u)] + \
+                [(uni, want_u)] * 8:
+            outs, _ = codec.compact(ins, 4096, 1 << 20, 1)
+            assert len(outs) == len(want) and all(np.array_equal(o, w) for o, w in zip(outs, want))
+            plans.append(_seg_stats(codec))
+        assert plans[0] == (1, 0) and plans[1] == (1, 0)  # the chain held: alone from then on
+        assert plans[2] == (2, 1)  # chain alone failed on Zipf sizes: the tail ran twice, walk alone next
+        assert plans[3] == (2, 1) and plans[4] == (2, 1)  # walk alone (a uniform job too, until the probe)
+        assert (1, 1) in plans[5:]  # the probe ran both paths, the chain held again
+    finally:
+        codec.close()
