@@ -134,7 +134,12 @@ int sstc_ctx_drop_stream(sstc_ctx *ctx);
 /* Pre-size the workspace for up to max_blocks blocks and max_records records. */
 int sstc_ctx_reserve(sstc_ctx *ctx, uint64_t max_blocks, uint64_t max_records);
 /* Synchronise the stream; return the number of blocks that failed since the
- * last reset (per-block codes are in the callers' d_block_status arrays). */
+ * last reset (per-block codes are in the callers' d_block_status arrays).
+ * The count also includes any prefix scan of sstc_count_records /
+ * sstc_segment_records / sstc_encode_blocks whose decoupled look-back gave up
+ * waiting for a predecessor workgroup (its sums are wrong; never seen unless
+ * the GPU stalls a workgroup for seconds); the compaction calls reject such a
+ * job with SSTC_E_INTERNAL instead. */
 int sstc_ctx_error_count(sstc_ctx *ctx, uint64_t *out);
 int sstc_ctx_reset_errors(sstc_ctx *ctx);
 

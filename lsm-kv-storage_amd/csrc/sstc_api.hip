@@ -300,6 +300,7 @@ int sstc_count_records(sstc_ctx *c, const uint8_t *d_src, const uint64_t *d_blk_
   a.rec_base = d_rec_base;
   a.ws = c->scan_ws;
   a.epoch = ep;
+  a.lb_fail = c->err_count; // a look-back that gave up counts as an error
   SSTC_HIP(sstc::launch_count_scan(a, false, c->stream), "count + scan kernel");
   return SSTC_OK;
 }
@@ -336,7 +337,8 @@ int sstc_segment_records(sstc_ctx *c, const uint32_t *d_key_len, const uint32_t 
   // weights = entry_size + 16 (block_builder.cc:33), Pw = exclusive scan
   uint32_t ep = 0;
   if (int r = next_epoch(c, ep)) return r;
-  SSTC_HIP(sstc::launch_scan_entry_sizes(d_key_len, d_val_len, nrec, 16, c->P, c->scan_ws, c->stream, ep), "scan");
+  SSTC_HIP(sstc::launch_scan_entry_sizes(d_key_len, d_val_len, nrec, 16, c->P, c->scan_ws, c->stream, ep,
+                                                 c->err_count), "scan");
   SSTC_HIP(sstc::launch_segment(c->P, nrec, block_threshold, c->jump, d_nblocks, d_blk_first, c->stream),
            "segment kernels");
   return SSTC_OK;
@@ -362,7 +364,7 @@ int sstc_encode_blocks(sstc_ctx *c, const uint8_t *d_key_src, const uint8_t *d_v
   // profiles/r02_ab/encode_ab.md); c->P is the workspace of the blocks past an
   // LDS slot, which their own wave encodes (Zipf 64 KiB set 329 -> 236 us)
   SSTC_HIP(sstc::launch_enc_offsets(in.key_len, in.val_len, d_blk_first, nblocks, out_base, d_out_blk_off,
-                                    d_out_blk_len, c->scan_ws, c->stream, ep),
+                                    d_out_blk_len, c->scan_ws, c->stream, ep, c->err_count),
            "block offsets");
   sstc::EncArgs a{d_key_src, d_val_src, in, d_blk_first, nblocks, c->P, d_out_blk_off, d_out_blk_len, d_dst};
   SSTC_HIP(sstc::launch_enc_emit(a, c->stream), "emit kernel");

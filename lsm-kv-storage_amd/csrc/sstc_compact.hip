@@ -1024,7 +1024,10 @@ __global__ __launch_bounds__(kFtThreads) void ck_filter_kernel(const SK *s, uint
         const uint32_t need = inc ? static_cast<uint32_t>(__ffsll(static_cast<long long>(inc))) : kWave;
         const uint64_t zero = __ballot((st >> 62) == 0 && lane < need);
         if (zero) {
-          if (++spins > kLbSpinLimit) break; // a predecessor never published: give up (wrong sums, no hang)
+          if (++spins > kLbSpinLimit) { // a predecessor never published: give up (no hang), the job rejected
+            if (lane == 0) atomicOr(guard, kGuardLookback);
+            break;
+          }
           __builtin_amdgcn_s_sleep(1);
           continue;
         }
@@ -1668,6 +1671,10 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
       wait_seq(arena, s, flag, seq);
     }
     const uint64_t in_bytes = arena.host[0]; // every survivor's entry lies in these bytes
+    if (in_bytes == ~0ull) { // count_scan_kernel<true>: a look-back gave up (kGuardLookback)
+      err = "device consistency check failed (a look-back of the record count scan gave up): nothing was written";
+      return SSTC_E_INTERNAL;
+    }
     std::vector<uint64_t> run_start(arena.host + 1, arena.host + 2 + ntables);
     const uint64_t n = run_start[ntables];
     res[0] = n;
@@ -1843,6 +1850,11 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
         err = "input SST records are not sorted (key asc)";
         return SSTC_E_INVALID_ARG;
       }
+      if (h[3] & kGuardLookback) {
+        err = "device consistency check failed (a decoupled look-back gave up waiting for a predecessor "
+              "workgroup): nothing was written";
+        return SSTC_E_INTERNAL;
+      }
       if (h[3] & kGuardMergeId) {
         err = "device consistency check failed after the merge (merged record ids out of range)";
         return SSTC_E_INTERNAL;
@@ -1875,6 +1887,9 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
                                                                         totals, stop, guard, txn_mode, rb,
                                                                         static_cast<uint32_t>(nruns));
     if (arena.fault == 1) CK(hipMemsetAsync(KR.ko, 0xFF, n * sizeof(uint64_t), s)); // test: bad key offsets
+    if (arena.fault == 3) { // test: a look-back that gave up (kGuardLookback, byte 1 of the guard word)
+      CK(hipMemsetAsync(reinterpret_cast<uint8_t *>(guard) + 1, static_cast<int>(kGuardLookback >> 8), 1, s));
+    }
     if (arena.fault == 2) CK(hipMemsetAsync(Pe, 0x5A, (n + 1) * sizeof(uint64_t), s)); // test: bad prefix sums
     if (max_tables == 0) { // no room for the first table (m >= 1 unless the job is rejected)
       fetch(arena, s, err_words, nullptr, 0, true);
@@ -1934,14 +1949,14 @@ int compact_impl(Arena &arena, hipStream_t s, unsigned long long *err_count, con
       CK(launch_segment(Pe, n, block_threshold, Jb, dn + 1, bf, s, tf, dn, 16, false, totals, m, guard));
       ck_block_info_kernel<<<grid(nb_max), 256, 0, s>>>(bf, L, Pe, KR.kl, tf, blen, msz, btab, tbf, ws3, 2 * nzb,
                                                         guard);
-      CK(launch_scan(msz, nb_max, 0, MS, ws3 + nzb, s, true));
+      CK(launch_scan(msz, nb_max, 0, MS, ws3 + nzb, s, true, 0, guard));
       if (nt_max + 1 <= kTiThreads) {
         ck_table_info_kernel<true><<<1, kTiThreads, 0, s>>>(tf, L, bf, BL, MS, tbf, tdata, tmeta, d_table_len,
                                                             d_table_off);
       } else {
         ck_table_info_kernel<false><<<grid(nt_max + 1), 256, 0, s>>>(tf, L, bf, BL, MS, tbf, tdata, tmeta,
                                                                      d_table_len, nullptr);
-        CK(launch_scan(d_table_len, nt_max, 0, d_table_off, ws2, s)); // nt_max + 1 <= max_tables + 1 elements
+        CK(launch_scan(d_table_len, nt_max, 0, d_table_off, ws2, s, false, 0, guard)); // <= max_tables + 1 elements
       }
       ck_block_off_kernel<<<grid(nb_max), 256, 0, s>>>(btab, L, BL, tbf, d_table_off, tdata, MS, bo, brel, mo);
       // 6. encode blocks, meta entries, footers

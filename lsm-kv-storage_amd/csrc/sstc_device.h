@@ -166,6 +166,21 @@ constexpr uint64_t kLbAgg = 1ull << 62, kLbInc = 2ull << 62, kLbVal = (1ull << 4
 constexpr uint32_t kLbEpochShift = 48;
 constexpr uint64_t kLbSpinLimit = 1ull << 24; // never reached unless a tile died
 
+// Where a look-back that gave up (kLbSpinLimit: a predecessor tile never
+// published, e.g. a workgroup dispatched out of id order) reports it, so the
+// caller rejects the wrong prefix sums instead of using them: bit != 0 ORs the
+// bit into *p (a compaction guard word), bit == 0 counts into *p (a context's
+// error counter).  p == nullptr: not reported.
+struct LbFail {
+  unsigned long long *p = nullptr;
+  unsigned long long bit = 0;
+  __device__ void report() const {
+    if (!p) return;
+    if (bit) atomicOr(p, bit);
+    else atomicAdd(p, 1ull);
+  }
+};
+
 __device__ __forceinline__ uint64_t readlane_u64(uint64_t v, uint32_t l) {
   return (static_cast<uint64_t>(__builtin_amdgcn_readlane(static_cast<uint32_t>(v >> 32), l)) << 32) |
          __builtin_amdgcn_readlane(static_cast<uint32_t>(v), l);
@@ -182,7 +197,7 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
 // publishes its own inclusive prefix and returns the exclusive prefix
 // (wave-uniform; tile 0: 0).  Words of another epoch are not published yet.
 __device__ __forceinline__ uint64_t lb_publish_lookback(uint64_t *status, uint64_t tile, uint64_t total,
-                                                        uint32_t epoch) {
+                                                        uint32_t epoch, const LbFail &fail = LbFail{}) {
   const uint32_t lane = lane_id();
   const uint64_t tag = static_cast<uint64_t>(epoch) << kLbEpochShift;
   if (tile == 0) {
@@ -201,7 +216,10 @@ __device__ __forceinline__ uint64_t lb_publish_lookback(uint64_t *status, uint64
     const uint32_t need = inc ? static_cast<uint32_t>(__ffsll(static_cast<long long>(inc))) : kWave;
     const uint64_t zero = __ballot((st >> 62) == 0 && lane < need);
     if (zero) {
-      if (++spins > kLbSpinLimit) break; // a predecessor never published: give up (wrong sums, no hang)
+      if (++spins > kLbSpinLimit) { // a predecessor never published: give up (no hang), reported
+        if (lane == 0) fail.report();
+        break;
+      }
       __builtin_amdgcn_s_sleep(1);
       continue;
     }

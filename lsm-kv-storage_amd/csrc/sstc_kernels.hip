@@ -2165,7 +2165,7 @@ __device__ __forceinline__ uint32_t lb_idx(uint32_t i) { return i + (i >> 4); } 
 template <class In, uint32_t kItems = kLbItems>
 __global__ __launch_bounds__(kScanThreads) void scan_lookback_kernel(In in, uint64_t n, uint64_t carry_in,
                                                                      uint64_t *out, uint64_t *ws, uint32_t epoch,
-                                                                     const uint64_t *skip) {
+                                                                     const uint64_t *skip, LbFail fail) {
   if (skip && *skip) return; // uniform: every tile returns (launch_segment: the arithmetic chain held)
   constexpr uint32_t kTile = kScanThreads * kItems;
   __shared__ uint64_t sm[kTile + kTile / 16];
@@ -2211,7 +2211,7 @@ __global__ __launch_bounds__(kScanThreads) void scan_lookback_kernel(In in, uint
     total += x;
   }
   if (w == 0) {
-    const uint64_t prefix = lb_publish_lookback(status, tile, total, epoch);
+    const uint64_t prefix = lb_publish_lookback(status, tile, total, epoch, fail);
     if (lane == 0) s_prefix = prefix;
   }
   __syncthreads();
@@ -2254,14 +2254,17 @@ constexpr uint32_t kCsItems = SSTC_CS_ITEMS, kCsTile = kScanThreads * kCsItems, 
 uint64_t count_scan_tiles(uint64_t nblocks) { return nblocks ? (nblocks + kCsTile - 1) / kCsTile : 1; }
 uint64_t count_scan_workspace(uint64_t nblocks) { return kCsStatus + count_scan_tiles(nblocks); }
 
+constexpr uint64_t kPartGaveUp = 1ull << 63; // part[2 t]: tile t's look-back gave up
 template <bool kStart>
 __global__ __launch_bounds__(kScanThreads) void count_scan_kernel(CountScanArgs a) {
   __shared__ uint64_t sm[kCsTile + kCsTile / 16];
   __shared__ uint64_t s_wsum[kScanThreads / kWave], s_bytes[kScanThreads / kWave], s_end[kScanThreads / kWave];
   __shared__ uint64_t s_prefix;
   __shared__ uint32_t s_last;
+  __shared__ unsigned long long s_gave; // start: a look-back (this tile's, or any tile's in the last) gave up
   const uint32_t tid = threadIdx.x, lane = lane_id(), w = tid / kWave;
   const uint64_t n = a.nblocks, tile = blockIdx.x, base = tile * kCsTile;
+  if (kStart && tid == 0) s_gave = 0; // (read after the barriers below)
   // masked-off extras read 16 B of the ticket line no thread writes
   const uint8_t *safe = reinterpret_cast<const uint8_t *>(a.ws + 8);
   uint64_t len[kCsItems], off[kCsItems];
@@ -2319,7 +2322,8 @@ __global__ __launch_bounds__(kScanThreads) void count_scan_kernel(CountScanArgs 
     total += x;
   }
   if (w == 0) {
-    const uint64_t prefix = lb_publish_lookback(a.ws + kCsStatus, tile, total, a.epoch);
+    const uint64_t prefix = lb_publish_lookback(a.ws + kCsStatus, tile, total, a.epoch,
+                                                kStart ? LbFail{&s_gave, 1} : LbFail{a.lb_fail, 0});
     if (lane == 0) s_prefix = prefix;
   }
   __syncthreads();
@@ -2344,7 +2348,7 @@ __global__ __launch_bounds__(kScanThreads) void count_scan_kernel(CountScanArgs 
         by += s_bytes[k];
         e = s_end[k] > e ? s_end[k] : e;
       }
-      a.part[2 * tile] = by;
+      a.part[2 * tile] = by | (s_gave ? kPartGaveUp : 0ull); // (block bytes < 2^63)
       a.part[2 * tile + 1] = e;
     }
     // the tile's stores drained, then released at agent scope before its
@@ -2365,9 +2369,11 @@ __global__ __launch_bounds__(kScanThreads) void count_scan_kernel(CountScanArgs 
     }
     __syncthreads();
     if (!s_last) return;
-    uint64_t by = 0, e = 0;
+    uint64_t by = 0, e = 0, gave = 0;
     for (uint64_t p = tid; p < gridDim.x; p += kScanThreads) {
-      by += __hip_atomic_load(a.part + 2 * p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint64_t b = __hip_atomic_load(a.part + 2 * p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      by += b & ~kPartGaveUp;
+      gave |= b & kPartGaveUp;
       const uint64_t x = __hip_atomic_load(a.part + 2 * p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       e = x > e ? x : e;
     }
@@ -2380,6 +2386,7 @@ __global__ __launch_bounds__(kScanThreads) void count_scan_kernel(CountScanArgs 
       s_bytes[w] = by;
       s_end[w] = e;
     }
+    if (gave) s_gave = 1;
     for (uint64_t i = tid; i < a.ntfb; i += kScanThreads) {
       const uint64_t r = __hip_atomic_load(a.rec_base + a.tfb[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       a.run_start[i] = r;
@@ -2394,10 +2401,10 @@ __global__ __launch_bounds__(kScanThreads) void count_scan_kernel(CountScanArgs 
         by += s_bytes[k];
         e = s_end[k] > e ? s_end[k] : e;
       }
-      a.host[0] = by; // input block bytes
+      a.host[0] = s_gave ? ~0ull : by; // input block bytes (~0: the run starts are wrong)
       *a.errs = *a.err_count;
       *a.bad = 0;
-      a.guard[0] = 0; // consistency-guard bits
+      a.guard[0] = s_gave ? kGuardLookback : 0; // consistency-guard bits
       a.guard[1] = e; // the end of the source bytes the input blocks span
       for (int g = 0; g < 10; g++) a.guard[32 + 32 * g] = 0; // the check kernel's 9 tickets, the footer's
       a.ws[0] = 0; // the ticket, for the next job
@@ -2490,7 +2497,8 @@ uint64_t scan_status_words(uint64_t n) { return n <= kScanTile ? 0 : (n + kArrTi
 
 template <class In, uint32_t kItems = kLbItems>
 static hipError_t scan_any(In in, uint64_t n, uint64_t carry_in, uint64_t *out, uint64_t *ws, hipStream_t s,
-                           bool ws_zeroed, uint32_t epoch, const uint64_t *skip = nullptr) {
+                           bool ws_zeroed, uint32_t epoch, const uint64_t *skip = nullptr,
+                           LbFail fail = LbFail{}) {
   constexpr uint64_t kTile = kScanThreads * kItems;
   if (n <= kScanTile) {
     scan_apply_kernel<In><<<1, kScanThreads, 0, s>>>(in, n, nullptr, carry_in, out, skip);
@@ -2504,19 +2512,21 @@ static hipError_t scan_any(In in, uint64_t n, uint64_t carry_in, uint64_t *out, 
     if (e != hipSuccess) return e;
   }
   scan_lookback_kernel<In, kItems><<<static_cast<uint32_t>(tiles), kScanThreads, 0, s>>>(in, n, carry_in, out, ws,
-                                                                                        epoch, skip);
+                                                                                        epoch, skip, fail);
   return hipGetLastError();
 }
 
 hipError_t launch_scan(const uint64_t *in, uint64_t n, uint64_t carry_in, uint64_t *out, uint64_t *ws,
-                       hipStream_t s, bool ws_zeroed, uint32_t epoch) {
-  return scan_any<ArrIn, kArrItems>(ArrIn{in}, n, carry_in, out, ws, s, ws_zeroed, epoch);
+                       hipStream_t s, bool ws_zeroed, uint32_t epoch, unsigned long long *guard) {
+  return scan_any<ArrIn, kArrItems>(ArrIn{in}, n, carry_in, out, ws, s, ws_zeroed, epoch, nullptr,
+                                    LbFail{guard, kGuardLookback});
 }
 
 hipError_t launch_scan_entry_sizes(const uint32_t *klen, const uint32_t *vlen, uint64_t nrec, uint64_t add,
-                                   uint64_t *out, uint64_t *ws, hipStream_t s, uint32_t epoch) {
+                                   uint64_t *out, uint64_t *ws, hipStream_t s, uint32_t epoch,
+                                   unsigned long long *err_count) {
   // 16 items per thread: 4 and 8 were slower (37.9 / 24.8 vs 20.4 us at 1.8 M records, the look-back chain)
-  return scan_any(EntryIn{klen, vlen, add}, nrec, 0, out, ws, s, false, epoch);
+  return scan_any(EntryIn{klen, vlen, add}, nrec, 0, out, ws, s, false, epoch, nullptr, LbFail{err_count, 0});
 }
 
 // Block lengths and offsets of a records -> blocks encode in ONE kernel
@@ -2533,7 +2543,8 @@ constexpr uint32_t kBoScanWaves = kBoTile / kWave;
 __global__ __launch_bounds__(kBoThreads) void enc_offsets_kernel(const uint32_t *kl, const uint32_t *vl,
                                                                  const uint64_t *blk_first, uint64_t nblocks,
                                                                  uint64_t out_base, uint64_t *blk_off,
-                                                                 uint64_t *blk_len, uint64_t *ws, uint32_t epoch) {
+                                                                 uint64_t *blk_len, uint64_t *ws, uint32_t epoch,
+                                                                 LbFail fail) {
   __shared__ uint64_t s_len[kBoTile];
   __shared__ uint64_t s_wsum[kBoScanWaves];
   __shared__ uint64_t s_tile, s_prefix;
@@ -2613,7 +2624,10 @@ __global__ __launch_bounds__(kBoThreads) void enc_offsets_kernel(const uint32_t 
         const uint64_t inc = __ballot((st >> 62) == 2);
         const uint32_t need = inc ? static_cast<uint32_t>(__ffsll(static_cast<long long>(inc))) : kWave;
         if (__ballot((st >> 62) == 0 && lane < need)) {
-          if (++spins > kLbSpinLimit) break; // a predecessor never published: give up (wrong sums, no hang)
+          if (++spins > kLbSpinLimit) { // a predecessor never published: give up (no hang), reported
+            if (lane == 0) fail.report();
+            break;
+          }
           __builtin_amdgcn_s_sleep(1);
           continue;
         }
@@ -2641,18 +2655,19 @@ uint64_t enc_offsets_workspace(uint64_t nblocks) { return (nblocks + kBoTile - 1
 
 hipError_t launch_enc_offsets(const uint32_t *kl, const uint32_t *vl, const uint64_t *blk_first, uint64_t nblocks,
                               uint64_t out_base, uint64_t *blk_off, uint64_t *blk_len, uint64_t *ws, hipStream_t s,
-                              uint32_t epoch) {
+                              uint32_t epoch, unsigned long long *err_count) {
   if (nblocks == 0) { // blk_first may be NULL
     enc_none_kernel<<<1, 1, 0, s>>>(out_base, blk_off);
     return hipGetLastError();
   }
   if (nblocks <= kScanTile || epoch == 0) { // one workgroup's scan / no epoch: sum kernel + scan
     enc_bsum_kernel<<<grid_for(nblocks * kBsG, 256), 256, 0, s>>>(kl, vl, blk_first, nblocks, blk_len);
-    return scan_any<ArrIn, kArrItems>(ArrIn{blk_len}, nblocks, out_base, blk_off, ws, s, false, epoch);
+    return scan_any<ArrIn, kArrItems>(ArrIn{blk_len}, nblocks, out_base, blk_off, ws, s, false, epoch, nullptr,
+                                      LbFail{err_count, 0});
   }
   // ws: enc_offsets_workspace(nblocks) words
   enc_offsets_kernel<<<static_cast<uint32_t>((nblocks + kBoTile - 1) / kBoTile), kBoThreads, 0, s>>>(
-      kl, vl, blk_first, nblocks, out_base, blk_off, blk_len, ws, epoch);
+      kl, vl, blk_first, nblocks, out_base, blk_off, blk_len, ws, epoch, LbFail{err_count, 0});
   return hipGetLastError();
 }
 
@@ -2888,7 +2903,8 @@ hipError_t launch_segment(const uint64_t *Pw, uint64_t nrec, uint64_t threshold,
             sws, scan_status_words(L.tiles), tentry, d_nrec, ar};
   seg_walk_kernel<<<static_cast<uint32_t>(L.tiles), kChThreads, 0, s>>>(a);
   // base[tiles] = node count
-  hipError_t e = scan_any<ArrIn, kArrItems>(ArrIn{win}, L.tiles, 0, base, sws, s, true, 0, ar);
+  hipError_t e = scan_any<ArrIn, kArrItems>(ArrIn{win}, L.tiles, 0, base, sws, s, true, 0, ar,
+                                            LbFail{fail, kGuardLookback});
   if (e != hipSuccess) return e;
   const uint64_t *nn = base + L.tiles;
   NodeArgs na{J + L.Fx, J + L.Fc, base, nrec, L.tiles, J + L.Nx, J + L.Nc, J + L.Nt, d_nrec, ar};

@@ -86,9 +86,13 @@ constexpr unsigned long long kGuardTieBoth = kGuardTieCross | kGuardTieDiff;
 // kArithOnly), so the split is not the greedy one: every writer stands down
 // and the host runs the job's tail again with the general walk.
 constexpr unsigned long long kGuardArithFail = 1024, kGuardSplitRedo = 2048;
+// A decoupled look-back of the job gave up waiting for a predecessor tile
+// (kLbSpinLimit, sstc_device.h LbFail): its prefix sums are wrong, the writers
+// stand down and the job returns SSTC_E_INTERNAL.
+constexpr unsigned long long kGuardLookback = 4096;
 // the job's writers (encode, meta, footer) write nothing
 __host__ __device__ inline bool writers_stand_down(unsigned long long g) {
-  return (g & kGuardSplitRedo) || (g & kGuardTieBoth) == kGuardTieBoth;
+  return (g & (kGuardSplitRedo | kGuardLookback)) || (g & kGuardTieBoth) == kGuardTieBoth;
 }
 // block split launch plan (launch_segment): both paths (the general walk's
 // kernels return at once when the chain holds), the chain alone, the walk alone
@@ -187,6 +191,9 @@ struct CountScanArgs {
   unsigned long long *bad, *guard;      // cleared (guard[1] = the source end)
   uint64_t *host;                       // pinned: [0] input bytes, [1..ntfb] run starts
   uint64_t seq, flag;                   // host[flag] = seq last
+  // not start: counts a look-back that gave up (a context's error counter);
+  // start: such a tile makes host[0] = ~0 and sets kGuardLookback instead
+  unsigned long long *lb_fail = nullptr;
 };
 uint64_t count_scan_tiles(uint64_t nblocks);
 uint64_t count_scan_workspace(uint64_t nblocks);
@@ -202,11 +209,15 @@ uint64_t scan_status_words(uint64_t n);
 // other epochs (a context's own workspace, see sstc_api.hip next_epoch): no
 // memset either.  Neither: the status words are cleared with a memset.
 constexpr uint32_t kScanEpochs = 1u << 14;
+// guard: a look-back that gave up sets kGuardLookback there (may be null).
 hipError_t launch_scan(const uint64_t *in, uint64_t n, uint64_t carry_in, uint64_t *out, uint64_t *ws,
-                       hipStream_t s, bool ws_zeroed = false, uint32_t epoch = 0);
-// out = exclusive scan of the entry sizes (+ add) of records (klen, vlen)
+                       hipStream_t s, bool ws_zeroed = false, uint32_t epoch = 0,
+                       unsigned long long *guard = nullptr);
+// out = exclusive scan of the entry sizes (+ add) of records (klen, vlen);
+// err_count counts a look-back that gave up (may be null)
 hipError_t launch_scan_entry_sizes(const uint32_t *klen, const uint32_t *vlen, uint64_t nrec, uint64_t add,
-                                   uint64_t *out, uint64_t *ws, hipStream_t s, uint32_t epoch);
+                                   uint64_t *out, uint64_t *ws, hipStream_t s, uint32_t epoch,
+                                   unsigned long long *err_count = nullptr);
 // block offsets (nblocks + 1) and lengths of a records -> blocks encode: block
 // lengths by reduction over each block's records and their scan, one kernel
 // (ws: enc_offsets_workspace(nblocks) words, epoch != 0) or, for one
@@ -214,7 +225,7 @@ hipError_t launch_scan_entry_sizes(const uint32_t *klen, const uint32_t *vlen, u
 uint64_t enc_offsets_workspace(uint64_t nblocks);
 hipError_t launch_enc_offsets(const uint32_t *kl, const uint32_t *vl, const uint64_t *blk_first, uint64_t nblocks,
                               uint64_t out_base, uint64_t *blk_off, uint64_t *blk_len, uint64_t *ws, hipStream_t s,
-                              uint32_t epoch);
+                              uint32_t epoch, unsigned long long *err_count = nullptr);
 hipError_t launch_enc_emit(const EncArgs &a, hipStream_t s);
 // greedy segmentation; J = segment_workspace_u32(nrec) u32 of device workspace
 uint64_t segment_workspace_u32(uint64_t nrec);

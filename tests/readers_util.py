@@ -1,6 +1,7 @@
-"""The record stream of an SST file in the canonical dump format of
-tests/cpp/compact_loop.cc --readers (per record: u8 type, u64 txn, u32 key
-length, key, u8 value-is-non-null, u32 value length, value; little endian),
+"""The record stream of an SST file in the canonical dump format (per record:
+u8 type, u64 txn, u32 key length, key, u8 value-is-non-null, u32 value length,
+value; little endian) that tests/cpp/readers_check.cc --readers writes from
+the sstc::TableReader iterators (tests/test_gpu_dropin.py compares the two),
 made from block decodes of the file's index.  With RefLib (the reference's own
 TableReader index + BlockReaderIterator, oracle/_ref/libsstref.so) it is the
 reference-decoded stream; with the oracle it is the restatement's."""

@@ -355,17 +355,18 @@ def test_compact_long_keys_many_windows(codec, oracle):
             assert np.array_equal(o, w)
 
 
-@pytest.mark.parametrize("fault", [1, 2])
+@pytest.mark.parametrize("fault", [1, 2, 3])
 @pytest.mark.parametrize("case", ["mixed", "zipf"])
 def test_compact_guard_rejects_corrupted_filter_output(codec, oracle, fault, case):
     """Downstream of the keep / drop filter, the encode, meta and footer
     kernels index with device-produced offsets (survivor key offsets, entry
     prefix sums).  With the filter output deliberately corrupted on the device
     (test hook sstc__ctx_set_fault: 1 = survivor key offsets 0xFF.., 2 = entry
-    prefix sums garbage), the job's consistency guard must reject it
-    (SSTC_E_INTERNAL) without an out-of-range access, and the context must stay
-    usable.  'zipf' has blocks past the encode's LDS slot (the large-block
-    path)."""
+    prefix sums garbage, 3 = the guard bit a decoupled look-back sets when it
+    gives up waiting for a predecessor workgroup, kGuardLookback), the job's
+    consistency guard must reject it (SSTC_E_INTERNAL) without an out-of-range
+    access, and the context must stay usable.  'zipf' has blocks past the
+    encode's LDS slot (the large-block path)."""
     import sstcodec
     if case == "zipf":
         sets = W.compaction_inputs(4, 600, 1200, seed=5, vmax=65536, vmin=8, zipf=1.1, p_delete=0.1)
@@ -375,7 +376,7 @@ def test_compact_guard_rejects_corrupted_filter_output(codec, oracle, fault, cas
     want, _ = oracle.compact(ins, 4096, 4 << 20, 1)
     assert codec.lib.sstc__ctx_set_fault(codec.h, fault) == 0
     try:
-        with pytest.raises(sstcodec.SstcError, match=r"\(-6\).*consistency"):
+        with pytest.raises(sstcodec.SstcError, match=r"\(-6\).*consistency" + (".*look-back" if fault == 3 else "")):
             codec.compact(ins, 4096, 4 << 20, 1)
     finally:
         codec.lib.sstc__ctx_set_fault(codec.h, 0)
@@ -452,3 +453,69 @@ def test_block_split_plan_follows_the_workload(oracle):
         assert (1, 1) in plans[5:]  # the probe ran both paths, the chain held again
     finally:
         codec.close()
+
+
+def _table_blocks_vs_segment(oracle, tables, T):
+    """Every output table's block split (record counts per block, decoded
+    back) equals oracle.segment over that table's own records: the split is
+    clamped at the table ends."""
+    for t, img in enumerate(tables):
+        idx = oracle.table_index(img)
+        kl, vl, counts = [], [], []
+        for o, n in zip(idx["blk_off"], idx["blk_len"]):
+            st, r = oracle.decode_block(img[int(o):int(o + n)])
+            assert st == 0
+            kl.append(r["key_len"])
+            vl.append(r["val_len"])
+            counts.append(len(r["key_len"]))
+        kl, vl = np.concatenate(kl), np.concatenate(vl)
+        z = np.zeros(len(kl), np.uint64)
+        rec = {"type": np.zeros(len(kl), np.uint8), "key_len": kl, "val_len": vl, "txn": z, "key_off": z,
+               "val_off": z, "key_src": np.zeros(1, np.uint8), "val_src": np.zeros(1, np.uint8)}
+        want = oracle.segment(rec, T)
+        got = np.concatenate([[0], np.cumsum(counts)]).astype(np.uint64)
+        assert np.array_equal(got, want), t
+
+
+@pytest.mark.parametrize("case", ["ends_hold", "ends_one_fails", "over_1024_tables"])
+def test_block_split_with_table_ends(oracle, case):
+    """the block split's arithmetic chain with table ends (the
+    compaction's multi-table split, seg_arith_kernel over ends = the table
+    starts).  ends_hold: equal entries in ~30 output tables, every table's
+    chain holds (the next job's plan: the chain alone); ends_one_fails: one
+    record 3000 B heavier in one table, so that table's chain fails and the
+    others would hold (the whole verdict falls back to the general walk, a
+    note); over_1024_tables: more output tables than the chain takes (kArMax
+    = 1024: the general walk).  Outputs bit-exact against the oracle and each
+    table's blocks against oracle.segment."""
+    import sstcodec
+    sets = W.config_inputs(3, ssts=4, keys=5000)
+    T, limit = 4096, 64 << 10
+    if case == "ends_one_fails":
+        r = dict(sets[2])
+        j = 2500
+        extra = W.random_bytes(77, 3100)
+        r["val_off"] = r["val_off"].copy()
+        r["val_len"] = r["val_len"].copy()
+        r["val_off"][j] = r["val_src"].size
+        r["val_len"][j] = 3100
+        r["val_src"] = np.concatenate([r["val_src"], extra])
+        sets[2] = r
+    elif case == "over_1024_tables":
+        T, limit = 512, 2048
+    ins = [oracle.table_build(r, 4096) for r in sets]
+    want, _ = oracle.compact(ins, T, limit, 1)
+    if case == "over_1024_tables":
+        assert len(want) > 1024
+    else:
+        assert 10 < len(want) <= 1024
+    codec = sstcodec.Codec(0)  # a fresh context: plan "both"
+    try:
+        outs, _ = codec.compact(ins, T, limit, 1)
+        assert len(outs) == len(want) and all(np.array_equal(o, w) for o, w in zip(outs, want))
+        mode, redos = _seg_stats(codec)
+        assert redos == 0
+        assert mode == (1 if case == "ends_hold" else 2), mode  # the chain held / failed
+    finally:
+        codec.close()
+    _table_blocks_vs_segment(oracle, want, T)
