@@ -6,7 +6,7 @@
 #   bench    python bench.py --steps 30
 #   profile  tools/profile.sh: rocprofv3 kernel trace + stats and FETCH / WRITE passes of the bench
 #   trace    rocprofv3 kernel traces of the compaction job, configs 3 4 5 (tools/trace_compact.py tables)
-#   pmc      FETCH_SIZE / WRITE_SIZE of one config-3 and one config-4 compaction call
+#   pmc      FETCH_SIZE / WRITE_SIZE of one config-3, one config-4 and one config-5 compaction call
 #   configs  tools/bench_compact.py configs 3, 3-overlap, 4, 5 with the reference driver beside them
 # Env: PYTEST_K (pytest -k filter), CONFIGS (trace configs).
 set -o pipefail
@@ -45,6 +45,8 @@ if has pmc; then
   cp gpurun_out/pmc_compact/summary.json $out/pmc_c3.json; tail -1 $out/pmc_c3.log
   bash tools/pmc_compact_job.sh --config 4 --steps 1 --no-ref --no-files > $out/pmc_c4.log 2>&1 || { tail -5 $out/pmc_c4.log; exit 7; }
   cp gpurun_out/pmc_compact/summary.json $out/pmc_c4.json; tail -1 $out/pmc_c4.log
+  bash tools/pmc_compact_job.sh --config 5 --steps 1 --no-ref --no-files > $out/pmc_c5.log 2>&1 || { tail -5 $out/pmc_c5.log; exit 7; }
+  cp gpurun_out/pmc_compact/summary.json $out/pmc_c5.json; tail -1 $out/pmc_c5.log
 fi
 if has configs; then
   for c in "3" "3 --overlap" "4" "5"; do
