@@ -305,10 +305,35 @@ def _merge_sets(name, oracle):
         return [oracle.table_build(ragged_sorted(900 + 300 * t, 610 + t), 4096) for t in range(4)]
     if name == "one_table":
         return [oracle.table_build(W.compaction_inputs(1, 3000, 9000, seed=9)[0], 4096)]
+    if name == "reftest":  # tests/test_mergeIterator.cc:65-184's data: "key<i>" -> "value<i>", txn 0
+        return [oracle.table_build(_reftest_records(t), 4096) for t in range(REFTEST_TABLES)]
     raise KeyError(name)
 
 
-MERGE_CASES = sorted(CJ) + ["ties_same", "ties_diff", "versions", "ragged", "one_table"]
+REFTEST_TABLES, REFTEST_PER = 4, 5000
+
+
+def _reftest_pairs(t):
+    """table t of the reference's TableTest.MergeIterator shape: memtable t
+    holds Put("key" + i, "value" + i, 0) for a consecutive range of i, flushed
+    sorted by key (so "key10" < "key2")"""
+    return sorted((f"key{i}".encode(), f"value{i}".encode()) for i in range(t * REFTEST_PER, (t + 1) * REFTEST_PER))
+
+
+def _reftest_records(t):
+    pairs = _reftest_pairs(t)
+    n = len(pairs)
+    kl = np.array([len(k) for k, _ in pairs], np.uint32)
+    vl = np.array([len(v) for _, v in pairs], np.uint32)
+    ko = np.concatenate([[0], np.cumsum(kl[:-1], dtype=np.uint64)]).astype(np.uint64)
+    vo = np.concatenate([[0], np.cumsum(vl[:-1], dtype=np.uint64)]).astype(np.uint64)
+    return {"type": np.zeros(n, np.uint8), "key_len": kl, "val_len": vl, "txn": np.zeros(n, np.uint64),
+            "key_off": ko, "val_off": vo,
+            "key_src": np.frombuffer(b"".join(k for k, _ in pairs), np.uint8).copy(),
+            "val_src": np.frombuffer(b"".join(v for _, v in pairs), np.uint8).copy()}
+
+
+MERGE_CASES = sorted(CJ) + ["ties_same", "ties_diff", "versions", "ragged", "one_table", "reftest"]
 
 
 @pytest.mark.timeout(300)
@@ -349,6 +374,13 @@ def test_merge_iterator_trace_equals_reference(oracle, tmp_path, name):
         dumps.append((tag, r.stdout.strip(), open(d, "rb").read()))
     assert dumps[0][1].startswith("merge ok ") and len(dumps[0][2]) > 1000
     want = merge_steps(dumps[0][2])
+    if name == "reftest":  # test_mergeIterator.cc's own expectations: the forward walk is the sorted
+        # list of every pair, the SeekToLast + Prev loop after it is empty (IsValid reads the min heap)
+        pairs = sorted(p for t in range(REFTEST_TABLES) for p in _reftest_pairs(t))
+        fwd = [(x[4][1], x[5][1]) for x in want if x[0] == "N" and len(x) > 2]
+        assert fwd[:len(pairs)] == pairs and len([x for x in want if x[0] == "N"]) >= len(pairs)
+        first_pass = want[:want.index(("L", 0)) + 1] if ("L", 0) in want else want
+        assert not any(x[0] == "P" for x in first_pass)
     for tag, out, dump in dumps[1:]:
         got = merge_steps(dump)
         bad = next((i for i, (a, b) in enumerate(zip(got, want)) if a != b), None)
