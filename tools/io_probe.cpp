@@ -2,7 +2,7 @@
 // (maps of page-cache-hot SST files, H2D from them, D2H into pageable memory,
 // pwrite + fsync of output-sized files).  Diagnostic only.
 //   hipcc -O2 -std=c++20 tools/io_probe.cpp -o tools/io_probe -lpthread
-//   tools/io_probe <dir> <files> <MiB per file>
+//   tools/io_probe <dir> <files> <MiB per file> [writes]   (writes: only the output-file section)
 #include <hip/hip_runtime.h>
 
 #include <fcntl.h>
@@ -10,6 +10,7 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -43,6 +44,7 @@ int main(int argc, char **argv) {
       close(fd);
     }
   }
+  const bool writes_only = argc > 4 && std::string(argv[4]) == "writes";
   CK(hipSetDevice(0));
   CK(hipFree(nullptr));
   hipStream_t s;
@@ -62,14 +64,14 @@ int main(int argc, char **argv) {
     for (void *p : maps) munmap(p, sz);
   };
   std::vector<void *> maps;
-  for (int rep = 0; rep < 2; rep++) {
+  for (int rep = 0; rep < (writes_only ? 0 : 2); rep++) {
     double t0 = now();
     map_all(true, maps);
     double t1 = now();
     std::printf("mmap populate serial: %.1f ms (%.2f GiB)\n", (t1 - t0) * 1e3, gib);
     unmap_all(maps);
   }
-  {
+  if (!writes_only) {
     maps.assign(nf, nullptr);
     double t0 = now();
     std::vector<std::thread> th;
@@ -136,7 +138,7 @@ int main(int argc, char **argv) {
     unmap_all(maps);
   }
   // pread into a pinned ring + H2D (what sstc_compact_files does), single thread
-  {
+  if (!writes_only) {
     double t0 = now();
     void *pin = nullptr;
     CK(hipHostMalloc(&pin, 64 << 20, hipHostMallocDefault));
@@ -153,7 +155,7 @@ int main(int argc, char **argv) {
     CK(hipHostFree(pin));
   }
   // D2H of 256 MiB into pageable memory
-  {
+  if (!writes_only) {
     const size_t n = size_t(256) << 20;
     double t0 = now();
     std::vector<uint8_t> h(n);
@@ -201,6 +203,48 @@ int main(int argc, char **argv) {
       close(fd);
       std::printf("44 MiB pwrite x4 threads %.2f ms fsync %.2f ms\n", (t1 - t0) * 1e3, (t2 - t1) * 1e3);
     }
+  }
+  // O_DIRECT writes of a 44 MB table image from page-locked memory (what
+  // TableBuilder::Finish does), one pwrite, 1 MiB / 8 MiB pieces, and the
+  // image split over 2 / 4 / 8 threads writing their slices at once
+  {
+    const size_t n = 44u << 20;
+    uint8_t *img = nullptr;
+    CK(hipHostMalloc(reinterpret_cast<void **>(&img), n, hipHostMallocDefault));
+    std::memset(img, 7, n);
+    auto run = [&](const char *what, int threads, size_t piece) {
+      for (int rep = 0; rep < 3; rep++) {
+        std::string p = dir + "/outd" + std::to_string(rep) + ".sst";
+        int fd = open(p.c_str(), O_CREAT | O_TRUNC | O_WRONLY | O_DIRECT, 0644);
+        if (fd < 0) {
+          std::printf("O_DIRECT open refused\n");
+          return;
+        }
+        double t0 = now();
+        std::vector<std::thread> th;
+        const size_t slice = n / threads;
+        for (int q = 0; q < threads; q++)
+          th.emplace_back([&, q] {
+            for (size_t at = q * slice; at < (q + 1) * slice; at += piece)
+              (void)!pwrite(fd, img + at, std::min(piece, (q + 1) * slice - at), at);
+          });
+        for (auto &t : th) t.join();
+        double t1 = now();
+        fsync(fd);
+        double t2 = now();
+        close(fd);
+        std::printf("44 MiB O_DIRECT %s: pwrite %.2f ms (%.1f GB/s) fsync %.2f ms\n", what, (t1 - t0) * 1e3,
+                    n / (t1 - t0) / 1e9, (t2 - t1) * 1e3);
+      }
+    };
+    run("1 pwrite", 1, n);
+    run("8 MiB pieces", 1, 8u << 20);
+    run("1 MiB pieces", 1, 1u << 20);
+    run("2 threads", 2, n);
+    run("4 threads", 4, n);
+    run("8 threads", 8, n);
+    run("4 threads 1 MiB pieces", 4, 1u << 20);
+    CK(hipHostFree(img));
   }
   CK(hipFree(dev));
   std::printf("done\n");
