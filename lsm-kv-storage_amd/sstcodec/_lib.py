@@ -42,6 +42,11 @@ class CompactResult(ctypes.Structure):
                 ("blocks_out", ctypes.c_uint64), ("tables_out", ctypes.c_uint64), ("bytes_out", ctypes.c_uint64)]
 
 
+class MergeResult(ctypes.Structure):
+    """sstc_merge_result"""
+    _fields_ = [("records", ctypes.c_uint64), ("cross_ties", ctypes.c_uint64), ("tie_diffs", ctypes.c_uint64)]
+
+
 class BlockIndex(ctypes.Structure):
     """sstc_block_index (device pointers)."""
     _fields_ = [("blk_off", c_vp), ("blk_len", c_vp), ("last_key_off", c_vp), ("last_key_len", c_vp),
@@ -63,6 +68,8 @@ class FilesTiming(ctypes.Structure):
                 ("store_s", ctypes.c_double), ("total_s", ctypes.c_double)]
 
 
+SSTC_E_INVALID_ARG = -1
+SSTC_E_CAPACITY = -5
 SSTC_E_INTERNAL = -6  # include/sstcodec.h: a device-side consistency check failed
 SSTC_E_TIE_ORDER = -7  # include/sstcodec.h: equal (key, txn) records with different contents in different inputs
 
@@ -107,6 +114,8 @@ def load():
         "sstc_roundtrip_blocks": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_u64, c_u32, c_vp, c_vp]),
         "sstc_compact": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_u64, c_vp, c_u32, P(CompactParams), c_vp, c_u64,
                                         c_vp, c_vp, c_u64, P(CompactResult)]),
+        "sstc_merge_records": (ctypes.c_int, [c_vp, c_vp, c_vp, c_vp, c_u64, c_vp, c_u32, c_u32, c_vp, c_u64,
+                                              P(MergeResult)]),
         "sstc_get_batch": (ctypes.c_int, [c_vp, c_vp, P(BlockIndex), c_vp, c_vp, c_u64, c_vp, c_vp, c_u64, c_vp, c_vp,
                                           c_vp, c_vp]),
         "sstc_roundtrip_host": (ctypes.c_int, [c_vp, c_vp, c_vp, c_u64, c_vp, c_vp, c_u64, c_u32, c_u64, c_vp,

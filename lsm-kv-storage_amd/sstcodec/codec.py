@@ -280,6 +280,37 @@ class Codec:
         return [d[int(o[t]):int(o[t + 1])] for t in range(nt)], res
 
 
+    def merge_records(self, tables, txn_mode=_lib.SSTC_TXN_COMPAT, max_records=None):
+        """sstc_merge_records over SST images (numpy u8 arrays, iterator
+        order): MergeIterator's SeekToFirst + Next order of every record.
+        Returns (records: numpy (n, 2) u64 of [key offset into the tables
+        concatenated, txn as read], MergeResult).  max_records=None sizes the
+        output by a first call that reports the count (SSTC_E_CAPACITY)."""
+        import numpy as np
+        from ._lib import SSTC_E_CAPACITY, MergeResult
+        files = [np.ascontiguousarray(t, np.uint8) for t in tables]
+        src = torch.from_numpy(np.concatenate(files)).to(self.device)
+        idx = self.open_tables(src, [f.size for f in files], strict=True)
+        blk_off, blk_len, h_tfb = idx["blk_off"], idx["blk_len"], idx["table_first_block"]
+        res = MergeResult()
+
+        def call(cap):
+            out = torch.empty((max(cap, 1), 2), dtype=torch.int64, device=self.device)
+            self._stream()
+            rc = self.lib.sstc_merge_records(self.h, _p(src), _p(blk_off), _p(blk_len), int(blk_off.numel()),
+                                             h_tfb.ctypes.data_as(ctypes.c_void_p), len(files), txn_mode, _p(out),
+                                             cap, ctypes.byref(res))
+            return rc, out
+        if max_records is None:
+            rc, out = call(0)
+            if rc == SSTC_E_CAPACITY:
+                rc, out = call(int(res.records))
+        else:
+            rc, out = call(int(max_records))
+        check(rc, "sstc_merge_records")
+        return out[: res.records].cpu().numpy().view(np.uint64), res
+
+
 def _queries(keys):
     import numpy as np
     lens = np.array([len(k) for k in keys], np.uint32)
