@@ -807,11 +807,39 @@ def dropin_leg(paths, ranges, fixture, td, in_bytes, reps=2):
             shutil.rmtree(d, ignore_errors=True)
     if not ok:
         raise SystemExit("dropin leg: the unchanged compact.cc with the drop-ins wrote other bytes than the reference")
+    # one more run with the library's host trace on (SSTC_TRACE_HOST=1): where the seconds go
+    phases = None
+    try:
+        d = os.path.join(td, "pick_traced")
+        os.makedirs(d)
+        os.sync()
+        r = subprocess.run([exe, d] + args, capture_output=True, text=True, timeout=600,
+                           env=dict(os.environ, SSTC_TRACE_HOST="1"))
+        import re
+        import shutil
+        shutil.rmtree(d, ignore_errors=True)
+        tot = {}
+        for ln in r.stderr.splitlines():
+            m = re.match(r"\[sstc\] (resident inputs: .*?|MergeIterator life.*?) ([0-9.]+) ms$", ln)
+            if m:
+                tot[m.group(1)] = tot.get(m.group(1), 0.0) + float(m.group(2))
+            elif ln.startswith("[sstc] Finish"):
+                tot["Finish (sum)"] = tot.get("Finish (sum)", 0.0) + float(ln.split(": ")[1].split(" ms")[0])
+                tot["Finish calls"] = tot.get("Finish calls", 0) + 1
+                for part, v in re.findall(r"(pwrite|fsync) ([0-9.]+)", ln):
+                    tot[f"Finish {part} (sum)"] = tot.get(f"Finish {part} (sum)", 0.0) + float(v)
+        if r.returncode == 0 and tot:
+            t = float(next(ln.split()[1] for ln in r.stdout.splitlines() if ln.startswith("time ")))
+            phases = {"s": round(t, 4), **{k: round(v, 2) for k, v in tot.items()}}
+    except (OSError, ValueError, StopIteration, subprocess.TimeoutExpired):
+        phases = None
     g = float(np.median(gpu))
     leg = {"what": "Compact::PickCompact (db/compact.cc unchanged) with the drop-in MergeIterator (device merge), "
                    "TableReaderIterator and TableBuilder (device encode), input files page-cache-hot, outputs "
                    "written + fsync'd", "s_runs": [round(x, 4) for x in gpu], "s_median": round(g, 4),
            "GiBps_in": round(in_bytes / g / 2 ** 30, 3), "verified_vs_reference": bool(ok)}
+    if phases:
+        leg["phases_ms_traced_run"] = phases
     if cpu:
         c = float(np.median(cpu))
         leg["cpu_baseline"] = {"value": round(c, 4), "unit": "s", "s_runs": [round(x, 4) for x in cpu],
