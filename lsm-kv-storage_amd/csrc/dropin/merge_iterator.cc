@@ -77,7 +77,15 @@ void MergeIterator::SeekToFirst() {
 
 void MergeIterator::WaitRecords() {
   if (pos_ > n_) pos_ = n_;
-  if (pos_ < n_) avail_ = resident_->WaitRecords(pos_ + 1);
+  if (pos_ >= n_) return;
+  try {
+    avail_ = resident_->WaitRecords(pos_ + 1);
+  } catch (const std::exception &e) { // the records' download failed: the heaps from here on (the views
+                                      // handed out so far stay valid: resident_ lives on)
+    std::fprintf(stderr, "[sstc] MergeIterator: %s; heap mode from record %llu\n", e.what(),
+                 static_cast<unsigned long long>(pos_));
+    LeaveDevice();
+  }
 }
 
 // ---------------------------------------------------------------- heap mode

@@ -21,6 +21,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <cstdlib>
 #include <map>
 #include <stdexcept>
 
@@ -100,8 +101,13 @@ void ResidentInputs::Download() {
     DeviceScope on(device_);
     hipStream_t s = nullptr;
     if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) throw std::runtime_error("stream");
+    // test hook: the download fails once this many records are down (the
+    // drop-in MergeIterator must continue on the heaps)
+    static const char *fail_at_env = std::getenv("SSTC_TEST_DOWNLOAD_FAIL_AT");
+    const uint64_t fail_at = fail_at_env ? std::strtoull(fail_at_env, nullptr, 10) : ~0ull;
     uint64_t done = 0, chunk = 1ull << 15;
     while (done < n_) {
+      if (done >= fail_at) throw std::runtime_error("test hook: download stopped");
       const uint64_t k = std::min(chunk, n_ - done);
       if (hipMemcpyAsync(rec_.get() + done, static_cast<sstc_merged_record *>(drec_) + done,
                          k * sizeof(sstc_merged_record), hipMemcpyDeviceToHost, s) != hipSuccess ||

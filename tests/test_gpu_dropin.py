@@ -92,8 +92,26 @@ def case_inputs(name):
 @pytest.mark.parametrize("name", RUNNABLE)
 def test_unmodified_compact_cc_gpu_decode_and_encode(tmp_path, name):
     """Compact::PickCompact as written, with GPU decode (drop-in
-    TableReaderIterator) and GPU encode (drop-in TableBuilder): every output
-    file, GetFileSize() and VersionEdit key range equal to the reference's."""
+    TableReaderIterator), the device merge (drop-in MergeIterator) and GPU
+    encode (drop-in TableBuilder): every output file, GetFileSize() and
+    VersionEdit key range equal to the reference's."""
+    _pick_compact_case(tmp_path, name, {})
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("name", [n for n in ("config5", "config3") if n in RUNNABLE])
+def test_unmodified_compact_cc_download_failure_falls_back(tmp_path, name):
+    """The merged records' download failing midway (test hook
+    SSTC_TEST_DOWNLOAD_FAIL_AT: after the first 32 K-record chunk) does not
+    fail the compaction: the drop-in MergeIterator replays the reference's
+    heaps to its position and walks on with them, the builders mix resident
+    references with copied records, and the outputs are still the
+    reference's."""
+    r = _pick_compact_case(tmp_path, name, {"SSTC_TEST_DOWNLOAD_FAIL_AT": "1"})
+    assert "heap mode from record 32768" in r.stderr, r.stderr[-2000:]
+
+
+def _pick_compact_case(tmp_path, name, env):
     need(EXE)
     from oracle import table_key_range
     case = MANIFEST[name]
@@ -107,9 +125,9 @@ def test_unmodified_compact_cc_gpu_decode_and_encode(tmp_path, name):
         lo, hi = table_key_range(rec)
         args += [p, str(fs), lo.hex() or "-", hi.hex() or "-"]
     ins = None
-    r = subprocess.run(args, capture_output=True, text=True, timeout=540)
+    r = subprocess.run(args, capture_output=True, text=True, timeout=540, env=dict(os.environ, **env))
     assert r.returncode == 0, r.stderr[-2000:]
-    if name in TIMED and os.path.exists(REF_EXE):  # the same PickCompact as written (CPU decode + encode)
+    if name in TIMED and os.path.exists(REF_EXE) and not env:  # the same PickCompact as written (CPU decode + encode)
         t_gpu = pick_time(r.stdout)
         d = tmp_path / "db_ref"
         d.mkdir()
@@ -127,8 +145,9 @@ def test_unmodified_compact_cc_gpu_decode_and_encode(tmp_path, name):
         got.append((sha(img), fs))
         assert (lo, hi) == first_last_key(img)  # what VersionEdit::AddNewFiles recorded
     assert got == [(o["sha256"], o["file_size"]) for o in case["fixed_outputs"]]
-    print(f"{name}: db/compact.cc + db/merge_iterator.cc unchanged, GPU decode + GPU encode -> "
+    print(f"{name}: db/compact.cc unchanged over the drop-ins, GPU decode + merge + encode -> "
           f"{len(outs)} outputs equal to the reference's", flush=True)
+    return r
 
 
 TIMED = ("config3", "config4_rank0", "config5")
