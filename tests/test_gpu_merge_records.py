@@ -114,3 +114,27 @@ def test_merge_records_tie_counters(codec, name):
     recs, res = codec.merge_records(ins)
     assert res.records == len(recs) > 0 and res.cross_ties > 0
     assert (res.tie_diffs > 0) == (name == "diff")
+
+
+def fuzz_sets(seed):
+    """random merge shapes: 1-40 inputs, 50-1500 records each, keys 4-40 B
+    from a small or large space (versions inside inputs or not), values
+    0 B-20 KiB with empty ones, 0-30 % DELETEs"""
+    rng = np.random.default_rng(1000 + seed)
+    k = int(rng.choice([1, 2, 5, 9, 17, 40]))
+    n = int(rng.integers(50, 1500))
+    space = int(rng.choice([40, 2000, 10 ** 6]))
+    vmax = int(rng.choice([0, 16, 300, 20000]))
+    width = int(rng.choice([4, 16, 40]))
+    width = 16 if width == 4 and space > 999 else width  # "k" + 3 digits: keys in order only below 1000
+    return W.compaction_inputs(k, n, space, seed=2000 + seed, p_delete=float(rng.choice([0.0, 0.1, 0.3])),
+                               vmin=0, vmax=vmax, key_width=width, distinct=bool(rng.integers(0, 2)) and n <= space)
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_merge_records_fuzz_vs_oracle(codec, oracle, seed):
+    """random shapes (fuzz_sets; the model is pinned to the reference's own
+    MergeIterator on three of them in test_oracle_merge_order.py)"""
+    files = [oracle.table_build(r, int(np.random.default_rng(seed).choice([256, 4096, 32768])))
+             for r in fuzz_sets(seed)]
+    _check(codec, oracle, files)

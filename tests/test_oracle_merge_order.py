@@ -11,7 +11,7 @@ import subprocess
 import pytest
 from sstcodec import workload as W
 from test_gpu_dropin import REF_EXE, merge_steps, need
-from test_gpu_merge_records import _expected
+from test_gpu_merge_records import _expected, fuzz_sets
 
 CASES = {
     "overlap": lambda: W.compaction_inputs(5, 2000, 3000, seed=11, vmin=1, vmax=300),
@@ -19,6 +19,9 @@ CASES = {
     "many_inputs": lambda: W.compaction_inputs(20, 400, 5000, seed=12, vmin=1, vmax=120, distinct=False),
     "one_input": lambda: W.compaction_inputs(1, 3000, 9000, seed=9),
     "empty_values": lambda: W.compaction_inputs(4, 800, 900, seed=13, vmin=0, vmax=0, distinct=False),
+    "fuzz0": lambda: fuzz_sets(0),
+    "fuzz3": lambda: fuzz_sets(3),
+    "fuzz5": lambda: fuzz_sets(5),
 }
 
 
