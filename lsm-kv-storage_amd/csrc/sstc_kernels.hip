@@ -1289,7 +1289,10 @@ __device__ void enc_wave_offsets(const EncArgs &a, uint64_t b) {
 // neighbouring entries of the same inputs (config 4: 1-entry runs from 128
 // inputs), so their source lines are fetched once per L2: config 4 encode
 // FETCH 3.89 -> 2.33 GB, 845 -> 832 us (profiles/r05/encode_xcd.md)
-constexpr uint32_t kEncXcdChunk = 16;
+#ifndef SSTC_ENC_XCD_CHUNK
+#define SSTC_ENC_XCD_CHUNK 16
+#endif
+constexpr uint32_t kEncXcdChunk = SSTC_ENC_XCD_CHUNK;
 
 template <uint32_t kMode, uint32_t GK = 2, uint32_t GV = 8, uint32_t kQ = 2, uint32_t kU = kWaveSpanUnroll>
 __global__ __launch_bounds__(kEncWaves *kWave) void enc_lds_kernel(EncArgs a) {
