@@ -2,7 +2,8 @@
 // (maps of page-cache-hot SST files, H2D from them, D2H into pageable memory,
 // pwrite + fsync of output-sized files).  Diagnostic only.
 //   hipcc -O2 -std=c++20 tools/io_probe.cpp -o tools/io_probe -lpthread
-//   tools/io_probe <dir> <files> <MiB per file> [writes]   (writes: only the output-file section)
+//   tools/io_probe <dir> <files> <MiB per file> [writes|pin]   (writes: only the output-file section;
+//   pin: only the page-locking section)
 #include <hip/hip_runtime.h>
 
 #include <fcntl.h>
@@ -44,7 +45,8 @@ int main(int argc, char **argv) {
       close(fd);
     }
   }
-  const bool writes_only = argc > 4 && std::string(argv[4]) == "writes";
+  const bool writes_only = argc > 4 && (std::string(argv[4]) == "writes" || std::string(argv[4]) == "pin");
+  const bool pin_only = argc > 4 && std::string(argv[4]) == "pin";
   CK(hipSetDevice(0));
   CK(hipFree(nullptr));
   hipStream_t s;
@@ -203,6 +205,41 @@ int main(int argc, char **argv) {
       close(fd);
       std::printf("44 MiB pwrite x4 threads %.2f ms fsync %.2f ms\n", (t1 - t0) * 1e3, (t2 - t1) * 1e3);
     }
+  }
+  // page locking: hipHostMalloc against an anonymous map (populated) +
+  // hipHostRegister, alloc + free, and a 64 MiB H2D from each
+  if (pin_only) {
+    for (size_t mb : {size_t(1), size_t(8), size_t(32), size_t(64)}) {
+      const size_t n = mb << 20;
+      for (int rep = 0; rep < 2; rep++) {
+        double t0 = now();
+        void *p = nullptr;
+        CK(hipHostMalloc(&p, n, hipHostMallocPortable));
+        double t1 = now();
+        CK(hipHostFree(p));
+        double t2 = now();
+        void *q = mmap(nullptr, n, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_POPULATE, -1, 0);
+        double t3 = now();
+        CK(hipHostRegister(q, n, hipHostRegisterPortable));
+        double t4 = now();
+        if (mb == 64) {
+          double a = now();
+          CK(hipMemcpyAsync(dev, q, n, hipMemcpyHostToDevice, s));
+          CK(hipStreamSynchronize(s));
+          double b = now();
+          std::printf("  H2D 64 MiB from registered map: %.2f ms = %.1f GB/s\n", (b - a) * 1e3, n / (b - a) / 1e9);
+        }
+        CK(hipHostUnregister(q));
+        munmap(q, n);
+        double t5 = now();
+        std::printf("%zu MiB: hipHostMalloc %.2f ms (free %.2f) | mmap+populate %.2f + hipHostRegister %.2f ms "
+                    "(unregister+munmap %.2f)\n", mb, (t1 - t0) * 1e3, (t2 - t1) * 1e3, (t3 - t2) * 1e3,
+                    (t4 - t3) * 1e3, (t5 - t4) * 1e3);
+      }
+    }
+    CK(hipFree(dev));
+    std::printf("done\n");
+    return 0;
   }
   // O_DIRECT writes of a 44 MB table image from page-locked memory (what
   // TableBuilder::Finish does), one pwrite, 1 MiB / 8 MiB pieces, and the
